@@ -1,0 +1,268 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X hot path (the driver's contract).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--quick]
+
+One "step" = one fused flash-attention prefill forward over the BASELINE
+config (ch06, B=8 S=4096 H=32 D=128, bf16, non-causal) on every rank.
+Flash is "replicas only" (each rank an independent replica, no collective),
+so ``value`` = N x per-replica work / max-over-ranks time (weak scaling).
+
+The same JSON line carries, as sub-objects, the other hot-path rows:
+  gemv    ch03 decode GEMV 4096x4096 bf16 (W rotated over >256 MiB so every
+          launch streams from HBM, not the 256 MiB Infinity Cache)
+  gemm    ch05/ch03 4096^3 bf16 NN GEMM
+  tp_gemm ch09 row-parallel 8192x8192 GEMM, M=8192, + RCCL all-reduce over
+          xGMI when N > 1 (compute / all-reduce / total / bus bandwidth)
+  cpu_baseline  the reference tile loop restated on torch CPU (oracle, kind
+          "port"), rank 0, N=1 only, on a bounded sample of the workload.
+
+All device times are HIP events recorded on the stream the kernels run on.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "physics-llm-inference_amd")
+for _p in (PKG, ROOT):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "flash-attn prefill TFLOP/s + GEMV decode GB/s, as % of MI355X roofline"
+PEAK_BF16_TFLOPS = 2516.6   # 256 CU x 4096 FLOP/clk x 2.4 GHz (dense)
+PEAK_HBM_GBPS = 8000.0      # HBM3E datasheet
+B, H, S, D = 8, 32, 4096, 128
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def event_time_ms(fn, iters: int, stream) -> float:
+    """Mean ms per call of ``fn`` over ``iters`` back-to-back calls, HIP events
+    recorded on ``stream`` (the stream the kernels are launched on)."""
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    s.record(stream)
+    for _ in range(iters):
+        fn()
+    e.record(stream)
+    e.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def load_traffic(kernel: str):
+    """Per-launch HBM bytes of ``kernel`` from the committed rocprofv3 PMC
+    summary (profiles/traffic.json), or None."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get(kernel, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def bench_gemv(stream, iters: int) -> dict:
+    import pli_hip
+    from ch03 import gemv_bytes
+    m = k = 4096
+    copies = 12  # 12 x 32 MiB = 384 MiB > 256 MiB Infinity Cache
+    ws = [torch.randn(m, k, device="cuda", dtype=torch.bfloat16) for _ in range(copies)]
+    x = torch.randn(k, device="cuda", dtype=torch.bfloat16)
+    y = torch.empty(m, device="cuda", dtype=torch.bfloat16)
+    state = {"i": 0}
+
+    def call():
+        pli_hip.gemv(ws[state["i"] % copies], x, out=y)
+        state["i"] += 1
+
+    for _ in range(2 * copies):
+        call()
+    ms = event_time_ms(call, max(iters, 4 * copies), stream)
+    nbytes = gemv_bytes(m, k, torch.bfloat16)
+    gbps = nbytes / (ms * 1e-3) / 1e9
+    return {"workload": "ch03 GEMV 4096x4096 bf16, batch 1, W rotated over 384 MiB",
+            "us_per_launch": ms * 1e3, "GB/s": gbps,
+            "roofline": {"bound": "hbm", "achieved": gbps, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                         "frac": gbps / PEAK_HBM_GBPS, "algorithmic_bytes": nbytes,
+                         "traffic": load_traffic("gemv_vec")}}
+
+
+def bench_gemm(stream, iters: int) -> dict:
+    import pli_hip
+    n = 4096
+    a = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
+    c = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
+    for _ in range(3):
+        pli_hip.gemm(a, b, out=c)
+    ms = event_time_ms(lambda: pli_hip.gemm(a, b, out=c), iters, stream)
+    tf = 2 * n ** 3 / (ms * 1e-3) / 1e12
+    ms_t = event_time_ms(lambda: torch.mm(a, b), iters, stream)
+    return {"workload": "ch05/ch03 GEMM 4096^3 bf16 NN", "us_per_launch": ms * 1e3,
+            "TFLOP/s": tf, "torch_mm_TFLOP/s": 2 * n ** 3 / (ms_t * 1e-3) / 1e12,
+            "roofline": {"bound": "mfma", "achieved": tf, "peak": PEAK_BF16_TFLOPS,
+                         "unit": "TFLOP/s", "frac": tf / PEAK_BF16_TFLOPS}}
+
+
+def bench_tp(stream, world: int, rank: int, iters: int) -> dict:
+    """RowParallel 8192x8192 (K split over ranks), M = 8192, + RCCL all-reduce."""
+    import pli_hip
+    from ch09 import row_parallel_forward_overlapped, xgmi_all_reduce_bounds
+    M, N, K = 8192, 8192, 8192
+    kl = K // world
+    x = torch.randn(M, kl, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, kl, device="cuda", dtype=torch.bfloat16) * kl ** -0.5
+    y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    gemm = lambda: pli_hip.gemm(x, w, trans_b=True, out=y)  # noqa: E731
+    for _ in range(2):
+        gemm()
+    ms_gemm = event_time_ms(gemm, iters, stream)
+    out = {"workload": f"ch09 RowParallel 8192x8192 TP={world}, M={M}, bf16",
+           "gemm_us": ms_gemm * 1e3, "gemm_TFLOP/s": 2 * M * N * kl / (ms_gemm * 1e-3) / 1e12}
+    if world > 1:
+        def ar():
+            dist.all_reduce(y)
+        for _ in range(2):
+            ar()
+        torch.cuda.synchronize()
+        ms_ar = event_time_ms(ar, iters, stream)
+
+        def full():
+            gemm()
+            dist.all_reduce(y)
+        ms_full = event_time_ms(full, iters, stream)
+        ms_ovl = event_time_ms(lambda: row_parallel_forward_overlapped(x, w, chunks=4), iters, stream)
+        payload = M * N * 2
+        bounds = xgmi_all_reduce_bounds(payload, world)
+        out.update({"allreduce_us": ms_ar * 1e3, "total_us": ms_full * 1e3,
+                    "overlapped_total_us": ms_ovl * 1e3,
+                    "allreduce_busbw_GB/s": payload / (ms_ar * 1e-3) / 1e9 * bounds["bus_factor"],
+                    "xgmi_mesh_bound_us": bounds["mesh_us"], "xgmi_ring_bound_us": bounds["ring_us"]})
+    return out
+
+
+def cpu_baseline(seconds: float = 15.0) -> dict:
+    """The reference tile loop (oracle restatement, torch CPU) on a sample of
+    the flash workload: B=1 (1/8 of the batch), all 32 heads, S=4096, D=128."""
+    from oracle.attention import flash_tile_loop_torch
+    b = 1
+    g = torch.Generator().manual_seed(0)
+    q, k, v = (torch.randn(b, H, S, D, generator=g).to(torch.bfloat16) for _ in range(3))
+    flops = 4 * b * H * S * S * D
+    flash_tile_loop_torch(q[:, :2], k[:, :2], v[:, :2])  # warm
+    times, t_end = [], time.perf_counter() + seconds
+    while len(times) < 1 or (time.perf_counter() < t_end and len(times) < 5):
+        t0 = time.perf_counter()
+        flash_tile_loop_torch(q, k, v)
+        times.append(time.perf_counter() - t0)
+    sec = min(times)
+    return {"value": flops / sec / 1e12, "unit": "TFLOP/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"reference tile loop (ch06/flash_attention.py:14-74 restated, oracle/attention.py) "
+                      f"on torch CPU bf16, B=1 H=32 S=4096 D=128 = 1/8 of the workload, "
+                      f"best of {len(times)} runs ({sec:.2f} s each)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--quick", action="store_true", help="skip gemm/tp/cpu legs")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import pli_hip
+    assert pli_hip.available(), "libpli_hip.so must be built and a ROCm device visible"
+
+    stream = torch.cuda.current_stream()
+    gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
+    q, k, v = (torch.randn(B, H, S, D, device="cuda", dtype=torch.bfloat16, generator=gen)
+               for _ in range(3))
+    o = torch.empty_like(q)
+    step = lambda: pli_hip.flash_attn_fwd(q, k, v, out=o)  # noqa: E731
+    flops_step = 4 * B * H * S * S * D
+
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    ev_s, ev_e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev_s.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev_e.record(stream)
+    barrier()
+    wall = time.perf_counter() - t0
+    kernel_ms = ev_s.elapsed_time(ev_e) / args.steps  # per launch, on the launch stream
+    t = torch.tensor([wall], device="cuda", dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_max = t.item()
+    value = world * flops_step * args.steps / wall_max / 1e12
+    achieved = flops_step / (kernel_ms * 1e-3) / 1e12
+
+    extra = {}
+    if not args.quick:
+        extra["gemv"] = bench_gemv(stream, 200)
+        extra["gemm"] = bench_gemm(stream, 20)
+        extra["tp_gemm"] = bench_tp(stream, world, rank, 10)
+    else:
+        extra["gemv"] = bench_gemv(stream, 200)
+
+    result = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "TFLOP/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": wall_max / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (torch.randn N(0,1), seeded)",
+        "config": {"workload": "ch06 flash-attention prefill fwd, B=8 S=4096 H=32 D=128 bf16, "
+                               "non-causal, one fused HIP launch per step",
+                   "batch": B, "seq_len": S, "heads": H, "head_dim": D,
+                   "parallelism": f"replicas x{world} (flash does not shard; TP GEMM row-parallel)"},
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS,
+                     "unit": "TFLOP/s", "frac": achieved / PEAK_BF16_TFLOPS,
+                     "traffic": load_traffic("attn_fwd_mfma"),
+                     "kernel": "attn_fwd_mfma<bf16,128,4>", "algorithmic_flops": flops_step,
+                     "kernel_ms": kernel_ms},
+        **extra,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.quick:
+        result["cpu_baseline"] = cpu_baseline()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,125 @@
+/*
+ * pli.h -- C ABI of libpli_hip.so, the MI355X (gfx950) hot path of
+ * Infatoshi/physics-llm-inference re-built as hand-written HIP kernels.
+ *
+ * Conventions (every entry point):
+ *   - plain pointers and sizes only; no torch / HIP types in signatures.
+ *     `stream` is a hipStream_t passed as void* (NULL = the null stream).
+ *   - the CALLER owns every buffer, outputs included; the library never
+ *     allocates, frees or synchronises (calls are graph-capturable).
+ *   - device pointers must be 16-byte aligned for the vectorised kernels;
+ *     misaligned / oddly strided operands are routed to the generic kernels.
+ *   - strides are in ELEMENTS; the innermost (head_dim / K) stride is 1.
+ *   - return value: PLI_OK (0), a hipError_t code (1..999) from the launch,
+ *     or one of the PLI_E* codes below.  pli_last_error() returns a
+ *     thread-local message for the last failing call on this thread.
+ *
+ * The reference has no FFI layer: its boundary is a set of
+ * Python call signatures.  Each entry point below names the reference
+ * function whose device arithmetic it replaces; the Python mirror packages
+ * (physics-llm-inference_amd/ch0X) keep those signatures and call in here.
+ */
+#ifndef PLI_H
+#define PLI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* element types */
+enum {
+    PLI_F32 = 0,
+    PLI_F16 = 1,
+    PLI_BF16 = 2
+};
+
+/* status codes beyond hipError_t */
+enum {
+    PLI_OK = 0,
+    PLI_EINVAL = 1000,      /* bad argument (shape, stride, dtype, null)     */
+    PLI_EUNSUPPORTED = 1001 /* valid but not implemented on this path        */
+};
+
+/* Library version string, e.g. "pli_hip 0.1.0 gfx950". */
+const char* pli_version(void);
+
+/* Message for the last non-zero return on the calling thread ("" if none). */
+const char* pli_last_error(void);
+
+/*
+ * Fused attention forward:  O = softmax(Q K^T * scale [+ causal mask]) V.
+ *
+ * Replaces the device work of
+ *   ch06/flash_attention.py:14-74   flash_attention_forward (tile loop)
+ *   ch06/attention_memory.py:19-33  naive_attention
+ *   ch01/attention.py:65-69         MultiHeadAttention.forward core
+ *   ch01/gqa.py:30-34               GQA (kv head = h / (H / Hkv), no repeat)
+ *
+ * Layout: logical [batch, heads, n, head_dim]; q/o have `heads` heads and
+ * n_q rows, k/v have `kv_heads` heads and n_kv rows.  strides[12] holds, in
+ * elements, {q_b, q_h, q_n, k_b, k_h, k_n, v_b, v_h, v_n, o_b, o_h, o_n}.
+ * causal != 0 masks key j for query i when j > i + (n_kv - n_q)
+ * (bottom-right aligned, = torch.triu(ones, diagonal=1) when n_q == n_kv).
+ * dtype: PLI_BF16 / PLI_F16 run the MFMA kernel (head_dim 64 or 128),
+ * PLI_F32 (and any other head_dim <= 256) the generic fp32-accumulate kernel.
+ * Softmax statistics are fp32 regardless of dtype.
+ */
+int pli_flash_attn_fwd(const void* q, const void* k, const void* v, void* o,
+                       int batch, int heads, int kv_heads, int n_q, int n_kv,
+                       int head_dim, const int64_t* strides, float scale,
+                       int causal, int dtype, void* stream);
+
+/*
+ * GEMV  y[m] = sum_k W[m, k] * x[k]   (fp32 accumulate, output in dtype).
+ * Replaces torch.mv in ch03/gemv_benchmark.py:38 (decode weight GEMV).
+ * W row-major with leading dimension ldw (elements, >= k).
+ */
+int pli_gemv(const void* w, const void* x, void* y, int m, int k, int64_t ldw,
+             int dtype, void* stream);
+
+/*
+ * GEMM  C[m, n] = A[m, k] * op(B) (+ bias[n])   (fp32 accumulate).
+ * trans_b = 0: B is [k, n] row-major (torch.mm, ch03/gemm_benchmark.py:35,
+ *              ch05/tiled_matmul.cu:22-61);
+ * trans_b = 1: B is [n, k] row-major, i.e. C = A B^T (F.linear,
+ *              ch09/tensor_parallel.py:39,67; ch01/attention.py:59-61,71;
+ *              x @ weight.T of ch03/batching_benchmark.py:30).
+ * bias may be NULL.  A, C row-major with leading dimensions lda, ldc.
+ */
+int pli_gemm(const void* a, const void* b, void* c, const void* bias, int m,
+             int n, int k, int64_t lda, int64_t ldb, int64_t ldc, int trans_b,
+             int dtype, void* stream);
+
+/*
+ * HBM calibration kernels of ch05/coalescing.cu:7-20 (fp32):
+ *   out[i] = 2 * in[i * stride],  i in [0, n_out).
+ * stride == 1 is the coalesced stream (16-byte vector loads), the roofline
+ * denominator measured on the device; stride > 1 is the strided contrast.
+ */
+int pli_scale_copy(const float* in, float* out, int64_t n_out, int stride,
+                   void* stream);
+
+/*
+ * Row softmax with the single-pass online (max, sum) recurrence of
+ * ch06/online_softmax.py:13-25 (== standard_softmax, :5-10), over the last
+ * dimension of a contiguous [rows, n] tensor; statistics in fp32.
+ */
+int pli_softmax_rows(const void* x, void* y, int64_t rows, int n, int dtype,
+                     void* stream);
+
+/*
+ * ch06/online_softmax.py:28-53 online_softmax_with_output over contiguous
+ * x [rows, n] and v [rows, n, dv]:  o[r] = sum_i softmax(x[r])_i v[r, i],
+ * d[r] = sum_i exp(x[r, i] - max_r).  o is [rows, dv], d is [rows].
+ */
+int pli_online_softmax_with_output(const void* x, const void* v, void* o,
+                                   void* d, int64_t rows, int n, int dv,
+                                   int dtype, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PLI_H */

@@ -1,0 +1,46 @@
+"""GEMV / GEMM / tensor-parallel oracles in float64 (test infrastructure only)."""
+from __future__ import annotations
+
+import numpy as np
+
+
+def gemv(w, x):
+    """y = W x, ``torch.mv(weight, x)`` of ``ch03/gemv_benchmark.py:34-48``."""
+    return np.asarray(w, dtype=np.float64) @ np.asarray(x, dtype=np.float64)
+
+
+def batched_gemv(x, w):
+    """Y = X W^T, ``x @ weight.T`` of ``ch03/batching_benchmark.py:25-39``."""
+    return np.asarray(x, dtype=np.float64) @ np.asarray(w, dtype=np.float64).T
+
+
+def gemm(a, b):
+    """C = A B (NN), ``torch.mm(a, b)`` of ``ch03/gemm_benchmark.py:35-49``."""
+    return np.asarray(a, dtype=np.float64) @ np.asarray(b, dtype=np.float64)
+
+
+def linear(x, w, bias=None):
+    """Y = X W^T + b, ``F.linear`` as called in ``ch09/tensor_parallel.py:39,67``."""
+    y = np.asarray(x, dtype=np.float64) @ np.asarray(w, dtype=np.float64).T
+    if bias is not None:
+        y = y + np.asarray(bias, dtype=np.float64)
+    return y
+
+
+def row_parallel_sum(x_full, w_full, world_size: int):
+    """Sum over ranks of the row-parallel partials X[:, s_r] W[:, s_r]^T.
+
+    ``RowParallelLinear`` (``ch09/tensor_parallel.py:43-68``) holds the column
+    slice s_r of W; the all-reduce this build adds must reproduce the full
+    ``F.linear(x_full, w_full)``.
+    """
+    x_full = np.asarray(x_full, dtype=np.float64)
+    w_full = np.asarray(w_full, dtype=np.float64)
+    k = x_full.shape[-1]
+    assert k % world_size == 0
+    part = k // world_size
+    total = np.zeros(x_full.shape[:-1] + (w_full.shape[0],))
+    for r in range(world_size):
+        s = slice(r * part, (r + 1) * part)
+        total += x_full[..., s] @ w_full[:, s].T
+    return total

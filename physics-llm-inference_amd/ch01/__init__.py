@@ -1,0 +1,10 @@
+"""Chapter 01 attention on MI355X (the hot-path subset: attention modules)."""
+
+from .attention import (
+    MultiHeadAttention,
+    SingleHeadAttention,
+    causal_attention,
+    naive_attention,
+)
+
+__all__ = ["MultiHeadAttention", "SingleHeadAttention", "causal_attention", "naive_attention"]

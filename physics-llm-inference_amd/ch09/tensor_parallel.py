@@ -1,0 +1,153 @@
+"""Tensor-parallel linear layers -- mirror of ``ch09/tensor_parallel.py``, with
+the communication the reference only describes made real.
+
+Reference behaviour kept (``:15-100``): the same constructor arguments, the
+same shard shapes (column: W [out/ws, in]; row: W [out, in/ws]), the same
+``kaiming_uniform_`` init order, ``RowParallelLinear`` ignores its bias and
+returns the partial product when it runs outside a process group, so the
+single-process ``world_size=4`` behaviour is unchanged.
+
+MI355X additions:
+
+* on a ROCm device every shard GEMM is the HIP kernel ``pli_gemm``
+  (NT layout: W stays [out, in] row-major; bias fused in the epilogue);
+* when ``torch.distributed`` is initialised with ``world_size`` ranks,
+  ``RowParallelLinear.forward`` completes the row-parallel product with
+  ``all_reduce(SUM)`` -- backend "nccl", which is RCCL over xGMI on ROCm
+  (one process per GPU, launched by torchrun);
+* ``row_parallel_forward_overlapped`` splits the rows of X into chunks and
+  all-reduces chunk i (async, on RCCL's stream) while the GEMM of chunk i+1
+  runs, hiding compute under the xGMI transfer.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+
+import pli_hip
+
+
+@dataclass
+class TensorParallelConfig:
+    world_size: int = 1
+    rank: int = 0
+    hidden_dim: int = 4096
+    intermediate_dim: int = 14336
+
+
+def _shard_linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None) -> torch.Tensor:
+    """y = x W^T (+ b) on the local shard; HIP on ROCm tensors."""
+    if not x.is_cuda:
+        return F.linear(x, w, bias)
+    lead = x.shape[:-1]
+    y = pli_hip.gemm(x.reshape(-1, x.shape[-1]), w.detach(), trans_b=True,
+                     bias=None if bias is None else bias.detach())
+    return y.view(*lead, w.shape[0])
+
+
+def tp_group_active(world_size: int, group=None) -> bool:
+    """True when a process group of exactly ``world_size`` ranks exists."""
+    return (world_size > 1 and dist.is_available() and dist.is_initialized()
+            and dist.get_world_size(group) == world_size)
+
+
+class ColumnParallelLinear(nn.Module):
+    """Y_r = X W_r^T + b_r with W_r the rank's [out/ws, in] row block.  No
+    communication: like the reference, the layer returns its output shard."""
+
+    def __init__(self, in_features: int, out_features: int, world_size: int = 1, rank: int = 0,
+                 bias: bool = False):
+        super().__init__()
+        self.world_size = world_size
+        self.rank = rank
+        assert out_features % world_size == 0
+        self.out_features_per_partition = out_features // world_size
+        self.weight = nn.Parameter(torch.empty(self.out_features_per_partition, in_features))
+        self.bias = nn.Parameter(torch.zeros(self.out_features_per_partition)) if bias else None
+        nn.init.kaiming_uniform_(self.weight)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return _shard_linear(x, self.weight, self.bias)
+
+
+class RowParallelLinear(nn.Module):
+    """Y = sum_r X_r W_r^T with W_r the rank's [out, in/ws] column block."""
+
+    def __init__(self, in_features: int, out_features: int, world_size: int = 1, rank: int = 0,
+                 bias: bool = False, group=None):
+        super().__init__()
+        self.world_size = world_size
+        self.rank = rank
+        self.group = group
+        assert in_features % world_size == 0
+        self.in_features_per_partition = in_features // world_size
+        self.weight = nn.Parameter(torch.empty(out_features, self.in_features_per_partition))
+        self.bias = nn.Parameter(torch.zeros(out_features)) if bias else None
+        nn.init.kaiming_uniform_(self.weight)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        y = _shard_linear(x, self.weight, None)  # reference ignores the bias (:66-68)
+        if tp_group_active(self.world_size, self.group):
+            dist.all_reduce(y, op=dist.ReduceOp.SUM, group=self.group)
+        return y
+
+
+def row_parallel_forward_overlapped(x: torch.Tensor, weight: torch.Tensor, chunks: int = 4,
+                                    group=None) -> torch.Tensor:
+    """Chunked RowParallel forward: GEMM of rows-chunk i+1 overlaps the async
+    all-reduce of chunk i (RCCL runs on its own stream).  Same result as
+    ``RowParallelLinear.forward`` up to fp32-accumulate rounding."""
+    x2 = x.reshape(-1, x.shape[-1])
+    m = x2.shape[0]
+    out = torch.empty(m, weight.shape[0], dtype=x.dtype, device=x.device)
+    bounds = [m * i // chunks for i in range(chunks + 1)]
+    handles = []
+    for i in range(chunks):
+        lo, hi = bounds[i], bounds[i + 1]
+        if hi == lo:
+            continue
+        part = out[lo:hi]
+        if x2.is_cuda:
+            pli_hip.gemm(x2[lo:hi], weight.detach(), trans_b=True, out=part)
+        else:
+            part.copy_(F.linear(x2[lo:hi], weight))
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+            handles.append(dist.all_reduce(part, op=dist.ReduceOp.SUM, group=group, async_op=True))
+    for h in handles:
+        h.wait()
+    return out.view(*x.shape[:-1], weight.shape[0])
+
+
+class TensorParallelMLP(nn.Module):
+    """gate/up column-parallel, down row-parallel: one all-reduce per MLP."""
+
+    def __init__(self, config: TensorParallelConfig):
+        super().__init__()
+        self.config = config
+        self.gate_proj = ColumnParallelLinear(config.hidden_dim, config.intermediate_dim,
+                                              config.world_size, config.rank)
+        self.up_proj = ColumnParallelLinear(config.hidden_dim, config.intermediate_dim,
+                                            config.world_size, config.rank)
+        self.down_proj = RowParallelLinear(config.intermediate_dim, config.hidden_dim,
+                                           config.world_size, config.rank)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.down_proj(F.silu(self.gate_proj(x)) * self.up_proj(x))
+
+
+def compute_tp_memory_savings(hidden_dim: int, intermediate_dim: int, world_size: int,
+                              dtype_bytes: int = 2) -> dict:
+    """MLP weight bytes dense vs per rank (gate + up + down = 3 h i params)."""
+    params = 3 * hidden_dim * intermediate_dim
+    per_gpu = params / world_size
+    return {
+        "dense_params": params,
+        "dense_memory_mb": params * dtype_bytes / 1024 / 1024,
+        "tp_params_per_gpu": per_gpu,
+        "tp_memory_per_gpu_mb": per_gpu * dtype_bytes / 1024 / 1024,
+        "memory_reduction": world_size,
+    }

@@ -1,0 +1,443 @@
+// Fused attention forward for gfx950 (MI355X).
+//
+// Replaces the Python tile loop of ch06/flash_attention.py:14-74 (about 12
+// torch launches per (q-block, k-block) pair, every intermediate through HBM)
+// with ONE launch: Q stays in registers, K/V tiles stream through LDS, the
+// online softmax runs in registers with fp32 statistics.
+//
+// MFMA kernel (bf16 / fp16, head_dim 64 or 128), one wave = 32 query rows:
+//   S^T = K Q^T      v_mfma_f32_32x32x16  A = K tile (ds_read_b128, LDS),
+//                                         B = Q fragment (registers)
+//   -> lane l owns query row l&31; its 64 tile scores sit in 32 registers
+//      split over the two half-waves, so the row max / sum are 31 VALU ops
+//      plus one cross-half exchange (no LDS, no per-tile cross-lane sum: l is
+//      kept per lane and combined once at the end).
+//   O^T += V^T P^T   v_mfma_f32_32x32x16  A = V^T (ds_read_b64_tr_b16 from the
+//                                         row-major V tile), B = P straight
+//                                         from the S^T accumulator registers
+//   -> O^T keeps the query row on the lane too, so the online-softmax rescale
+//      and the final 1/l are lane-local.
+// K and V share one XOR-swizzled LDS image layout that is conflict-free for
+// both the row reads (b128) and the transposed reads (tr_b16); tiles are
+// register-staged (global loads for tile t+1 issued before tile t's MFMAs,
+// written to the other LDS buffer after them), one barrier per tile.
+// Blocks are remapped so each XCD works through a contiguous range of heads:
+// a head's K/V is then read from HBM once and re-read from that XCD's L2 by
+// all of the head's query blocks.
+//
+// Generic kernel (fp32, or any head_dim <= 128, or unaligned operands):
+// LDS-tiled VALU kernel with the same online recurrence, fp32 accumulate.
+#include <cmath>
+
+#include "pli_common.h"
+
+namespace pli {
+namespace {
+
+struct AttnStrides {
+    int64_t qb, qh, qn, kb, kh, kn, vb, vh, vn, ob, oh, on;
+};
+
+constexpr int KT = 64;  // keys per LDS tile
+constexpr int QW = 32;  // query rows per wave
+
+// Byte offset of 16-byte chunk `ch` of row `row` in a [KT][D] 16-bit tile.
+// D=128 (256-B rows): chunk ^= ((row&3)<<2 | (row>>2)&3);  D=64 (128-B rows,
+// two rows per 256-B bank row): chunk ^= g((row>>1)&7) with g(i) =
+// ((i&1)<<2)|(i>>1).  Both are conflict-free for a b128 read of 16 distinct
+// rows mod 16 and for a tr_b16 read of 4 aligned rows x 4 aligned chunks.
+template <int D>
+__device__ __forceinline__ int swz_off(int row, int ch) {
+    if constexpr (D == 128) {
+        const int f = ((row & 3) << 2) | ((row >> 2) & 3);
+        return row * 256 + ((ch ^ f) << 4);
+    } else {
+        static_assert(D == 64, "MFMA attention supports head_dim 64 and 128");
+        const int i = (row >> 1) & 7;
+        const int g = ((i & 1) << 2) | (i >> 1);
+        return row * 128 + ((ch ^ g) << 4);
+    }
+}
+
+template <typename T, int D, int NW>
+__global__ __launch_bounds__(NW * 64, 2) void attn_fwd_mfma(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
+    const uint16_t* __restrict__ v, uint16_t* __restrict__ o, int H, int group,
+    int Nq, int Nk, AttnStrides st, float c, int causal, int qblocks,
+    int nblocks) {
+    constexpr int NT = NW * 64;
+    constexpr int TILE = KT * D * 2;  // bytes of one K (or V) tile
+    constexpr int CPR = D / 8;        // 16-byte chunks per row
+    constexpr int CPT = KT * CPR / NT;
+    static_assert((KT * CPR) % NT == 0, "tile chunks must split evenly");
+    __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h32 = lane >> 5, l32 = lane & 31;
+
+    const int lb = xcd_remap(blockIdx.x, nblocks);
+    const int bh = lb / qblocks, qblk = lb % qblocks;
+    const int b = bh / H, hq = bh % H, hk = hq / group;
+    const int qbase = qblk * (NW * QW);
+    const int q0 = qbase + wave * QW;
+    const int off_diag = Nk - Nq;  // causal: row i sees keys <= i + off_diag
+
+    const uint16_t* qp = q + b * st.qb + hq * st.qh;
+    const uint16_t* kp = k + b * st.kb + hk * st.kh;
+    const uint16_t* vp = v + b * st.vb + hk * st.vh;
+
+    // Q^T fragments (B operand): query row q0+l32, d = 16kk + 8h32 .. +7.
+    i32x4 qf[D / 16];
+    {
+        const int qr = q0 + l32;
+        const bool ok = qr < Nq;
+        const uint16_t* src = qp + (int64_t)(ok ? qr : 0) * st.qn + 8 * h32;
+#pragma unroll
+        for (int kk = 0; kk < D / 16; ++kk) {
+            const i32x4 x = *reinterpret_cast<const i32x4*>(src + 16 * kk);
+            qf[kk] = ok ? x : i32x4{0, 0, 0, 0};
+        }
+    }
+
+    int kv_end = Nk;
+    if (causal) kv_end = min(Nk, qbase + NW * QW + off_diag);
+    const int ntiles = kv_end > 0 ? cdiv(kv_end, KT) : 0;
+
+    // register staging of one K tile + one V tile
+    i32x4 kst[CPT], vst[CPT];
+    auto load_tile = [&](int t) {
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+            const int cidx = tid + i * NT;
+            const int row = cidx / CPR, ch = cidx % CPR;
+            const int key = t * KT + row;
+            const int kc = min(key, Nk - 1);  // always issue the load
+            const i32x4 kx = *reinterpret_cast<const i32x4*>(kp + (int64_t)kc * st.kn + ch * 8);
+            const i32x4 vx = *reinterpret_cast<const i32x4*>(vp + (int64_t)kc * st.vn + ch * 8);
+            const bool ok = key < Nk;
+            kst[i] = ok ? kx : i32x4{0, 0, 0, 0};
+            vst[i] = ok ? vx : i32x4{0, 0, 0, 0};
+        }
+    };
+    auto store_tile = [&](int buf) {
+        char* kb = smem + buf * 2 * TILE;
+        char* vb = kb + TILE;
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+            const int cidx = tid + i * NT;
+            const int off = swz_off<D>(cidx / CPR, cidx % CPR);
+            lds_write_b128(kb, off, kst[i]);
+            lds_write_b128(vb, off, vst[i]);
+        }
+    };
+
+    f32x16 oacc[D / 32];
+#pragma unroll
+    for (int d = 0; d < D / 32; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[d][r] = 0.f;
+    float m_run = -1e30f;  // running max, already scaled by c (log2 domain)
+    float l_run = 0.f;     // this lane's share of the running denominator
+
+    // tr_b16 addressing: lane 4qq+pp of 16-lane group g reads row qq,
+    // columns 4pp..4pp+3 of a 4x16 block.
+    const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+
+    if (ntiles > 0) {
+        load_tile(0);
+        store_tile(0);
+    }
+    __syncthreads();
+
+    for (int t = 0; t < ntiles; ++t) {
+        const int buf = t & 1;
+        if (t + 1 < ntiles) load_tile(t + 1);
+        const char* kb = smem + buf * 2 * TILE;
+        const char* vb = kb + TILE;
+
+        // ---- S^T = K Q^T : s[tt][r] = score(key tt*32 + krow(r), query l32)
+        f32x16 s[2];
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[tt][r] = 0.f;
+#pragma unroll
+            for (int kk = 0; kk < D / 16; ++kk) {
+                const i32x4 kf = lds_read_b128(kb, swz_off<D>(tt * 32 + l32, 2 * kk + h32));
+                s[tt] = mfma32x32x16<T>(kf, qf[kk], s[tt]);
+            }
+        }
+
+        // ---- masks: ragged last tile, causal diagonal (wave-uniform test)
+        const int key0 = t * KT;
+        const bool need_mask = (key0 + KT > Nk) || (causal && key0 + KT - 1 > q0 + off_diag);
+        if (need_mask) {
+            const int lim = causal ? q0 + l32 + off_diag : Nk;
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int key = key0 + tt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
+                    if (key >= Nk || key > lim) s[tt][r] = -INFINITY;
+                }
+        }
+
+        // ---- online softmax, row = l32
+        float mx = s[0][0];
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[tt][r]);
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float m_new = fmaxf(m_run, mx * c);
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+        m_run = m_new;
+        float rs = 0.f;
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float p = __builtin_amdgcn_exp2f(fmaf(s[tt][r], c, -m_new));
+                s[tt][r] = p;
+                rs += p;
+            }
+        l_run = fmaf(l_run, alpha, rs);
+#pragma unroll
+        for (int d = 0; d < D / 32; ++d)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
+
+        // P^T fragments: registers 8s2..8s2+7 of s[tt] are k-step s2 (keys
+        // 16s2 + 8(j>>2) + 4h32 + (j&3) of the 32-key half tt).
+        i32x4 pb[2][2];
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const int r0 = 8 * s2;
+                pb[tt][s2] = i32x4{(int)pack2<T>(s[tt][r0 + 0], s[tt][r0 + 1]),
+                                   (int)pack2<T>(s[tt][r0 + 2], s[tt][r0 + 3]),
+                                   (int)pack2<T>(s[tt][r0 + 4], s[tt][r0 + 5]),
+                                   (int)pack2<T>(s[tt][r0 + 6], s[tt][r0 + 7])};
+            }
+
+        // ---- O^T += V^T P^T ; V^T fragment via two transposed reads
+#pragma unroll
+        for (int dblk = 0; dblk < D / 32; ++dblk) {
+            const int ch = dblk * 4 + 2 * (g & 1) + (pp >> 1);
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    const int row = tt * 32 + 16 * s2 + 4 * h32 + qq;
+                    const i32x2 lo = lds_read_tr16(vb, swz_off<D>(row, ch) + 8 * (pp & 1));
+                    const i32x2 hi = lds_read_tr16(vb, swz_off<D>(row + 8, ch) + 8 * (pp & 1));
+                    const i32x4 vf = {lo.x, lo.y, hi.x, hi.y};
+                    oacc[dblk] = mfma32x32x16<T>(vf, pb[tt][s2], oacc[dblk]);
+                }
+        }
+
+        if (t + 1 < ntiles) store_tile(buf ^ 1);
+        __syncthreads();
+    }
+
+    // ---- epilogue: O = O^T / l, query row l32, d = dblk*32 + 8i + 4h32 + 0..3
+    const float l = l_run + __shfl_xor(l_run, 32, 64);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const int qr = q0 + l32;
+    if (qr < Nq) {
+        uint16_t* op = o + b * st.ob + hq * st.oh + (int64_t)qr * st.on;
+#pragma unroll
+        for (int dblk = 0; dblk < D / 32; ++dblk)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int d = dblk * 32 + 8 * i + 4 * h32;
+                const i32x2 w = {(int)pack2<T>(oacc[dblk][4 * i] * inv, oacc[dblk][4 * i + 1] * inv),
+                                 (int)pack2<T>(oacc[dblk][4 * i + 2] * inv, oacc[dblk][4 * i + 3] * inv)};
+                *reinterpret_cast<i32x2*>(op + d) = w;
+            }
+    }
+}
+
+// --------------------------------------------------------------------------
+// Generic kernel: 256 threads own 32 query rows (8 threads per row, each
+// thread owns columns sub + 8u of the score tile and d = sub + 8u of O).
+constexpr int GQ = 32, GK = 64, GDMAX = 128;
+
+template <typename T>
+__global__ __launch_bounds__(256) void attn_fwd_generic(
+    const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v,
+    T* __restrict__ o, int H, int group, int Nq, int Nk, int D, AttnStrides st,
+    float scale, int causal, int qblocks) {
+    extern __shared__ __attribute__((aligned(16))) float gsm[];
+    const int ldq = D + 1;
+    float* Qs = gsm;                 // [GQ][D+1]
+    float* Ks = Qs + GQ * ldq;       // [GK][D+1]
+    float* Vs = Ks + GK * ldq;       // [GK][D]
+    float* Ps = Vs + GK * D;         // [GQ][GK+1]
+
+    const int tid = threadIdx.x, row = tid >> 3, sub = tid & 7;
+    const int bh = blockIdx.x / qblocks, qblk = blockIdx.x % qblocks;
+    const int b = bh / H, hq = bh % H, hk = hq / group;
+    const int q0 = qblk * GQ;
+    const int off_diag = Nk - Nq;
+    const T* qp = q + b * st.qb + hq * st.qh;
+    const T* kp = k + b * st.kb + hk * st.kh;
+    const T* vp = v + b * st.vb + hk * st.vh;
+
+    for (int i = tid; i < GQ * D; i += 256) {
+        const int r = i / D, d = i % D;
+        Qs[r * ldq + d] = (q0 + r < Nq) ? elem<T>::to_f32(qp[(int64_t)(q0 + r) * st.qn + d]) : 0.f;
+    }
+
+    float acc[GDMAX / 8];
+#pragma unroll
+    for (int u = 0; u < GDMAX / 8; ++u) acc[u] = 0.f;
+    float m_run = -INFINITY, l_run = 0.f;
+    const int qi = q0 + row;
+    const int lim = causal ? qi + off_diag : Nk - 1;
+    int kv_end = Nk;
+    if (causal) kv_end = min(Nk, q0 + GQ + off_diag);
+
+    for (int k0 = 0; k0 < kv_end; k0 += GK) {
+        __syncthreads();
+        for (int i = tid; i < GK * D; i += 256) {
+            const int r = i / D, d = i % D;
+            const bool ok = k0 + r < Nk;
+            Ks[r * ldq + d] = ok ? elem<T>::to_f32(kp[(int64_t)(k0 + r) * st.kn + d]) : 0.f;
+            Vs[r * D + d] = ok ? elem<T>::to_f32(vp[(int64_t)(k0 + r) * st.vn + d]) : 0.f;
+        }
+        __syncthreads();
+        float sc[GK / 8];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int u = 0; u < GK / 8; ++u) {
+            const int j = sub + 8 * u;
+            float dot = 0.f;
+            for (int d = 0; d < D; ++d) dot = fmaf(Qs[row * ldq + d], Ks[j * ldq + d], dot);
+            const int key = k0 + j;
+            dot = (key < Nk && key <= lim) ? dot * scale : -INFINITY;
+            sc[u] = dot;
+            mx = fmaxf(mx, dot);
+        }
+#pragma unroll
+        for (int o2 = 1; o2 < 8; o2 <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o2, 64));
+        const float m_new = fmaxf(m_run, mx);
+        const float alpha = (m_new == -INFINITY) ? 1.f : expf(m_run - m_new);
+        float rs = 0.f;
+#pragma unroll
+        for (int u = 0; u < GK / 8; ++u) {
+            const float p = (m_new == -INFINITY) ? 0.f : expf(sc[u] - m_new);
+            Ps[row * (GK + 1) + sub + 8 * u] = p;
+            rs += p;
+        }
+#pragma unroll
+        for (int o2 = 1; o2 < 8; o2 <<= 1) rs += __shfl_xor(rs, o2, 64);
+        l_run = l_run * alpha + rs;
+        m_run = m_new;
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < GDMAX / 8; ++u) {
+            const int d = sub + 8 * u;
+            if (d < D) {
+                float a = acc[u] * alpha;
+                for (int j = 0; j < GK; ++j) a = fmaf(Ps[row * (GK + 1) + j], Vs[j * D + d], a);
+                acc[u] = a;
+            }
+        }
+    }
+    if (qi < Nq) {
+        const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+        T* op = o + b * st.ob + hq * st.oh + (int64_t)qi * st.on;
+#pragma unroll
+        for (int u = 0; u < GDMAX / 8; ++u) {
+            const int d = sub + 8 * u;
+            if (d < D) op[d] = elem<T>::from_f32(acc[u] * inv);
+        }
+    }
+}
+
+template <typename T, int D>
+int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int H,
+                int group, int Nq, int Nk, const AttnStrides& st, float scale,
+                int causal, hipStream_t stream) {
+    constexpr int NW = 4;
+    const int qblocks = cdiv(Nq, NW * QW);
+    const int64_t nb = (int64_t)B * H * qblocks;
+    PLI_REQUIRE(nb < (1ll << 31), "pli_flash_attn_fwd: grid too large");
+    const float c = scale * 1.4426950408889634f;  // fold log2(e) into the scale
+    hipLaunchKernelGGL((attn_fwd_mfma<T, D, NW>), dim3((unsigned)nb), dim3(NW * 64), 0, stream,
+                       (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o,
+                       H, group, Nq, Nk, st, c, causal, qblocks, (int)nb);
+    return launch_status("attn_fwd_mfma");
+}
+
+template <typename T>
+int launch_generic(const void* q, const void* k, const void* v, void* o, int B, int H,
+                   int group, int Nq, int Nk, int D, const AttnStrides& st, float scale,
+                   int causal, hipStream_t stream) {
+    const int qblocks = cdiv(Nq, GQ);
+    const int64_t nb = (int64_t)B * H * qblocks;
+    PLI_REQUIRE(nb < (1ll << 31), "pli_flash_attn_fwd: grid too large");
+    const size_t lds = sizeof(float) * ((size_t)GQ * (D + 1) + (size_t)GK * (D + 1) +
+                                        (size_t)GK * D + (size_t)GQ * (GK + 1));
+    hipLaunchKernelGGL((attn_fwd_generic<T>), dim3((unsigned)nb), dim3(256), lds, stream,
+                       (const T*)q, (const T*)k, (const T*)v, (T*)o, H, group, Nq, Nk, D, st,
+                       scale, causal, qblocks);
+    return launch_status("attn_fwd_generic");
+}
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+}  // namespace pli
+
+extern "C" int pli_flash_attn_fwd(const void* q, const void* k, const void* v, void* o,
+                                  int batch, int heads, int kv_heads, int n_q, int n_kv,
+                                  int head_dim, const int64_t* strides, float scale,
+                                  int causal, int dtype, void* stream) {
+    using namespace pli;
+    clear_error();
+    PLI_REQUIRE(q && k && v && o && strides, "pli_flash_attn_fwd: null pointer");
+    PLI_REQUIRE(batch >= 0 && heads > 0 && kv_heads > 0 && n_q >= 0 && n_kv >= 0 && head_dim > 0,
+                "pli_flash_attn_fwd: bad shape B=%d H=%d Hkv=%d Nq=%d Nk=%d D=%d", batch, heads,
+                kv_heads, n_q, n_kv, head_dim);
+    PLI_REQUIRE(heads % kv_heads == 0, "pli_flash_attn_fwd: heads %d not a multiple of kv_heads %d",
+                heads, kv_heads);
+    PLI_REQUIRE(dtype == PLI_F32 || dtype == PLI_F16 || dtype == PLI_BF16,
+                "pli_flash_attn_fwd: bad dtype %d", dtype);
+    PLI_REQUIRE(std::isfinite(scale), "pli_flash_attn_fwd: non-finite scale");
+    if (batch == 0 || n_q == 0) return PLI_OK;
+    const AttnStrides st{strides[0], strides[1], strides[2], strides[3], strides[4], strides[5],
+                         strides[6], strides[7], strides[8], strides[9], strides[10], strides[11]};
+    const int group = heads / kv_heads;
+    hipStream_t s = (hipStream_t)stream;
+    // n_kv == 0 (softmax over no keys) goes to the generic kernel, which
+    // defines the output as zeros.
+    bool vec = (dtype == PLI_BF16 || dtype == PLI_F16) && (head_dim == 64 || head_dim == 128) &&
+               aligned16(q) && aligned16(k) && aligned16(v) && aligned16(o) && n_kv > 0;
+    for (int i = 0; i < 12; ++i) {
+        const bool inner = (i % 3) == 2;
+        vec = vec && (strides[i] % 8 == 0) && (!inner || strides[i] >= head_dim);
+    }
+    if (vec) {
+        if (dtype == PLI_BF16)
+            return head_dim == 128 ? launch_mfma<bf16_t, 128>(q, k, v, o, batch, heads, group, n_q, n_kv, st, scale, causal, s)
+                                   : launch_mfma<bf16_t, 64>(q, k, v, o, batch, heads, group, n_q, n_kv, st, scale, causal, s);
+        return head_dim == 128 ? launch_mfma<f16_t, 128>(q, k, v, o, batch, heads, group, n_q, n_kv, st, scale, causal, s)
+                               : launch_mfma<f16_t, 64>(q, k, v, o, batch, heads, group, n_q, n_kv, st, scale, causal, s);
+    }
+    if (head_dim > GDMAX) {
+        set_error("pli_flash_attn_fwd: head_dim %d > %d unsupported on the generic path", head_dim,
+                  GDMAX);
+        return PLI_EUNSUPPORTED;
+    }
+    switch (dtype) {
+        case PLI_F32:
+            return launch_generic<float>(q, k, v, o, batch, heads, group, n_q, n_kv, head_dim, st, scale, causal, s);
+        case PLI_F16:
+            return launch_generic<f16_t>(q, k, v, o, batch, heads, group, n_q, n_kv, head_dim, st, scale, causal, s);
+        default:
+            return launch_generic<bf16_t>(q, k, v, o, batch, heads, group, n_q, n_kv, head_dim, st, scale, causal, s);
+    }
+}

@@ -1,0 +1,137 @@
+// Decode GEMV y = W x for gfx950 (MI355X): the torch.mv of
+// ch03/gemv_benchmark.py:38.  HBM-bound (AI ~1 FLOP/B): no MFMA, no LDS.
+//
+// Each wave owns ROWS consecutive rows.  Lane l streams the 16-byte chunks
+// l, l+64, ... of every row with global_load_dwordx4 (non-temporal: W is read
+// exactly once per call), all ROWS x CPL loads issued before the first use so
+// a CU keeps ROWS*CPL KiB per wave in flight; the x chunks are loaded once per
+// k-step and reused for the ROWS rows.  fp32 accumulate, one 64-lane
+// shuffle reduction per row, output rounded once to the output dtype.
+#include "pli_common.h"
+
+namespace pli {
+namespace {
+
+template <typename T>
+__device__ __forceinline__ void dot_chunk(const i32x4& w, const i32x4& x, float& acc);
+
+template <>
+__device__ __forceinline__ void dot_chunk<bf16_t>(const i32x4& w, const i32x4& x, float& acc) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t a = (uint32_t)w[i], b = (uint32_t)x[i];
+        acc = fmaf(__uint_as_float(a << 16), __uint_as_float(b << 16), acc);
+        acc = fmaf(__uint_as_float(a & 0xffff0000u), __uint_as_float(b & 0xffff0000u), acc);
+    }
+}
+template <>
+__device__ __forceinline__ void dot_chunk<f16_t>(const i32x4& w, const i32x4& x, float& acc) {
+    typedef __attribute__((ext_vector_type(2))) _Float16 h2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const h2 a = __builtin_bit_cast(h2, w[i]), b = __builtin_bit_cast(h2, x[i]);
+        acc = fmaf((float)a.x, (float)b.x, acc);
+        acc = fmaf((float)a.y, (float)b.y, acc);
+    }
+}
+template <>
+__device__ __forceinline__ void dot_chunk<float>(const i32x4& w, const i32x4& x, float& acc) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc = fmaf(__int_as_float(w[i]), __int_as_float(x[i]), acc);
+}
+
+template <typename T, int ROWS, int CPL>
+__global__ __launch_bounds__(256) void gemv_vec(const char* __restrict__ w,
+                                                const char* __restrict__ x, T* __restrict__ y,
+                                                int M, int nchunks, int64_t ldw_bytes) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int row0 = (blockIdx.x * 4 + wave) * ROWS;
+    if (row0 >= M) return;
+    float acc[ROWS];
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) acc[r] = 0.f;
+    const char* wrow[ROWS];
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) wrow[r] = w + (int64_t)min(row0 + r, M - 1) * ldw_bytes;
+
+    for (int c0 = 0; c0 < nchunks; c0 += 64 * CPL) {
+        i32x4 xv[CPL], wv[ROWS][CPL];
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) {
+            const int cc = min(c0 + lane + 64 * u, nchunks - 1);
+            xv[u] = *reinterpret_cast<const i32x4*>(x + (int64_t)cc * 16);
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r)
+                wv[r][u] = __builtin_nontemporal_load(
+                    reinterpret_cast<const i32x4*>(wrow[r] + (int64_t)cc * 16));
+        }
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) {
+            if (c0 + lane + 64 * u < nchunks) {
+#pragma unroll
+                for (int r = 0; r < ROWS; ++r) dot_chunk<T>(wv[r][u], xv[u], acc[r]);
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) acc[r] = wave_sum(acc[r]);
+    if (lane < ROWS && row0 + lane < M) {
+        float out = acc[0];
+#pragma unroll
+        for (int r = 1; r < ROWS; ++r) out = (lane == r) ? acc[r] : out;
+        y[row0 + lane] = elem<T>::from_f32(out);
+    }
+}
+
+// Scalar fallback for ragged K / unaligned operands: one wave per row.
+template <typename T>
+__global__ __launch_bounds__(256) void gemv_scalar(const T* __restrict__ w, const T* __restrict__ x,
+                                                   T* __restrict__ y, int M, int K, int64_t ldw) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    float acc = 0.f;
+    for (int kk = lane; kk < K; kk += 64)
+        acc = fmaf(elem<T>::to_f32(w[(int64_t)row * ldw + kk]), elem<T>::to_f32(x[kk]), acc);
+    acc = wave_sum(acc);
+    if (lane == 0) y[row] = elem<T>::from_f32(acc);
+}
+
+template <typename T>
+int launch(const void* w, const void* x, void* y, int m, int k, int64_t ldw, hipStream_t s) {
+    constexpr int EPC = 16 / elem<T>::bytes;  // elements per 16-byte chunk
+    const bool vec = (k % EPC == 0) && (ldw % EPC == 0) &&
+                     ((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(x)) & 15) == 0;
+    if (!vec) {
+        hipLaunchKernelGGL(gemv_scalar<T>, dim3(cdiv(m, 4)), dim3(256), 0, s, (const T*)w,
+                           (const T*)x, (T*)y, m, k, ldw);
+        return launch_status("gemv_scalar");
+    }
+    const int nchunks = k / EPC;
+    const int64_t ldw_b = ldw * elem<T>::bytes;
+    constexpr int ROWS = 2, CPL = 8;
+    hipLaunchKernelGGL((gemv_vec<T, ROWS, CPL>), dim3(cdiv(m, 4 * ROWS)), dim3(256), 0, s,
+                       (const char*)w, (const char*)x, (T*)y, m, nchunks, ldw_b);
+    return launch_status("gemv_vec");
+}
+
+}  // namespace
+}  // namespace pli
+
+extern "C" int pli_gemv(const void* w, const void* x, void* y, int m, int k, int64_t ldw,
+                        int dtype, void* stream) {
+    using namespace pli;
+    clear_error();
+    PLI_REQUIRE(w && x && y, "pli_gemv: null pointer");
+    PLI_REQUIRE(m >= 0 && k >= 0 && ldw >= k, "pli_gemv: bad shape m=%d k=%d ldw=%lld", m, k,
+                (long long)ldw);
+    if (m == 0) return PLI_OK;
+    PLI_REQUIRE(k > 0, "pli_gemv: k must be positive");
+    hipStream_t s = (hipStream_t)stream;
+    switch (dtype) {
+        case PLI_F32: return launch<float>(w, x, y, m, k, ldw, s);
+        case PLI_F16: return launch<f16_t>(w, x, y, m, k, ldw, s);
+        case PLI_BF16: return launch<bf16_t>(w, x, y, m, k, ldw, s);
+        default: set_error("pli_gemv: bad dtype %d", dtype); return PLI_EINVAL;
+    }
+}

@@ -1,0 +1,238 @@
+"""ctypes binding of ``libpli_hip.so`` (the C ABI declared in ``include/pli.h``).
+
+Every wrapper takes torch tensors that already live on a ROCm device, passes
+raw ``data_ptr()`` values plus sizes/strides and the current HIP stream across
+the C ABI, and raises ``PliError`` on a non-zero status.  There is no CPU or
+torch fallback in here: if the library is missing or a tensor is not on the
+GPU, the call fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+__all__ = [
+    "PliError", "lib", "library_path", "available", "DTYPE_CODE",
+    "flash_attn_fwd", "gemv", "gemm", "scale_copy", "softmax_rows",
+    "online_softmax_with_output",
+]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "libpli_hip.so")
+_lib = None
+
+DTYPE_CODE = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}
+
+_c_int, _c_i64, _c_f32, _vp = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
+
+# name -> argtypes, mirroring include/pli.h
+_SIGS = {
+    "pli_version": [],
+    "pli_last_error": [],
+    "pli_flash_attn_fwd": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
+                           ctypes.POINTER(_c_i64), _c_f32, _c_int, _c_int, _vp],
+    "pli_gemv": [_vp, _vp, _vp, _c_int, _c_int, _c_i64, _c_int, _vp],
+    "pli_gemm": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_i64, _c_i64, _c_i64, _c_int,
+                 _c_int, _vp],
+    "pli_scale_copy": [_vp, _vp, _c_i64, _c_int, _vp],
+    "pli_softmax_rows": [_vp, _vp, _c_i64, _c_int, _c_int, _vp],
+    "pli_online_softmax_with_output": [_vp, _vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_int, _vp],
+}
+
+
+class PliError(RuntimeError):
+    """A libpli_hip entry point returned a non-zero status."""
+
+
+def library_path() -> str:
+    return _LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    """Load libpli_hip.so (after torch, so both share torch's HIP runtime)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            raise PliError(
+                f"{_LIB_PATH} is not built; run `python physics-llm-inference_amd/build.py` "
+                "(or __graft_entry__.build())")
+        L = ctypes.CDLL(_LIB_PATH)
+        for name, argtypes in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = argtypes
+            fn.restype = ctypes.c_char_p if name in ("pli_version", "pli_last_error") else _c_int
+        _lib = L
+    return _lib
+
+
+def available() -> bool:
+    """True when the library loads AND a ROCm device is visible."""
+    try:
+        lib()
+    except (PliError, OSError):
+        return False
+    return torch.cuda.is_available()
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().pli_last_error().decode(errors="replace")
+        raise PliError(f"{what} failed with status {rc}: {msg}")
+
+
+def _dtype_code(t: torch.Tensor) -> int:
+    try:
+        return DTYPE_CODE[t.dtype]
+    except KeyError:
+        raise PliError(f"unsupported dtype {t.dtype} (HIP path supports fp32/fp16/bf16)") from None
+
+
+def _require_gpu(*ts: torch.Tensor) -> torch.device:
+    dev = ts[0].device
+    for t in ts:
+        if not t.is_cuda:
+            raise PliError("HIP path called with a CPU tensor")
+        if t.device != dev:
+            raise PliError(f"tensors on different devices: {t.device} vs {dev}")
+        if t.dtype != ts[0].dtype:
+            raise PliError(f"mixed dtypes {t.dtype} vs {ts[0].dtype}")
+    return dev
+
+
+def _stream(dev: torch.device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _ptr(t: torch.Tensor | None) -> ctypes.c_void_p:
+    return ctypes.c_void_p(t.data_ptr() if t is not None else None)
+
+
+# ------------------------------------------------------------------ attention
+def flash_attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | None = None,
+                   causal: bool = False, out: torch.Tensor | None = None) -> torch.Tensor:
+    """O = softmax(Q K^T * scale [+ causal]) V on [B, H, N, D] tensors (any
+    strides with a unit head_dim stride); K/V may have fewer (GQA) heads."""
+    dev = _require_gpu(q, k, v)
+    if q.dim() != 4 or k.dim() != 4 or v.dim() != 4:
+        raise PliError("flash_attn_fwd expects [B, H, N, D] tensors")
+    B, H, Nq, D = q.shape
+    Bk, Hkv, Nk, Dk = k.shape
+    if (Bk, Dk) != (B, D) or tuple(v.shape) != tuple(k.shape):
+        raise PliError(f"shape mismatch q{tuple(q.shape)} k{tuple(k.shape)} v{tuple(v.shape)}")
+    if H % Hkv != 0:
+        raise PliError(f"heads {H} not a multiple of kv heads {Hkv}")
+    q, k, v = (t if t.stride(-1) == 1 else t.contiguous() for t in (q, k, v))
+    if out is None:
+        out = torch.empty_like(q, memory_format=torch.contiguous_format)
+    _require_gpu(q, out)
+    if tuple(out.shape) != tuple(q.shape) or out.stride(-1) != 1:
+        raise PliError("bad output tensor")
+    if scale is None:
+        scale = D ** -0.5
+    st = (_c_i64 * 12)(*(int(x) for t in (q, k, v, out) for x in t.stride()[:3]))
+    with torch.cuda.device(dev):
+        rc = lib().pli_flash_attn_fwd(_ptr(q), _ptr(k), _ptr(v), _ptr(out), B, H, Hkv, Nq, Nk, D,
+                                      st, float(scale), int(bool(causal)), _dtype_code(q),
+                                      _stream(dev))
+    _check(rc, "pli_flash_attn_fwd")
+    return out
+
+
+# ---------------------------------------------------------------------- GEMV
+def gemv(w: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """y = W x (torch.mv semantics), W [m, k] with unit column stride."""
+    dev = _require_gpu(w, x)
+    if w.dim() != 2 or x.dim() != 1 or w.shape[1] != x.shape[0]:
+        raise PliError(f"gemv shape mismatch {tuple(w.shape)} x {tuple(x.shape)}")
+    if w.stride(1) != 1:
+        w = w.contiguous()
+    x = x.contiguous()
+    m, k = w.shape
+    if out is None:
+        out = torch.empty(m, dtype=w.dtype, device=dev)
+    with torch.cuda.device(dev):
+        rc = lib().pli_gemv(_ptr(w), _ptr(x), _ptr(out), m, k, max(w.stride(0), k),
+                            _dtype_code(w), _stream(dev))
+    _check(rc, "pli_gemv")
+    return out
+
+
+# ---------------------------------------------------------------------- GEMM
+def gemm(a: torch.Tensor, b: torch.Tensor, trans_b: bool = False,
+         bias: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """C = A B (trans_b=False, torch.mm) or A B^T (+ bias) (trans_b=True, F.linear)."""
+    ts = (a, b) if bias is None else (a, b, bias)
+    dev = _require_gpu(*ts)
+    if a.dim() != 2 or b.dim() != 2:
+        raise PliError("gemm expects 2-D operands")
+    m, k = a.shape
+    n, kb = (b.shape if trans_b else (b.shape[1], b.shape[0]))
+    if kb != k:
+        raise PliError(f"gemm inner dims differ: {tuple(a.shape)} vs {tuple(b.shape)} trans_b={trans_b}")
+    if a.stride(1) != 1:
+        a = a.contiguous()
+    if b.stride(1) != 1:
+        b = b.contiguous()
+    if bias is not None:
+        bias = bias.contiguous()
+        if bias.shape != (n,):
+            raise PliError(f"bias must be [{n}]")
+    if out is None:
+        out = torch.empty((m, n), dtype=a.dtype, device=dev)
+    lda = a.stride(0) if m > 1 else k
+    ldb = b.stride(0) if b.shape[0] > 1 else b.shape[1]
+    with torch.cuda.device(dev):
+        rc = lib().pli_gemm(_ptr(a), _ptr(b), _ptr(out), _ptr(bias), m, n, k, max(lda, 1),
+                            max(ldb, 1), max(out.stride(0), n), int(bool(trans_b)),
+                            _dtype_code(a), _stream(dev))
+    _check(rc, "pli_gemm")
+    return out
+
+
+# -------------------------------------------------------------- calibration
+def scale_copy(inp: torch.Tensor, out: torch.Tensor, stride: int = 1) -> torch.Tensor:
+    """out[i] = 2 * inp[i * stride] (fp32), the ch05/coalescing.cu probes."""
+    dev = _require_gpu(inp, out)
+    if inp.dtype != torch.float32 or not inp.is_contiguous() or not out.is_contiguous():
+        raise PliError("scale_copy expects contiguous fp32 tensors")
+    n_out = out.numel()
+    if (n_out - 1) * stride >= inp.numel() and n_out > 0:
+        raise PliError("scale_copy: input too short for stride")
+    with torch.cuda.device(dev):
+        rc = lib().pli_scale_copy(_ptr(inp), _ptr(out), n_out, int(stride), _stream(dev))
+    _check(rc, "pli_scale_copy")
+    return out
+
+
+# ------------------------------------------------------------------ softmax
+def softmax_rows(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Softmax over the last dim with the single-pass online (m, d) recurrence."""
+    dev = _require_gpu(x)
+    x = x.contiguous()
+    n = x.shape[-1] if x.dim() > 0 else 1
+    rows = x.numel() // max(n, 1)
+    if out is None:
+        out = torch.empty_like(x)
+    with torch.cuda.device(dev):
+        rc = lib().pli_softmax_rows(_ptr(x), _ptr(out), rows, n, _dtype_code(x), _stream(dev))
+    _check(rc, "pli_softmax_rows")
+    return out
+
+
+def online_softmax_with_output(x: torch.Tensor, v: torch.Tensor):
+    """(o, d): softmax(x)-weighted rows of v, and the denominator at the final max."""
+    dev = _require_gpu(x, v)
+    x, v = x.contiguous(), v.contiguous()
+    n, dv = x.shape[-1], v.shape[-1]
+    if tuple(v.shape[:-1]) != tuple(x.shape):
+        raise PliError(f"v shape {tuple(v.shape)} does not match x {tuple(x.shape)}")
+    rows = x.numel() // n
+    o = torch.empty(x.shape[:-1] + (dv,), dtype=x.dtype, device=dev)
+    d = torch.empty(x.shape[:-1], dtype=x.dtype, device=dev)
+    with torch.cuda.device(dev):
+        rc = lib().pli_online_softmax_with_output(_ptr(x), _ptr(v), _ptr(o), _ptr(d), rows, n, dv,
+                                                  _dtype_code(x), _stream(dev))
+    _check(rc, "pli_online_softmax_with_output")
+    return o, d

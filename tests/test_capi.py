@@ -1,0 +1,90 @@
+"""C ABI checks that need no GPU: the library loads, exports every entry point
+include/pli.h declares, validates arguments before touching the device, and
+the product path has no route to the oracle or to a CPU fallback."""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+from conftest import PKG, ROOT
+
+HEADER = os.path.join(ROOT, "include", "pli.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(pli_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_the_hot_path():
+    syms = declared_symbols()
+    for s in ("pli_flash_attn_fwd", "pli_gemv", "pli_gemm", "pli_scale_copy", "pli_softmax_rows",
+              "pli_online_softmax_with_output", "pli_last_error", "pli_version"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol(built_lib):
+    lib = ctypes.CDLL(built_lib)
+    for s in declared_symbols():
+        assert hasattr(lib, s), f"{s} declared in pli.h but not exported"
+
+
+def test_version_and_error_strings(built_lib):
+    import pli_hip
+    L = pli_hip.lib()
+    assert L.pli_version().decode().startswith("pli_hip")
+    assert L.pli_last_error() is not None
+
+
+def test_argument_validation_without_gpu(built_lib):
+    """Null pointers / bad shapes are rejected with PLI_EINVAL and a message,
+    before any HIP call (so this runs on a GPU-less host)."""
+    import pli_hip
+    L = pli_hip.lib()
+    EINVAL = 1000
+    rc = L.pli_gemv(None, None, None, 16, 16, 16, 2, None)
+    assert rc == EINVAL and b"null" in L.pli_last_error()
+    p = ctypes.c_void_p(16)  # never dereferenced: validation fails first
+    assert L.pli_gemv(p, p, p, 16, 32, 16, 2, None) == EINVAL  # ldw < k
+    assert b"bad shape" in L.pli_last_error()
+    assert L.pli_gemm(p, p, p, None, 8, 8, 8, 8, 8, 8, 0, 7, None) == EINVAL  # bad dtype
+    st = (ctypes.c_int64 * 12)(*([0] * 12))
+    assert L.pli_flash_attn_fwd(p, p, p, p, 1, 6, 4, 8, 8, 64, st, 0.1, 0, 2, None) == EINVAL
+    assert b"multiple of kv_heads" in L.pli_last_error()
+    assert L.pli_flash_attn_fwd(p, p, p, p, 1, 4, 4, 8, 8, 64, st, float("nan"), 0, 2, None) == EINVAL
+    assert L.pli_scale_copy(p, p, 16, 0, None) == EINVAL
+    assert L.pli_softmax_rows(p, p, 4, 0, 0, None) == EINVAL
+
+
+def test_hip_path_refuses_cpu_tensors(built_lib):
+    import pli_hip
+    x = torch.randn(4, 4)
+    with pytest.raises(pli_hip.PliError):
+        pli_hip.gemm(x, x)
+    with pytest.raises(pli_hip.PliError):
+        pli_hip.flash_attn_fwd(x[None, None], x[None, None], x[None, None])
+
+
+def test_product_never_imports_the_oracle():
+    """Nothing under physics-llm-inference_amd/ may import or reach oracle/."""
+    offenders = []
+    for dirpath, _, files in os.walk(PKG):
+        for f in files:
+            if f.endswith(".py"):
+                src = open(os.path.join(dirpath, f)).read()
+                if re.search(r"^\s*(from|import)\s+oracle\b", src, re.M) or "oracle/" in src:
+                    offenders.append(os.path.join(dirpath, f))
+    assert not offenders, offenders
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    import pli_hip
+    monkeypatch.setattr(pli_hip, "_lib", None)
+    monkeypatch.setattr(pli_hip, "_LIB_PATH", str(tmp_path / "absent.so"))
+    with pytest.raises(pli_hip.PliError, match="not built"):
+        pli_hip.lib()
+    assert not pli_hip.available()

@@ -1,0 +1,290 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the pinned oracle.
+
+Tolerances (north_star): 1e-3 for fp32, 1e-2 for bf16/fp16 outputs of the
+attention path, measured against the float64 oracle on the same rounded
+inputs.  GEMV/GEMM outputs grow like sqrt(K), so their bound is relative:
+|err| <= tol * (|ref| + 1) with the per-dtype tol below (output rounding to
+bf16 alone is 2^-9 relative).
+"""
+from __future__ import annotations
+
+import glob
+import os
+import zlib
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, load_golden
+from oracle import attention as oatt
+from oracle import linear as olin
+from oracle.numerics import bf16_from_bits, seeded_normal
+
+pytestmark = pytest.mark.gpu
+
+TDT = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}
+ATTN_TOL = {"fp32": 1e-3, "fp16": 1e-2, "bf16": 1e-2}
+LIN_TOL = {"fp32": 1e-4, "fp16": 4e-3, "bf16": 1e-2}
+DEV = "cuda"
+
+
+def dev(a, dt):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV).to(TDT[dt])
+
+
+def assert_attn_close(out, ref, dt, what=""):
+    out = out.float().cpu().numpy().astype(np.float64)
+    err = np.abs(out - ref).max()
+    assert np.isfinite(out).all(), f"{what}: non-finite output"
+    assert err <= ATTN_TOL[dt], f"{what}: max |err| {err:.3e} > {ATTN_TOL[dt]}"
+    return err
+
+
+def assert_lin_close(out, ref, dt, what=""):
+    out = out.float().cpu().numpy().astype(np.float64)
+    bound = LIN_TOL[dt] * (np.abs(ref) + 1.0)
+    bad = np.abs(out - ref) > bound
+    assert not bad.any(), f"{what}: {bad.sum()} elements beyond tol, max err {np.abs(out - ref).max():.3e}"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    import pli_hip
+    assert pli_hip.available(), "libpli_hip.so must load on the GPU box"
+    yield
+
+
+# ------------------------------------------------------------- attention ---
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "flash_*.npz"))),
+                         ids=os.path.basename)
+def test_flash_golden(path):
+    """HIP flash vs the reference naive attention in f64 (fixture), and no
+    worse than the reference's own flash output."""
+    from ch06 import flash_attention_forward
+    g = load_golden(os.path.basename(path))
+    B, H, N, D = (int(x) for x in g["shape"])
+    dt, seed = str(g["dtype"]), int(g["seed"])
+    q, k, v = (seeded_normal((B, H, N, D), seed * 10 + i, dt) for i in range(3))
+    out = flash_attention_forward(dev(q, dt), dev(k, dt), dev(v, dt))
+    assert out.dtype == TDT[dt] and tuple(out.shape) == (B, H, N, D)
+    ref = g["ref_naive_f64"].astype(np.float64)
+    err = assert_attn_close(out, ref, dt, os.path.basename(path))
+    ref_flash = bf16_from_bits(g["ref_flash"]) if dt == "bf16" else g["ref_flash"].astype(np.float32)
+    assert err <= np.abs(ref_flash - ref).max() + ATTN_TOL[dt] / 2
+
+
+CASES = [
+    # B, H, Hkv, Nq, Nk, D, dtype, causal
+    (1, 4, 4, 1024, 1024, 128, "bf16", False),
+    (2, 4, 4, 333, 333, 128, "bf16", False),
+    (1, 3, 3, 257, 257, 64, "fp16", False),
+    (2, 4, 4, 256, 256, 128, "bf16", True),
+    (1, 2, 2, 200, 200, 64, "bf16", True),
+    (1, 8, 2, 384, 384, 128, "bf16", True),    # GQA 4:1
+    (1, 8, 2, 130, 130, 64, "fp16", False),    # GQA, ragged
+    (1, 4, 4, 64, 300, 128, "bf16", True),     # Nq < Nk: bottom-right causal
+    (1, 2, 2, 1, 77, 64, "bf16", False),       # single query row
+    (1, 2, 2, 100, 100, 32, "fp32", True),     # generic kernel, odd head_dim
+    (1, 2, 2, 150, 150, 128, "fp32", False),
+    (1, 2, 2, 96, 96, 80, "bf16", False),      # generic kernel for bf16 (D=80)
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "b{}h{}kv{}q{}k{}d{}_{}{}".format(*c[:7], "_causal" if c[7] else ""))
+def test_flash_vs_oracle(case):
+    import pli_hip
+    B, H, Hkv, Nq, Nk, D, dt, causal = case
+    seed = zlib.crc32(repr(case).encode()) % 1000
+    q = seeded_normal((B, H, Nq, D), seed, dt)
+    k = seeded_normal((B, Hkv, Nk, D), seed + 1, dt)
+    v = seeded_normal((B, Hkv, Nk, D), seed + 2, dt)
+    out = pli_hip.flash_attn_fwd(dev(q, dt), dev(k, dt), dev(v, dt), causal=causal)
+    ref = oatt.naive_attention(q, k, v, causal=causal)
+    assert_attn_close(out, ref, dt, str(case))
+
+
+def test_flash_strided_views_and_out_param():
+    """Non-contiguous [B,H,S,hd] views (the MHA layout) read/written in place."""
+    import pli_hip
+    B, S, H, D = 2, 192, 4, 128
+    x = seeded_normal((3, B, S, H, D), 5, "bf16")
+    t = dev(x, "bf16")
+    q, k, v = (t[i].transpose(1, 2) for i in range(3))
+    o = torch.empty(B, S, H, D, dtype=torch.bfloat16, device=DEV)
+    pli_hip.flash_attn_fwd(q, k, v, causal=True, out=o.transpose(1, 2))
+    ref = oatt.naive_attention(*(x[i].transpose(0, 2, 1, 3) for i in range(3)), causal=True)
+    assert_attn_close(o.transpose(1, 2), ref, "bf16", "strided")
+
+
+def test_flash_forced_rescale_spike():
+    """A key spike in a late tile forces the online max to jump (rule 26)."""
+    import pli_hip
+    B, H, N, D = 1, 2, 512, 128
+    q = seeded_normal((B, H, N, D), 7, "bf16")
+    k = seeded_normal((B, H, N, D), 8, "bf16")
+    v = seeded_normal((B, H, N, D), 9, "bf16")
+    k[:, :, 450] = np.float32(4.0) * np.sign(q[:, :, 3])  # row 3 jumps at tile 7
+    from oracle.numerics import round_to_bf16
+    k = round_to_bf16(k)
+    out = pli_hip.flash_attn_fwd(dev(q, "bf16"), dev(k, "bf16"), dev(v, "bf16"))
+    assert_attn_close(out, oatt.naive_attention(q, k, v), "bf16", "spike")
+
+
+def test_flash_full_config_properties():
+    """B=8 S=4096 H=32 D=128 bf16 (the bench config): v = 1 gives exactly 1;
+    two heads checked against the f64 oracle; key permutation invariance."""
+    import pli_hip
+    B, H, N, D = 8, 32, 4096, 128
+    g = torch.Generator(device=DEV).manual_seed(0)
+    q, k, v = (torch.randn(B, H, N, D, device=DEV, dtype=torch.bfloat16, generator=g) for _ in range(3))
+    out = pli_hip.flash_attn_fwd(q, k, v)
+    ones = pli_hip.flash_attn_fwd(q, k, torch.ones_like(v))
+    assert (ones.float() - 1).abs().max().item() <= 2 ** -8  # one bf16 ulp below 1
+    for (b, h) in ((0, 0), (7, 31)):
+        ref = oatt.naive_attention(*(t[b:b + 1, h:h + 1].float().cpu().numpy() for t in (q, k, v)))
+        assert_attn_close(out[b:b + 1, h:h + 1], ref, "bf16", f"full b{b} h{h}")
+    perm = torch.randperm(N, device=DEV, generator=g)
+    out_p = pli_hip.flash_attn_fwd(q[:, :2], k[:, :2, perm], v[:, :2, perm])
+    assert (out_p.float() - out[:, :2].float()).abs().max().item() <= 1e-2
+
+
+def test_mha_hip_matches_reference_golden():
+    from ch01 import MultiHeadAttention
+    g = load_golden("mha.npz")
+    torch.manual_seed(0)
+    mha = MultiHeadAttention(512, 8).to(DEV)
+    x = torch.from_numpy(seeded_normal((1, 128, 512), 31)).to(DEV)
+    with torch.no_grad():
+        for causal, key in ((True, "y_causal"), (False, "y_noncausal")):
+            y = mha(x, causal=causal).cpu().numpy()
+            np.testing.assert_allclose(y, g[key], rtol=1e-3, atol=1e-4)
+
+
+def test_ch06_reference_gpu_cases():
+    """ch06/test_ch06.py:158-189 restated: fp16 flash vs naive (torch) on device."""
+    from ch06 import flash_attention_forward, naive_attention
+    torch.manual_seed(0)
+    for (B, H, N, D), tol in (((2, 4, 128, 64), 0.01), ((1, 8, 512, 64), 0.02)):
+        q, k, v = (torch.randn(B, H, N, D, device=DEV, dtype=torch.float16) for _ in range(3))
+        torch.testing.assert_close(flash_attention_forward(q, k, v), naive_attention(q, k, v),
+                                   rtol=tol, atol=tol)
+
+
+# ------------------------------------------------------------------ GEMV ---
+@pytest.mark.parametrize("m,k,dt", [(4096, 4096, "bf16"), (4096, 4096, "fp16"), (1000, 4096, "fp32"),
+                                    (333, 1000, "bf16"), (128, 4104, "bf16"), (64, 37, "bf16"),
+                                    (7, 8192, "fp16"), (8192, 8192, "bf16")])
+def test_gemv_vs_oracle(m, k, dt):
+    import pli_hip
+    w = seeded_normal((m, k), m + k, dt)
+    x = seeded_normal((k,), m * 3 + 1, dt)
+    y = pli_hip.gemv(dev(w, dt), dev(x, dt))
+    assert_lin_close(y, olin.gemv(w, x), dt, f"gemv {m}x{k} {dt}")
+
+
+def test_gemv_strided_rows():
+    import pli_hip
+    w = seeded_normal((256, 1024), 3, "bf16")
+    wt = dev(w, "bf16")[:, :1000]  # ldw 1024 > k 1000
+    x = seeded_normal((1000,), 4, "bf16")
+    y = pli_hip.gemv(wt, dev(x, "bf16"))
+    assert_lin_close(y, olin.gemv(w[:, :1000], x), "bf16", "strided gemv")
+
+
+# ------------------------------------------------------------------ GEMM ---
+@pytest.mark.parametrize("m,n,k,dt,tb", [
+    (512, 512, 512, "bf16", False), (512, 512, 512, "bf16", True),
+    (300, 264, 200, "bf16", False), (300, 264, 200, "fp16", True),
+    (129, 72, 64, "bf16", True), (64, 64, 64, "fp32", False), (100, 60, 70, "fp32", True),
+    (8, 4096, 4096, "bf16", True), (1, 256, 512, "bf16", False), (77, 77, 13, "bf16", False)])
+def test_gemm_vs_oracle(m, n, k, dt, tb):
+    import pli_hip
+    a = seeded_normal((m, k), 10 + m, dt)
+    b = seeded_normal((n, k) if tb else (k, n), 20 + n, dt)
+    c = pli_hip.gemm(dev(a, dt), dev(b, dt), trans_b=tb)
+    ref = olin.linear(a, b) if tb else olin.gemm(a, b)
+    assert_lin_close(c, ref, dt, f"gemm {m}x{n}x{k} {dt} tb={tb}")
+
+
+def test_gemm_bias_epilogue():
+    import pli_hip
+    a, w = seeded_normal((192, 256), 1, "bf16"), seeded_normal((136, 256), 2, "bf16")
+    bias = seeded_normal((136,), 3, "bf16")
+    c = pli_hip.gemm(dev(a, "bf16"), dev(w, "bf16"), trans_b=True, bias=dev(bias, "bf16"))
+    assert_lin_close(c, olin.linear(a, w, bias), "bf16", "bias")
+
+
+def test_gemm_4096_cube_rows():
+    """The ch05/ch03 config (4096^3 bf16, NN): 64 random rows vs f64."""
+    import pli_hip
+    m = n = k = 4096
+    a, b = seeded_normal((m, k), 31, "bf16"), seeded_normal((k, n), 32, "bf16")
+    c = pli_hip.gemm(dev(a, "bf16"), dev(b, "bf16")).float().cpu().numpy()
+    rows = np.random.RandomState(0).choice(m, 64, replace=False)
+    assert_lin_close(torch.from_numpy(c[rows]), olin.gemm(a[rows], b), "bf16", "4096^3")
+
+
+# ------------------------------------------------------- softmax / stream ---
+@pytest.mark.parametrize("shape,dt", [((4, 8, 64), "fp32"), ((5,), "fp32"), ((33, 1000), "bf16"),
+                                      ((7, 4097), "fp16")])
+def test_softmax_rows(shape, dt):
+    from ch06 import online_softmax, standard_softmax
+    x = seeded_normal(shape, 42, dt)
+    ref = oatt.standard_softmax(x)
+    for fn in (online_softmax, standard_softmax):
+        y = fn(dev(x, dt)).float().cpu().numpy()
+        np.testing.assert_allclose(y, ref, rtol=LIN_TOL[dt] * 2, atol=1e-6 if dt == "fp32" else 2e-3)
+
+
+def test_softmax_large_logits_stable():
+    from ch06 import online_softmax
+    x = torch.tensor([1000.0, 1001.0, 1002.0], device=DEV)
+    y = online_softmax(x)
+    assert torch.isfinite(y).all()
+    np.testing.assert_allclose(y.cpu().numpy(), oatt.standard_softmax(x.cpu().numpy()), rtol=1e-6)
+
+
+def test_online_softmax_with_output_golden():
+    from ch06 import online_softmax_with_output
+    g = load_golden("softmax.npz")
+    x4, v4 = seeded_normal((2, 4, 32), 22), seeded_normal((2, 4, 32, 16), 23)
+    o, d = online_softmax_with_output(dev(x4, "fp32"), dev(v4, "fp32"))
+    np.testing.assert_allclose(o.cpu().numpy(), g["x4_o"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(d.cpu().numpy(), g["x4_d"], rtol=1e-5, atol=1e-6)
+
+
+def test_scale_copy_exact():
+    import pli_hip
+    src = torch.randn(1 << 20, device=DEV)
+    out = torch.empty_like(src)
+    pli_hip.scale_copy(src, out)
+    assert torch.equal(out, src * 2)
+    out_s = torch.empty((1 << 20) // 32, device=DEV)
+    pli_hip.scale_copy(src, out_s, stride=32)
+    assert torch.equal(out_s, src[::32] * 2)
+
+
+# ------------------------------------------------------------------- TP ----
+def test_tensor_parallel_shards_sum_to_full_linear():
+    """Row-parallel partials of 4 shards (one process) sum to F.linear; the
+    chunked/overlapped path equals the plain one."""
+    from ch09 import ColumnParallelLinear, RowParallelLinear, row_parallel_forward_overlapped
+    ws, M, K, N = 4, 96, 512, 256
+    x = seeded_normal((M, K), 1, "bf16")
+    w = seeded_normal((N, K), 2, "bf16")
+    total = None
+    for r in range(ws):
+        layer = RowParallelLinear(K, N, world_size=ws, rank=r).to(DEV).to(torch.bfloat16)
+        sl = slice(r * K // ws, (r + 1) * K // ws)
+        layer.weight.data.copy_(dev(w[:, sl], "bf16"))
+        y = layer(dev(x[:, sl], "bf16")).float()
+        y2 = row_parallel_forward_overlapped(dev(x[:, sl], "bf16"), layer.weight, chunks=3).float()
+        torch.testing.assert_close(y2, y, rtol=0, atol=0)
+        total = y if total is None else total + y
+    assert_lin_close(total, olin.row_parallel_sum(x, w, ws), "bf16", "row-parallel sum")
+    col = ColumnParallelLinear(K, 4 * N, world_size=4, rank=1, bias=True).to(DEV)
+    xx = torch.from_numpy(x).to(DEV)
+    yc = col(xx).cpu().numpy()
+    ref = olin.linear(x, col.weight.detach().cpu().numpy(), col.bias.detach().cpu().numpy())
+    np.testing.assert_allclose(yc, ref, rtol=1e-4, atol=1e-4)

@@ -1,0 +1,29 @@
+#!/bin/bash
+# GPU-box check: parity tests, a bench line, a rocprofv3 kernel-trace summary.
+# Stops at the first crash / timeout (exit status other than 0 or 1).
+cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
+MODE=${1:-all}
+python -c "import torch;print(torch.cuda.get_device_name(0))" > gpurun_out/device.txt 2>&1
+if [ "$MODE" = all ] || [ "$MODE" = tests ]; then
+  timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 -rf \
+      > gpurun_out/pytest_gpu.log 2>&1
+  rc=$?; echo "pytest rc=$rc"; tail -30 gpurun_out/pytest_gpu.log
+  ok $rc || exit $rc
+fi
+if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
+  timeout -k 10 600 python bench.py ${BENCH_ARGS:---quick} > gpurun_out/bench.json 2> gpurun_out/bench.err
+  rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench.json; tail -5 gpurun_out/bench.err
+  [ $rc -eq 0 ] || exit $rc
+fi
+if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
+  cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
+      -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run -- \
+      python "$GRAFT_REPO_ROOT/bench.py" --quick --steps 10 --warmup 2 \
+      > "$GRAFT_REPO_ROOT/gpurun_out/prof_bench.json" 2> "$GRAFT_REPO_ROOT/gpurun_out/prof.err"
+  rc=$?; echo "rocprof rc=$rc"; cd "$GRAFT_REPO_ROOT"
+  find gpurun_out/prof -name "*kernel_stats.csv" -exec cat {} \; | cut -c1-250 | head -20
+  [ $rc -eq 0 ] || exit $rc
+fi
