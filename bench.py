@@ -250,8 +250,8 @@ def main():
                    "parallelism": f"replicas x{world} (flash does not shard; TP GEMM row-parallel)"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved / PEAK_BF16_TFLOPS,
-                     "traffic": load_traffic("attn_fwd_mfma"),
-                     "kernel": "attn_fwd_mfma<bf16,128,4>", "algorithmic_flops": flops_step,
+                     "traffic": load_traffic("attn_fwd_v2"),
+                     "kernel": "attn_fwd_v2<bf16,128,8 waves>", "algorithmic_flops": flops_step,
                      "kernel_ms": kernel_ms},
         **extra,
     }

@@ -260,6 +260,462 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_mfma(
 }
 
 // --------------------------------------------------------------------------
+// attn_fwd_v2: attn_fwd_mfma's fragment mapping and register staging, with
+// the per-tile overheads removed:
+//  * padded LDS rows instead of an XOR swizzle -- K rows 2D+16 B, V rows
+//    2D+64 B.  K's b128 reads of 16 consecutive rows land on 16 distinct
+//    16-byte slots (stride = 17 slots mod 16); V's tr_b16 reads of 4 rows x
+//    64 B land on 4 disjoint 16-bank quarters (stride = 80 dwords = 16 mod 64).
+//    Every fragment address is then one per-lane base register + an
+//    immediate offset: no per-read address arithmetic in the loop.
+//  * global staging addresses are one per-lane base + scalar tile offset;
+//    the clamp for rows past Nk only runs on a ragged last tile.
+//  * the O rescale is skipped (exactly) when no row's max moved this tile.
+// (A software-pipelined variant that issued QK^T(t+1) beside softmax(t) with
+// LDS-DMA staging spilled at D=128 and ran 1.5-2.5x slower: every spill
+// reload's vmcnt(0) also drained the in-flight DMA.  See DESIGN.md.)
+template <int D> struct PadLayout {
+    static constexpr int KS = 2 * D + 16;  // K row stride (bytes)
+    static constexpr int VS = 2 * D + 64;  // V row stride (bytes)
+    static constexpr int KSZ = KT * KS, VSZ = KT * VS, BUF = KSZ + VSZ;
+};
+
+template <typename T, int D, int NW, bool LAZY>
+__global__ __launch_bounds__(NW * 64, 2) void attn_fwd_v2(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
+    const uint16_t* __restrict__ v, uint16_t* __restrict__ o, int H, int group,
+    int Nq, int Nk, AttnStrides st, float c, int causal, int qblocks,
+    int nblocks) {
+    using L = PadLayout<D>;
+    constexpr int NT = NW * 64;
+    constexpr int CPR = D / 8;          // 16-byte chunks per row
+    constexpr int RPI = NT / CPR;       // rows covered by one staging step
+    constexpr int CPT = KT / RPI;       // staging steps per tile
+    static_assert(NT % CPR == 0 && KT % RPI == 0, "staging must tile evenly");
+    __shared__ __attribute__((aligned(16))) char smem[2 * L::BUF];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h32 = lane >> 5, l32 = lane & 31;
+    const int lb = xcd_remap(blockIdx.x, nblocks);
+    const int bh = lb / qblocks, qblk = lb % qblocks;
+    const int b = bh / H, hq = bh % H, hk = hq / group;
+    const int qbase = qblk * (NW * QW);
+    const int q0 = qbase + wave * QW;
+    const int off_diag = Nk - Nq;
+
+    const uint16_t* qp = q + b * st.qb + hq * st.qh;
+    const uint16_t* kp = k + b * st.kb + hk * st.kh;
+    const uint16_t* vp = v + b * st.vb + hk * st.vh;
+
+    i32x4 qf[D / 16];
+    {
+        const int qr = q0 + l32;
+        const bool ok = qr < Nq;
+        const uint16_t* src = qp + (int64_t)(ok ? qr : 0) * st.qn + 8 * h32;
+#pragma unroll
+        for (int kk = 0; kk < D / 16; ++kk) {
+            const i32x4 x = *reinterpret_cast<const i32x4*>(src + 16 * kk);
+            qf[kk] = ok ? x : i32x4{0, 0, 0, 0};
+        }
+    }
+
+    int kv_end = Nk;
+    if (causal) kv_end = min(Nk, qbase + NW * QW + off_diag);
+    const int nt = kv_end > 0 ? cdiv(kv_end, KT) : 0;
+    const int t_full = Nk / KT;  // tiles [0, t_full) need no row clamp
+    int t_mask = t_full;         // first tile this wave must mask
+    if (causal) t_mask = min(t_mask, max(0, (q0 + off_diag + 1) / KT));
+
+    // staging: thread owns chunk `sch` of rows srow + i*RPI
+    const int srow = tid / CPR, sch = tid % CPR;
+    const uint16_t* kg = kp + (int64_t)srow * st.kn + sch * 8;
+    const uint16_t* vg = vp + (int64_t)srow * st.vn + sch * 8;
+    const int kw = srow * L::KS + sch * 16, vw = L::KSZ + srow * L::VS + sch * 16;
+    i32x4 kst[CPT], vst[CPT];
+    auto load_tile = [&](int t) {
+        if (t < t_full) {
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) {
+                const int64_t r = (int64_t)t * KT + i * RPI;
+                kst[i] = *reinterpret_cast<const i32x4*>(kg + r * st.kn);
+                vst[i] = *reinterpret_cast<const i32x4*>(vg + r * st.vn);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) {
+                const int key = t * KT + i * RPI + srow;
+                const int64_t r = min(key, Nk - 1) - srow;
+                const i32x4 kx = *reinterpret_cast<const i32x4*>(kg + r * st.kn);
+                const i32x4 vx = *reinterpret_cast<const i32x4*>(vg + r * st.vn);
+                kst[i] = key < Nk ? kx : i32x4{0, 0, 0, 0};
+                vst[i] = key < Nk ? vx : i32x4{0, 0, 0, 0};
+            }
+        }
+    };
+    auto store_tile = [&](int buf) {
+        char* base = smem + buf * L::BUF;
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+            lds_write_b128(base, kw + i * RPI * L::KS, kst[i]);
+            lds_write_b128(base, vw + i * RPI * L::VS, vst[i]);
+        }
+    };
+
+    // per-lane fragment bases (byte offsets inside one buffer)
+    const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+    const int kr = l32 * L::KS + h32 * 16;
+    const int vr = L::KSZ + (4 * h32 + qq) * L::VS + (2 * (g & 1) + (pp >> 1)) * 16 + 8 * (pp & 1);
+
+    f32x16 oacc[D / 32];
+#pragma unroll
+    for (int d = 0; d < D / 32; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[d][r] = 0.f;
+    float m_run = -1e30f, l_run = 0.f;
+
+    if (nt > 0) {
+        load_tile(0);
+        store_tile(0);
+    }
+    __syncthreads();
+
+    for (int t = 0; t < nt; ++t) {
+        if (t + 1 < nt) load_tile(t + 1);
+        const char* kb = smem + (t & 1) * L::BUF + kr;
+        const char* vb = smem + (t & 1) * L::BUF + vr;
+
+        f32x16 s[2];
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[tt][r] = 0.f;
+#pragma unroll
+            for (int kk = 0; kk < D / 16; ++kk) {
+                const i32x4 kf = lds_read_b128(kb, tt * 32 * L::KS + kk * 32);
+                s[tt] = mfma32x32x16<T>(kf, qf[kk], s[tt]);
+            }
+        }
+
+        if (t >= t_mask) {
+            const int lim = causal ? q0 + l32 + off_diag : Nk;
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int key = t * KT + tt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
+                    if (key >= Nk || key > lim) s[tt][r] = -INFINITY;
+                }
+        }
+
+        float mx = max3(s[0][0], s[1][0], s[0][1]);
+        float my = max3(s[1][1], s[0][2], s[1][2]);
+#pragma unroll
+        for (int r = 3; r < 15; r += 2) {
+            mx = max3(mx, s[0][r], s[1][r]);
+            my = max3(my, s[0][r + 1], s[1][r + 1]);
+        }
+        mx = max3(mx, my, max3(s[0][15], s[1][15], mx));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float m_new = fmaxf(m_run, mx * c);
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+        m_run = m_new;
+        float rs = 0.f;
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float p = __builtin_amdgcn_exp2f(fmaf(s[tt][r], c, -m_new));
+                s[tt][r] = p;
+                rs += p;
+            }
+        l_run = fmaf(l_run, alpha, rs);
+        if (!LAZY || __ballot(alpha != 1.f)) {
+#pragma unroll
+            for (int d = 0; d < D / 32; ++d)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
+        }
+
+        i32x4 pb[2][2];
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const int r0 = 8 * s2;
+                pb[tt][s2] = i32x4{(int)pack2<T>(s[tt][r0 + 0], s[tt][r0 + 1]),
+                                   (int)pack2<T>(s[tt][r0 + 2], s[tt][r0 + 3]),
+                                   (int)pack2<T>(s[tt][r0 + 4], s[tt][r0 + 5]),
+                                   (int)pack2<T>(s[tt][r0 + 6], s[tt][r0 + 7])};
+            }
+#pragma unroll
+        for (int dblk = 0; dblk < D / 32; ++dblk)
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    const int ro = (tt * 32 + 16 * s2) * L::VS + dblk * 64;
+                    const i32x2 lo = lds_read_tr16(vb, ro);
+                    const i32x2 hi = lds_read_tr16(vb, ro + 8 * L::VS);
+                    oacc[dblk] = mfma32x32x16<T>(i32x4{lo.x, lo.y, hi.x, hi.y}, pb[tt][s2], oacc[dblk]);
+                }
+
+        if (t + 1 < nt) store_tile((t + 1) & 1);
+        __syncthreads();
+    }
+
+    const float l = l_run + __shfl_xor(l_run, 32, 64);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const int qr = q0 + l32;
+    if (qr < Nq) {
+        uint16_t* op = o + b * st.ob + hq * st.oh + (int64_t)qr * st.on;
+#pragma unroll
+        for (int dblk = 0; dblk < D / 32; ++dblk)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int d = dblk * 32 + 8 * i + 4 * h32;
+                const i32x2 w = {(int)pack2<T>(oacc[dblk][4 * i] * inv, oacc[dblk][4 * i + 1] * inv),
+                                 (int)pack2<T>(oacc[dblk][4 * i + 2] * inv, oacc[dblk][4 * i + 3] * inv)};
+                *reinterpret_cast<i32x2*>(op + d) = w;
+            }
+    }
+}
+
+// --------------------------------------------------------------------------
+// attn_fwd_v3: v2 with the two waves of each SIMD staggered.  A workgroup's
+// waves w and w+4 share a SIMD; in v2 both run QK^T-MFMA, softmax-VALU,
+// PV-MFMA in lockstep between barriers, so the SIMD alternates between a
+// saturated matrix pipe and a saturated VALU.  Here waves 0-3 ("A") run
+//     QK^T(t) | softmax(t) | PV(t)
+// and waves 4-7 ("B") run the rotated body
+//     softmax(t) | PV(t) | QK^T(t+1)
+// inside the same barrier interval: B's softmax VALU overlaps A's QK^T MFMAs
+// and A's softmax overlaps B's PV, so only the last third is MFMA vs MFMA.
+// B needs K[t+1] during interval t, so K runs in a 3-buffer ring
+// (K[t], K[t+1] read, K[t+2] being staged) and V in 2 buffers.
+template <typename T, int D, bool QLDS>
+__global__ __launch_bounds__(512, 2) void attn_fwd_v3(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
+    const uint16_t* __restrict__ v, uint16_t* __restrict__ o, int H, int group,
+    int Nq, int Nk, AttnStrides st, float c, int causal, int qblocks,
+    int nblocks) {
+    using L = PadLayout<D>;
+    constexpr int NW = 8, NT = 512;
+    constexpr int CPR = D / 8;
+    constexpr int RPI = NT / CPR;
+    constexpr int CPT = KT / RPI;
+    static_assert(NT % CPR == 0 && KT % RPI == 0, "staging must tile evenly");
+    constexpr int QSZ = QLDS ? NW * QW * L::KS : 0;  // Q tile, K-style padded rows
+    __shared__ __attribute__((aligned(16))) char smem[3 * L::KSZ + 2 * L::VSZ + QSZ];
+    char* const vbase = smem + 3 * L::KSZ;
+    char* const qbase_lds = vbase + 2 * L::VSZ;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h32 = lane >> 5, l32 = lane & 31;
+    const bool grpB = __builtin_amdgcn_readfirstlane(wave) >= 4;
+    const int lb = xcd_remap(blockIdx.x, nblocks);
+    const int bh = lb / qblocks, qblk = lb % qblocks;
+    const int b = bh / H, hq = bh % H, hk = hq / group;
+    const int qbase = qblk * (NW * QW);
+    const int q0 = qbase + wave * QW;
+    const int off_diag = Nk - Nq;
+
+    const uint16_t* qp = q + b * st.qb + hq * st.qh;
+    const uint16_t* kp = k + b * st.kb + hk * st.kh;
+    const uint16_t* vp = v + b * st.vb + hk * st.vh;
+
+    // Q^T fragments: in registers, or (QLDS) in a padded LDS tile re-read per
+    // tile (frees 32 VGPRs at D=128).  Lane: row q0+l32, d = 16kk + 8h32 .. +7.
+    i32x4 qf[QLDS ? 1 : D / 16];
+    {
+        const int qr = q0 + l32;
+        const bool ok = qr < Nq;
+        const uint16_t* src = qp + (int64_t)(ok ? qr : 0) * st.qn + 8 * h32;
+#pragma unroll
+        for (int kk = 0; kk < D / 16; ++kk) {
+            const i32x4 x = *reinterpret_cast<const i32x4*>(src + 16 * kk);
+            if constexpr (QLDS)
+                lds_write_b128(qbase_lds, (wave * QW + l32) * L::KS + (2 * kk + h32) * 16,
+                               ok ? x : i32x4{0, 0, 0, 0});
+            else
+                qf[kk] = ok ? x : i32x4{0, 0, 0, 0};
+        }
+    }
+    const char* qfr = qbase_lds + (wave * QW + l32) * L::KS + h32 * 16;
+
+    int kv_end = Nk;
+    if (causal) kv_end = min(Nk, qbase + NW * QW + off_diag);
+    const int nt = kv_end > 0 ? cdiv(kv_end, KT) : 0;
+    const int t_full = Nk / KT;
+    int t_mask = t_full;
+    if (causal) t_mask = min(t_mask, max(0, (q0 + off_diag + 1) / KT));
+
+    const int srow = tid / CPR, sch = tid % CPR;
+    const uint16_t* kg = kp + (int64_t)srow * st.kn + sch * 8;
+    const uint16_t* vg = vp + (int64_t)srow * st.vn + sch * 8;
+    const int kw = srow * L::KS + sch * 16, vw = srow * L::VS + sch * 16;
+    auto load_rows = [&](i32x4 (&dst)[CPT], const uint16_t* g, int64_t ld, int t) {
+        if (t < t_full) {
+#pragma unroll
+            for (int i = 0; i < CPT; ++i)
+                dst[i] = *reinterpret_cast<const i32x4*>(g + ((int64_t)t * KT + i * RPI) * ld);
+        } else {
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) {
+                const int key = t * KT + i * RPI + srow;
+                const i32x4 x = *reinterpret_cast<const i32x4*>(g + (int64_t)(min(key, Nk - 1) - srow) * ld);
+                dst[i] = key < Nk ? x : i32x4{0, 0, 0, 0};
+            }
+        }
+    };
+    auto store_k = [&](int buf, const i32x4 (&src)[CPT]) {
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) lds_write_b128(smem + buf * L::KSZ, kw + i * RPI * L::KS, src[i]);
+    };
+    auto store_v = [&](int buf, const i32x4 (&src)[CPT]) {
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) lds_write_b128(vbase + buf * L::VSZ, vw + i * RPI * L::VS, src[i]);
+    };
+
+    const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+    const int kr = l32 * L::KS + h32 * 16;
+    const int vr = (4 * h32 + qq) * L::VS + (2 * (g & 1) + (pp >> 1)) * 16 + 8 * (pp & 1);
+
+    f32x16 oacc[D / 32];
+#pragma unroll
+    for (int d = 0; d < D / 32; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[d][r] = 0.f;
+    float m_run = -1e30f, l_run = 0.f;
+    f32x16 s[2];
+
+    auto qk = [&](int kbuf) {
+        const char* kb = smem + kbuf * L::KSZ + kr;
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[tt][r] = 0.f;
+#pragma unroll
+            for (int kk = 0; kk < D / 16; ++kk) {
+                const i32x4 qv = QLDS ? lds_read_b128(qfr, kk * 32) : qf[QLDS ? 0 : kk];
+                s[tt] = mfma32x32x16<T>(lds_read_b128(kb, tt * 32 * L::KS + kk * 32), qv, s[tt]);
+            }
+        }
+    };
+    auto softmax_pv = [&](int t, int vbuf) {
+        if (t >= t_mask) {
+            const int lim = causal ? q0 + l32 + off_diag : Nk;
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int key = t * KT + tt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
+                    if (key >= Nk || key > lim) s[tt][r] = -INFINITY;
+                }
+        }
+        float mx = max3(s[0][0], s[1][0], s[0][1]);
+        float my = max3(s[1][1], s[0][2], s[1][2]);
+#pragma unroll
+        for (int r = 3; r < 15; r += 2) {
+            mx = max3(mx, s[0][r], s[1][r]);
+            my = max3(my, s[0][r + 1], s[1][r + 1]);
+        }
+        mx = max3(mx, my, max3(s[0][15], s[1][15], mx));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float m_new = fmaxf(m_run, mx * c);
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+        m_run = m_new;
+        float rs = 0.f;
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float p = __builtin_amdgcn_exp2f(fmaf(s[tt][r], c, -m_new));
+                s[tt][r] = p;
+                rs += p;
+            }
+        l_run = fmaf(l_run, alpha, rs);
+#pragma unroll
+        for (int d = 0; d < D / 32; ++d)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
+        i32x4 pb[2][2];
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const int r0 = 8 * s2;
+                pb[tt][s2] = i32x4{(int)pack2<T>(s[tt][r0 + 0], s[tt][r0 + 1]),
+                                   (int)pack2<T>(s[tt][r0 + 2], s[tt][r0 + 3]),
+                                   (int)pack2<T>(s[tt][r0 + 4], s[tt][r0 + 5]),
+                                   (int)pack2<T>(s[tt][r0 + 6], s[tt][r0 + 7])};
+            }
+        const char* vb = vbase + vbuf * L::VSZ + vr;
+#pragma unroll
+        for (int dblk = 0; dblk < D / 32; ++dblk)
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    const int ro = (tt * 32 + 16 * s2) * L::VS + dblk * 64;
+                    const i32x2 lo = lds_read_tr16(vb, ro);
+                    const i32x2 hi = lds_read_tr16(vb, ro + 8 * L::VS);
+                    oacc[dblk] = mfma32x32x16<T>(i32x4{lo.x, lo.y, hi.x, hi.y}, pb[tt][s2], oacc[dblk]);
+                }
+    };
+
+    i32x4 kst[CPT], vst[CPT];
+    if (nt > 0) {
+        load_rows(kst, kg, st.kn, 0);
+        load_rows(vst, vg, st.vn, 0);
+        store_k(0, kst);
+        store_v(0, vst);
+        if (nt > 1) {
+            load_rows(kst, kg, st.kn, 1);
+            store_k(1, kst);
+        }
+    }
+    __syncthreads();
+    if (grpB && nt > 0) qk(0);
+
+    int kc = 0;  // K ring slot of tile t
+    for (int t = 0; t < nt; ++t) {
+        const int kn1 = kc == 2 ? 0 : kc + 1, kn2 = kn1 == 2 ? 0 : kn1 + 1;
+        if (t + 1 < nt) load_rows(vst, vg, st.vn, t + 1);
+        if (t + 2 < nt) load_rows(kst, kg, st.kn, t + 2);
+        if (!grpB) {
+            qk(kc);
+            softmax_pv(t, t & 1);
+        } else {
+            softmax_pv(t, t & 1);
+            // keep QK^T(t+1)'s fragment reads below the PV MFMAs: hoisting
+            // them above doubles the live fragment registers and spills
+            __builtin_amdgcn_sched_barrier(0);
+            if (t + 1 < nt) qk(kn1);
+        }
+        if (t + 1 < nt) store_v((t + 1) & 1, vst);
+        if (t + 2 < nt) store_k(kn2, kst);
+        __syncthreads();
+        kc = kn1;
+    }
+
+    const float l = l_run + __shfl_xor(l_run, 32, 64);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const int qr = q0 + l32;
+    if (qr < Nq) {
+        uint16_t* op = o + b * st.ob + hq * st.oh + (int64_t)qr * st.on;
+#pragma unroll
+        for (int dblk = 0; dblk < D / 32; ++dblk)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int d = dblk * 32 + 8 * i + 4 * h32;
+                const i32x2 w = {(int)pack2<T>(oacc[dblk][4 * i] * inv, oacc[dblk][4 * i + 1] * inv),
+                                 (int)pack2<T>(oacc[dblk][4 * i + 2] * inv, oacc[dblk][4 * i + 3] * inv)};
+                *reinterpret_cast<i32x2*>(op + d) = w;
+            }
+    }
+}
+
+// --------------------------------------------------------------------------
 // Generic kernel: 256 threads own 32 query rows (8 threads per row, each
 // thread owns columns sub + 8u of the score tile and d = sub + 8u of O).
 constexpr int GQ = 32, GK = 64, GDMAX = 128;
@@ -357,19 +813,44 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
     }
 }
 
+// Kernel variants behind the same ABI (A/B-able via pli_flash_attn_fwd_variant):
+//   0: attn_fwd_mfma (XOR-swizzled LDS), 4 waves
+//   1: attn_fwd_v2, 4 waves, lazy rescale    2: attn_fwd_v2, 8 waves, lazy rescale
+//   3: attn_fwd_v2, 4 waves, eager rescale
+//   4: attn_fwd_v3, 8 waves, staggered (waves 4-7 run a rotated body)
+//   5: attn_fwd_v3 with Q in LDS
+constexpr int kDefaultVariant = 2;
+
 template <typename T, int D>
 int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int H,
                 int group, int Nq, int Nk, const AttnStrides& st, float scale,
-                int causal, hipStream_t stream) {
-    constexpr int NW = 4;
-    const int qblocks = cdiv(Nq, NW * QW);
+                int causal, hipStream_t stream, int variant) {
+    const int nw = (variant == 2 || variant >= 4) ? 8 : 4;
+    const int qblocks = cdiv(Nq, nw * QW);
     const int64_t nb = (int64_t)B * H * qblocks;
     PLI_REQUIRE(nb < (1ll << 31), "pli_flash_attn_fwd: grid too large");
     const float c = scale * 1.4426950408889634f;  // fold log2(e) into the scale
-    hipLaunchKernelGGL((attn_fwd_mfma<T, D, NW>), dim3((unsigned)nb), dim3(NW * 64), 0, stream,
-                       (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o,
-                       H, group, Nq, Nk, st, c, causal, qblocks, (int)nb);
-    return launch_status("attn_fwd_mfma");
+    const auto* qq = (const uint16_t*)q;
+    const auto* kk = (const uint16_t*)k;
+    const auto* vv = (const uint16_t*)v;
+    auto* oo = (uint16_t*)o;
+    const dim3 grid((unsigned)nb), block(nw * 64);
+#define PLI_ATTN_LAUNCH(KERNEL) \
+    hipLaunchKernelGGL(KERNEL, grid, block, 0, stream, qq, kk, vv, oo, H, group, Nq, Nk, st, c, \
+                       causal, qblocks, (int)nb)
+    switch (variant) {
+        case 0: PLI_ATTN_LAUNCH((attn_fwd_mfma<T, D, 4>)); break;
+        case 1: PLI_ATTN_LAUNCH((attn_fwd_v2<T, D, 4, true>)); break;
+        case 2: PLI_ATTN_LAUNCH((attn_fwd_v2<T, D, 8, true>)); break;
+        case 3: PLI_ATTN_LAUNCH((attn_fwd_v2<T, D, 4, false>)); break;
+        case 4: PLI_ATTN_LAUNCH((attn_fwd_v3<T, D, false>)); break;
+        case 5: PLI_ATTN_LAUNCH((attn_fwd_v3<T, D, true>)); break;
+        default:
+            set_error("pli_flash_attn_fwd: unknown variant %d", variant);
+            return PLI_EINVAL;
+    }
+#undef PLI_ATTN_LAUNCH
+    return launch_status("attn_fwd");
 }
 
 template <typename T>
@@ -392,10 +873,12 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 }  // namespace
 }  // namespace pli
 
-extern "C" int pli_flash_attn_fwd(const void* q, const void* k, const void* v, void* o,
-                                  int batch, int heads, int kv_heads, int n_q, int n_kv,
-                                  int head_dim, const int64_t* strides, float scale,
-                                  int causal, int dtype, void* stream) {
+// Not in pli.h: same contract as pli_flash_attn_fwd plus an explicit kernel
+// variant (tuning / A-B runs); variant < 0 selects the default.
+extern "C" int pli_flash_attn_fwd_variant(const void* q, const void* k, const void* v, void* o,
+                                          int batch, int heads, int kv_heads, int n_q, int n_kv,
+                                          int head_dim, const int64_t* strides, float scale,
+                                          int causal, int dtype, void* stream, int variant) {
     using namespace pli;
     clear_error();
     PLI_REQUIRE(q && k && v && o && strides, "pli_flash_attn_fwd: null pointer");
@@ -421,11 +904,12 @@ extern "C" int pli_flash_attn_fwd(const void* q, const void* k, const void* v, v
         vec = vec && (strides[i] % 8 == 0) && (!inner || strides[i] >= head_dim);
     }
     if (vec) {
+        if (variant < 0) variant = kDefaultVariant;
         if (dtype == PLI_BF16)
-            return head_dim == 128 ? launch_mfma<bf16_t, 128>(q, k, v, o, batch, heads, group, n_q, n_kv, st, scale, causal, s)
-                                   : launch_mfma<bf16_t, 64>(q, k, v, o, batch, heads, group, n_q, n_kv, st, scale, causal, s);
-        return head_dim == 128 ? launch_mfma<f16_t, 128>(q, k, v, o, batch, heads, group, n_q, n_kv, st, scale, causal, s)
-                               : launch_mfma<f16_t, 64>(q, k, v, o, batch, heads, group, n_q, n_kv, st, scale, causal, s);
+            return head_dim == 128 ? launch_mfma<bf16_t, 128>(q, k, v, o, batch, heads, group, n_q, n_kv, st, scale, causal, s, variant)
+                                   : launch_mfma<bf16_t, 64>(q, k, v, o, batch, heads, group, n_q, n_kv, st, scale, causal, s, variant);
+        return head_dim == 128 ? launch_mfma<f16_t, 128>(q, k, v, o, batch, heads, group, n_q, n_kv, st, scale, causal, s, variant)
+                               : launch_mfma<f16_t, 64>(q, k, v, o, batch, heads, group, n_q, n_kv, st, scale, causal, s, variant);
     }
     if (head_dim > GDMAX) {
         set_error("pli_flash_attn_fwd: head_dim %d > %d unsupported on the generic path", head_dim,
@@ -440,4 +924,12 @@ extern "C" int pli_flash_attn_fwd(const void* q, const void* k, const void* v, v
         default:
             return launch_generic<bf16_t>(q, k, v, o, batch, heads, group, n_q, n_kv, head_dim, st, scale, causal, s);
     }
+}
+
+extern "C" int pli_flash_attn_fwd(const void* q, const void* k, const void* v, void* o,
+                                  int batch, int heads, int kv_heads, int n_q, int n_kv,
+                                  int head_dim, const int64_t* strides, float scale,
+                                  int causal, int dtype, void* stream) {
+    return pli_flash_attn_fwd_variant(q, k, v, o, batch, heads, kv_heads, n_q, n_kv, head_dim,
+                                      strides, scale, causal, dtype, stream, -1);
 }

@@ -29,7 +29,10 @@ __device__ __forceinline__ void dot_chunk<f16_t>(const i32x4& w, const i32x4& x,
     typedef __attribute__((ext_vector_type(2))) _Float16 h2;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const h2 a = __builtin_bit_cast(h2, w[i]), b = __builtin_bit_cast(h2, x[i]);
+        // copy the lanes out first: __builtin_bit_cast of an ext-vector
+        // element lvalue reads element 0 for every i (hipcc 7.2)
+        const int wi = w[i], xi = x[i];
+        const h2 a = __builtin_bit_cast(h2, wi), b = __builtin_bit_cast(h2, xi);
         acc = fmaf((float)a.x, (float)b.x, acc);
         acc = fmaf((float)a.y, (float)b.y, acc);
     }
@@ -40,7 +43,7 @@ __device__ __forceinline__ void dot_chunk<float>(const i32x4& w, const i32x4& x,
     for (int i = 0; i < 4; ++i) acc = fmaf(__int_as_float(w[i]), __int_as_float(x[i]), acc);
 }
 
-template <typename T, int ROWS, int CPL>
+template <typename T, int ROWS, int CPL, bool NTL>
 __global__ __launch_bounds__(256) void gemv_vec(const char* __restrict__ w,
                                                 const char* __restrict__ x, T* __restrict__ y,
                                                 int M, int nchunks, int64_t ldw_bytes) {
@@ -62,8 +65,9 @@ __global__ __launch_bounds__(256) void gemv_vec(const char* __restrict__ w,
             xv[u] = *reinterpret_cast<const i32x4*>(x + (int64_t)cc * 16);
 #pragma unroll
             for (int r = 0; r < ROWS; ++r)
-                wv[r][u] = __builtin_nontemporal_load(
-                    reinterpret_cast<const i32x4*>(wrow[r] + (int64_t)cc * 16));
+                wv[r][u] = NTL ? __builtin_nontemporal_load(
+                                     reinterpret_cast<const i32x4*>(wrow[r] + (int64_t)cc * 16))
+                               : *reinterpret_cast<const i32x4*>(wrow[r] + (int64_t)cc * 16);
         }
 #pragma unroll
         for (int u = 0; u < CPL; ++u) {
@@ -97,8 +101,22 @@ __global__ __launch_bounds__(256) void gemv_scalar(const T* __restrict__ w, cons
     if (lane == 0) y[row] = elem<T>::from_f32(acc);
 }
 
+// Variants (A/B via pli_gemv_variant): rows per wave x 16-B chunks per lane
+// per k-step x non-temporal W loads.
+//   0: 2x8 nt  1: 4x8 nt  2: 1x8 nt  3: 2x8 plain  4: 4x4 nt  5: 8x4 nt
+constexpr int kDefaultGemvVariant = 0;
+
+template <typename T, int ROWS, int CPL, bool NTL>
+int launch_vec(const void* w, const void* x, void* y, int m, int nchunks, int64_t ldw_b,
+               hipStream_t s) {
+    hipLaunchKernelGGL((gemv_vec<T, ROWS, CPL, NTL>), dim3(cdiv(m, 4 * ROWS)), dim3(256), 0, s,
+                       (const char*)w, (const char*)x, (T*)y, m, nchunks, ldw_b);
+    return launch_status("gemv_vec");
+}
+
 template <typename T>
-int launch(const void* w, const void* x, void* y, int m, int k, int64_t ldw, hipStream_t s) {
+int launch(const void* w, const void* x, void* y, int m, int k, int64_t ldw, hipStream_t s,
+           int variant) {
     constexpr int EPC = 16 / elem<T>::bytes;  // elements per 16-byte chunk
     const bool vec = (k % EPC == 0) && (ldw % EPC == 0) &&
                      ((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(x)) & 15) == 0;
@@ -109,17 +127,23 @@ int launch(const void* w, const void* x, void* y, int m, int k, int64_t ldw, hip
     }
     const int nchunks = k / EPC;
     const int64_t ldw_b = ldw * elem<T>::bytes;
-    constexpr int ROWS = 2, CPL = 8;
-    hipLaunchKernelGGL((gemv_vec<T, ROWS, CPL>), dim3(cdiv(m, 4 * ROWS)), dim3(256), 0, s,
-                       (const char*)w, (const char*)x, (T*)y, m, nchunks, ldw_b);
-    return launch_status("gemv_vec");
+    switch (variant < 0 ? kDefaultGemvVariant : variant) {
+        case 0: return launch_vec<T, 2, 8, true>(w, x, y, m, nchunks, ldw_b, s);
+        case 1: return launch_vec<T, 4, 8, true>(w, x, y, m, nchunks, ldw_b, s);
+        case 2: return launch_vec<T, 1, 8, true>(w, x, y, m, nchunks, ldw_b, s);
+        case 3: return launch_vec<T, 2, 8, false>(w, x, y, m, nchunks, ldw_b, s);
+        case 4: return launch_vec<T, 4, 4, true>(w, x, y, m, nchunks, ldw_b, s);
+        case 5: return launch_vec<T, 8, 4, true>(w, x, y, m, nchunks, ldw_b, s);
+        default: set_error("pli_gemv: unknown variant %d", variant); return PLI_EINVAL;
+    }
 }
 
 }  // namespace
 }  // namespace pli
 
-extern "C" int pli_gemv(const void* w, const void* x, void* y, int m, int k, int64_t ldw,
-                        int dtype, void* stream) {
+// Not in pli.h: pli_gemv with an explicit kernel variant (tuning / A-B runs).
+extern "C" int pli_gemv_variant(const void* w, const void* x, void* y, int m, int k, int64_t ldw,
+                                int dtype, void* stream, int variant) {
     using namespace pli;
     clear_error();
     PLI_REQUIRE(w && x && y, "pli_gemv: null pointer");
@@ -129,9 +153,14 @@ extern "C" int pli_gemv(const void* w, const void* x, void* y, int m, int k, int
     PLI_REQUIRE(k > 0, "pli_gemv: k must be positive");
     hipStream_t s = (hipStream_t)stream;
     switch (dtype) {
-        case PLI_F32: return launch<float>(w, x, y, m, k, ldw, s);
-        case PLI_F16: return launch<f16_t>(w, x, y, m, k, ldw, s);
-        case PLI_BF16: return launch<bf16_t>(w, x, y, m, k, ldw, s);
+        case PLI_F32: return launch<float>(w, x, y, m, k, ldw, s, variant);
+        case PLI_F16: return launch<f16_t>(w, x, y, m, k, ldw, s, variant);
+        case PLI_BF16: return launch<bf16_t>(w, x, y, m, k, ldw, s, variant);
         default: set_error("pli_gemv: bad dtype %d", dtype); return PLI_EINVAL;
     }
+}
+
+extern "C" int pli_gemv(const void* w, const void* x, void* y, int m, int k, int64_t ldw,
+                        int dtype, void* stream) {
+    return pli_gemv_variant(w, x, y, m, k, ldw, dtype, stream, -1);
 }

@@ -112,6 +112,14 @@ __device__ __forceinline__ i32x2 lds_read_tr16(const char* base, int byte_off) {
     return __builtin_bit_cast(i32x2, r);
 }
 
+// max3 without the IEEE-mode canonicalising v_max_f32 that hipcc puts in
+// front of fmaxf on MFMA results (values here are finite or -inf, never NaN).
+__device__ __forceinline__ float max3(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 // ------------------------------------------------------- wave reductions --
 __device__ __forceinline__ float wave_max(float x) {
 #pragma unroll

@@ -39,6 +39,11 @@ _SIGS = {
     "pli_scale_copy": [_vp, _vp, _c_i64, _c_int, _vp],
     "pli_softmax_rows": [_vp, _vp, _c_i64, _c_int, _c_int, _vp],
     "pli_online_softmax_with_output": [_vp, _vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_int, _vp],
+    # tuning entry points (not part of include/pli.h): explicit kernel variant
+    "pli_flash_attn_fwd_variant": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int,
+                                   _c_int, ctypes.POINTER(_c_i64), _c_f32, _c_int, _c_int, _vp,
+                                   _c_int],
+    "pli_gemv_variant": [_vp, _vp, _vp, _c_int, _c_int, _c_i64, _c_int, _vp, _c_int],
 }
 
 
@@ -111,7 +116,8 @@ def _ptr(t: torch.Tensor | None) -> ctypes.c_void_p:
 
 # ------------------------------------------------------------------ attention
 def flash_attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | None = None,
-                   causal: bool = False, out: torch.Tensor | None = None) -> torch.Tensor:
+                   causal: bool = False, out: torch.Tensor | None = None,
+                   variant: int | None = None) -> torch.Tensor:
     """O = softmax(Q K^T * scale [+ causal]) V on [B, H, N, D] tensors (any
     strides with a unit head_dim stride); K/V may have fewer (GQA) heads."""
     dev = _require_gpu(q, k, v)
@@ -132,16 +138,20 @@ def flash_attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: flo
     if scale is None:
         scale = D ** -0.5
     st = (_c_i64 * 12)(*(int(x) for t in (q, k, v, out) for x in t.stride()[:3]))
+    args = (_ptr(q), _ptr(k), _ptr(v), _ptr(out), B, H, Hkv, Nq, Nk, D, st, float(scale),
+            int(bool(causal)), _dtype_code(q), _stream(dev))
     with torch.cuda.device(dev):
-        rc = lib().pli_flash_attn_fwd(_ptr(q), _ptr(k), _ptr(v), _ptr(out), B, H, Hkv, Nq, Nk, D,
-                                      st, float(scale), int(bool(causal)), _dtype_code(q),
-                                      _stream(dev))
+        if variant is None:
+            rc = lib().pli_flash_attn_fwd(*args)
+        else:
+            rc = lib().pli_flash_attn_fwd_variant(*args, int(variant))
     _check(rc, "pli_flash_attn_fwd")
     return out
 
 
 # ---------------------------------------------------------------------- GEMV
-def gemv(w: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+def gemv(w: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None,
+         variant: int | None = None) -> torch.Tensor:
     """y = W x (torch.mv semantics), W [m, k] with unit column stride."""
     dev = _require_gpu(w, x)
     if w.dim() != 2 or x.dim() != 1 or w.shape[1] != x.shape[0]:
@@ -152,9 +162,12 @@ def gemv(w: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None) -> t
     m, k = w.shape
     if out is None:
         out = torch.empty(m, dtype=w.dtype, device=dev)
+    args = (_ptr(w), _ptr(x), _ptr(out), m, k, max(w.stride(0), k), _dtype_code(w), _stream(dev))
     with torch.cuda.device(dev):
-        rc = lib().pli_gemv(_ptr(w), _ptr(x), _ptr(out), m, k, max(w.stride(0), k),
-                            _dtype_code(w), _stream(dev))
+        if variant is None:
+            rc = lib().pli_gemv(*args)
+        else:
+            rc = lib().pli_gemv_variant(*args, int(variant))
     _check(rc, "pli_gemv")
     return out
 

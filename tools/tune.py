@@ -1,0 +1,124 @@
+#!/usr/bin/env python3
+"""A/B kernel variants in ONE process (interleaved rounds), GPU box only.
+
+    python tools/tune.py [flash] [gemv] [hbm] [gemm]
+
+Prints one JSON object per measurement; correctness of every variant is
+checked against variant 0 (and flash against the f64 oracle on one head).
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "physics-llm-inference_amd"), ROOT]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import pli_hip  # noqa: E402
+
+
+def ev_ms(fn, iters):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def interleave(fns: dict, iters: int, rounds: int):
+    res = {k: [] for k in fns}
+    for _ in range(rounds):
+        for k, fn in fns.items():
+            res[k].append(ev_ms(fn, iters))
+    return {k: (float(np.median(v)), float(np.min(v))) for k, v in res.items()}
+
+
+def tune_flash(variants=(0, 2, 4, 5), causal=False, B=8, H=32, S=4096, D=128):
+    from oracle.attention import naive_attention
+    g = torch.Generator(device="cuda").manual_seed(0)
+    q, k, v = (torch.randn(B, H, S, D, device="cuda", dtype=torch.bfloat16, generator=g) for _ in range(3))
+    outs = {vv: torch.empty_like(q) for vv in variants}
+    for vv in variants:
+        pli_hip.flash_attn_fwd(q, k, v, causal=causal, out=outs[vv], variant=vv)
+    torch.cuda.synchronize()
+    ref = naive_attention(*(t[0:1, 0:1].float().cpu().numpy() for t in (q, k, v)), causal=causal)
+    fns = {vv: (lambda vv=vv: pli_hip.flash_attn_fwd(q, k, v, causal=causal, out=outs[vv], variant=vv))
+           for vv in variants}
+    t = interleave(fns, 5, 3)
+    flops = 4 * B * H * S * S * D * (0.5 if causal else 1.0)
+    for vv in variants:
+        diff = (outs[vv].float() - outs[variants[0]].float()).abs().max().item()
+        err = float(np.abs(outs[vv][0:1, 0:1].float().cpu().numpy() - ref).max())
+        print(json.dumps({"kernel": "flash", "variant": vv, "causal": causal, "ms_med": t[vv][0],
+                          "ms_min": t[vv][1], "TFLOP/s": flops / t[vv][0] / 1e9,
+                          "maxdiff_vs_v0": diff, "err_vs_f64_head0": err}), flush=True)
+
+
+def tune_gemv(variants=(0, 1, 2, 3, 4, 5), m=4096, k=4096, copies=12):
+    ws = [torch.randn(m, k, device="cuda", dtype=torch.bfloat16) for _ in range(copies)]
+    x = torch.randn(k, device="cuda", dtype=torch.bfloat16)
+    ys = {vv: torch.empty(m, device="cuda", dtype=torch.bfloat16) for vv in variants}
+    ref = (ws[0].float() @ x.float())
+    st = {"i": 0}
+
+    def mk(vv):
+        def f():
+            pli_hip.gemv(ws[st["i"] % copies], x, out=ys[vv], variant=vv)
+            st["i"] += 1
+        return f
+    fns = {vv: mk(vv) for vv in variants}
+    for f in fns.values():
+        for _ in range(copies):
+            f()
+    t = interleave(fns, 240, 5)
+    nbytes = (m * k + m + k) * 2
+    for vv in variants:
+        pli_hip.gemv(ws[0], x, out=ys[vv], variant=vv)
+        err = ((ys[vv].float() - ref).abs() / (ref.abs() + 1)).max().item()
+        print(json.dumps({"kernel": "gemv", "variant": vv, "us_med": t[vv][0] * 1e3,
+                          "us_min": t[vv][1] * 1e3, "GB/s": nbytes / (t[vv][0] * 1e-3) / 1e9,
+                          "rel_err": err}), flush=True)
+
+
+def tune_hbm():
+    for nbytes in (1 << 28, 1 << 30):
+        n = nbytes // 4
+        src = torch.randn(n, device="cuda")
+        dst = torch.empty_like(src)
+        t = interleave({"copy": lambda: pli_hip.scale_copy(src, dst)}, 20, 3)["copy"][0]
+        t_torch = interleave({"c": lambda: dst.copy_(src)}, 20, 3)["c"][0]
+        print(json.dumps({"kernel": "scale_copy", "bytes": nbytes, "GB/s": 2 * nbytes / (t * 1e-3) / 1e9,
+                          "torch_copy_GB/s": 2 * nbytes / (t_torch * 1e-3) / 1e9}), flush=True)
+
+
+def tune_gemm():
+    for n in (4096, 8192):
+        a = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
+        b = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
+        c = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
+        fns = {"hip_nn": lambda: pli_hip.gemm(a, b, out=c),
+               "hip_nt": lambda: pli_hip.gemm(a, b, trans_b=True, out=c),
+               "torch_nn": lambda: torch.mm(a, b)}
+        t = interleave(fns, 5, 3)
+        for kname, (med, mn) in t.items():
+            print(json.dumps({"kernel": "gemm", "n": n, "impl": kname, "ms_med": med,
+                              "TFLOP/s": 2 * n ** 3 / med / 1e9}), flush=True)
+
+
+if __name__ == "__main__":
+    what = sys.argv[1:] or ["hbm", "gemv", "flash", "gemm"]
+    if "hbm" in what:
+        tune_hbm()
+    if "gemv" in what:
+        tune_gemv()
+    if "flash" in what:
+        tune_flash()
+        tune_flash(causal=True)
+    if "gemm" in what:
+        tune_gemm()
