@@ -28,6 +28,7 @@
 // Generic kernel (fp32, or any head_dim <= 128, or unaligned operands):
 // LDS-tiled VALU kernel with the same online recurrence, fp32 accumulate.
 #include <cmath>
+#include <type_traits>
 
 #include "pli_common.h"
 
@@ -481,6 +482,458 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_v2(
 }
 
 // --------------------------------------------------------------------------
+// attn_fwd_v2b: v2 with the softmax restructured for the scheduler.
+//  * one instance of the tile body per mask mode (template), so an unmasked
+//    tile is a single scheduling region (QK^T MFMAs .. PV MFMAs);
+//  * the 32 scores are exponentiated, packed and fed to PV 8 at a time
+//    (keys of one P fragment), so the exps of block i+1 issue in the gaps of
+//    block i's 4 PV MFMAs instead of all 32 exps preceding all 16 MFMAs;
+//  * the row max and row sum run as 4 independent chains (the serial
+//    32-long v_add chain exposed ~8 cycles of latency per add);
+//  * eager rescale (no branch inside the region); optional s_setprio(1)
+//    around the MFMA clusters (PRIO).
+template <typename T, int D, bool PRIO>
+__global__ __launch_bounds__(512, 2) void attn_fwd_v2b(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
+    const uint16_t* __restrict__ v, uint16_t* __restrict__ o, int H, int group,
+    int Nq, int Nk, AttnStrides st, float c, int causal, int qblocks,
+    int nblocks) {
+    using L = PadLayout<D>;
+    constexpr int NW = 8, NT = 512;
+    constexpr int CPR = D / 8;
+    constexpr int RPI = NT / CPR;
+    constexpr int CPT = KT / RPI;
+    static_assert(NT % CPR == 0 && KT % RPI == 0, "staging must tile evenly");
+    __shared__ __attribute__((aligned(16))) char smem[2 * L::BUF];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h32 = lane >> 5, l32 = lane & 31;
+    const int lb = xcd_remap(blockIdx.x, nblocks);
+    const int bh = lb / qblocks, qblk = lb % qblocks;
+    const int b = bh / H, hq = bh % H, hk = hq / group;
+    const int qbase = qblk * (NW * QW);
+    const int q0 = qbase + wave * QW;
+    const int off_diag = Nk - Nq;
+
+    const uint16_t* qp = q + b * st.qb + hq * st.qh;
+    const uint16_t* kp = k + b * st.kb + hk * st.kh;
+    const uint16_t* vp = v + b * st.vb + hk * st.vh;
+
+    i32x4 qf[D / 16];
+    {
+        const int qr = q0 + l32;
+        const bool ok = qr < Nq;
+        const uint16_t* src = qp + (int64_t)(ok ? qr : 0) * st.qn + 8 * h32;
+#pragma unroll
+        for (int kk = 0; kk < D / 16; ++kk) {
+            const i32x4 x = *reinterpret_cast<const i32x4*>(src + 16 * kk);
+            qf[kk] = ok ? x : i32x4{0, 0, 0, 0};
+        }
+    }
+
+    int kv_end = Nk;
+    if (causal) kv_end = min(Nk, qbase + NW * QW + off_diag);
+    const int nt = kv_end > 0 ? cdiv(kv_end, KT) : 0;
+    const int t_full = Nk / KT;
+    int t_mask = t_full;
+    if (causal) t_mask = min(t_mask, max(0, (q0 + off_diag + 1) / KT));
+
+    const int srow = tid / CPR, sch = tid % CPR;
+    const uint16_t* kg = kp + (int64_t)srow * st.kn + sch * 8;
+    const uint16_t* vg = vp + (int64_t)srow * st.vn + sch * 8;
+    const int kw = srow * L::KS + sch * 16, vw = L::KSZ + srow * L::VS + sch * 16;
+    i32x4 kst[CPT], vst[CPT];
+    auto load_tile = [&](int t) {
+        if (t < t_full) {
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) {
+                const int64_t r = (int64_t)t * KT + i * RPI;
+                kst[i] = *reinterpret_cast<const i32x4*>(kg + r * st.kn);
+                vst[i] = *reinterpret_cast<const i32x4*>(vg + r * st.vn);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) {
+                const int key = t * KT + i * RPI + srow;
+                const int64_t r = min(key, Nk - 1) - srow;
+                const i32x4 kx = *reinterpret_cast<const i32x4*>(kg + r * st.kn);
+                const i32x4 vx = *reinterpret_cast<const i32x4*>(vg + r * st.vn);
+                kst[i] = key < Nk ? kx : i32x4{0, 0, 0, 0};
+                vst[i] = key < Nk ? vx : i32x4{0, 0, 0, 0};
+            }
+        }
+    };
+    auto store_tile = [&](int buf) {
+        char* base = smem + buf * L::BUF;
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+            lds_write_b128(base, kw + i * RPI * L::KS, kst[i]);
+            lds_write_b128(base, vw + i * RPI * L::VS, vst[i]);
+        }
+    };
+
+    const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+    const int kr = l32 * L::KS + h32 * 16;
+    const int vr = L::KSZ + (4 * h32 + qq) * L::VS + (2 * (g & 1) + (pp >> 1)) * 16 + 8 * (pp & 1);
+
+    f32x16 oacc[D / 32];
+#pragma unroll
+    for (int d = 0; d < D / 32; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[d][r] = 0.f;
+    float m_run = -1e30f, l_run = 0.f;
+
+    auto body = [&](auto mask_tag, int t) {
+        constexpr bool MASK = decltype(mask_tag)::value;
+        if (t + 1 < nt) load_tile(t + 1);
+        const char* kb = smem + (t & 1) * L::BUF + kr;
+        const char* vb = smem + (t & 1) * L::BUF + vr;
+
+        f32x16 s[2];
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[tt][r] = 0.f;
+#pragma unroll
+            for (int kk = 0; kk < D / 16; ++kk)
+                s[tt] = mfma32x32x16<T>(lds_read_b128(kb, tt * 32 * L::KS + kk * 32), qf[kk], s[tt]);
+        }
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+        if constexpr (MASK) {
+            const int lim = causal ? q0 + l32 + off_diag : Nk;
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int key = t * KT + tt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
+                    if (key >= Nk || key > lim) s[tt][r] = -INFINITY;
+                }
+        }
+        float m4[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) m4[j] = max3(s[0][4 * j], s[1][4 * j], s[0][4 * j + 1]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            m4[j] = max3(m4[j], s[1][4 * j + 1], s[0][4 * j + 2]);
+            m4[j] = max3(m4[j], s[1][4 * j + 2], s[0][4 * j + 3]);
+            m4[j] = fmaxf(m4[j], s[1][4 * j + 3]);
+        }
+        float mx = max3(m4[0], m4[1], max3(m4[2], m4[3], m4[0]));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float m_new = fmaxf(m_run, mx * c);
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+        m_run = m_new;
+#pragma unroll
+        for (int d = 0; d < D / 32; ++d)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
+        float rs[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                float p[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    p[j] = __builtin_amdgcn_exp2f(fmaf(s[tt][8 * s2 + j], c, -m_new));
+                    rs[j & 3] += p[j];
+                }
+                const i32x4 pb = {(int)pack2<T>(p[0], p[1]), (int)pack2<T>(p[2], p[3]),
+                                  (int)pack2<T>(p[4], p[5]), (int)pack2<T>(p[6], p[7])};
+                if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+                for (int dblk = 0; dblk < D / 32; ++dblk) {
+                    const int ro = (tt * 32 + 16 * s2) * L::VS + dblk * 64;
+                    const i32x2 lo = lds_read_tr16(vb, ro);
+                    const i32x2 hi = lds_read_tr16(vb, ro + 8 * L::VS);
+                    oacc[dblk] = mfma32x32x16<T>(i32x4{lo.x, lo.y, hi.x, hi.y}, pb, oacc[dblk]);
+                }
+                if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+            }
+        l_run = fmaf(l_run, alpha, (rs[0] + rs[1]) + (rs[2] + rs[3]));
+        if (t + 1 < nt) store_tile((t + 1) & 1);
+        __syncthreads();
+    };
+
+    if (nt > 0) {
+        load_tile(0);
+        store_tile(0);
+    }
+    __syncthreads();
+    for (int t = 0; t < nt; ++t) {
+        if (t < t_mask)
+            body(std::false_type{}, t);
+        else
+            body(std::true_type{}, t);
+    }
+
+    const float l = l_run + __shfl_xor(l_run, 32, 64);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const int qr = q0 + l32;
+    if (qr < Nq) {
+        uint16_t* op = o + b * st.ob + hq * st.oh + (int64_t)qr * st.on;
+#pragma unroll
+        for (int dblk = 0; dblk < D / 32; ++dblk)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int d = dblk * 32 + 8 * i + 4 * h32;
+                const i32x2 w = {(int)pack2<T>(oacc[dblk][4 * i] * inv, oacc[dblk][4 * i + 1] * inv),
+                                 (int)pack2<T>(oacc[dblk][4 * i + 2] * inv, oacc[dblk][4 * i + 3] * inv)};
+                *reinterpret_cast<i32x2*>(op + d) = w;
+            }
+    }
+}
+
+// --------------------------------------------------------------------------
+// attn_fwd_v4: intra-wave software pipeline on the v2b body.  Iteration t
+// holds S(t) from the previous iteration and issues QK^T(t+1) in the same
+// scheduling region as softmax(t), so the 16 QK MFMAs of the next tile run
+// under this tile's ~150 softmax VALU instructions; PV(t) follows.  K runs one
+// tile ahead of V (iteration t reads K[t+1], V[t]; stages K[t+2], V[t+1]),
+// register-staged into 2+2 LDS buffers, one barrier per tile.  S(t)/S(t+1)
+// live in two named register sets (loop unrolled by 2: no runtime-indexed
+// register arrays).
+template <typename T, int D, int SGB>
+__global__ __launch_bounds__(512, 2) void attn_fwd_v4(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
+    const uint16_t* __restrict__ v, uint16_t* __restrict__ o, int H, int group,
+    int Nq, int Nk, AttnStrides st, float c, int causal, int qblocks,
+    int nblocks) {
+    using L = PadLayout<D>;
+    constexpr int NW = 8, NT = 512;
+    constexpr int CPR = D / 8;
+    constexpr int RPI = NT / CPR;
+    constexpr int CPT = KT / RPI;
+    static_assert(NT % CPR == 0 && KT % RPI == 0, "staging must tile evenly");
+    __shared__ __attribute__((aligned(16))) char smem[2 * L::BUF];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h32 = lane >> 5, l32 = lane & 31;
+    const int lb = xcd_remap(blockIdx.x, nblocks);
+    const int bh = lb / qblocks, qblk = lb % qblocks;
+    const int b = bh / H, hq = bh % H, hk = hq / group;
+    const int qbase = qblk * (NW * QW);
+    const int q0 = qbase + wave * QW;
+    const int off_diag = Nk - Nq;
+
+    const uint16_t* qp = q + b * st.qb + hq * st.qh;
+    const uint16_t* kp = k + b * st.kb + hk * st.kh;
+    const uint16_t* vp = v + b * st.vb + hk * st.vh;
+
+    i32x4 qf[D / 16];
+    {
+        const int qr = q0 + l32;
+        const bool ok = qr < Nq;
+        const uint16_t* src = qp + (int64_t)(ok ? qr : 0) * st.qn + 8 * h32;
+#pragma unroll
+        for (int kk = 0; kk < D / 16; ++kk) {
+            const i32x4 x = *reinterpret_cast<const i32x4*>(src + 16 * kk);
+            qf[kk] = ok ? x : i32x4{0, 0, 0, 0};
+        }
+    }
+
+    int kv_end = Nk;
+    if (causal) kv_end = min(Nk, qbase + NW * QW + off_diag);
+    const int nt = kv_end > 0 ? cdiv(kv_end, KT) : 0;
+    const int t_full = Nk / KT;
+    int t_mask = t_full;
+    if (causal) t_mask = min(t_mask, max(0, (q0 + off_diag + 1) / KT));
+
+    const int srow = tid / CPR, sch = tid % CPR;
+    const uint16_t* kg = kp + (int64_t)srow * st.kn + sch * 8;
+    const uint16_t* vg = vp + (int64_t)srow * st.vn + sch * 8;
+    const int kw = srow * L::KS + sch * 16, vw = L::KSZ + srow * L::VS + sch * 16;
+    auto load_rows = [&](i32x4 (&dst)[CPT], const uint16_t* gp, int64_t ld, int t) {
+        if (t < t_full) {
+#pragma unroll
+            for (int i = 0; i < CPT; ++i)
+                dst[i] = *reinterpret_cast<const i32x4*>(gp + ((int64_t)t * KT + i * RPI) * ld);
+        } else {
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) {
+                const int key = t * KT + i * RPI + srow;
+                const i32x4 x = *reinterpret_cast<const i32x4*>(gp + (int64_t)(min(key, Nk - 1) - srow) * ld);
+                dst[i] = key < Nk ? x : i32x4{0, 0, 0, 0};
+            }
+        }
+    };
+    auto store_rows = [&](char* base, int off0, int stride, const i32x4 (&src)[CPT]) {
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) lds_write_b128(base, off0 + i * RPI * stride, src[i]);
+    };
+
+    const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+    const int kr = l32 * L::KS + h32 * 16;
+    const int vr = L::KSZ + (4 * h32 + qq) * L::VS + (2 * (g & 1) + (pp >> 1)) * 16 + 8 * (pp & 1);
+
+    f32x16 oacc[D / 32];
+#pragma unroll
+    for (int d = 0; d < D / 32; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[d][r] = 0.f;
+    float m_run = -1e30f, l_run = 0.f;
+
+    auto qk = [&](int buf, f32x16 (&s)[2]) {
+        const char* kb = smem + buf * L::BUF + kr;
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[tt][r] = 0.f;
+#pragma unroll
+            for (int kk = 0; kk < D / 16; ++kk)
+                s[tt] = mfma32x32x16<T>(lds_read_b128(kb, tt * 32 * L::KS + kk * 32), qf[kk], s[tt]);
+        }
+    };
+
+    i32x4 kst[CPT], vst[CPT];
+    auto body = [&](auto mask_tag, f32x16 (&cur)[2], f32x16 (&nxt)[2], int t) {
+        constexpr bool MASK = decltype(mask_tag)::value;
+        if (t + 2 < nt) load_rows(kst, kg, st.kn, t + 2);
+        if (t + 1 < nt) load_rows(vst, vg, st.vn, t + 1);
+
+        // QK^T of tile t+1 (K[t+1] is resident; garbage and unused when t+1 == nt)
+        qk((t + 1) & 1, nxt);
+
+        if constexpr (MASK) {
+            const int lim = causal ? q0 + l32 + off_diag : Nk;
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int key = t * KT + tt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
+                    if (key >= Nk || key > lim) cur[tt][r] = -INFINITY;
+                }
+        }
+        float m4[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) m4[j] = max3(cur[0][4 * j], cur[1][4 * j], cur[0][4 * j + 1]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            m4[j] = max3(m4[j], cur[1][4 * j + 1], cur[0][4 * j + 2]);
+            m4[j] = max3(m4[j], cur[1][4 * j + 2], cur[0][4 * j + 3]);
+            m4[j] = fmaxf(m4[j], cur[1][4 * j + 3]);
+        }
+        float mx = max3(m4[0], m4[1], max3(m4[2], m4[3], m4[0]));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float m_new = fmaxf(m_run, mx * c);
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+        m_run = m_new;
+        float rs[4] = {0.f, 0.f, 0.f, 0.f};
+        i32x4 pb[2][2];
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                float p[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    p[j] = __builtin_amdgcn_exp2f(fmaf(cur[tt][8 * s2 + j], c, -m_new));
+                    rs[j & 3] += p[j];
+                }
+                pb[tt][s2] = i32x4{(int)pack2<T>(p[0], p[1]), (int)pack2<T>(p[2], p[3]),
+                                   (int)pack2<T>(p[4], p[5]), (int)pack2<T>(p[6], p[7])};
+            }
+        l_run = fmaf(l_run, alpha, (rs[0] + rs[1]) + (rs[2] + rs[3]));
+#pragma unroll
+        for (int d = 0; d < D / 32; ++d)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
+
+        const char* vb = smem + (t & 1) * L::BUF + vr;
+#pragma unroll
+        for (int dblk = 0; dblk < D / 32; ++dblk)
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    const int ro = (tt * 32 + 16 * s2) * L::VS + dblk * 64;
+                    const i32x2 lo = lds_read_tr16(vb, ro);
+                    const i32x2 hi = lds_read_tr16(vb, ro + 8 * L::VS);
+                    oacc[dblk] = mfma32x32x16<T>(i32x4{lo.x, lo.y, hi.x, hi.y}, pb[tt][s2], oacc[dblk]);
+                }
+
+        if constexpr (SGB == 2) {
+            // as SGB==1 but with the LDS fragment reads issued 3 MFMAs ahead
+            __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                if (i < 13) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x402, 9, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+#pragma unroll
+            for (int i = 0; i < 4 * (D / 32); ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                if (i < 4 * (D / 32) - 3) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x402, 2, 0);
+            }
+        }
+        if constexpr (SGB == 1) {
+            // Scheduling recipe for this region (LLVM SchedGroupMask bits:
+            // VALU 0x2, MFMA 0x8, DS_READ 0x100, TRANS 0x400): QK^T(t+1)'s 16
+            // MFMAs each followed by ~9 softmax VALU/TRANS ops, then PV's 16
+            // MFMAs each behind its two transposed V reads.
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x402, 9, 0);
+            }
+#pragma unroll
+            for (int i = 0; i < 4 * (D / 32); ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x402, 2, 0);
+            }
+        }
+
+        if (t + 2 < nt) store_rows(smem + (t & 1) * L::BUF, kw, L::KS, kst);
+        if (t + 1 < nt) store_rows(smem + ((t + 1) & 1) * L::BUF, vw, L::VS, vst);
+        __syncthreads();
+    };
+
+    f32x16 sA[2], sB[2];
+    if (nt > 0) {
+        load_rows(kst, kg, st.kn, 0);
+        load_rows(vst, vg, st.vn, 0);
+        store_rows(smem, kw, L::KS, kst);
+        store_rows(smem, vw, L::VS, vst);
+        if (nt > 1) {
+            load_rows(kst, kg, st.kn, 1);
+            store_rows(smem + L::BUF, kw, L::KS, kst);
+        }
+    }
+    __syncthreads();
+    if (nt > 0) qk(0, sA);
+    for (int t = 0; t < nt;) {
+        if (t < t_mask) body(std::false_type{}, sA, sB, t);
+        else body(std::true_type{}, sA, sB, t);
+        if (++t >= nt) break;
+        if (t < t_mask) body(std::false_type{}, sB, sA, t);
+        else body(std::true_type{}, sB, sA, t);
+        ++t;
+    }
+
+    const float l = l_run + __shfl_xor(l_run, 32, 64);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const int qr = q0 + l32;
+    if (qr < Nq) {
+        uint16_t* op = o + b * st.ob + hq * st.oh + (int64_t)qr * st.on;
+#pragma unroll
+        for (int dblk = 0; dblk < D / 32; ++dblk)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int d = dblk * 32 + 8 * i + 4 * h32;
+                const i32x2 w = {(int)pack2<T>(oacc[dblk][4 * i] * inv, oacc[dblk][4 * i + 1] * inv),
+                                 (int)pack2<T>(oacc[dblk][4 * i + 2] * inv, oacc[dblk][4 * i + 3] * inv)};
+                *reinterpret_cast<i32x2*>(op + d) = w;
+            }
+    }
+}
+
+// --------------------------------------------------------------------------
 // attn_fwd_v3: v2 with the two waves of each SIMD staggered.  A workgroup's
 // waves w and w+4 share a SIMD; in v2 both run QK^T-MFMA, softmax-VALU,
 // PV-MFMA in lockstep between barriers, so the SIMD alternates between a
@@ -819,6 +1272,9 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
 //   3: attn_fwd_v2, 4 waves, eager rescale
 //   4: attn_fwd_v3, 8 waves, staggered (waves 4-7 run a rotated body)
 //   5: attn_fwd_v3 with Q in LDS
+//   6: attn_fwd_v2b (block-wise softmax/PV)   7: attn_fwd_v2b + s_setprio
+//   8: attn_fwd_v4 (intra-wave pipeline: QK^T(t+1) beside softmax(t))
+//   9: attn_fwd_v4 + sched_group_barrier interleave  10: same, reads 3 ahead
 constexpr int kDefaultVariant = 2;
 
 template <typename T, int D>
@@ -845,6 +1301,11 @@ int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int
         case 3: PLI_ATTN_LAUNCH((attn_fwd_v2<T, D, 4, false>)); break;
         case 4: PLI_ATTN_LAUNCH((attn_fwd_v3<T, D, false>)); break;
         case 5: PLI_ATTN_LAUNCH((attn_fwd_v3<T, D, true>)); break;
+        case 6: PLI_ATTN_LAUNCH((attn_fwd_v2b<T, D, false>)); break;
+        case 7: PLI_ATTN_LAUNCH((attn_fwd_v2b<T, D, true>)); break;
+        case 8: PLI_ATTN_LAUNCH((attn_fwd_v4<T, D, 0>)); break;
+        case 9: PLI_ATTN_LAUNCH((attn_fwd_v4<T, D, 1>)); break;
+        case 10: PLI_ATTN_LAUNCH((attn_fwd_v4<T, D, 2>)); break;
         default:
             set_error("pli_flash_attn_fwd: unknown variant %d", variant);
             return PLI_EINVAL;
