@@ -1,0 +1,62 @@
+"""Run the reference's OWN test files, unmodified, against this build's packages.
+
+Each ``/root/reference/chXX/test_chXX.py`` is read at test time (never copied
+into this repository) and executed as a submodule of this build's ``chXX``
+package, so its relative imports (``from .flash_attention import ...``)
+resolve to the MI355X implementation.  Test classes / methods are collected
+here and run one pytest case each; the reference's ``skipif`` markers are
+honoured (its CUDA-gated classes run on a ROCm box, skip elsewhere).
+
+Only chapters whose test modules import nothing outside the hot-path scope
+are run (ch03, ch06); ch01/ch05/ch09's test modules import out-of-scope
+symbols (FFN/GQA/transformer, shared_memory, MoE) at module level -- their
+in-scope assertions are restated in test_host_cpu.py / test_gpu_parity.py.
+Skipped entirely when /root/reference is absent (e.g. on the GPU box).
+"""
+from __future__ import annotations
+
+import importlib.util
+import inspect
+import os
+
+import pytest
+
+REF = os.environ.get("PLI_REFERENCE", "/root/reference")
+CHAPTERS = ("ch03", "ch06")
+
+
+def _load(chapter: str):
+    path = os.path.join(REF, chapter, f"test_{chapter}.py")
+    pkg = __import__(chapter)  # this build's package
+    name = f"{chapter}._reference_test_{chapter}"
+    spec = importlib.util.spec_from_file_location(name, path)
+    mod = importlib.util.module_from_spec(spec)
+    mod.__package__ = chapter
+    spec.loader.exec_module(mod)
+    assert os.path.dirname(pkg.__file__) != os.path.join(REF, chapter)
+    return mod
+
+
+def _cases():
+    if not os.path.isdir(REF):
+        return []
+    out = []
+    for ch in CHAPTERS:
+        mod = _load(ch)
+        for cname, cls in inspect.getmembers(mod, inspect.isclass):
+            if not cname.startswith("Test") or cls.__module__ != mod.__name__:
+                continue
+            marks = getattr(cls, "pytestmark", [])
+            for mname, _ in inspect.getmembers(cls, inspect.isfunction):
+                if mname.startswith("test_"):
+                    out.append(pytest.param(cls, mname, marks=marks, id=f"{ch}::{cname}::{mname}"))
+    return out
+
+
+CASES = _cases()
+
+
+@pytest.mark.skipif(not CASES, reason="reference tree not present")
+@pytest.mark.parametrize("cls,method", CASES or [pytest.param(None, None, id="none")])
+def test_reference_case(cls, method):
+    getattr(cls(), method)()
