@@ -298,7 +298,10 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_v2(
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int h32 = lane >> 5, l32 = lane & 31;
     const int lb = xcd_remap(blockIdx.x, nblocks);
-    const int bh = lb / qblocks, qblk = lb % qblocks;
+    const int bh = lb / qblocks;
+    // causal: a query block's work grows with its index; start each head's
+    // heaviest blocks first so the grid drains on light ones
+    const int qblk = causal ? qblocks - 1 - lb % qblocks : lb % qblocks;
     const int b = bh / H, hq = bh % H, hk = hq / group;
     const int qbase = qblk * (NW * QW);
     const int q0 = qbase + wave * QW;
@@ -934,6 +937,285 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v4(
 }
 
 // --------------------------------------------------------------------------
+// attn_fwd_v5: 64 query rows per wave (two 32-row blocks), 4 waves = 256 rows
+// per workgroup, ONE wave per SIMD with the 512-register budget.
+//  * every K fragment read from LDS feeds two QK^T MFMAs and every V^T
+//    fragment two PV MFMAs: half v2's LDS read traffic per MFMA;
+//  * software pipeline across tiles inside the wave: the loop body is one
+//    scheduling region holding QK^T(t+1) for both row blocks (32 MFMAs),
+//    softmax(t) for both blocks (VALU), the O rescale and PV(t) (32 MFMAs),
+//    so the softmax VALU fills the QK^T MFMA gaps of the same wave (there is
+//    no partner wave on the SIMD to hide it);
+//  * K runs one tile ahead of V (iteration t reads K[t+1], V[t]; stages
+//    K[t+2], V[t+1] through registers into the padded 2+2 buffer ring).
+template <typename T, int D, int SGB, bool DMA>
+__global__ __launch_bounds__(256, 1) void attn_fwd_v5(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
+    const uint16_t* __restrict__ v, uint16_t* __restrict__ o, int H, int group,
+    int Nq, int Nk, AttnStrides st, float c, int causal, int qblocks,
+    int nblocks) {
+    using L = PadLayout<D>;
+    constexpr int NW = 4, NT = 256;
+    constexpr int CPR = D / 8;
+    constexpr int RPI = NT / CPR;
+    constexpr int CPT = KT / RPI;
+    static_assert(NT % CPR == 0 && KT % RPI == 0, "staging must tile evenly");
+    __shared__ __attribute__((aligned(16))) char smem[2 * L::BUF];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h32 = lane >> 5, l32 = lane & 31;
+    const int lb = xcd_remap(blockIdx.x, nblocks);
+    const int bh = lb / qblocks, qblk = lb % qblocks;
+    const int b = bh / H, hq = bh % H, hk = hq / group;
+    const int qbase = qblk * (NW * 2 * QW);
+    const int qw0 = qbase + wave * 2 * QW;  // first row of this wave's 64
+    const int off_diag = Nk - Nq;
+
+    const uint16_t* qp = q + b * st.qb + hq * st.qh;
+    const uint16_t* kp = k + b * st.kb + hk * st.kh;
+    const uint16_t* vp = v + b * st.vb + hk * st.vh;
+
+    i32x4 qf0[D / 16], qf1[D / 16];
+    {
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+            const int qr = qw0 + rb * QW + l32;
+            const bool ok = qr < Nq;
+            const uint16_t* src = qp + (int64_t)(ok ? qr : 0) * st.qn + 8 * h32;
+#pragma unroll
+            for (int kk = 0; kk < D / 16; ++kk) {
+                const i32x4 x = *reinterpret_cast<const i32x4*>(src + 16 * kk);
+                (rb ? qf1 : qf0)[kk] = ok ? x : i32x4{0, 0, 0, 0};
+            }
+        }
+    }
+
+    int kv_end = Nk;
+    if (causal) kv_end = min(Nk, qbase + NW * 2 * QW + off_diag);
+    const int nt = kv_end > 0 ? cdiv(kv_end, KT) : 0;
+    const int t_full = Nk / KT;
+    int t_mask = t_full;
+    if (causal) t_mask = min(t_mask, max(0, (qw0 + off_diag + 1) / KT));
+
+    const int srow = tid / CPR, sch = tid % CPR;
+    const uint16_t* kg = kp + (int64_t)srow * st.kn + sch * 8;
+    const uint16_t* vg = vp + (int64_t)srow * st.vn + sch * 8;
+    const int kw = srow * L::KS + sch * 16, vw = L::KSZ + srow * L::VS + sch * 16;
+    auto load_rows = [&](i32x4 (&dst)[CPT], const uint16_t* gp, int64_t ld, int t) {
+        if (t < t_full) {
+#pragma unroll
+            for (int i = 0; i < CPT; ++i)
+                dst[i] = *reinterpret_cast<const i32x4*>(gp + ((int64_t)t * KT + i * RPI) * ld);
+        } else {
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) {
+                const int key = t * KT + i * RPI + srow;
+                const i32x4 x = *reinterpret_cast<const i32x4*>(gp + (int64_t)(min(key, Nk - 1) - srow) * ld);
+                dst[i] = key < Nk ? x : i32x4{0, 0, 0, 0};
+            }
+        }
+    };
+    auto store_rows = [&](char* base, int off0, int stride, const i32x4 (&src)[CPT]) {
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) lds_write_b128(base, off0 + i * RPI * stride, src[i]);
+    };
+    // DMA staging (global_load_lds_dwordx4): the padded tile is filled as
+    // consecutive 1 KiB pieces; each lane derives its (row, chunk) from its
+    // linear LDS position, lanes landing on a row's pad load a dummy chunk.
+    // Rows past Nk are clamped to Nk-1 (finite; masked to -inf / weight 0).
+    auto dma_tile = [&](char* dst, const uint16_t* base, int64_t ld, int stride, int bytes, int t) {
+        for (int piece = wave; piece * 1024 < bytes; piece += NW) {
+            const int pos = piece * 1024 + lane * 16;
+            const int row = pos / stride, off = pos - row * stride;
+            const int ch = off < 2 * D ? off >> 4 : 0;
+            const int key = min(t * KT + row, Nk - 1);
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void*)(base + (int64_t)key * ld + ch * 8),
+                (__attribute__((address_space(3))) void*)(dst + piece * 1024), 16, 0, 0);
+        }
+    };
+
+    const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+    const int kr = l32 * L::KS + h32 * 16;
+    const int vr = L::KSZ + (4 * h32 + qq) * L::VS + (2 * (g & 1) + (pp >> 1)) * 16 + 8 * (pp & 1);
+
+    f32x16 o0[D / 32], o1[D / 32];
+#pragma unroll
+    for (int d = 0; d < D / 32; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o0[d][r] = o1[d][r] = 0.f;
+    float m0 = -1e30f, m1 = -1e30f, l0 = 0.f, l1 = 0.f;
+
+    // S^T for both row blocks from one pass over K: each K fragment -> 2 MFMAs
+    auto qk2 = [&](int buf, f32x16 (&s0)[2], f32x16 (&s1)[2]) {
+        const char* kb = smem + buf * L::BUF + kr;
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s0[tt][r] = s1[tt][r] = 0.f;
+#pragma unroll
+            for (int kk = 0; kk < D / 16; ++kk) {
+                const i32x4 kf = lds_read_b128(kb, tt * 32 * L::KS + kk * 32);
+                s0[tt] = mfma32x32x16<T>(kf, qf0[kk], s0[tt]);
+                s1[tt] = mfma32x32x16<T>(kf, qf1[kk], s1[tt]);
+            }
+        }
+    };
+    auto mask = [&](f32x16 (&s)[2], int row0, int t) {
+        const int lim = causal ? row0 + l32 + off_diag : Nk;
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int key = t * KT + tt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
+                if (key >= Nk || key > lim) s[tt][r] = -INFINITY;
+            }
+    };
+    // online softmax of one 32-row block: returns alpha, fills pb, updates m/l
+    auto softmax = [&](f32x16 (&s)[2], float& m_run, float& l_run, i32x4 (&pb)[2][2]) {
+        float m4[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) m4[j] = max3(s[0][4 * j], s[1][4 * j], s[0][4 * j + 1]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            m4[j] = max3(m4[j], s[1][4 * j + 1], s[0][4 * j + 2]);
+            m4[j] = max3(m4[j], s[1][4 * j + 2], s[0][4 * j + 3]);
+            m4[j] = fmaxf(m4[j], s[1][4 * j + 3]);
+        }
+        float mx = max3(m4[0], m4[1], max3(m4[2], m4[3], m4[0]));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float m_new = fmaxf(m_run, mx * c);
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+        m_run = m_new;
+        float rs[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                float p[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    p[j] = __builtin_amdgcn_exp2f(fmaf(s[tt][8 * s2 + j], c, -m_new));
+                    rs[j & 3] += p[j];
+                }
+                pb[tt][s2] = i32x4{(int)pack2<T>(p[0], p[1]), (int)pack2<T>(p[2], p[3]),
+                                   (int)pack2<T>(p[4], p[5]), (int)pack2<T>(p[6], p[7])};
+            }
+        l_run = fmaf(l_run, alpha, (rs[0] + rs[1]) + (rs[2] + rs[3]));
+        return alpha;
+    };
+
+    i32x4 kst[CPT], vst[CPT];
+    auto body = [&](auto mask_tag, f32x16 (&c0)[2], f32x16 (&c1)[2], f32x16 (&n0)[2],
+                    f32x16 (&n1)[2], int t) {
+        constexpr bool MASK = decltype(mask_tag)::value;
+        if constexpr (DMA) {
+            if (t + 2 < nt) dma_tile(smem + (t & 1) * L::BUF, kp, st.kn, L::KS, L::KSZ, t + 2);
+            if (t + 1 < nt) dma_tile(smem + ((t + 1) & 1) * L::BUF + L::KSZ, vp, st.vn, L::VS, L::VSZ, t + 1);
+        } else {
+            if (t + 2 < nt) load_rows(kst, kg, st.kn, t + 2);
+            if (t + 1 < nt) load_rows(vst, vg, st.vn, t + 1);
+        }
+
+        qk2((t + 1) & 1, n0, n1);  // QK^T(t+1), unused when t+1 == nt
+        if constexpr (MASK) {
+            mask(c0, qw0, t);
+            mask(c1, qw0 + QW, t);
+        }
+        i32x4 pb0[2][2], pb1[2][2];
+        const float a0 = softmax(c0, m0, l0, pb0);
+        const float a1 = softmax(c1, m1, l1, pb1);
+#pragma unroll
+        for (int d = 0; d < D / 32; ++d)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                o0[d][r] *= a0;
+                o1[d][r] *= a1;
+            }
+        const char* vb = smem + (t & 1) * L::BUF + vr;
+#pragma unroll
+        for (int dblk = 0; dblk < D / 32; ++dblk)
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    const int ro = (tt * 32 + 16 * s2) * L::VS + dblk * 64;
+                    const i32x2 lo = lds_read_tr16(vb, ro);
+                    const i32x2 hi = lds_read_tr16(vb, ro + 8 * L::VS);
+                    const i32x4 vf = {lo.x, lo.y, hi.x, hi.y};
+                    o0[dblk] = mfma32x32x16<T>(vf, pb0[tt][s2], o0[dblk]);
+                    o1[dblk] = mfma32x32x16<T>(vf, pb1[tt][s2], o1[dblk]);
+                }
+        if constexpr (SGB == 1) {
+            // QK^T phase: K reads 4 ahead, ~8 softmax VALU/TRANS per MFMA gap;
+            // PV phase: one tr read + 2 VALU per MFMA.
+            __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+            for (int i = 0; i < 32; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                if ((i & 1) && i < 24) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x402, 8, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+            for (int i = 0; i < 32; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x402, 2, 0);
+            }
+        }
+        if constexpr (!DMA) {
+            if (t + 2 < nt) store_rows(smem + (t & 1) * L::BUF, kw, L::KS, kst);
+            if (t + 1 < nt) store_rows(smem + ((t + 1) & 1) * L::BUF, vw, L::VS, vst);
+        }
+        __syncthreads();  // (DMA: vmcnt(0) first -- the prefetched tiles have landed)
+    };
+
+    f32x16 sA0[2], sA1[2], sB0[2], sB1[2];
+    if (nt > 0) {
+        load_rows(kst, kg, st.kn, 0);
+        load_rows(vst, vg, st.vn, 0);
+        store_rows(smem, kw, L::KS, kst);
+        store_rows(smem, vw, L::VS, vst);
+        if (nt > 1) {
+            load_rows(kst, kg, st.kn, 1);
+            store_rows(smem + L::BUF, kw, L::KS, kst);
+        }
+    }
+    __syncthreads();
+    if (nt > 0) qk2(0, sA0, sA1);
+    for (int t = 0; t < nt;) {
+        if (t < t_mask) body(std::false_type{}, sA0, sA1, sB0, sB1, t);
+        else body(std::true_type{}, sA0, sA1, sB0, sB1, t);
+        if (++t >= nt) break;
+        if (t < t_mask) body(std::false_type{}, sB0, sB1, sA0, sA1, t);
+        else body(std::true_type{}, sB0, sB1, sA0, sA1, t);
+        ++t;
+    }
+
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+        const float lr = rb ? l1 : l0;
+        const float l = lr + __shfl_xor(lr, 32, 64);
+        const float inv = l > 0.f ? 1.f / l : 0.f;
+        const int qr = qw0 + rb * QW + l32;
+        if (qr < Nq) {
+            uint16_t* op = o + b * st.ob + hq * st.oh + (int64_t)qr * st.on;
+#pragma unroll
+            for (int dblk = 0; dblk < D / 32; ++dblk)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const f32x16& acc = rb ? o1[dblk] : o0[dblk];
+                    const int d = dblk * 32 + 8 * i + 4 * h32;
+                    const i32x2 w = {(int)pack2<T>(acc[4 * i] * inv, acc[4 * i + 1] * inv),
+                                     (int)pack2<T>(acc[4 * i + 2] * inv, acc[4 * i + 3] * inv)};
+                    *reinterpret_cast<i32x2*>(op + d) = w;
+                }
+        }
+    }
+}
+
+// --------------------------------------------------------------------------
 // attn_fwd_v3: v2 with the two waves of each SIMD staggered.  A workgroup's
 // waves w and w+4 share a SIMD; in v2 both run QK^T-MFMA, softmax-VALU,
 // PV-MFMA in lockstep between barriers, so the SIMD alternates between a
@@ -1275,13 +1557,15 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
 //   6: attn_fwd_v2b (block-wise softmax/PV)   7: attn_fwd_v2b + s_setprio
 //   8: attn_fwd_v4 (intra-wave pipeline: QK^T(t+1) beside softmax(t))
 //   9: attn_fwd_v4 + sched_group_barrier interleave  10: same, reads 3 ahead
+//  11: attn_fwd_v5 (64 rows/wave, 1 wave/SIMD)  12: v5 + sched_group_barrier
+//  13: v5 with LDS-DMA staging                  14: v5 + DMA + sched_group_barrier
 constexpr int kDefaultVariant = 2;
 
 template <typename T, int D>
 int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int H,
                 int group, int Nq, int Nk, const AttnStrides& st, float scale,
                 int causal, hipStream_t stream, int variant) {
-    const int nw = (variant == 2 || variant >= 4) ? 8 : 4;
+    const int nw = (variant == 2 || variant >= 4) ? 8 : 4;  // v5 (11-14): 4 waves x 64 rows
     const int qblocks = cdiv(Nq, nw * QW);
     const int64_t nb = (int64_t)B * H * qblocks;
     PLI_REQUIRE(nb < (1ll << 31), "pli_flash_attn_fwd: grid too large");
@@ -1306,6 +1590,14 @@ int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int
         case 8: PLI_ATTN_LAUNCH((attn_fwd_v4<T, D, 0>)); break;
         case 9: PLI_ATTN_LAUNCH((attn_fwd_v4<T, D, 1>)); break;
         case 10: PLI_ATTN_LAUNCH((attn_fwd_v4<T, D, 2>)); break;
+#define PLI_ATTN_V5(SGB, DMA)                                                                    \
+    hipLaunchKernelGGL((attn_fwd_v5<T, D, SGB, DMA>), grid, dim3(256), 0, stream, qq, kk, vv, oo, \
+                       H, group, Nq, Nk, st, c, causal, qblocks, (int)nb)
+        case 11: PLI_ATTN_V5(0, false); break;
+        case 12: PLI_ATTN_V5(1, false); break;
+        case 13: PLI_ATTN_V5(0, true); break;
+        case 14: PLI_ATTN_V5(1, true); break;
+#undef PLI_ATTN_V5
         default:
             set_error("pli_flash_attn_fwd: unknown variant %d", variant);
             return PLI_EINVAL;

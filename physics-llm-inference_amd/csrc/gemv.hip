@@ -1,7 +1,8 @@
 // Decode GEMV y = W x for gfx950 (MI355X): the torch.mv of
 // ch03/gemv_benchmark.py:38.  HBM-bound (AI ~1 FLOP/B): no MFMA, no LDS.
 //
-// Each wave owns ROWS consecutive rows.  Lane l streams the 16-byte chunks
+// Each wave owns ROWS consecutive rows (default: 1 row per wave, 2-wave blocks;
+// variants A/B-measured in tools/tune.py under HIP-graph timing).  Lane l streams the 16-byte chunks
 // l, l+64, ... of every row with global_load_dwordx4 (non-temporal: W is read
 // exactly once per call), all ROWS x CPL loads issued before the first use so
 // a CU keeps ROWS*CPL KiB per wave in flight; the x chunks are loaded once per
@@ -43,12 +44,12 @@ __device__ __forceinline__ void dot_chunk<float>(const i32x4& w, const i32x4& x,
     for (int i = 0; i < 4; ++i) acc = fmaf(__int_as_float(w[i]), __int_as_float(x[i]), acc);
 }
 
-template <typename T, int ROWS, int CPL, bool NTL>
-__global__ __launch_bounds__(256) void gemv_vec(const char* __restrict__ w,
-                                                const char* __restrict__ x, T* __restrict__ y,
-                                                int M, int nchunks, int64_t ldw_bytes) {
+template <typename T, int ROWS, int CPL, bool NTL, int WPB = 4>
+__global__ __launch_bounds__(WPB * 64) void gemv_vec(const char* __restrict__ w,
+                                                     const char* __restrict__ x, T* __restrict__ y,
+                                                     int M, int nchunks, int64_t ldw_bytes) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int row0 = (blockIdx.x * 4 + wave) * ROWS;
+    const int row0 = (blockIdx.x * WPB + wave) * ROWS;
     if (row0 >= M) return;
     float acc[ROWS];
 #pragma unroll
@@ -104,13 +105,15 @@ __global__ __launch_bounds__(256) void gemv_scalar(const T* __restrict__ w, cons
 // Variants (A/B via pli_gemv_variant): rows per wave x 16-B chunks per lane
 // per k-step x non-temporal W loads.
 //   0: 2x8 nt  1: 4x8 nt  2: 1x8 nt  3: 2x8 plain  4: 4x4 nt  5: 8x4 nt
-constexpr int kDefaultGemvVariant = 0;
+//   6: 2x8 nt, 1-wave blocks   7: 2x8 nt, 8-wave blocks   8: 1x8 nt, 2-wave blocks
+constexpr int kDefaultGemvVariant = 8;
 
-template <typename T, int ROWS, int CPL, bool NTL>
+template <typename T, int ROWS, int CPL, bool NTL, int WPB = 4>
 int launch_vec(const void* w, const void* x, void* y, int m, int nchunks, int64_t ldw_b,
                hipStream_t s) {
-    hipLaunchKernelGGL((gemv_vec<T, ROWS, CPL, NTL>), dim3(cdiv(m, 4 * ROWS)), dim3(256), 0, s,
-                       (const char*)w, (const char*)x, (T*)y, m, nchunks, ldw_b);
+    hipLaunchKernelGGL((gemv_vec<T, ROWS, CPL, NTL, WPB>), dim3(cdiv(m, WPB * ROWS)),
+                       dim3(WPB * 64), 0, s, (const char*)w, (const char*)x, (T*)y, m, nchunks,
+                       ldw_b);
     return launch_status("gemv_vec");
 }
 
@@ -134,6 +137,9 @@ int launch(const void* w, const void* x, void* y, int m, int k, int64_t ldw, hip
         case 3: return launch_vec<T, 2, 8, false>(w, x, y, m, nchunks, ldw_b, s);
         case 4: return launch_vec<T, 4, 4, true>(w, x, y, m, nchunks, ldw_b, s);
         case 5: return launch_vec<T, 8, 4, true>(w, x, y, m, nchunks, ldw_b, s);
+        case 6: return launch_vec<T, 2, 8, true, 1>(w, x, y, m, nchunks, ldw_b, s);
+        case 7: return launch_vec<T, 2, 8, true, 8>(w, x, y, m, nchunks, ldw_b, s);
+        case 8: return launch_vec<T, 1, 8, true, 2>(w, x, y, m, nchunks, ldw_b, s);
         default: set_error("pli_gemv: unknown variant %d", variant); return PLI_EINVAL;
     }
 }

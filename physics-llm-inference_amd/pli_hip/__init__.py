@@ -106,12 +106,32 @@ def _require_gpu(*ts: torch.Tensor) -> torch.device:
     return dev
 
 
-def _stream(dev: torch.device) -> ctypes.c_void_p:
-    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+def _stream(dev: torch.device) -> int:
+    # raw hipStream_t of the current stream (cheaper than building a Stream object)
+    return torch._C._cuda_getCurrentRawStream(dev.index)
 
 
-def _ptr(t: torch.Tensor | None) -> ctypes.c_void_p:
-    return ctypes.c_void_p(t.data_ptr() if t is not None else None)
+class _on_device:
+    """Device guard that costs nothing when ``dev`` is already current."""
+
+    __slots__ = ("dev", "prev")
+
+    def __init__(self, dev: torch.device):
+        self.dev, self.prev = dev, None
+
+    def __enter__(self):
+        cur = torch.cuda.current_device()
+        if self.dev.index is not None and cur != self.dev.index:
+            self.prev = cur
+            torch.cuda.set_device(self.dev.index)
+
+    def __exit__(self, *exc):
+        if self.prev is not None:
+            torch.cuda.set_device(self.prev)
+
+
+def _ptr(t: torch.Tensor | None):
+    return t.data_ptr() if t is not None else None
 
 
 # ------------------------------------------------------------------ attention
@@ -140,7 +160,7 @@ def flash_attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: flo
     st = (_c_i64 * 12)(*(int(x) for t in (q, k, v, out) for x in t.stride()[:3]))
     args = (_ptr(q), _ptr(k), _ptr(v), _ptr(out), B, H, Hkv, Nq, Nk, D, st, float(scale),
             int(bool(causal)), _dtype_code(q), _stream(dev))
-    with torch.cuda.device(dev):
+    with _on_device(dev):
         if variant is None:
             rc = lib().pli_flash_attn_fwd(*args)
         else:
@@ -163,7 +183,7 @@ def gemv(w: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None,
     if out is None:
         out = torch.empty(m, dtype=w.dtype, device=dev)
     args = (_ptr(w), _ptr(x), _ptr(out), m, k, max(w.stride(0), k), _dtype_code(w), _stream(dev))
-    with torch.cuda.device(dev):
+    with _on_device(dev):
         if variant is None:
             rc = lib().pli_gemv(*args)
         else:
@@ -196,7 +216,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, trans_b: bool = False,
         out = torch.empty((m, n), dtype=a.dtype, device=dev)
     lda = a.stride(0) if m > 1 else k
     ldb = b.stride(0) if b.shape[0] > 1 else b.shape[1]
-    with torch.cuda.device(dev):
+    with _on_device(dev):
         rc = lib().pli_gemm(_ptr(a), _ptr(b), _ptr(out), _ptr(bias), m, n, k, max(lda, 1),
                             max(ldb, 1), max(out.stride(0), n), int(bool(trans_b)),
                             _dtype_code(a), _stream(dev))
@@ -213,7 +233,7 @@ def scale_copy(inp: torch.Tensor, out: torch.Tensor, stride: int = 1) -> torch.T
     n_out = out.numel()
     if (n_out - 1) * stride >= inp.numel() and n_out > 0:
         raise PliError("scale_copy: input too short for stride")
-    with torch.cuda.device(dev):
+    with _on_device(dev):
         rc = lib().pli_scale_copy(_ptr(inp), _ptr(out), n_out, int(stride), _stream(dev))
     _check(rc, "pli_scale_copy")
     return out
@@ -228,7 +248,7 @@ def softmax_rows(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tens
     rows = x.numel() // max(n, 1)
     if out is None:
         out = torch.empty_like(x)
-    with torch.cuda.device(dev):
+    with _on_device(dev):
         rc = lib().pli_softmax_rows(_ptr(x), _ptr(out), rows, n, _dtype_code(x), _stream(dev))
     _check(rc, "pli_softmax_rows")
     return out
@@ -244,7 +264,7 @@ def online_softmax_with_output(x: torch.Tensor, v: torch.Tensor):
     rows = x.numel() // n
     o = torch.empty(x.shape[:-1] + (dv,), dtype=x.dtype, device=dev)
     d = torch.empty(x.shape[:-1], dtype=x.dtype, device=dev)
-    with torch.cuda.device(dev):
+    with _on_device(dev):
         rc = lib().pli_online_softmax_with_output(_ptr(x), _ptr(v), _ptr(o), _ptr(d), rows, n, dv,
                                                   _dtype_code(x), _stream(dev))
     _check(rc, "pli_online_softmax_with_output")

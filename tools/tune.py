@@ -39,7 +39,7 @@ def interleave(fns: dict, iters: int, rounds: int):
     return {k: (float(np.median(v)), float(np.min(v))) for k, v in res.items()}
 
 
-def tune_flash(variants=(2, 8, 9, 10), causal=False, B=8, H=32, S=4096, D=128):
+def tune_flash(variants=(2, 11, 12, 13, 14), causal=False, B=8, H=32, S=4096, D=128):
     from oracle.attention import naive_attention
     g = torch.Generator(device="cuda").manual_seed(0)
     q, k, v = (torch.randn(B, H, S, D, device="cuda", dtype=torch.bfloat16, generator=g) for _ in range(3))
@@ -60,30 +60,81 @@ def tune_flash(variants=(2, 8, 9, 10), causal=False, B=8, H=32, S=4096, D=128):
                           "maxdiff_vs_v0": diff, "err_vs_f64_head0": err}), flush=True)
 
 
-def tune_gemv(variants=(0, 1, 2, 3, 4, 5), m=4096, k=4096, copies=12):
+def tune_gemv(variants=(0, 1, 2, 3, 4, 5, 6, 7, 8), m=4096, k=4096, copies=24):
+    """GEMV variants, each as a HIP graph of `copies` launches over rotated
+    weights (device time per launch incl. kernel boundaries, no host cost)."""
     ws = [torch.randn(m, k, device="cuda", dtype=torch.bfloat16) for _ in range(copies)]
     x = torch.randn(k, device="cuda", dtype=torch.bfloat16)
     ys = {vv: torch.empty(m, device="cuda", dtype=torch.bfloat16) for vv in variants}
     ref = (ws[0].float() @ x.float())
-    st = {"i": 0}
-
-    def mk(vv):
-        def f():
-            pli_hip.gemv(ws[st["i"] % copies], x, out=ys[vv], variant=vv)
-            st["i"] += 1
-        return f
-    fns = {vv: mk(vv) for vv in variants}
-    for f in fns.values():
-        for _ in range(copies):
-            f()
-    t = interleave(fns, 240, 5)
+    graphs = {}
+    for vv in variants:
+        for w in ws:
+            pli_hip.gemv(w, x, out=ys[vv], variant=vv)
+        torch.cuda.synchronize()
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr):
+            for w in ws:
+                pli_hip.gemv(w, x, out=ys[vv], variant=vv)
+        graphs[vv] = gr
+    t = interleave({vv: graphs[vv].replay for vv in variants}, 10, 5)
     nbytes = (m * k + m + k) * 2
     for vv in variants:
         pli_hip.gemv(ws[0], x, out=ys[vv], variant=vv)
         err = ((ys[vv].float() - ref).abs() / (ref.abs() + 1)).max().item()
-        print(json.dumps({"kernel": "gemv", "variant": vv, "us_med": t[vv][0] * 1e3,
-                          "us_min": t[vv][1] * 1e3, "GB/s": nbytes / (t[vv][0] * 1e-3) / 1e9,
-                          "rel_err": err}), flush=True)
+        us = t[vv][0] * 1e3 / copies
+        print(json.dumps({"kernel": "gemv", "variant": vv, "us_per_launch": us,
+                          "GB/s": nbytes / (us * 1e-6) / 1e9, "rel_err": err}), flush=True)
+
+
+def tune_gemv_sweep():
+    """Per-launch time vs size: separates fixed launch/latency cost from
+    streaming bandwidth (t = t0 + bytes / BW)."""
+    for m in (1024, 2048, 4096, 8192, 16384):
+        k = m
+        copies = max(2, (768 << 20) // (m * k * 2))
+        ws = [torch.randn(m, k, device="cuda", dtype=torch.bfloat16) for _ in range(copies)]
+        x = torch.randn(k, device="cuda", dtype=torch.bfloat16)
+        y = torch.empty(m, device="cuda", dtype=torch.bfloat16)
+        st = {"i": 0}
+
+        def f():
+            pli_hip.gemv(ws[st["i"] % copies], x, out=y)
+            st["i"] += 1
+        for _ in range(2 * copies):
+            f()
+        t = interleave({"g": f}, max(4 * copies, 40), 3)["g"][0]
+        nbytes = (m * k + m + k) * 2
+        print(json.dumps({"kernel": "gemv_sweep", "m": m, "copies": copies, "us": t * 1e3,
+                          "GB/s": nbytes / (t * 1e-3) / 1e9}), flush=True)
+        del ws
+    # the same launches captured in a HIP graph: device time incl. the kernel
+    # boundary, without Python launch overhead
+    for m in (4096, 8192):
+        k = m
+        copies = max(2, (768 << 20) // (m * k * 2))
+        ws = [torch.randn(m, k, device="cuda", dtype=torch.bfloat16) for _ in range(copies)]
+        x = torch.randn(k, device="cuda", dtype=torch.bfloat16)
+        y = torch.empty(m, device="cuda", dtype=torch.bfloat16)
+        for w in ws:
+            pli_hip.gemv(w, x, out=y)
+        torch.cuda.synchronize()
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr):
+            for w in ws:
+                pli_hip.gemv(w, x, out=y)
+        for _ in range(3):
+            gr.replay()
+        t = interleave({"g": gr.replay}, 10, 3)["g"][0] / copies
+        nbytes = (m * k + m + k) * 2
+        print(json.dumps({"kernel": "gemv_graph", "m": m, "copies": copies, "us": t * 1e3,
+                          "GB/s": nbytes / (t * 1e-3) / 1e9}), flush=True)
+        del ws
+    # empty-kernel launch gap: a 1-element scale_copy back to back
+    a = torch.zeros(4, device="cuda")
+    b = torch.zeros(4, device="cuda")
+    t = interleave({"e": lambda: pli_hip.scale_copy(a, b)}, 200, 3)["e"][0]
+    print(json.dumps({"kernel": "empty_launch", "us": t * 1e3}), flush=True)
 
 
 def tune_hbm():
@@ -117,8 +168,12 @@ if __name__ == "__main__":
         tune_hbm()
     if "gemv" in what:
         tune_gemv()
+    if "gemvsweep" in what:
+        tune_gemv_sweep()
     if "flash" in what:
         tune_flash()
         tune_flash(causal=True)
+    if "flash64" in what:
+        tune_flash(D=64, H=64)
     if "gemm" in what:
         tune_gemm()
