@@ -232,6 +232,180 @@ __global__ __launch_bounds__(256) void gemm_generic(const T* __restrict__ A, con
     }
 }
 
+// ---------------------------------------------------------------------------
+// Skinny NT path for decode batches (x @ W^T with M <= 16 rows of X,
+// ch03/batching_benchmark.py:25-39): HBM-bound on W like the GEMV.  One W row
+// per wave, each lane streams 16-byte W chunks (non-temporal, read once) and
+// dots them with the matching chunk of every X row (X is tiny and stays in
+// L1/L2); NB fp32 accumulators per lane, one shuffle reduction per output.
+template <typename T, int NB, int CPL>
+__global__ __launch_bounds__(128) void gemm_skinny_nt(const uint16_t* __restrict__ X,
+                                                      const uint16_t* __restrict__ W,
+                                                      uint16_t* __restrict__ C,
+                                                      const uint16_t* __restrict__ bias, int M,
+                                                      int N, int nchunks, int64_t ldx, int64_t ldw,
+                                                      int64_t ldc) {
+    const int lane = threadIdx.x & 63;
+    const int n = blockIdx.x * 2 + (threadIdx.x >> 6);
+    if (n >= N) return;
+    const uint16_t* wrow = W + (int64_t)n * ldw;
+    float acc[NB];
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb) acc[bb] = 0.f;
+    for (int c0 = 0; c0 < nchunks; c0 += 64 * CPL) {
+        i32x4 wv[CPL];
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) {
+            const int cc = min(c0 + lane + 64 * u, nchunks - 1);
+            wv[u] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wrow + cc * 8));
+        }
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) {
+            const int cc = c0 + lane + 64 * u;
+            if (cc < nchunks) {
+#pragma unroll
+                for (int bb = 0; bb < NB; ++bb) {
+                    if (bb < M) {
+                        const i32x4 xv = *reinterpret_cast<const i32x4*>(X + bb * ldx + cc * 8);
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const int wi = wv[u][i], xi = xv[i];
+                            const float w0 = elem<T>::to_f32(T{(uint16_t)(wi & 0xffff)});
+                            const float w1 = elem<T>::to_f32(T{(uint16_t)((uint32_t)wi >> 16)});
+                            const float x0 = elem<T>::to_f32(T{(uint16_t)(xi & 0xffff)});
+                            const float x1 = elem<T>::to_f32(T{(uint16_t)((uint32_t)xi >> 16)});
+                            acc[bb] = fmaf(w1, x1, fmaf(w0, x0, acc[bb]));
+                        }
+                    }
+                }
+            }
+        }
+    }
+    const float bn = bias ? elem<T>::to_f32(T{bias[n]}) : 0.f;
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb) {
+        if (bb < M) {
+            const float r = wave_sum(acc[bb]);
+            if (lane == 0) C[bb * ldc + n] = __builtin_bit_cast(uint16_t, elem<T>::from_f32(r + bn));
+        }
+    }
+}
+
+template <typename T>
+int launch_skinny(const void* a, const void* b, void* c, const void* bias, int M, int N, int K,
+                  int64_t lda, int64_t ldb, int64_t ldc, hipStream_t s) {
+    const dim3 grid(cdiv(N, 2)), block(128);
+    const int nch = K / 8;
+#define PLI_SKINNY(NB)                                                                        \
+    hipLaunchKernelGGL((gemm_skinny_nt<T, NB, 8>), grid, block, 0, s, (const uint16_t*)a,     \
+                       (const uint16_t*)b, (uint16_t*)c, (const uint16_t*)bias, M, N, nch, lda, \
+                       ldb, ldc)
+    if (M <= 1) PLI_SKINNY(1);
+    else if (M <= 2) PLI_SKINNY(2);
+    else if (M <= 4) PLI_SKINNY(4);
+    else if (M <= 8) PLI_SKINNY(8);
+    else PLI_SKINNY(16);
+#undef PLI_SKINNY
+    return launch_status("gemm_skinny_nt");
+}
+
+// ---------------------------------------------------------------------------
+// Small-M NT path (16 < M <= 128 decode batches / short prefill chunks):
+// C^T[16 W rows][M] = W[16 rows, K] . X^T on v_mfma_f32_16x16x32.  One
+// workgroup per 16 W rows (N/16 workgroups: 256 at N=4096, one per CU), K
+// split over its 4 waves; W fragments (16 rows x 64 B per wave-instruction)
+// are streamed from HBM exactly once and feed NBG MFMAs (one per 16 batch
+// rows), X fragments come from L2.  Partial C^T tiles are summed through LDS.
+template <typename T, int NBG, bool BIAS>
+__global__ __launch_bounds__(256) void gemm_smallm_nt(const uint16_t* __restrict__ X,
+                                                      const uint16_t* __restrict__ W,
+                                                      uint16_t* __restrict__ C,
+                                                      const uint16_t* __restrict__ bias, int M,
+                                                      int N, int K, int64_t ldx, int64_t ldw,
+                                                      int64_t ldc) {
+    constexpr int U = 8;  // k-steps issued ahead per wave (8 KiB of W in flight)
+    __shared__ __attribute__((aligned(16))) float part[4][NBG][4][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int n0 = blockIdx.x * 16;
+    const int r16 = lane & 15, kq = 8 * (lane >> 4);
+    const int kw = K / 4;  // this wave's K range
+    const uint16_t* wp = W + (int64_t)min(n0 + r16, N - 1) * ldw + wave * kw + kq;
+    const uint16_t* xp[NBG];
+#pragma unroll
+    for (int gi = 0; gi < NBG; ++gi)
+        xp[gi] = X + (int64_t)min(gi * 16 + r16, M - 1) * ldx + wave * kw + kq;
+    f32x4 acc[NBG];
+#pragma unroll
+    for (int gi = 0; gi < NBG; ++gi) acc[gi] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int k0 = 0;
+    for (; k0 + 32 * U <= kw; k0 += 32 * U) {
+        i32x4 wf[U], xf[U][NBG];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            wf[u] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wp + k0 + 32 * u));
+#pragma unroll
+            for (int gi = 0; gi < NBG; ++gi)
+                xf[u][gi] = *reinterpret_cast<const i32x4*>(xp[gi] + k0 + 32 * u);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int gi = 0; gi < NBG; ++gi) acc[gi] = mfma16x16x32<T>(wf[u], xf[u][gi], acc[gi]);
+    }
+    for (; k0 < kw; k0 += 32) {  // remainder k-steps (kw % 32 == 0)
+        const i32x4 wf = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wp + k0));
+#pragma unroll
+        for (int gi = 0; gi < NBG; ++gi)
+            acc[gi] = mfma16x16x32<T>(wf, *reinterpret_cast<const i32x4*>(xp[gi] + k0), acc[gi]);
+    }
+#pragma unroll
+    for (int gi = 0; gi < NBG; ++gi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) part[wave][gi][r][lane] = acc[gi][r];
+    __syncthreads();
+    // wave w reduces batch groups gi = w, w+4, ...; lane (col = batch, rows 4q..4q+3 = W rows)
+    for (int gi = wave; gi < NBG; gi += 4) {
+        const int bt = gi * 16 + r16;
+        const int nr = n0 + 4 * (lane >> 4);
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            v[r] = part[0][gi][r][lane] + part[1][gi][r][lane] + part[2][gi][r][lane] +
+                   part[3][gi][r][lane];
+        if (bt < M && nr < N) {
+            if constexpr (BIAS) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] += elem<T>::to_f32(T{bias[nr + r]});
+            }
+            *reinterpret_cast<i32x2*>(C + (int64_t)bt * ldc + nr) =
+                i32x2{(int)pack2<T>(v[0], v[1]), (int)pack2<T>(v[2], v[3])};
+        }
+    }
+}
+
+template <typename T>
+int launch_smallm(const void* a, const void* b, void* c, const void* bias, int M, int N, int K,
+                  int64_t lda, int64_t ldb, int64_t ldc, hipStream_t s) {
+    const dim3 grid(cdiv(N, 16)), block(256);
+#define PLI_SMALLM(G)                                                                          \
+    do {                                                                                       \
+        if (bias)                                                                              \
+            hipLaunchKernelGGL((gemm_smallm_nt<T, G, true>), grid, block, 0, s,                \
+                               (const uint16_t*)a, (const uint16_t*)b, (uint16_t*)c,           \
+                               (const uint16_t*)bias, M, N, K, lda, ldb, ldc);                 \
+        else                                                                                   \
+            hipLaunchKernelGGL((gemm_smallm_nt<T, G, false>), grid, block, 0, s,               \
+                               (const uint16_t*)a, (const uint16_t*)b, (uint16_t*)c,           \
+                               (const uint16_t*)bias, M, N, K, lda, ldb, ldc);                 \
+    } while (0)
+    if (M <= 16) PLI_SMALLM(1);
+    else if (M <= 32) PLI_SMALLM(2);
+    else if (M <= 64) PLI_SMALLM(4);
+    else PLI_SMALLM(8);
+#undef PLI_SMALLM
+    return launch_status("gemm_smallm_nt");
+}
+
 template <typename T>
 int launch_mfma(const void* a, const void* b, void* c, const void* bias, int M, int N, int K,
                 int64_t lda, int64_t ldb, int64_t ldc, int trans_b, hipStream_t s) {
@@ -293,6 +467,23 @@ extern "C" int pli_gemm(const void* a, const void* b, void* c, const void* bias,
     const bool vec = (dtype == PLI_BF16 || dtype == PLI_F16) && k % 8 == 0 && n % 8 == 0 &&
                      lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0 && al16(a) && al16(b) &&
                      al16(c) && (bias == nullptr || ((uintptr_t)bias & 7) == 0);
+    // decode batches: W streamed once.  M == 1: GEMV-style VALU kernel;
+    // M <= 128 (K a multiple of 128, N of 16): small-M MFMA kernel.
+    if (vec && trans_b && m == 1) {
+        if (dtype == PLI_BF16)
+            return launch_skinny<bf16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, s);
+        return launch_skinny<f16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, s);
+    }
+    if (vec && trans_b && m <= 128 && k % 128 == 0 && n % 16 == 0) {
+        if (dtype == PLI_BF16)
+            return launch_smallm<bf16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, s);
+        return launch_smallm<f16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, s);
+    }
+    if (vec && trans_b && m <= 16) {
+        if (dtype == PLI_BF16)
+            return launch_skinny<bf16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, s);
+        return launch_skinny<f16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, s);
+    }
     if (vec) {
         if (dtype == PLI_BF16)
             return launch_mfma<bf16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, s);

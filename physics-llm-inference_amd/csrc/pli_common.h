@@ -94,6 +94,21 @@ __device__ __forceinline__ f32x16 mfma32x32x16<f16_t>(i32x4 a, i32x4 b, f32x16 c
                                                   __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
 }
 
+// D(16x16,f32) += A(16x32) * B(32x16): lane l holds A[l&15][8(l>>4)+j],
+// B[8(l>>4)+j][l&15]; D col = l&15, row = 4(l>>4) + reg.
+template <typename T>
+__device__ __forceinline__ f32x4 mfma16x16x32(i32x4 a, i32x4 b, f32x4 c);
+template <>
+__device__ __forceinline__ f32x4 mfma16x16x32<bf16_t>(i32x4 a, i32x4 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                   __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+template <>
+__device__ __forceinline__ f32x4 mfma16x16x32<f16_t>(i32x4 a, i32x4 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+
 // ------------------------------------------------------------ LDS access --
 typedef __attribute__((address_space(3))) void lds_void;
 

@@ -197,7 +197,13 @@ def test_gemv_strided_rows():
     (512, 512, 512, "bf16", False), (512, 512, 512, "bf16", True),
     (300, 264, 200, "bf16", False), (300, 264, 200, "fp16", True),
     (129, 72, 64, "bf16", True), (64, 64, 64, "fp32", False), (100, 60, 70, "fp32", True),
-    (8, 4096, 4096, "bf16", True), (1, 256, 512, "bf16", False), (77, 77, 13, "bf16", False)])
+    (8, 4096, 4096, "bf16", True), (1, 256, 512, "bf16", False), (77, 77, 13, "bf16", False),
+    # decode batches (skinny NT path, M <= 16)
+    (1, 4096, 4096, "bf16", True), (3, 264, 520, "bf16", True), (5, 1000, 4096, "fp16", True),
+    (16, 512, 8192, "bf16", True), (12, 96, 64, "fp16", True),
+    # small-M MFMA NT path (M <= 128, K % 512 == 0, N % 16 == 0)
+    (8, 4096, 4096, "fp16", True), (17, 1024, 1024, "bf16", True), (33, 528, 2048, "bf16", True),
+    (64, 4096, 4096, "bf16", True), (100, 256, 512, "fp16", True), (128, 1024, 1536, "bf16", True)])
 def test_gemm_vs_oracle(m, n, k, dt, tb):
     import pli_hip
     a = seeded_normal((m, k), 10 + m, dt)
@@ -207,12 +213,20 @@ def test_gemm_vs_oracle(m, n, k, dt, tb):
     assert_lin_close(c, ref, dt, f"gemm {m}x{n}x{k} {dt} tb={tb}")
 
 
-def test_gemm_bias_epilogue():
+@pytest.mark.parametrize("m", [192, 4, 48])
+def test_gemm_bias_epilogue(m):
     import pli_hip
-    a, w = seeded_normal((192, 256), 1, "bf16"), seeded_normal((136, 256), 2, "bf16")
-    bias = seeded_normal((136,), 3, "bf16")
+    a, w = seeded_normal((m, 512), 1, "bf16"), seeded_normal((144, 512), 2, "bf16")
+    bias = seeded_normal((144,), 3, "bf16")
     c = pli_hip.gemm(dev(a, "bf16"), dev(w, "bf16"), trans_b=True, bias=dev(bias, "bf16"))
     assert_lin_close(c, olin.linear(a, w, bias), "bf16", "bias")
+
+
+def test_batched_gemv_benchmark_api():
+    """ch03.benchmark_batched_gemv runs the HIP skinny path end to end."""
+    from ch03 import benchmark_batched_gemv
+    r = benchmark_batched_gemv(4, 1024, 1024, dtype=torch.bfloat16, warmup=2, iterations=5)
+    assert r.batch_size == 4 and r.mean_us > 0 and r.tokens_per_second > 0
 
 
 def test_gemm_4096_cube_rows():

@@ -137,6 +137,32 @@ def tune_gemv_sweep():
     print(json.dumps({"kernel": "empty_launch", "us": t * 1e3}), flush=True)
 
 
+def tune_bgemv():
+    """x @ W^T for decode batches: HIP (skinny <= 16, MFMA tile above) vs torch."""
+    m = k = 4096
+    copies = 24
+    ws = [torch.randn(m, k, device="cuda", dtype=torch.bfloat16) for _ in range(copies)]
+    for bsz in (1, 2, 4, 8, 16, 32, 64):
+        x = torch.randn(bsz, k, device="cuda", dtype=torch.bfloat16)
+        y = torch.empty(bsz, m, device="cuda", dtype=torch.bfloat16)
+        graphs = {}
+        for name, fn in (("hip", lambda w: pli_hip.gemm(x, w, trans_b=True, out=y)),
+                         ("torch", lambda w: torch.matmul(x, w.t(), out=y))):
+            for w in ws:
+                fn(w)
+            torch.cuda.synchronize()
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr):
+                for w in ws:
+                    fn(w)
+            graphs[name] = gr
+        t = interleave({n: g.replay for n, g in graphs.items()}, 5, 3)
+        nbytes = (m * k + bsz * (m + k)) * 2
+        print(json.dumps({"kernel": "batched_gemv", "batch": bsz,
+                          **{f"{n}_us": t[n][0] * 1e3 / copies for n in t},
+                          **{f"{n}_GB/s": nbytes / (t[n][0] * 1e-3 / copies) / 1e9 for n in t}}), flush=True)
+
+
 def tune_hbm():
     for nbytes in (1 << 28, 1 << 30):
         n = nbytes // 4
@@ -168,6 +194,8 @@ if __name__ == "__main__":
         tune_hbm()
     if "gemv" in what:
         tune_gemv()
+    if "bgemv" in what:
+        tune_bgemv()
     if "gemvsweep" in what:
         tune_gemv_sweep()
     if "flash" in what:
