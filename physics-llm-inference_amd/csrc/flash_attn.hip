@@ -1216,6 +1216,229 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v5(
 }
 
 // --------------------------------------------------------------------------
+// attn_fwd_v6: v2's structure on v_mfma_f32_16x16x32 (the shape MI355X holds
+// a higher clock on under load).  Each wave owns 32 query rows as two 16-row
+// blocks, so every K and V^T fragment read from LDS feeds two MFMAs.
+//   S^T[16 keys][16 q] = K[16 keys, 32 d] . Q^T : lane l holds query row l&15
+//      of its block and keys 4(l>>4)+r (r = 0..3) of each 16-key block;
+//   P^T fragment of a 32-key k-step s = the S registers of key blocks 2s and
+//      2s+1 (k order permuted: j<4 -> key 32s+4g+j, j>=4 -> 32s+16+4g+j-4),
+//      V^T fragment = two ds_read_b64_tr_b16 of the same permuted rows.
+// V rows are padded to 2D+32 B so the 8 rows x 32 B of a half-wave's
+// transposed read cover all 64 banks.
+template <int D> struct PadLayout16 {
+    static constexpr int KS = 2 * D + 16;
+    static constexpr int VS = 2 * D + 32;
+    static constexpr int KSZ = KT * KS, VSZ = KT * VS, BUF = KSZ + VSZ;
+};
+
+template <typename T, int D>
+__global__ __launch_bounds__(512, 2) void attn_fwd_v6(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
+    const uint16_t* __restrict__ v, uint16_t* __restrict__ o, int H, int group,
+    int Nq, int Nk, AttnStrides st, float c, int causal, int qblocks,
+    int nblocks) {
+    using L = PadLayout16<D>;
+    constexpr int NW = 8, NT = 512;
+    constexpr int CPR = D / 8;
+    constexpr int RPI = NT / CPR;
+    constexpr int CPT = KT / RPI;
+    constexpr int KSTEPS = D / 32;  // 32-d k-steps of QK^T
+    constexpr int DB = D / 16;      // 16-d output blocks
+    static_assert(NT % CPR == 0 && KT % RPI == 0, "staging must tile evenly");
+    __shared__ __attribute__((aligned(16))) char smem[2 * L::BUF];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int l16 = lane & 15, g = lane >> 4;
+    const int lb = xcd_remap(blockIdx.x, nblocks);
+    const int bh = lb / qblocks;
+    const int qblk = causal ? qblocks - 1 - lb % qblocks : lb % qblocks;
+    const int b = bh / H, hq = bh % H, hk = hq / group;
+    const int qbase = qblk * (NW * QW);
+    const int q0 = qbase + wave * QW;
+    const int off_diag = Nk - Nq;
+
+    const uint16_t* qp = q + b * st.qb + hq * st.qh;
+    const uint16_t* kp = k + b * st.kb + hk * st.kh;
+    const uint16_t* vp = v + b * st.vb + hk * st.vh;
+
+    // Q^T fragments: block qb, k-step ks: Q[q0+16qb+l16][32ks+8g .. +7]
+    i32x4 qf[2][KSTEPS];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+        const int qr = q0 + 16 * qb + l16;
+        const bool ok = qr < Nq;
+        const uint16_t* src = qp + (int64_t)(ok ? qr : 0) * st.qn + 8 * g;
+#pragma unroll
+        for (int ks = 0; ks < KSTEPS; ++ks) {
+            const i32x4 x = *reinterpret_cast<const i32x4*>(src + 32 * ks);
+            qf[qb][ks] = ok ? x : i32x4{0, 0, 0, 0};
+        }
+    }
+
+    int kv_end = Nk;
+    if (causal) kv_end = min(Nk, qbase + NW * QW + off_diag);
+    const int nt = kv_end > 0 ? cdiv(kv_end, KT) : 0;
+    const int t_full = Nk / KT;
+    int t_mask = t_full;
+    if (causal) t_mask = min(t_mask, max(0, (q0 + off_diag + 1) / KT));
+
+    const int srow = tid / CPR, sch = tid % CPR;
+    const uint16_t* kg = kp + (int64_t)srow * st.kn + sch * 8;
+    const uint16_t* vg = vp + (int64_t)srow * st.vn + sch * 8;
+    const int kw = srow * L::KS + sch * 16, vw = L::KSZ + srow * L::VS + sch * 16;
+    i32x4 kst[CPT], vst[CPT];
+    auto load_tile = [&](int t) {
+        if (t < t_full) {
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) {
+                const int64_t r = (int64_t)t * KT + i * RPI;
+                kst[i] = *reinterpret_cast<const i32x4*>(kg + r * st.kn);
+                vst[i] = *reinterpret_cast<const i32x4*>(vg + r * st.vn);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) {
+                const int key = t * KT + i * RPI + srow;
+                const int64_t r = min(key, Nk - 1) - srow;
+                const i32x4 kx = *reinterpret_cast<const i32x4*>(kg + r * st.kn);
+                const i32x4 vx = *reinterpret_cast<const i32x4*>(vg + r * st.vn);
+                kst[i] = key < Nk ? kx : i32x4{0, 0, 0, 0};
+                vst[i] = key < Nk ? vx : i32x4{0, 0, 0, 0};
+            }
+        }
+    };
+    auto store_tile = [&](int buf) {
+        char* base = smem + buf * L::BUF;
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+            lds_write_b128(base, kw + i * RPI * L::KS, kst[i]);
+            lds_write_b128(base, vw + i * RPI * L::VS, vst[i]);
+        }
+    };
+
+    const int qq = l16 >> 2, pp = lane & 3;
+    const int kr = l16 * L::KS + g * 16;                                  // K: key l16, chunk g
+    const int vr = L::KSZ + (4 * g + qq) * L::VS + 8 * pp;                 // V: key 4g+qq, col 4pp
+
+    f32x4 oacc[2][DB];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int d = 0; d < DB; ++d) oacc[qb][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m_run[2] = {-1e30f, -1e30f}, l_run[2] = {0.f, 0.f};
+
+    if (nt > 0) {
+        load_tile(0);
+        store_tile(0);
+    }
+    __syncthreads();
+
+    for (int t = 0; t < nt; ++t) {
+        if (t + 1 < nt) load_tile(t + 1);
+        const char* kb = smem + (t & 1) * L::BUF + kr;
+        const char* vb = smem + (t & 1) * L::BUF + vr;
+
+        f32x4 s[2][4];  // [q block][16-key block]
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+            for (int kb2 = 0; kb2 < 4; ++kb2) s[qb][kb2] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kb2 = 0; kb2 < 4; ++kb2)
+#pragma unroll
+            for (int ks = 0; ks < KSTEPS; ++ks) {
+                const i32x4 kf = lds_read_b128(kb, kb2 * 16 * L::KS + ks * 64);
+                s[0][kb2] = mfma16x16x32<T>(kf, qf[0][ks], s[0][kb2]);
+                s[1][kb2] = mfma16x16x32<T>(kf, qf[1][ks], s[1][kb2]);
+            }
+
+        if (t >= t_mask) {
+#pragma unroll
+            for (int qb = 0; qb < 2; ++qb) {
+                const int lim = causal ? q0 + 16 * qb + l16 + off_diag : Nk;
+#pragma unroll
+                for (int kb2 = 0; kb2 < 4; ++kb2)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int key = t * KT + 16 * kb2 + 4 * g + r;
+                        if (key >= Nk || key > lim) s[qb][kb2][r] = -INFINITY;
+                    }
+            }
+        }
+
+        i32x4 pb[2][2];
+        float alpha[2];
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+            float mx = max3(s[qb][0][0], s[qb][0][1], s[qb][0][2]);
+            float my = max3(s[qb][0][3], s[qb][1][0], s[qb][1][1]);
+            mx = max3(mx, s[qb][1][2], s[qb][1][3]);
+            my = max3(my, s[qb][2][0], s[qb][2][1]);
+            mx = max3(mx, s[qb][2][2], s[qb][2][3]);
+            my = max3(my, s[qb][3][0], s[qb][3][1]);
+            mx = max3(mx, s[qb][3][2], s[qb][3][3]);
+            mx = fmaxf(mx, my);
+            mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+            const float m_new = fmaxf(m_run[qb], mx * c);
+            alpha[qb] = __builtin_amdgcn_exp2f(m_run[qb] - m_new);
+            m_run[qb] = m_new;
+            float rs0 = 0.f, rs1 = 0.f;
+#pragma unroll
+            for (int kb2 = 0; kb2 < 4; ++kb2)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float pv = __builtin_amdgcn_exp2f(fmaf(s[qb][kb2][r], c, -m_new));
+                    s[qb][kb2][r] = pv;
+                    if (r & 1) rs1 += pv; else rs0 += pv;
+                }
+            l_run[qb] = fmaf(l_run[qb], alpha[qb], rs0 + rs1);
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2)
+                pb[qb][s2] = i32x4{(int)pack2<T>(s[qb][2 * s2][0], s[qb][2 * s2][1]),
+                                   (int)pack2<T>(s[qb][2 * s2][2], s[qb][2 * s2][3]),
+                                   (int)pack2<T>(s[qb][2 * s2 + 1][0], s[qb][2 * s2 + 1][1]),
+                                   (int)pack2<T>(s[qb][2 * s2 + 1][2], s[qb][2 * s2 + 1][3])};
+#pragma unroll
+            for (int d = 0; d < DB; ++d) oacc[qb][d] *= alpha[qb];
+        }
+
+#pragma unroll
+        for (int d = 0; d < DB; ++d)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const int ro = 32 * s2 * L::VS + d * 32;
+                const i32x2 lo = lds_read_tr16(vb, ro);
+                const i32x2 hi = lds_read_tr16(vb, ro + 16 * L::VS);
+                const i32x4 vf = {lo.x, lo.y, hi.x, hi.y};
+                oacc[0][d] = mfma16x16x32<T>(vf, pb[0][s2], oacc[0][d]);
+                oacc[1][d] = mfma16x16x32<T>(vf, pb[1][s2], oacc[1][d]);
+            }
+
+        if (t + 1 < nt) store_tile((t + 1) & 1);
+        __syncthreads();
+    }
+
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+        float l = l_run[qb] + __shfl_xor(l_run[qb], 16, 64);
+        l += __shfl_xor(l, 32, 64);
+        const float inv = l > 0.f ? 1.f / l : 0.f;
+        const int qr = q0 + 16 * qb + l16;
+        if (qr < Nq) {
+            uint16_t* op = o + b * st.ob + hq * st.oh + (int64_t)qr * st.on;
+#pragma unroll
+            for (int d = 0; d < DB; ++d) {
+                const f32x4 a = oacc[qb][d];
+                *reinterpret_cast<i32x2*>(op + d * 16 + 4 * g) =
+                    i32x2{(int)pack2<T>(a[0] * inv, a[1] * inv), (int)pack2<T>(a[2] * inv, a[3] * inv)};
+            }
+        }
+    }
+}
+
+// --------------------------------------------------------------------------
 // attn_fwd_v3: v2 with the two waves of each SIMD staggered.  A workgroup's
 // waves w and w+4 share a SIMD; in v2 both run QK^T-MFMA, softmax-VALU,
 // PV-MFMA in lockstep between barriers, so the SIMD alternates between a
@@ -1559,6 +1782,7 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
 //   9: attn_fwd_v4 + sched_group_barrier interleave  10: same, reads 3 ahead
 //  11: attn_fwd_v5 (64 rows/wave, 1 wave/SIMD)  12: v5 + sched_group_barrier
 //  13: v5 with LDS-DMA staging                  14: v5 + DMA + sched_group_barrier
+//  15: attn_fwd_v6 (v2 structure on 16x16x32 MFMA, 8 waves)
 constexpr int kDefaultVariant = 2;
 
 template <typename T, int D>
@@ -1596,6 +1820,8 @@ int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int
         case 11: PLI_ATTN_V5(0, false); break;
         case 12: PLI_ATTN_V5(1, false); break;
         case 13: PLI_ATTN_V5(0, true); break;
+        case 15: hipLaunchKernelGGL((attn_fwd_v6<T, D>), grid, dim3(512), 0, stream, qq, kk, vv, oo,
+                                    H, group, Nq, Nk, st, c, causal, qblocks, (int)nb); break;
         case 14: PLI_ATTN_V5(1, true); break;
 #undef PLI_ATTN_V5
         default:

@@ -104,6 +104,24 @@ def test_flash_vs_oracle(case):
     assert_attn_close(out, ref, dt, str(case))
 
 
+# every MFMA variant (alternates A/B-tested by tools/tune.py) on the MFMA-eligible cases
+MFMA_VARIANTS = (0, 1, 2, 3, 8, 15)
+
+
+@pytest.mark.parametrize("variant", MFMA_VARIANTS)
+@pytest.mark.parametrize("case", [c for c in CASES if c[6] != "fp32" and c[5] in (64, 128)],
+                         ids=lambda c: "b{}h{}kv{}q{}k{}d{}_{}{}".format(*c[:7], "_causal" if c[7] else ""))
+def test_flash_variants_vs_oracle(case, variant):
+    import pli_hip
+    B, H, Hkv, Nq, Nk, D, dt, causal = case
+    seed = zlib.crc32(repr(case).encode()) % 1000
+    q = seeded_normal((B, H, Nq, D), seed, dt)
+    k = seeded_normal((B, Hkv, Nk, D), seed + 1, dt)
+    v = seeded_normal((B, Hkv, Nk, D), seed + 2, dt)
+    out = pli_hip.flash_attn_fwd(dev(q, dt), dev(k, dt), dev(v, dt), causal=causal, variant=variant)
+    ref = oatt.naive_attention(q, k, v, causal=causal)
+    assert_attn_close(out, ref, dt, f"{case} variant {variant}")
+
 def test_flash_strided_views_and_out_param():
     """Non-contiguous [B,H,S,hd] views (the MHA layout) read/written in place."""
     import pli_hip
