@@ -281,7 +281,30 @@ template <int D> struct PadLayout {
     static constexpr int KSZ = KT * KS, VSZ = KT * VS, BUF = KSZ + VSZ;
 };
 
-template <typename T, int D, int NW, bool LAZY>
+// OPT bits (A/B levers on the v2 body, variants 16-20):
+//  1: the xor-32 row-max exchange as v_permlane32_swap instead of ds_bpermute
+//  2: static s_setprio 1 for the younger half of the workgroup (waves NW/2..)
+//  4: defer-max: keep the running max unless a tile raises it by > 8 (log2
+//     units), so P <= 2^8 and the O rescale almost never runs after tile 0
+//  8: row sum over the bf16/f16-ROUNDED P (v_dot2c with {1,1}), so l
+//     normalises exactly the weights P.V used.  Needed with 4: a dominant
+//     weight is no longer exactly 1 and its rounding would otherwise go
+//     uncorrected (measured 1.05e-2 on the spike test without it).
+// 16: epilogue: pair the two half-waves' 8-byte pieces of a row with
+//     v_permlane32_swap so each lane stores 16 B (8 dwordx4 instead of 16 dwordx2)
+constexpr int kOptPermlane = 1, kOptPrio = 2, kOptDefer = 4, kOptRoundedSum = 8, kOptWideStore = 16;
+constexpr float kDeferThr = 8.f;
+
+__device__ __forceinline__ float xor32_max(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xor32_sum(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+template <typename T, int D, int NW, bool LAZY, int OPT = 0>
 __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_v2(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
     const uint16_t* __restrict__ v, uint16_t* __restrict__ o, int H, int group,
@@ -382,6 +405,9 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_v2(
         store_tile(0);
     }
     __syncthreads();
+    if constexpr ((OPT & kOptPrio) != 0) {
+        if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+    }
 
     for (int t = 0; t < nt; ++t) {
         if (t + 1 < nt) load_tile(t + 1);
@@ -419,8 +445,10 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_v2(
             my = max3(my, s[0][r + 1], s[1][r + 1]);
         }
         mx = max3(mx, my, max3(s[0][15], s[1][15], mx));
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        const float m_new = fmaxf(m_run, mx * c);
+        if constexpr ((OPT & kOptPermlane) != 0) mx = xor32_max(mx);
+        else mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        float m_new = fmaxf(m_run, mx * c);
+        if constexpr ((OPT & kOptDefer) != 0) m_new = mx * c > m_run + kDeferThr ? m_new : m_run;
         const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
         m_run = m_new;
         float rs = 0.f;
@@ -430,9 +458,9 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_v2(
             for (int r = 0; r < 16; ++r) {
                 const float p = __builtin_amdgcn_exp2f(fmaf(s[tt][r], c, -m_new));
                 s[tt][r] = p;
-                rs += p;
+                if constexpr ((OPT & kOptRoundedSum) == 0) rs += p;
             }
-        l_run = fmaf(l_run, alpha, rs);
+        if constexpr ((OPT & kOptRoundedSum) == 0) l_run = fmaf(l_run, alpha, rs);
         if (!LAZY || __ballot(alpha != 1.f)) {
 #pragma unroll
             for (int d = 0; d < D / 32; ++d)
@@ -451,6 +479,19 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_v2(
                                    (int)pack2<T>(s[tt][r0 + 4], s[tt][r0 + 5]),
                                    (int)pack2<T>(s[tt][r0 + 6], s[tt][r0 + 7])};
             }
+        if constexpr ((OPT & kOptRoundedSum) != 0) {
+            float r0 = 0.f, r1 = 0.f;
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    r0 = add_pair<T>((uint32_t)pb[tt][s2][0], r0);
+                    r1 = add_pair<T>((uint32_t)pb[tt][s2][1], r1);
+                    r0 = add_pair<T>((uint32_t)pb[tt][s2][2], r0);
+                    r1 = add_pair<T>((uint32_t)pb[tt][s2][3], r1);
+                }
+            l_run = fmaf(l_run, alpha, r0 + r1);
+        }
 #pragma unroll
         for (int dblk = 0; dblk < D / 32; ++dblk)
 #pragma unroll
@@ -467,20 +508,43 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_v2(
         __syncthreads();
     }
 
-    const float l = l_run + __shfl_xor(l_run, 32, 64);
+    if constexpr ((OPT & kOptPrio) != 0) __builtin_amdgcn_s_setprio(0);
+    float l;
+    if constexpr ((OPT & kOptPermlane) != 0) l = xor32_sum(l_run);
+    else l = l_run + __shfl_xor(l_run, 32, 64);
     const float inv = l > 0.f ? 1.f / l : 0.f;
     const int qr = q0 + l32;
     if (qr < Nq) {
         uint16_t* op = o + b * st.ob + hq * st.oh + (int64_t)qr * st.on;
+        if constexpr ((OPT & kOptWideStore) != 0) {
+            // group k = 4*dblk + i holds columns 8k+4*h32 .. +3 of row qr; after
+            // swapping (k, k+1): lower lanes hold cols 8k..8k+7, upper 8k+8..8k+15
 #pragma unroll
-        for (int dblk = 0; dblk < D / 32; ++dblk)
+            for (int dblk = 0; dblk < D / 32; ++dblk)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int d = dblk * 32 + 8 * i + 4 * h32;
-                const i32x2 w = {(int)pack2<T>(oacc[dblk][4 * i] * inv, oacc[dblk][4 * i + 1] * inv),
-                                 (int)pack2<T>(oacc[dblk][4 * i + 2] * inv, oacc[dblk][4 * i + 3] * inv)};
-                *reinterpret_cast<i32x2*>(op + d) = w;
-            }
+                for (int i = 0; i < 4; i += 2) {
+                    const f32x16& a = oacc[dblk];
+                    uint32_t ax = pack2<T>(a[4 * i] * inv, a[4 * i + 1] * inv);
+                    uint32_t ay = pack2<T>(a[4 * i + 2] * inv, a[4 * i + 3] * inv);
+                    uint32_t bx = pack2<T>(a[4 * i + 4] * inv, a[4 * i + 5] * inv);
+                    uint32_t by = pack2<T>(a[4 * i + 6] * inv, a[4 * i + 7] * inv);
+                    const auto rx = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
+                    const auto ry = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
+                    const int d = dblk * 32 + 8 * i + 8 * h32;
+                    *reinterpret_cast<i32x4*>(op + d) =
+                        i32x4{(int)rx[0], (int)ry[0], (int)rx[1], (int)ry[1]};
+                }
+        } else {
+#pragma unroll
+            for (int dblk = 0; dblk < D / 32; ++dblk)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int d = dblk * 32 + 8 * i + 4 * h32;
+                    const i32x2 w = {(int)pack2<T>(oacc[dblk][4 * i] * inv, oacc[dblk][4 * i + 1] * inv),
+                                     (int)pack2<T>(oacc[dblk][4 * i + 2] * inv, oacc[dblk][4 * i + 3] * inv)};
+                    *reinterpret_cast<i32x2*>(op + d) = w;
+                }
+        }
     }
 }
 
@@ -1783,13 +1847,22 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
 //  11: attn_fwd_v5 (64 rows/wave, 1 wave/SIMD)  12: v5 + sched_group_barrier
 //  13: v5 with LDS-DMA staging                  14: v5 + DMA + sched_group_barrier
 //  15: attn_fwd_v6 (v2 structure on 16x16x32 MFMA, 8 waves)
-constexpr int kDefaultVariant = 2;
+//  16-20: v2 NW8 with OPT levers 1 (permlane max), 2 (younger-half prio),
+//         4 (defer-max), 7 (all), 5 (permlane + defer)
+//  21-23: v2 NW8 OPT 13 (permlane + defer + rounded sum), 12 (defer + rounded
+//         sum), 9 (permlane + rounded sum)
+//  24: variant 21 + epilogue stores widened to dwordx4 (OPT 16)
+//  (16 waves x 32 rows was tried: needs <= 128 VGPRs and spills 296 B/lane)
+// default: v2 NW8 + permlane row max + defer-max (THR 8, log2) + rounded-P row sum
+// (1057 TF vs 983 for plain v2 at B8 H32 S4096 D128; spike + variant parity green)
+constexpr int kDefaultVariant = 21;
 
 template <typename T, int D>
 int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int H,
                 int group, int Nq, int Nk, const AttnStrides& st, float scale,
                 int causal, hipStream_t stream, int variant) {
-    const int nw = (variant == 2 || variant >= 4) ? 8 : 4;  // v5 (11-14): 4 waves x 64 rows
+    // v5 (11-14): 4 waves x 64 rows; 24: 16 waves x 32 rows
+    const int nw = (variant == 2 || variant >= 4) ? 8 : 4;
     const int qblocks = cdiv(Nq, nw * QW);
     const int64_t nb = (int64_t)B * H * qblocks;
     PLI_REQUIRE(nb < (1ll << 31), "pli_flash_attn_fwd: grid too large");
@@ -1820,6 +1893,15 @@ int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int
         case 11: PLI_ATTN_V5(0, false); break;
         case 12: PLI_ATTN_V5(1, false); break;
         case 13: PLI_ATTN_V5(0, true); break;
+        case 16: PLI_ATTN_LAUNCH((attn_fwd_v2<T, D, 8, true, 1>)); break;
+        case 17: PLI_ATTN_LAUNCH((attn_fwd_v2<T, D, 8, true, 2>)); break;
+        case 18: PLI_ATTN_LAUNCH((attn_fwd_v2<T, D, 8, true, 4>)); break;
+        case 19: PLI_ATTN_LAUNCH((attn_fwd_v2<T, D, 8, true, 7>)); break;
+        case 20: PLI_ATTN_LAUNCH((attn_fwd_v2<T, D, 8, true, 5>)); break;
+        case 21: PLI_ATTN_LAUNCH((attn_fwd_v2<T, D, 8, true, 13>)); break;
+        case 22: PLI_ATTN_LAUNCH((attn_fwd_v2<T, D, 8, true, 12>)); break;
+        case 23: PLI_ATTN_LAUNCH((attn_fwd_v2<T, D, 8, true, 9>)); break;
+        case 24: PLI_ATTN_LAUNCH((attn_fwd_v2<T, D, 8, true, 29>)); break;
         case 15: hipLaunchKernelGGL((attn_fwd_v6<T, D>), grid, dim3(512), 0, stream, qq, kk, vv, oo,
                                     H, group, Nq, Nk, st, c, causal, qblocks, (int)nb); break;
         case 14: PLI_ATTN_V5(1, true); break;

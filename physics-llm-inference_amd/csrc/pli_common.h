@@ -79,6 +79,20 @@ template <> __device__ __forceinline__ uint32_t pack2<f16_t>(float lo, float hi)
     return __builtin_bit_cast(uint32_t, v);
 }
 
+// acc + lo + hi of a packed pair of T (v_dot2c against {1,1}): sums the
+// values exactly as rounded into the pair.
+template <typename T> __device__ __forceinline__ float add_pair(uint32_t p, float acc);
+template <> __device__ __forceinline__ float add_pair<bf16_t>(uint32_t p, float acc) {
+    typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+    const bf16x2 one = {(__bf16)1.0f, (__bf16)1.0f};
+    return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, p), one, acc, false);
+}
+template <> __device__ __forceinline__ float add_pair<f16_t>(uint32_t p, float acc) {
+    typedef __attribute__((ext_vector_type(2))) _Float16 f16x2;
+    const f16x2 one = {(_Float16)1.0f, (_Float16)1.0f};
+    return __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, p), one, acc, false);
+}
+
 // ------------------------------------------------------------- MFMA glue --
 // D(32x32,f32) += A(32x16) * B(16x32) for 16-bit inputs held as raw words.
 template <typename T>

@@ -105,7 +105,7 @@ def test_flash_vs_oracle(case):
 
 
 # every MFMA variant (alternates A/B-tested by tools/tune.py) on the MFMA-eligible cases
-MFMA_VARIANTS = (0, 1, 2, 3, 8, 15)
+MFMA_VARIANTS = (0, 1, 2, 3, 8, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24)
 
 
 @pytest.mark.parametrize("variant", MFMA_VARIANTS)
@@ -135,8 +135,10 @@ def test_flash_strided_views_and_out_param():
     assert_attn_close(o.transpose(1, 2), ref, "bf16", "strided")
 
 
-def test_flash_forced_rescale_spike():
-    """A key spike in a late tile forces the online max to jump (rule 26)."""
+@pytest.mark.parametrize("variant", [2, 21, 22, 23])
+def test_flash_forced_rescale_spike(variant):
+    """A key spike in a late tile forces the online max to jump past the
+    defer-max threshold (variants 18/19), exercising the rescale branch."""
     import pli_hip
     B, H, N, D = 1, 2, 512, 128
     q = seeded_normal((B, H, N, D), 7, "bf16")
@@ -145,7 +147,7 @@ def test_flash_forced_rescale_spike():
     k[:, :, 450] = np.float32(4.0) * np.sign(q[:, :, 3])  # row 3 jumps at tile 7
     from oracle.numerics import round_to_bf16
     k = round_to_bf16(k)
-    out = pli_hip.flash_attn_fwd(dev(q, "bf16"), dev(k, "bf16"), dev(v, "bf16"))
+    out = pli_hip.flash_attn_fwd(dev(q, "bf16"), dev(k, "bf16"), dev(v, "bf16"), variant=variant)
     assert_attn_close(out, oatt.naive_attention(q, k, v), "bf16", "spike")
 
 

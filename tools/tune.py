@@ -39,7 +39,7 @@ def interleave(fns: dict, iters: int, rounds: int):
     return {k: (float(np.median(v)), float(np.min(v))) for k, v in res.items()}
 
 
-def tune_flash(variants=(2, 15), causal=False, B=8, H=32, S=4096, D=128):
+def tune_flash(variants=(21, 24, 2), causal=False, B=8, H=32, S=4096, D=128):
     from oracle.attention import naive_attention
     g = torch.Generator(device="cuda").manual_seed(0)
     q, k, v = (torch.randn(B, H, S, D, device="cuda", dtype=torch.bfloat16, generator=g) for _ in range(3))
