@@ -22,6 +22,7 @@
 #ifndef PLI_H
 #define PLI_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -117,6 +118,26 @@ int pli_softmax_rows(const void* x, void* y, int64_t rows, int n, int dtype,
 int pli_online_softmax_with_output(const void* x, const void* v, void* o,
                                    void* d, int64_t rows, int n, int dv,
                                    int dtype, void* stream);
+
+/* Decode attention over a KV cache (split-K flash-decoding).
+ * Replaces the decode branch of ch02/kv_cache.py:74-101 (GQAWithCache.forward)
+ * and ch02/cached_generation.py:58-98 (CachedGQA.forward): repeat_interleave
+ * of the cache to Hq heads, matmul, softmax, matmul.
+ * Same operand conventions as pli_flash_attn_fwd (strides[12] in elements,
+ * q/o [B, Hq, n_q, D]-indexed, k/v [B, Hkv, n_kv, D]-indexed; the cache
+ * layout [B, S_max, Hkv, D] is k_b = S_max*Hkv*D, k_h = D, k_n = Hkv*D).
+ * causal masks bottom-right (query i sees keys j <= n_kv - n_q + i), the mask
+ * of ch02/kv_cache.py:91-95.  The fast path takes bf16/fp16, D in {64, 128}
+ * and n_q * Hq/Hkv <= 16 rows per kv head; other shapes run the prefill
+ * kernel.  `workspace` (16-byte aligned, fp32 partials) must hold
+ * pli_attn_decode_workspace_size(...) bytes; NULL when that is 0. */
+size_t pli_attn_decode_workspace_size(int batch, int heads, int kv_heads,
+                                      int n_q, int n_kv, int head_dim);
+int pli_attn_decode(const void* q, const void* k, const void* v, void* o,
+                    int batch, int heads, int kv_heads, int n_q, int n_kv,
+                    int head_dim, const int64_t* strides, float scale,
+                    int causal, void* workspace, size_t workspace_bytes,
+                    int dtype, void* stream);
 
 #ifdef __cplusplus
 }

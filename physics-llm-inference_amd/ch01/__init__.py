@@ -1,5 +1,6 @@
 """Chapter 01 attention on MI355X (the hot-path subset: attention modules)."""
 
+from .gqa import GroupedQueryAttention
 from .attention import (
     MultiHeadAttention,
     SingleHeadAttention,
@@ -7,4 +8,4 @@ from .attention import (
     naive_attention,
 )
 
-__all__ = ["MultiHeadAttention", "SingleHeadAttention", "causal_attention", "naive_attention"]
+__all__ = ["GroupedQueryAttention", "MultiHeadAttention", "SingleHeadAttention", "causal_attention", "naive_attention"]

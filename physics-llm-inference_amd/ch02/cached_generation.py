@@ -1,0 +1,185 @@
+"""Cached generation -- mirror of ``ch02/cached_generation.py``.
+
+Module names, constructor signatures, parameter names and creation order
+follow the reference (``ch02/cached_generation.py:20-201``), so seeded models
+and ``state_dict``s are interchangeable.  On a ROCm device:
+
+* ``CachedGQA`` projects on ``pli_gemm`` and attends over the cache with
+  ``pli_attn_decode`` (split-K flash-decoding in place on the
+  [B, S_max, Hkv, hd] buffer; the prompt goes to the prefill flash kernel
+  through the same entry point), replacing ``:71-94``;
+* ``SwiGLUFFN`` runs gate/up/down on ``pli_gemm``;
+* ``CachedTransformerModel``'s ``lm_head`` runs on ``pli_gemm``.
+Embedding lookup, RMSNorm, residual adds and sampling stay in torch (they
+are not on the measured path).  CPU tensors keep the reference math.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .kv_cache import _proj, attend_cached
+
+
+def _lin(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    return _proj(x, w) if x.is_cuda else F.linear(x, w)
+
+
+@dataclass
+class LayerKVCache:
+    """One layer's cache: k, v [batch, max_seq_len, num_kv_heads, head_dim]."""
+    k: torch.Tensor
+    v: torch.Tensor
+    seq_len: int = 0
+
+    def update(self, k_new: torch.Tensor, v_new: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+        """Append new K/V and return the valid prefixes (``:27-33``)."""
+        n = k_new.shape[1]
+        self.k[:, self.seq_len:self.seq_len + n] = k_new
+        self.v[:, self.seq_len:self.seq_len + n] = v_new
+        self.seq_len += n
+        return self.k[:, :self.seq_len], self.v[:, :self.seq_len]
+
+
+class CachedGQA(nn.Module):
+    def __init__(self, hidden_dim: int, num_heads: int, num_kv_heads: int):
+        super().__init__()
+        self.num_heads = num_heads
+        self.num_kv_heads = num_kv_heads
+        self.num_groups = num_heads // num_kv_heads
+        self.head_dim = hidden_dim // num_heads
+        self.hidden_dim = hidden_dim
+        self.q_proj = nn.Linear(hidden_dim, num_heads * self.head_dim, bias=False)
+        self.k_proj = nn.Linear(hidden_dim, num_kv_heads * self.head_dim, bias=False)
+        self.v_proj = nn.Linear(hidden_dim, num_kv_heads * self.head_dim, bias=False)
+        self.o_proj = nn.Linear(hidden_dim, hidden_dim, bias=False)
+
+    def forward(self, x: torch.Tensor, cache: LayerKVCache | None = None, start_pos: int = 0
+                ) -> torch.Tensor:
+        B, S, _ = x.shape
+        q = _lin(x, self.q_proj.weight).view(B, S, self.num_heads, self.head_dim)
+        k = _lin(x, self.k_proj.weight).view(B, S, self.num_kv_heads, self.head_dim)
+        v = _lin(x, self.v_proj.weight).view(B, S, self.num_kv_heads, self.head_dim)
+        if cache is not None:
+            cache.update(k, v)
+            k_buf, v_buf, n_kv = cache.k, cache.v, cache.seq_len
+        else:
+            k_buf, v_buf, n_kv = k, v, S
+        o = attend_cached(q, k_buf, v_buf, n_kv).reshape(B, S, self.hidden_dim)
+        return _lin(o, self.o_proj.weight)
+
+
+class RMSNorm(nn.Module):
+    def __init__(self, hidden_dim: int, eps: float = 1e-6):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(hidden_dim))
+        self.eps = eps
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return x / torch.sqrt(torch.mean(x ** 2, dim=-1, keepdim=True) + self.eps) * self.weight
+
+
+class SwiGLUFFN(nn.Module):
+    def __init__(self, hidden_dim: int, intermediate_dim: int):
+        super().__init__()
+        self.gate_proj = nn.Linear(hidden_dim, intermediate_dim, bias=False)
+        self.up_proj = nn.Linear(hidden_dim, intermediate_dim, bias=False)
+        self.down_proj = nn.Linear(intermediate_dim, hidden_dim, bias=False)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        h = F.silu(_lin(x, self.gate_proj.weight)) * _lin(x, self.up_proj.weight)
+        return _lin(h, self.down_proj.weight)
+
+
+class CachedTransformerBlock(nn.Module):
+    def __init__(self, hidden_dim: int, num_heads: int, num_kv_heads: int, intermediate_dim: int):
+        super().__init__()
+        self.input_norm = RMSNorm(hidden_dim)
+        self.attn = CachedGQA(hidden_dim, num_heads, num_kv_heads)
+        self.post_attn_norm = RMSNorm(hidden_dim)
+        self.ffn = SwiGLUFFN(hidden_dim, intermediate_dim)
+
+    def forward(self, x: torch.Tensor, cache: LayerKVCache | None = None, start_pos: int = 0
+                ) -> torch.Tensor:
+        h = x + self.attn(self.input_norm(x), cache, start_pos)
+        return h + self.ffn(self.post_attn_norm(h))
+
+
+class CachedTransformerModel(nn.Module):
+    """Decoder-only transformer whose layers append to per-layer KV caches."""
+
+    def __init__(self, vocab_size: int, hidden_dim: int, num_layers: int, num_heads: int,
+                 num_kv_heads: int, intermediate_dim: int):
+        super().__init__()
+        self.embed = nn.Embedding(vocab_size, hidden_dim)
+        self.layers = nn.ModuleList([
+            CachedTransformerBlock(hidden_dim, num_heads, num_kv_heads, intermediate_dim)
+            for _ in range(num_layers)
+        ])
+        self.norm = RMSNorm(hidden_dim)
+        self.lm_head = nn.Linear(hidden_dim, vocab_size, bias=False)
+        self.hidden_dim = hidden_dim
+        self.num_layers = num_layers
+        self.num_kv_heads = num_kv_heads
+        self.head_dim = hidden_dim // num_heads
+
+    def forward(self, input_ids: torch.Tensor, caches: list[LayerKVCache] | None = None,
+                start_pos: int = 0) -> torch.Tensor:
+        x = self.embed(input_ids)
+        for i, layer in enumerate(self.layers):
+            x = layer(x, caches[i] if caches is not None else None, start_pos)
+        return _lin(self.norm(x), self.lm_head.weight)
+
+    def create_caches(self, batch_size: int, max_seq_len: int, device: torch.device,
+                      dtype: torch.dtype) -> list[LayerKVCache]:
+        shape = (batch_size, max_seq_len, self.num_kv_heads, self.head_dim)
+        return [LayerKVCache(k=torch.zeros(shape, device=device, dtype=dtype),
+                             v=torch.zeros(shape, device=device, dtype=dtype), seq_len=0)
+                for _ in range(self.num_layers)]
+
+
+def _sync(device: torch.device) -> None:
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+
+
+def cached_generate(model: CachedTransformerModel, input_ids: torch.Tensor, max_new_tokens: int,
+                    temperature: float = 1.0) -> tuple[torch.Tensor, dict]:
+    """Prefill the prompt once, then decode one token per step over the caches
+    (``ch02/cached_generation.py:204-274``).  Returns the prompt followed by
+    the sampled tokens, and {prefill_ms, decode_ms[], total_ms}."""
+    model.eval()
+    device = input_ids.device
+    dtype = next(model.parameters()).dtype
+    batch_size, prompt_len = input_ids.shape
+    caches = model.create_caches(batch_size, prompt_len + max_new_tokens, device, dtype)
+    timings = {"prefill_ms": 0, "decode_ms": [], "total_ms": 0}
+    out = [input_ids]
+
+    def sample(logits):
+        probs = F.softmax(logits[:, -1, :] / temperature, dim=-1)
+        return torch.multinomial(probs, num_samples=1)
+
+    with torch.no_grad():
+        _sync(device)
+        t0 = time.perf_counter()
+        logits = model(input_ids, caches, start_pos=0)
+        _sync(device)
+        timings["prefill_ms"] = (time.perf_counter() - t0) * 1000
+        token = sample(logits)
+        out.append(token)
+        for i in range(max_new_tokens - 1):
+            _sync(device)
+            t0 = time.perf_counter()
+            logits = model(token, caches, start_pos=prompt_len + i)
+            _sync(device)
+            timings["decode_ms"].append((time.perf_counter() - t0) * 1000)
+            token = sample(logits)
+            out.append(token)
+
+    timings["total_ms"] = timings["prefill_ms"] + sum(timings["decode_ms"])
+    return torch.cat(out, dim=1), timings

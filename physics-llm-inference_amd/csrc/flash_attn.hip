@@ -1929,7 +1929,6 @@ int launch_generic(const void* q, const void* k, const void* v, void* o, int B, 
     return launch_status("attn_fwd_generic");
 }
 
-inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 }  // namespace
 }  // namespace pli

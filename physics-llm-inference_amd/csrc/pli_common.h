@@ -93,6 +93,8 @@ template <> __device__ __forceinline__ float add_pair<f16_t>(uint32_t p, float a
     return __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, p), one, acc, false);
 }
 
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
 // ------------------------------------------------------------- MFMA glue --
 // D(32x32,f32) += A(32x16) * B(16x32) for 16-bit inputs held as raw words.
 template <typename T>

@@ -39,11 +39,17 @@ _SIGS = {
     "pli_scale_copy": [_vp, _vp, _c_i64, _c_int, _vp],
     "pli_softmax_rows": [_vp, _vp, _c_i64, _c_int, _c_int, _vp],
     "pli_online_softmax_with_output": [_vp, _vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_int, _vp],
+    "pli_attn_decode_workspace_size": [_c_int] * 6,
+    "pli_attn_decode": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
+                        ctypes.POINTER(_c_i64), _c_f32, _c_int, _vp, ctypes.c_size_t, _c_int, _vp],
     # tuning entry points (not part of include/pli.h): explicit kernel variant
     "pli_flash_attn_fwd_variant": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int,
                                    _c_int, ctypes.POINTER(_c_i64), _c_f32, _c_int, _c_int, _vp,
                                    _c_int],
     "pli_gemv_variant": [_vp, _vp, _vp, _c_int, _c_int, _c_i64, _c_int, _vp, _c_int],
+    "pli_attn_decode_variant": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
+                                ctypes.POINTER(_c_i64), _c_f32, _c_int, _vp, ctypes.c_size_t,
+                                _c_int, _vp, _c_int, _c_int],
 }
 
 
@@ -67,7 +73,8 @@ def lib() -> ctypes.CDLL:
         for name, argtypes in _SIGS.items():
             fn = getattr(L, name)
             fn.argtypes = argtypes
-            fn.restype = ctypes.c_char_p if name in ("pli_version", "pli_last_error") else _c_int
+            fn.restype = (ctypes.c_char_p if name in ("pli_version", "pli_last_error") else
+                          ctypes.c_size_t if name.endswith("_workspace_size") else _c_int)
         _lib = L
     return _lib
 
@@ -166,6 +173,59 @@ def flash_attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: flo
         else:
             rc = lib().pli_flash_attn_fwd_variant(*args, int(variant))
     _check(rc, "pli_flash_attn_fwd")
+    return out
+
+
+# ------------------------------------------------------- decode attention
+def attn_decode_workspace_bytes(B: int, H: int, Hkv: int, Sq: int, n_kv: int, D: int) -> int:
+    return int(lib().pli_attn_decode_workspace_size(B, H, Hkv, Sq, n_kv, D))
+
+
+def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, n_kv: int,
+                scale: float | None = None, causal: bool = True,
+                out: torch.Tensor | None = None, variant: int | None = None,
+                target_wgs: int = 0) -> torch.Tensor:
+    """Attention of the new tokens over a KV cache, in the cache layout of
+    ch02/kv_cache.py:25-35: q [B, Sq, Hq, D], k/v caches [B, S_max, Hkv, D]
+    of which the first n_kv positions are valid (the current token's K/V
+    already appended).  Returns [B, Sq, Hq, D].  causal masks bottom-right
+    (ch02/kv_cache.py:91-95); with Sq == 1 it changes nothing."""
+    dev = _require_gpu(q, k_cache, v_cache)
+    if q.dim() != 4 or k_cache.dim() != 4 or v_cache.dim() != 4:
+        raise PliError("attn_decode expects q [B, Sq, Hq, D] and caches [B, S, Hkv, D]")
+    B, Sq, H, D = q.shape
+    Bk, S_max, Hkv, Dk = k_cache.shape
+    if (Bk, Dk) != (B, D) or tuple(v_cache.shape) != tuple(k_cache.shape):
+        raise PliError(f"shape mismatch q{tuple(q.shape)} k{tuple(k_cache.shape)} "
+                       f"v{tuple(v_cache.shape)}")
+    if H % Hkv != 0:
+        raise PliError(f"heads {H} not a multiple of kv heads {Hkv}")
+    if not 0 <= n_kv <= S_max:
+        raise PliError(f"n_kv {n_kv} outside the cache [0, {S_max}]")
+    q, k_cache, v_cache = (t if t.stride(-1) == 1 else t.contiguous() for t in (q, k_cache, v_cache))
+    if out is None:
+        out = torch.empty((B, Sq, H, D), device=q.device, dtype=q.dtype)
+    _require_gpu(q, out)
+    if tuple(out.shape) != (B, Sq, H, D) or out.stride(-1) != 1:
+        raise PliError("bad output tensor")
+    if scale is None:
+        scale = D ** -0.5
+    # [b, h, n] strides of the [B, N, H, D] tensors
+    st = (_c_i64 * 12)(*(int(x) for t in (q, k_cache, v_cache, out)
+                         for x in (t.stride(0), t.stride(2), t.stride(1))))
+    ws_bytes = int(lib().pli_attn_decode_workspace_size(B, H, Hkv, Sq, n_kv, D))
+    if target_wgs:  # tuning: room for the finest split (one 128-key chunk per block)
+        ws_bytes = B * Hkv * -(-n_kv // 128) * Sq * (H // Hkv) * (D + 2) * 4
+    ws = torch.empty(max(ws_bytes // 4, 1), device=q.device, dtype=torch.float32)
+    args = (_ptr(q), _ptr(k_cache), _ptr(v_cache), _ptr(out), B, H, Hkv, Sq, int(n_kv), D, st,
+            float(scale), int(bool(causal)), _ptr(ws), ws_bytes, _dtype_code(q), _stream(dev))
+    with _on_device(dev):
+        if variant is None and not target_wgs:
+            rc = lib().pli_attn_decode(*args)
+        else:
+            rc = lib().pli_attn_decode_variant(*args, -1 if variant is None else int(variant),
+                                               int(target_wgs))
+    _check(rc, "pli_attn_decode")
     return out
 
 

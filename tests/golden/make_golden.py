@@ -14,6 +14,11 @@ and records, for seeded inputs, what the reference computes:
 * ``mha.npz``      -- ``ch01.MultiHeadAttention(512, 8)`` built under
   ``torch.manual_seed(0)``: weight hashes and fp32 outputs (causal and not);
 * ``tp.npz``       -- ``ch09`` Column/RowParallelLinear seeded weights + outputs;
+* ``gqa.npz``      -- ``ch01.GroupedQueryAttention`` and the ``ch02`` cached
+  attention modules (``GQAWithCache`` over ``KVCache``, ``CachedGQA`` over
+  ``LayerKVCache``): seeded weights, a prompt, single-token decode steps and
+  a 3-token chunk (bottom-right causal mask), fp32;
+* ``kv_cache.json`` -- ``ch02.calculate_kv_cache_size`` over a small grid;
 * ``analytic.json`` -- exact values of the reference cost models
   (ch03 roofline / flops / bytes, ch06 memory + flops, ch09 comm models).
 
@@ -127,6 +132,52 @@ def gen_mha(ref_ch01, out_dir):
     print("mha: ok")
 
 
+def gen_gqa(ref_ch01, ref_ch02, out_dir):
+    import torch
+    hidden, heads, kv_heads = 512, 8, 2
+    d = {}
+    torch.manual_seed(1)
+    gqa = ref_ch01.GroupedQueryAttention(hidden, heads, kv_heads)
+    x = seeded_normal((1, 64, hidden), 41)
+    with torch.no_grad():
+        d["gqa_causal"] = gqa(torch.from_numpy(x), causal=True).numpy()
+        d["gqa_noncausal"] = gqa(torch.from_numpy(x), causal=False).numpy()
+    d.update({f"gqa_hash_{n}": np.array(array_hash(p.detach().numpy()))
+              for n, p in gqa.named_parameters()})
+    # the same token stream through both cached modules: prompt 40, two decode
+    # steps, then a 3-token chunk
+    steps = [seeded_normal((2, 40, hidden), 42), seeded_normal((2, 1, hidden), 43),
+             seeded_normal((2, 1, hidden), 44), seeded_normal((2, 3, hidden), 45)]
+    torch.manual_seed(2)
+    gwc = ref_ch02.GQAWithCache(hidden, heads, kv_heads)
+    cache = ref_ch02.KVCache.create(2, 64, kv_heads, hidden // heads, torch.device("cpu"),
+                                    torch.float32)
+    torch.manual_seed(3)
+    cg = ref_ch02.CachedGQA(hidden, heads, kv_heads)
+    lc = ref_ch02.LayerKVCache(k=torch.zeros(2, 64, kv_heads, hidden // heads),
+                               v=torch.zeros(2, 64, kv_heads, hidden // heads), seq_len=0)
+    pos = 0
+    with torch.no_grad():
+        for i, xs in enumerate(steps):
+            d[f"gwc_step{i}"] = gwc(torch.from_numpy(xs), kv_cache=cache)[0].numpy()
+            d[f"cg_step{i}"] = cg(torch.from_numpy(xs), cache=lc, start_pos=pos).numpy()
+            pos += xs.shape[1]
+        d["gwc_nocache"] = gwc(torch.from_numpy(steps[0]), kv_cache=None)[0].numpy()
+    d["cache_len"] = np.array([cache.seq_len, lc.seq_len])
+    d.update({f"gwc_hash_{n}": np.array(array_hash(p.detach().numpy()))
+              for n, p in gwc.named_parameters()})
+    d.update({f"cg_hash_{n}": np.array(array_hash(p.detach().numpy()))
+              for n, p in cg.named_parameters()})
+    np.savez_compressed(os.path.join(out_dir, "gqa.npz"), **d)
+    grid = [(b, s, l, h, hd, dt) for b in (1, 8) for s in (2048, 32768) for l in (1, 32)
+            for h in (2, 8) for hd in (64, 128) for dt in ("float16", "float32")]
+    kv = [[list(g), ref_ch02.calculate_kv_cache_size(*g[:5], dtype=getattr(torch, g[5]))]
+          for g in grid]
+    with open(os.path.join(out_dir, "kv_cache.json"), "w") as f:
+        json.dump(kv, f, indent=0)
+    print("gqa / kv_cache: ok")
+
+
 def gen_tp(ref_ch09, out_dir):
     import torch
     d = {}
@@ -214,11 +265,12 @@ def main():
     sys.path.insert(0, args.ref)
     sys.dont_write_bytecode = True
     import importlib
-    ref = {n: importlib.import_module(n) for n in ("ch01", "ch03", "ch06", "ch09")}
+    ref = {n: importlib.import_module(n) for n in ("ch01", "ch02", "ch03", "ch06", "ch09")}
     gen_flash(ref["ch06"], args.out)
     gen_softmax(ref["ch06"], args.out)
     gen_mha(ref["ch01"], args.out)
     gen_tp(ref["ch09"], args.out)
+    gen_gqa(ref["ch01"], ref["ch02"], args.out)
     gen_analytic(ref, args.out)
 
 

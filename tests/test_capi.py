@@ -23,7 +23,8 @@ def declared_symbols():
 def test_header_declares_the_hot_path():
     syms = declared_symbols()
     for s in ("pli_flash_attn_fwd", "pli_gemv", "pli_gemm", "pli_scale_copy", "pli_softmax_rows",
-              "pli_online_softmax_with_output", "pli_last_error", "pli_version"):
+              "pli_online_softmax_with_output", "pli_attn_decode", "pli_attn_decode_workspace_size",
+              "pli_last_error", "pli_version"):
         assert s in syms
 
 
@@ -58,6 +59,31 @@ def test_argument_validation_without_gpu(built_lib):
     assert L.pli_flash_attn_fwd(p, p, p, p, 1, 4, 4, 8, 8, 64, st, float("nan"), 0, 2, None) == EINVAL
     assert L.pli_scale_copy(p, p, 16, 0, None) == EINVAL
     assert L.pli_softmax_rows(p, p, 4, 0, 0, None) == EINVAL
+    dec = lambda *shape, causal=0, ws=0: L.pli_attn_decode(p, p, p, p, *shape, st, 0.1, causal,
+                                                           None, ws, 2, None)
+    assert dec(1, 6, 4, 1, 64, 64) == EINVAL and b"multiple of kv_heads" in L.pli_last_error()
+    assert dec(1, 8, 2, 4, 2, 64, causal=1) == EINVAL  # causal chunk longer than the cache
+    assert b"n_q" in L.pli_last_error()
+    # split-K needs its workspace: refused (not silently single-split) when short
+    need = L.pli_attn_decode_workspace_size(1, 32, 8, 1, 32768, 128)
+    assert need > 0
+    st_dec = (ctypes.c_int64 * 12)(*([8] * 12))
+    rc = L.pli_attn_decode(p, p, p, p, 1, 32, 8, 1, 32768, 128, st_dec, 0.1, 0, None, need - 1, 2, None)
+    assert rc == EINVAL and b"workspace" in L.pli_last_error()
+
+
+def test_decode_workspace_plan(built_lib):
+    """Split-K plan (host arithmetic, no GPU): one chunk per head when the
+    (batch, kv head) grid alone fills the chip; fp32 partials otherwise."""
+    import pli_hip
+    ws = pli_hip.attn_decode_workspace_bytes
+    assert ws(64, 32, 8, 1, 4096, 128) == 512 * 2 * 4 * (128 + 2) * 4  # 512 heads x 2 chunks
+    assert ws(128, 32, 8, 1, 4096, 128) == 0         # 1024 (b, kv head) pairs fill the grid
+    n = ws(1, 32, 8, 1, 32768, 128)                  # 8 heads -> 128 chunks each
+    assert n == 8 * 128 * 4 * (128 + 2) * 4
+    assert ws(1, 32, 8, 1, 100, 128) == 0            # one 128-key chunk
+    assert ws(1, 64, 2, 1, 4096, 128) == 0           # 32 rows per kv head: prefill kernel
+    assert ws(1, 8, 8, 1, 4096, 80) == 0             # head_dim 80: prefill kernel
 
 
 def test_hip_path_refuses_cpu_tensors(built_lib):

@@ -108,6 +108,7 @@ def test_flash_vs_oracle(case):
 MFMA_VARIANTS = (0, 1, 2, 3, 8, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24)
 
 
+
 @pytest.mark.parametrize("variant", MFMA_VARIANTS)
 @pytest.mark.parametrize("case", [c for c in CASES if c[6] != "fp32" and c[5] in (64, 128)],
                          ids=lambda c: "b{}h{}kv{}q{}k{}d{}_{}{}".format(*c[:7], "_causal" if c[7] else ""))

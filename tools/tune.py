@@ -163,6 +163,57 @@ def tune_bgemv():
                           **{f"{n}_GB/s": nbytes / (t[n][0] * 1e-3 / copies) / 1e9 for n in t}}), flush=True)
 
 
+def tune_decode(configs=((1, 32, 8, 32768), (8, 32, 8, 4096), (32, 32, 8, 4096), (8, 32, 8, 32768),
+                          (64, 32, 8, 2048), (1, 32, 8, 131072)), D=128,
+                modes=((13, 0), (0, 0))):
+    """Decode attention over a [B, S, Hkv, D] bf16 cache: HIP split-K vs the
+    reference formulation (repeat_interleave + matmul + softmax + matmul,
+    ch02/kv_cache.py:81-98) in torch.  Graph of `copies` launches over rotated
+    caches (> 1 GiB total, past the 256 MiB MALL)."""
+    import math
+    for B, H, Hkv, n in configs:
+        kv_bytes = 2 * B * n * Hkv * D * 2
+        copies = max(2, min(16, math.ceil((1 << 30) / kv_bytes)))
+        ks = [torch.randn(B, n, Hkv, D, device="cuda", dtype=torch.bfloat16) for _ in range(copies)]
+        vs = [torch.randn(B, n, Hkv, D, device="cuda", dtype=torch.bfloat16) for _ in range(copies)]
+        q = torch.randn(B, 1, H, D, device="cuda", dtype=torch.bfloat16)
+        out = torch.empty_like(q)
+
+        def ref(k, v):
+            qt = q.transpose(1, 2)
+            kt = k.transpose(1, 2).repeat_interleave(H // Hkv, dim=1)
+            vt = v.transpose(1, 2).repeat_interleave(H // Hkv, dim=1)
+            sc = torch.matmul(qt, kt.transpose(-2, -1)) / math.sqrt(D)
+            return torch.matmul(torch.softmax(sc, dim=-1), vt)
+
+        fns = {f"hip{m}_{tg}": (lambda k, v, m=m, tg=tg: pli_hip.attn_decode(
+            q, k, v, n, out=out, causal=False, variant=m, target_wgs=tg)) for m, tg in modes}
+        if kv_bytes * (H // Hkv) * 2 < (24 << 30):
+            fns["torch_ref"] = ref
+        graphs = {}
+        for name, fn in fns.items():
+            for k, v in zip(ks, vs):
+                fn(k, v)
+            torch.cuda.synchronize()
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr):
+                for k, v in zip(ks, vs):
+                    fn(k, v)
+            graphs[name] = gr
+        t = interleave({nm: g.replay for nm, g in graphs.items()}, 3, 3)
+        fns[f"hip{modes[0][0]}_{modes[0][1]}"](ks[-1], vs[-1])
+        ref_out = ref(ks[-1], vs[-1]).transpose(1, 2)
+        err = (ref_out.float() - out.float()).abs().max().item()
+        nbytes = kv_bytes + 2 * q.numel() * 2
+        print(json.dumps({"kernel": "attn_decode", "B": B, "Hq": H, "Hkv": Hkv, "n_kv": n, "D": D,
+                          "splits_ws_MB": pli_hip.attn_decode_workspace_bytes(B, H, Hkv, 1, n, D) / 2**20,
+                          **{f"{nm}_us": t[nm][0] * 1e3 / copies for nm in t},
+                          **{f"{nm}_GB/s": nbytes / (t[nm][0] * 1e-3 / copies) / 1e9 for nm in t},
+                          "maxdiff_vs_torch": err}), flush=True)
+        del ks, vs, graphs
+        torch.cuda.empty_cache()
+
+
 def tune_hbm():
     for nbytes in (1 << 28, 1 << 30):
         n = nbytes // 4
@@ -205,3 +256,5 @@ if __name__ == "__main__":
         tune_flash(D=64, H=64)
     if "gemm" in what:
         tune_gemm()
+    if "decode" in what:
+        tune_decode()
