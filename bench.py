@@ -11,6 +11,8 @@ so ``value`` = N x per-replica work / max-over-ranks time (weak scaling).
 The same JSON line carries, as sub-objects, the other hot-path rows:
   gemv    ch03 decode GEMV 4096x4096 bf16 (W rotated over >256 MiB so every
           launch streams from HBM, not the 256 MiB Infinity Cache)
+  decode_attn  ch02 decode attention over a [B, S, Hkv, D] KV cache (B=8,
+          Hq=32, Hkv=8, S=32768, D=128 bf16, 1 GiB), split-K flash-decoding
   gemm    ch05/ch03 4096^3 bf16 NN GEMM
   tp_gemm ch09 row-parallel 8192x8192 GEMM, M=8192, + RCCL all-reduce over
           xGMI when N > 1 (compute / all-reduce / total / bus bandwidth)
@@ -118,6 +120,50 @@ def bench_gemv(stream, iters: int) -> dict:
                          "traffic": load_traffic("gemv_vec")}}
 
 
+def bench_decode(stream, iters: int) -> dict:
+    """ch02 decode step attention: one new token per sequence over the cache
+    (GQA 32/8), bf16.  Two caches (2 GiB) alternate so no launch re-reads the
+    256 MiB Infinity Cache.  Algorithmic bytes = the valid K + V prefix + q + o.
+    The reference formulation (repeat_interleave + matmul + softmax + matmul,
+    ch02/kv_cache.py:81-98) is timed on the same device beside it."""
+    import math
+    import pli_hip
+    Bd, Hq, Hkv, n, Dd = 8, 32, 8, 32768, 128
+    caches = [(torch.randn(Bd, n, Hkv, Dd, device="cuda", dtype=torch.bfloat16),
+               torch.randn(Bd, n, Hkv, Dd, device="cuda", dtype=torch.bfloat16)) for _ in range(2)]
+    qd = torch.randn(Bd, 1, Hq, Dd, device="cuda", dtype=torch.bfloat16)
+    od = torch.empty_like(qd)
+    state = {"i": 0}
+
+    def step():
+        kc, vc = caches[state["i"] & 1]
+        state["i"] += 1
+        pli_hip.attn_decode(qd, kc, vc, n, out=od, causal=False)
+    for _ in range(4):
+        step()
+    ms = event_time_ms(step, iters, stream)
+    nbytes = 2 * Bd * n * Hkv * Dd * 2 + 2 * qd.numel() * 2
+    gbps = nbytes / (ms * 1e-3) / 1e9
+
+    def ref():
+        kc, vc = caches[0]
+        qt = qd.transpose(1, 2)
+        kt = kc.transpose(1, 2).repeat_interleave(Hq // Hkv, dim=1)
+        vt = vc.transpose(1, 2).repeat_interleave(Hq // Hkv, dim=1)
+        return torch.matmul(torch.softmax(torch.matmul(qt, kt.transpose(-2, -1)) / math.sqrt(Dd),
+                                          dim=-1), vt)
+    ref()
+    ms_ref = event_time_ms(ref, 3, stream)
+    del caches
+    torch.cuda.empty_cache()
+    return {"workload": "ch02 decode attention, B=8 Hq=32 Hkv=8 S=32768 D=128 bf16 (1 GiB cache)",
+            "us_per_launch": ms * 1e3, "GB/s": gbps, "timing": "events, 2 caches alternated",
+            "reference_formulation_GB/s": nbytes / (ms_ref * 1e-3) / 1e9,
+            "roofline": {"bound": "hbm", "achieved": gbps, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                         "frac": gbps / PEAK_HBM_GBPS, "algorithmic_bytes": nbytes,
+                         "traffic": load_traffic("attn_decode_chunk")}}
+
+
 def bench_gemm(stream, iters: int) -> dict:
     import pli_hip
     n = 4096
@@ -202,6 +248,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--quick", action="store_true", help="skip gemm/tp/cpu legs")
+    ap.add_argument("--with-decode", action="store_true", help="with --quick: keep the decode leg")
+    ap.add_argument("--flash-only", action="store_true",
+                    help="only the headline flash step (clean rocprof stats for that kernel)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -247,17 +296,26 @@ def main():
     achieved = flops_step / (kernel_ms * 1e-3) / 1e12
 
     extra = {}
+    if args.flash_only:
+        args.quick, args.no_cpu_baseline = True, True
     # causal variant of the same workload (ch01 MHA semantics), reported only
-    for _ in range(2):
+    for _ in range(2 if not args.flash_only else 0):
         pli_hip.flash_attn_fwd(q, k, v, causal=True, out=o)
-    ms_c = event_time_ms(lambda: pli_hip.flash_attn_fwd(q, k, v, causal=True, out=o), 5, stream)
-    extra["flash_causal"] = {"ms": ms_c, "TFLOP/s": 4 * B * H * D * (S * (S + 1) // 2) / (ms_c * 1e-3) / 1e12}
-    if not args.quick:
+    if not args.flash_only:
+        ms_c = event_time_ms(lambda: pli_hip.flash_attn_fwd(q, k, v, causal=True, out=o), 5, stream)
+        extra["flash_causal"] = {"ms": ms_c,
+                                 "TFLOP/s": 4 * B * H * D * (S * (S + 1) // 2) / (ms_c * 1e-3) / 1e12}
+    if args.flash_only:
+        pass
+    elif not args.quick:
         extra["gemv"] = bench_gemv(stream, 200)
+        extra["decode_attn"] = bench_decode(stream, 20)
         extra["gemm"] = bench_gemm(stream, 20)
         extra["tp_gemm"] = bench_tp(stream, world, rank, 10)
     else:
         extra["gemv"] = bench_gemv(stream, 200)
+        if args.with_decode:
+            extra["decode_attn"] = bench_decode(stream, 20)
 
     result = {
         "metric": METRIC,
@@ -279,7 +337,7 @@ def main():
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved / PEAK_BF16_TFLOPS,
                      "traffic": load_traffic("attn_fwd_v2"),
-                     "kernel": "attn_fwd_v2<bf16,128,8 waves>", "algorithmic_flops": flops_step,
+                     "kernel": "attn_fwd_v2<bf16,128,8 waves,OPT 13>", "algorithmic_flops": flops_step,
                      "kernel_ms": kernel_ms},
         **extra,
     }

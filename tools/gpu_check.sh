@@ -22,10 +22,18 @@ fi
 if [ "$MODE" = all ] || [ -n "$RUNALL" ] || [ "$MODE" = prof ]; then
   cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
       -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run -- \
-      python "$GRAFT_REPO_ROOT/bench.py" --quick --steps 10 --warmup 2 \
+      python "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --steps 10 --warmup 2 \
       > "$GRAFT_REPO_ROOT/gpurun_out/prof_bench.json" 2> "$GRAFT_REPO_ROOT/gpurun_out/prof.err"
   rc=$?; echo "rocprof rc=$rc"; cd "$GRAFT_REPO_ROOT"
   find gpurun_out/prof -name "*kernel_stats.csv" -exec cat {} \; | cut -c1-250 | head -20
+  [ $rc -eq 0 ] || exit $rc
+  python tools/trace_check.py gpurun_out/prof/run_kernel_trace.csv gpurun_out/prof_bench.json 2 10
+  # headline kernel alone: its stats average is the bench's kernel_ms
+  cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+      -d "$GRAFT_REPO_ROOT/gpurun_out/prof_flash" -o run -- \
+      python "$GRAFT_REPO_ROOT/bench.py" --flash-only --steps 20 --warmup 5 \
+      > "$GRAFT_REPO_ROOT/gpurun_out/prof_flash_bench.json" 2> "$GRAFT_REPO_ROOT/gpurun_out/prof_flash.err"
+  rc=$?; echo "rocprof flash-only rc=$rc"; cd "$GRAFT_REPO_ROOT"
   [ $rc -eq 0 ] || exit $rc
 fi
 if [ "$MODE" = pmc ] || [ "$MODE" = allpmc ]; then
@@ -35,9 +43,10 @@ if [ "$MODE" = pmc ] || [ "$MODE" = allpmc ]; then
     tag=$(echo $ctr | tr ' ' '_')
     cd /tmp && timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace --output-format csv \
         -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_$tag" -o run -- \
-        python "$GRAFT_REPO_ROOT/bench.py" --quick --steps 3 --warmup 1 \
+        python "$GRAFT_REPO_ROOT/bench.py" --quick --with-decode --steps 3 --warmup 1 \
         > "$GRAFT_REPO_ROOT/gpurun_out/pmc_$tag.json" 2> "$GRAFT_REPO_ROOT/gpurun_out/pmc_$tag.err"
     rc=$?; echo "pmc $ctr rc=$rc"; cd "$GRAFT_REPO_ROOT"
     [ $rc -eq 0 ] || exit $rc
   done
+  python tools/pmc_summary.py gpurun_out gpurun_out/traffic.json > /dev/null && cat gpurun_out/traffic.json
 fi
