@@ -94,6 +94,21 @@ int pli_gemm(const void* a, const void* b, void* c, const void* bias, int m,
              int dtype, void* stream);
 
 /*
+ * Fused SwiGLU projection  h[m, n] = silu(x Wg^T)[m, n] * (x Wu^T)[m, n]
+ * (fp32 accumulate, silu(g) = g / (1 + e^-g)).
+ * Replaces gate_proj -> silu, up_proj, multiply of
+ *   ch09/tensor_parallel.py:95-99   TensorParallelMLP.forward (per rank)
+ *   ch01/ffn.py:34-39               SwiGLUFFN; ch01/ffn.py:51-57 FusedSwiGLUFFN
+ *                                   (gate_up_proj halves: wg = W, wu = W + n*ldw)
+ *   ch02/cached_generation.py:119   SwiGLUFFN of the cached model
+ * x [m, k] (ldx), wg / wu [n, k] row-major (ldwg, ldwu), h [m, n] (ldh).
+ * Neither gate nor up is written to memory.
+ */
+int pli_gemm_swiglu(const void* x, const void* wg, const void* wu, void* h,
+                    int m, int n, int k, int64_t ldx, int64_t ldwg,
+                    int64_t ldwu, int64_t ldh, int dtype, void* stream);
+
+/*
  * HBM calibration kernels of ch05/coalescing.cu:7-20 (fp32):
  *   out[i] = 2 * in[i * stride],  i in [0, n_out).
  * stride == 1 is the coalesced stream (16-byte vector loads), the roofline

@@ -44,3 +44,21 @@ def row_parallel_sum(x_full, w_full, world_size: int):
         s = slice(r * part, (r + 1) * part)
         total += x_full[..., s] @ w_full[:, s].T
     return total
+
+
+def silu(x):
+    """x * sigmoid(x) (``F.silu``), float64."""
+    x = np.asarray(x, dtype=np.float64)
+    return x / (1.0 + np.exp(-x))
+
+
+def swiglu(x, w_gate, w_up):
+    """h = silu(x Wg^T) * (x Wu^T): the SwiGLU product of ``ch01/ffn.py:26-30``
+    and ``ch09/tensor_parallel.py:95-98`` (per rank: column shards of Wg/Wu)."""
+    x = np.asarray(x, dtype=np.float64)
+    return silu(x @ np.asarray(w_gate, np.float64).T) * (x @ np.asarray(w_up, np.float64).T)
+
+
+def swiglu_ffn(x, w_gate, w_up, w_down):
+    """down(silu(gate(x)) * up(x)), ``SwiGLUFFN.forward`` (``ch01/ffn.py:26-31``)."""
+    return swiglu(x, w_gate, w_up) @ np.asarray(w_down, np.float64).T

@@ -8,7 +8,8 @@ and ``state_dict``s are interchangeable.  On a ROCm device:
   ``pli_attn_decode`` (split-K flash-decoding in place on the
   [B, S_max, Hkv, hd] buffer; the prompt goes to the prefill flash kernel
   through the same entry point), replacing ``:71-94``;
-* ``SwiGLUFFN`` runs gate/up/down on ``pli_gemm``;
+* ``SwiGLUFFN`` runs gate + up + silu·mul as one ``pli_gemm_swiglu`` launch
+  and down on ``pli_gemm``;
 * ``CachedTransformerModel``'s ``lm_head`` runs on ``pli_gemm``.
 Embedding lookup, RMSNorm, residual adds and sampling stay in torch (they
 are not on the measured path).  CPU tensors keep the reference math.
@@ -21,6 +22,8 @@ from dataclasses import dataclass
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+import pli_hip
 
 from .kv_cache import _proj, attend_cached
 
@@ -91,6 +94,11 @@ class SwiGLUFFN(nn.Module):
         self.down_proj = nn.Linear(intermediate_dim, hidden_dim, bias=False)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if x.is_cuda:  # gate, up and silu*mul in one launch (pli_gemm_swiglu)
+            lead = x.shape[:-1]
+            h = pli_hip.gemm_swiglu(x.reshape(-1, x.shape[-1]), self.gate_proj.weight,
+                                    self.up_proj.weight)
+            return _lin(h.view(*lead, h.shape[-1]), self.down_proj.weight)
         h = F.silu(_lin(x, self.gate_proj.weight)) * _lin(x, self.up_proj.weight)
         return _lin(h, self.down_proj.weight)
 

@@ -136,6 +136,14 @@ class TensorParallelMLP(nn.Module):
                                            config.world_size, config.rank)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if x.is_cuda:
+            # gate/up column shards fused with the SwiGLU product in one launch
+            # (pli_gemm_swiglu): the rank's [.., I/tp] gate and up activations
+            # never reach HBM; down_proj then all-reduces as before
+            lead = x.shape[:-1]
+            h = pli_hip.gemm_swiglu(x.reshape(-1, x.shape[-1]), self.gate_proj.weight,
+                                    self.up_proj.weight)
+            return self.down_proj(h.view(*lead, h.shape[-1]))
         return self.down_proj(F.silu(self.gate_proj(x)) * self.up_proj(x))
 
 

@@ -21,6 +21,8 @@
 //
 // Generic kernel (fp32, ragged or unaligned shapes): 64x64 LDS-tiled VALU
 // kernel, 4x4 outputs per thread, fp32 accumulate.
+#include <type_traits>
+
 #include "pli_common.h"
 
 namespace pli {
@@ -40,13 +42,24 @@ __device__ __forceinline__ int off256(int row, int ch) {
     return row * 256 + ((ch ^ f) << 4);
 }
 
-template <typename T, bool TRANS_B, bool BIAS>
+__device__ __forceinline__ float silu_mul(float g, float u) {
+    return g / (1.f + __expf(-g)) * u;
+}
+
+// SWIGLU (NT only): C[m, n] = silu(A Bg^T)[m, n] * (A Bu^T)[m, n].  The B tile's
+// first 64 rows are Bg rows nb..nb+63 and its last 64 the same rows of Bu, so
+// waves wn = 0 hold gate and wn = 1 up accumulators for the same (m, n) at the
+// same lane/register; the up waves hand theirs over through LDS.
+template <typename T, bool TRANS_B, bool BIAS, bool SWIGLU = false>
 __global__ __launch_bounds__(256, 2) void gemm_mfma(const uint16_t* __restrict__ A,
                                                     const uint16_t* __restrict__ Bm,
                                                     uint16_t* __restrict__ C,
                                                     const uint16_t* __restrict__ bias, int M, int N,
                                                     int K, int64_t lda, int64_t ldb, int64_t ldc,
-                                                    int tiles_n, int nblocks) {
+                                                    int tiles_n, int nblocks,
+                                                    const uint16_t* __restrict__ Bu = nullptr,
+                                                    int64_t ldbu = 0) {
+    static_assert(!SWIGLU || TRANS_B, "SwiGLU GEMM takes weights as [n][k]");
     constexpr int TILE = BM * BK * 2;  // 16 KiB per operand tile
     __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
 
@@ -55,7 +68,7 @@ __global__ __launch_bounds__(256, 2) void gemm_mfma(const uint16_t* __restrict__
     const int wm = wave >> 1, wn = wave & 1;  // 2x2 waves, 64x64 each
 
     const int lb = xcd_remap(blockIdx.x, nblocks);
-    const int m0 = (lb / tiles_n) * BM, n0 = (lb % tiles_n) * BN;
+    const int m0 = (lb / tiles_n) * BM, n0 = (lb % tiles_n) * (SWIGLU ? BN / 2 : BN);
     const int ktiles = cdiv(K, BK);
 
     // staging: 1024 chunks of 16 B per operand tile, 4 per thread
@@ -71,7 +84,13 @@ __global__ __launch_bounds__(256, 2) void gemm_mfma(const uint16_t* __restrict__
                 const i32x4 x = *reinterpret_cast<const i32x4*>(A + (int64_t)mm * lda + min(kk, K - 8));
                 ast[i] = (m0 + r < M && kk < K) ? x : i32x4{0, 0, 0, 0};
             }
-            if constexpr (TRANS_B) {  // B [N][K]: row = n
+            if constexpr (SWIGLU) {  // rows 0..63 gate, 64..127 up, both n0 + (r & 63)
+                const int r = c >> 3, ch = c & 7, rn = n0 + (r & 63);
+                const int nn = min(rn, N - 1), kk = k0 + ch * 8;
+                const uint16_t* src = r < 64 ? Bm + (int64_t)nn * ldb : Bu + (int64_t)nn * ldbu;
+                const i32x4 x = *reinterpret_cast<const i32x4*>(src + min(kk, K - 8));
+                bst[i] = (rn < N && kk < K) ? x : i32x4{0, 0, 0, 0};
+            } else if constexpr (TRANS_B) {  // B [N][K]: row = n
                 const int r = c >> 3, ch = c & 7;
                 const int nn = min(n0 + r, N - 1), kk = k0 + ch * 8;
                 const i32x4 x = *reinterpret_cast<const i32x4*>(Bm + (int64_t)nn * ldb + min(kk, K - 8));
@@ -145,6 +164,41 @@ __global__ __launch_bounds__(256, 2) void gemm_mfma(const uint16_t* __restrict__
         __syncthreads();
     }
 
+    if constexpr (SWIGLU) {
+        // up waves park their accumulators; gate waves combine and store
+        float* xu = reinterpret_cast<float*>(smem) + wm * (2 * 2 * 16 * 64);
+        if (wn == 1) {
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+                for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) xu[((ni * 2 + mi) * 16 + r) * 64 + lane] = acc[ni][mi][r];
+        }
+        __syncthreads();
+        if (wn == 1) return;
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi) {
+            const int m = m0 + wm * 64 + mi * 32 + l32;
+            if (m >= M) continue;
+            uint16_t* crow = C + (int64_t)m * ldc;
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int n = n0 + ni * 32 + 8 * i + 4 * h32;
+                    if (n >= N) continue;
+                    float v[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        v[j] = silu_mul(acc[ni][mi][4 * i + j],
+                                        xu[((ni * 2 + mi) * 16 + 4 * i + j) * 64 + lane]);
+                    *reinterpret_cast<i32x2*>(crow + n) =
+                        i32x2{(int)pack2<T>(v[0], v[1]), (int)pack2<T>(v[2], v[3])};
+                }
+        }
+        return;
+    }
     // epilogue: acc[ni][mi][r] = C[m = m0+wm*64+mi*32+l32][n = n0+wn*64+ni*32+(r&3)+8(r>>2)+4h32]
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi) {
@@ -175,15 +229,18 @@ __global__ __launch_bounds__(256, 2) void gemm_mfma(const uint16_t* __restrict__
 // Generic LDS-tiled kernel (any dtype, any shape/stride), fp32 accumulate.
 constexpr int GT = 64, GKT = 16;
 
-template <typename T, bool TRANS_B>
+// SWIGLU (NT): the 64-column B tile is 32 gate + 32 up columns of the same
+// 32 outputs, so thread columns j = 0/2 and 1/3 pair up in registers.
+template <typename T, bool TRANS_B, bool SWIGLU = false>
 __global__ __launch_bounds__(256) void gemm_generic(const T* __restrict__ A, const T* __restrict__ Bm,
                                                     T* __restrict__ C, const T* __restrict__ bias,
                                                     int M, int N, int K, int64_t lda, int64_t ldb,
-                                                    int64_t ldc) {
+                                                    int64_t ldc, const T* __restrict__ Bu = nullptr,
+                                                    int64_t ldbu = 0) {
     __shared__ float As[GKT][GT + 4];
     __shared__ float Bs[GKT][GT + 4];
     const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
-    const int m0 = blockIdx.y * GT, n0 = blockIdx.x * GT;
+    const int m0 = blockIdx.y * GT, n0 = blockIdx.x * (SWIGLU ? GT / 2 : GT);
     float acc[4][4] = {};
     for (int k0 = 0; k0 < K; k0 += GKT) {
         for (int i = tid; i < GT * GKT; i += 256) {
@@ -192,7 +249,12 @@ __global__ __launch_bounds__(256) void gemm_generic(const T* __restrict__ A, con
                 const int m = m0 + r, kx = k0 + kk;
                 As[kk][r] = (m < M && kx < K) ? elem<T>::to_f32(A[(int64_t)m * lda + kx]) : 0.f;
             }
-            if constexpr (TRANS_B) {  // B[n][k] -> Bs[k][n]
+            if constexpr (SWIGLU) {  // cols 0..31 gate, 32..63 up of outputs n0 + (r & 31)
+                const int r = i / GKT, kk = i % GKT;
+                const int n = n0 + (r & 31), kx = k0 + kk;
+                const T* src = r < 32 ? Bm + (int64_t)n * ldb : Bu + (int64_t)n * ldbu;
+                Bs[kk][r] = (n < N && kx < K) ? elem<T>::to_f32(src[kx]) : 0.f;
+            } else if constexpr (TRANS_B) {  // B[n][k] -> Bs[k][n]
                 const int r = i / GKT, kk = i % GKT;
                 const int n = n0 + r, kx = k0 + kk;
                 Bs[kk][r] = (n < N && kx < K) ? elem<T>::to_f32(Bm[(int64_t)n * ldb + kx]) : 0.f;
@@ -217,6 +279,19 @@ __global__ __launch_bounds__(256) void gemm_generic(const T* __restrict__ A, con
         }
         __syncthreads();
     }
+    if constexpr (SWIGLU) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int m = m0 + ty + 16 * i;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int n = n0 + tx + 16 * j;
+                if (m < M && n < N)
+                    C[(int64_t)m * ldc + n] = elem<T>::from_f32(silu_mul(acc[i][j], acc[i][j + 2]));
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int m = m0 + ty + 16 * i;
@@ -238,27 +313,38 @@ __global__ __launch_bounds__(256) void gemm_generic(const T* __restrict__ A, con
 // per wave, each lane streams 16-byte W chunks (non-temporal, read once) and
 // dots them with the matching chunk of every X row (X is tiny and stays in
 // L1/L2); NB fp32 accumulators per lane, one shuffle reduction per output.
-template <typename T, int NB, int CPL>
+// SWIGLU: the wave streams row n of both Wg (W) and Wu and writes
+// silu(x.wg) * (x.wu): one pass over the two weight rows, no gate/up tensors.
+template <typename T, int NB, int CPL, bool SWIGLU = false>
 __global__ __launch_bounds__(128) void gemm_skinny_nt(const uint16_t* __restrict__ X,
                                                       const uint16_t* __restrict__ W,
                                                       uint16_t* __restrict__ C,
                                                       const uint16_t* __restrict__ bias, int M,
                                                       int N, int nchunks, int64_t ldx, int64_t ldw,
-                                                      int64_t ldc) {
+                                                      int64_t ldc,
+                                                      const uint16_t* __restrict__ Wu = nullptr,
+                                                      int64_t ldwu = 0) {
+    constexpr int NW = SWIGLU ? 2 : 1;  // weight rows per output
     const int lane = threadIdx.x & 63;
     const int n = blockIdx.x * 2 + (threadIdx.x >> 6);
     if (n >= N) return;
-    const uint16_t* wrow = W + (int64_t)n * ldw;
-    float acc[NB];
+    const uint16_t* wrow[NW];
+    wrow[0] = W + (int64_t)n * ldw;
+    if constexpr (SWIGLU) wrow[NW - 1] = Wu + (int64_t)n * ldwu;
+    float acc[NW][NB];
 #pragma unroll
-    for (int bb = 0; bb < NB; ++bb) acc[bb] = 0.f;
+    for (int w = 0; w < NW; ++w)
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) acc[w][bb] = 0.f;
     for (int c0 = 0; c0 < nchunks; c0 += 64 * CPL) {
-        i32x4 wv[CPL];
+        i32x4 wv[NW][CPL];
 #pragma unroll
-        for (int u = 0; u < CPL; ++u) {
-            const int cc = min(c0 + lane + 64 * u, nchunks - 1);
-            wv[u] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wrow + cc * 8));
-        }
+        for (int w = 0; w < NW; ++w)
+#pragma unroll
+            for (int u = 0; u < CPL; ++u) {
+                const int cc = min(c0 + lane + 64 * u, nchunks - 1);
+                wv[w][u] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wrow[w] + cc * 8));
+            }
 #pragma unroll
         for (int u = 0; u < CPL; ++u) {
             const int cc = c0 + lane + 64 * u;
@@ -269,23 +355,28 @@ __global__ __launch_bounds__(128) void gemm_skinny_nt(const uint16_t* __restrict
                         const i32x4 xv = *reinterpret_cast<const i32x4*>(X + bb * ldx + cc * 8);
 #pragma unroll
                         for (int i = 0; i < 4; ++i) {
-                            const int wi = wv[u][i], xi = xv[i];
-                            const float w0 = elem<T>::to_f32(T{(uint16_t)(wi & 0xffff)});
-                            const float w1 = elem<T>::to_f32(T{(uint16_t)((uint32_t)wi >> 16)});
+                            const int xi = xv[i];
                             const float x0 = elem<T>::to_f32(T{(uint16_t)(xi & 0xffff)});
                             const float x1 = elem<T>::to_f32(T{(uint16_t)((uint32_t)xi >> 16)});
-                            acc[bb] = fmaf(w1, x1, fmaf(w0, x0, acc[bb]));
+#pragma unroll
+                            for (int w = 0; w < NW; ++w) {
+                                const int wi = wv[w][u][i];
+                                const float w0 = elem<T>::to_f32(T{(uint16_t)(wi & 0xffff)});
+                                const float w1 = elem<T>::to_f32(T{(uint16_t)((uint32_t)wi >> 16)});
+                                acc[w][bb] = fmaf(w1, x1, fmaf(w0, x0, acc[w][bb]));
+                            }
                         }
                     }
                 }
             }
         }
     }
-    const float bn = bias ? elem<T>::to_f32(T{bias[n]}) : 0.f;
+    const float bn = (!SWIGLU && bias) ? elem<T>::to_f32(T{bias[n]}) : 0.f;
 #pragma unroll
     for (int bb = 0; bb < NB; ++bb) {
         if (bb < M) {
-            const float r = wave_sum(acc[bb]);
+            float r = wave_sum(acc[0][bb]);
+            if constexpr (SWIGLU) r = silu_mul(r, wave_sum(acc[NW - 1][bb]));
             if (lane == 0) C[bb * ldc + n] = __builtin_bit_cast(uint16_t, elem<T>::from_f32(r + bn));
         }
     }
@@ -316,33 +407,44 @@ int launch_skinny(const void* a, const void* b, void* c, const void* bias, int M
 // split over its 4 waves; W fragments (16 rows x 64 B per wave-instruction)
 // are streamed from HBM exactly once and feed NBG MFMAs (one per 16 batch
 // rows), X fragments come from L2.  Partial C^T tiles are summed through LDS.
-template <typename T, int NBG, bool BIAS>
+// SWIGLU: each wave streams the 16 rows of Wg (W) AND of Wu over its K range
+// into two accumulators per batch group; the epilogue writes silu(g) * u.
+template <typename T, int NBG, bool BIAS, bool SWIGLU = false>
 __global__ __launch_bounds__(256) void gemm_smallm_nt(const uint16_t* __restrict__ X,
                                                       const uint16_t* __restrict__ W,
                                                       uint16_t* __restrict__ C,
                                                       const uint16_t* __restrict__ bias, int M,
                                                       int N, int K, int64_t ldx, int64_t ldw,
-                                                      int64_t ldc) {
-    constexpr int U = 8;  // k-steps issued ahead per wave (8 KiB of W in flight)
-    __shared__ __attribute__((aligned(16))) float part[4][NBG][4][64];
+                                                      int64_t ldc,
+                                                      const uint16_t* __restrict__ Wu = nullptr,
+                                                      int64_t ldwu = 0) {
+    constexpr int NW = SWIGLU ? 2 : 1;     // weight matrices streamed
+    constexpr int U = SWIGLU ? 4 : 8;      // k-steps issued ahead per wave (8 KiB of W in flight)
+    __shared__ __attribute__((aligned(16))) float part[4][NBG][NW][4][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int n0 = blockIdx.x * 16;
     const int r16 = lane & 15, kq = 8 * (lane >> 4);
     const int kw = K / 4;  // this wave's K range
-    const uint16_t* wp = W + (int64_t)min(n0 + r16, N - 1) * ldw + wave * kw + kq;
+    const uint16_t* wp[NW];
+    wp[0] = W + (int64_t)min(n0 + r16, N - 1) * ldw + wave * kw + kq;
+    if constexpr (SWIGLU) wp[NW - 1] = Wu + (int64_t)min(n0 + r16, N - 1) * ldwu + wave * kw + kq;
     const uint16_t* xp[NBG];
 #pragma unroll
     for (int gi = 0; gi < NBG; ++gi)
         xp[gi] = X + (int64_t)min(gi * 16 + r16, M - 1) * ldx + wave * kw + kq;
-    f32x4 acc[NBG];
+    f32x4 acc[NW][NBG];
 #pragma unroll
-    for (int gi = 0; gi < NBG; ++gi) acc[gi] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int w = 0; w < NW; ++w)
+#pragma unroll
+        for (int gi = 0; gi < NBG; ++gi) acc[w][gi] = f32x4{0.f, 0.f, 0.f, 0.f};
     int k0 = 0;
     for (; k0 + 32 * U <= kw; k0 += 32 * U) {
-        i32x4 wf[U], xf[U][NBG];
+        i32x4 wf[NW][U], xf[U][NBG];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            wf[u] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wp + k0 + 32 * u));
+#pragma unroll
+            for (int w = 0; w < NW; ++w)
+                wf[w][u] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wp[w] + k0 + 32 * u));
 #pragma unroll
             for (int gi = 0; gi < NBG; ++gi)
                 xf[u][gi] = *reinterpret_cast<const i32x4*>(xp[gi] + k0 + 32 * u);
@@ -350,18 +452,26 @@ __global__ __launch_bounds__(256) void gemm_smallm_nt(const uint16_t* __restrict
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
-            for (int gi = 0; gi < NBG; ++gi) acc[gi] = mfma16x16x32<T>(wf[u], xf[u][gi], acc[gi]);
+            for (int w = 0; w < NW; ++w)
+#pragma unroll
+                for (int gi = 0; gi < NBG; ++gi)
+                    acc[w][gi] = mfma16x16x32<T>(wf[w][u], xf[u][gi], acc[w][gi]);
     }
     for (; k0 < kw; k0 += 32) {  // remainder k-steps (kw % 32 == 0)
-        const i32x4 wf = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wp + k0));
 #pragma unroll
-        for (int gi = 0; gi < NBG; ++gi)
-            acc[gi] = mfma16x16x32<T>(wf, *reinterpret_cast<const i32x4*>(xp[gi] + k0), acc[gi]);
+        for (int w = 0; w < NW; ++w) {
+            const i32x4 wf = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wp[w] + k0));
+#pragma unroll
+            for (int gi = 0; gi < NBG; ++gi)
+                acc[w][gi] = mfma16x16x32<T>(wf, *reinterpret_cast<const i32x4*>(xp[gi] + k0), acc[w][gi]);
+        }
     }
 #pragma unroll
-    for (int gi = 0; gi < NBG; ++gi)
+    for (int w = 0; w < NW; ++w)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) part[wave][gi][r][lane] = acc[gi][r];
+        for (int gi = 0; gi < NBG; ++gi)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) part[wave][gi][w][r][lane] = acc[w][gi][r];
     __syncthreads();
     // wave w reduces batch groups gi = w, w+4, ...; lane (col = batch, rows 4q..4q+3 = W rows)
     for (int gi = wave; gi < NBG; gi += 4) {
@@ -369,9 +479,13 @@ __global__ __launch_bounds__(256) void gemm_smallm_nt(const uint16_t* __restrict
         const int nr = n0 + 4 * (lane >> 4);
         float v[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-            v[r] = part[0][gi][r][lane] + part[1][gi][r][lane] + part[2][gi][r][lane] +
-                   part[3][gi][r][lane];
+        for (int r = 0; r < 4; ++r) {
+            v[r] = part[0][gi][0][r][lane] + part[1][gi][0][r][lane] + part[2][gi][0][r][lane] +
+                   part[3][gi][0][r][lane];
+            if constexpr (SWIGLU)
+                v[r] = silu_mul(v[r], part[0][gi][NW - 1][r][lane] + part[1][gi][NW - 1][r][lane] +
+                                          part[2][gi][NW - 1][r][lane] + part[3][gi][NW - 1][r][lane]);
+        }
         if (bt < M && nr < N) {
             if constexpr (BIAS) {
 #pragma unroll
@@ -441,8 +555,81 @@ int launch_generic(const void* a, const void* b, void* c, const void* bias, int 
 
 inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// ---- fused SwiGLU launches: h = silu(x Wg^T) * (x Wu^T)
+template <typename T>
+int launch_swiglu(const void* x, const void* wg, const void* wu, void* h, int M, int N, int K,
+                  int64_t ldx, int64_t ldwg, int64_t ldwu, int64_t ldh, bool vec, hipStream_t s) {
+    const auto* X = (const uint16_t*)x;
+    const auto* G = (const uint16_t*)wg;
+    const auto* U = (const uint16_t*)wu;
+    auto* Hh = (uint16_t*)h;
+    if constexpr (!std::is_same_v<T, float>) {
+    if (vec && (M == 1 || (M <= 16 && !(K % 128 == 0 && N % 16 == 0)))) {
+        const dim3 grid(cdiv(N, 2)), block(128);
+#define PLI_SKINNY_SW(NB)                                                                         \
+    hipLaunchKernelGGL((gemm_skinny_nt<T, NB, 4, true>), grid, block, 0, s, X, G, Hh, nullptr, M, \
+                       N, K / 8, ldx, ldwg, ldh, U, ldwu)
+        if (M <= 1) PLI_SKINNY_SW(1);
+        else if (M <= 2) PLI_SKINNY_SW(2);
+        else if (M <= 4) PLI_SKINNY_SW(4);
+        else if (M <= 8) PLI_SKINNY_SW(8);
+        else PLI_SKINNY_SW(16);
+#undef PLI_SKINNY_SW
+        return launch_status("gemm_skinny_nt<swiglu>");
+    }
+    if (vec && M <= 128 && K % 128 == 0 && N % 16 == 0) {
+        const dim3 grid(cdiv(N, 16)), block(256);
+#define PLI_SMALLM_SW(NBG)                                                                        \
+    hipLaunchKernelGGL((gemm_smallm_nt<T, NBG, false, true>), grid, block, 0, s, X, G, Hh,       \
+                       nullptr, M, N, K, ldx, ldwg, ldh, U, ldwu)
+        if (M <= 16) PLI_SMALLM_SW(1);
+        else if (M <= 32) PLI_SMALLM_SW(2);
+        else if (M <= 64) PLI_SMALLM_SW(4);
+        else PLI_SMALLM_SW(8);
+#undef PLI_SMALLM_SW
+        return launch_status("gemm_smallm_nt<swiglu>");
+    }
+    if (vec) {
+        const int tm = cdiv(M, BM), tn = cdiv(N, BN / 2);
+        const int64_t nb = (int64_t)tm * tn;
+        PLI_REQUIRE(nb < (1ll << 31), "pli_gemm_swiglu: grid too large");
+        hipLaunchKernelGGL((gemm_mfma<T, true, false, true>), dim3((unsigned)nb), dim3(256), 0, s,
+                           X, G, Hh, nullptr, M, N, K, ldx, ldwg, ldh, tn, (int)nb, U, ldwu);
+        return launch_status("gemm_mfma<swiglu>");
+    }
+    }  // 16-bit paths
+    const dim3 grid(cdiv(N, GT / 2), cdiv(M, GT)), block(256);
+    hipLaunchKernelGGL((gemm_generic<T, true, true>), grid, block, 0, s, (const T*)x, (const T*)wg,
+                       (T*)h, nullptr, M, N, K, ldx, ldwg, ldh, (const T*)wu, ldwu);
+    return launch_status("gemm_generic<swiglu>");
+}
+
 }  // namespace
 }  // namespace pli
+
+extern "C" int pli_gemm_swiglu(const void* x, const void* wg, const void* wu, void* h, int m,
+                               int n, int k, int64_t ldx, int64_t ldwg, int64_t ldwu, int64_t ldh,
+                               int dtype, void* stream) {
+    using namespace pli;
+    clear_error();
+    PLI_REQUIRE(x && wg && wu && h, "pli_gemm_swiglu: null pointer");
+    PLI_REQUIRE(m >= 0 && n >= 0 && k >= 0, "pli_gemm_swiglu: bad shape m=%d n=%d k=%d", m, n, k);
+    PLI_REQUIRE(dtype == PLI_F32 || dtype == PLI_F16 || dtype == PLI_BF16,
+                "pli_gemm_swiglu: bad dtype %d", dtype);
+    if (m == 0 || n == 0) return PLI_OK;
+    PLI_REQUIRE(ldx >= k && ldwg >= k && ldwu >= k && ldh >= n,
+                "pli_gemm_swiglu: leading dimension too small (ldx=%lld ldwg=%lld ldwu=%lld ldh=%lld)",
+                (long long)ldx, (long long)ldwg, (long long)ldwu, (long long)ldh);
+    hipStream_t s = (hipStream_t)stream;
+    const bool vec = (dtype == PLI_BF16 || dtype == PLI_F16) && k > 0 && k % 8 == 0 &&
+                     n % 8 == 0 && ldx % 8 == 0 && ldwg % 8 == 0 && ldwu % 8 == 0 && ldh % 8 == 0 &&
+                     al16(x) && al16(wg) && al16(wu) && al16(h);
+    switch (dtype) {
+        case PLI_BF16: return launch_swiglu<bf16_t>(x, wg, wu, h, m, n, k, ldx, ldwg, ldwu, ldh, vec, s);
+        case PLI_F16: return launch_swiglu<f16_t>(x, wg, wu, h, m, n, k, ldx, ldwg, ldwu, ldh, vec, s);
+        default: return launch_swiglu<float>(x, wg, wu, h, m, n, k, ldx, ldwg, ldwu, ldh, false, s);
+    }
+}
 
 extern "C" int pli_gemm(const void* a, const void* b, void* c, const void* bias, int m, int n,
                         int k, int64_t lda, int64_t ldb, int64_t ldc, int trans_b, int dtype,

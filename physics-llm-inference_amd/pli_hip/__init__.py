@@ -36,6 +36,8 @@ _SIGS = {
     "pli_gemv": [_vp, _vp, _vp, _c_int, _c_int, _c_i64, _c_int, _vp],
     "pli_gemm": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_i64, _c_i64, _c_i64, _c_int,
                  _c_int, _vp],
+    "pli_gemm_swiglu": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_i64, _c_i64, _c_i64,
+                        _c_i64, _c_int, _vp],
     "pli_scale_copy": [_vp, _vp, _c_i64, _c_int, _vp],
     "pli_softmax_rows": [_vp, _vp, _c_i64, _c_int, _c_int, _vp],
     "pli_online_softmax_with_output": [_vp, _vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_int, _vp],
@@ -226,6 +228,33 @@ def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, n
             rc = lib().pli_attn_decode_variant(*args, -1 if variant is None else int(variant),
                                                int(target_wgs))
     _check(rc, "pli_attn_decode")
+    return out
+
+
+# ------------------------------------------------------------ fused SwiGLU
+def gemm_swiglu(x: torch.Tensor, w_gate: torch.Tensor, w_up: torch.Tensor,
+                out: torch.Tensor | None = None) -> torch.Tensor:
+    """h = silu(x W_gate^T) * (x W_up^T) in one launch; x [m, k], W_* [n, k]
+    (unit column stride; any row stride, e.g. the two halves of a fused
+    gate_up weight)."""
+    dev = _require_gpu(x, w_gate, w_up)
+    if x.dim() != 2 or w_gate.dim() != 2 or tuple(w_up.shape) != tuple(w_gate.shape) \
+            or w_gate.shape[1] != x.shape[1]:
+        raise PliError(f"gemm_swiglu shape mismatch x{tuple(x.shape)} wg{tuple(w_gate.shape)} "
+                       f"wu{tuple(w_up.shape)}")
+    x, w_gate, w_up = (t if t.stride(1) == 1 else t.contiguous() for t in (x, w_gate, w_up))
+    m, k = x.shape
+    n = w_gate.shape[0]
+    if out is None:
+        out = torch.empty(m, n, device=x.device, dtype=x.dtype)
+    _require_gpu(x, out)
+    if tuple(out.shape) != (m, n) or out.stride(1) != 1:
+        raise PliError("bad output tensor")
+    with _on_device(dev):
+        rc = lib().pli_gemm_swiglu(_ptr(x), _ptr(w_gate), _ptr(w_up), _ptr(out), m, n, k,
+                                   x.stride(0), w_gate.stride(0), w_up.stride(0), out.stride(0),
+                                   _dtype_code(x), _stream(dev))
+    _check(rc, "pli_gemm_swiglu")
     return out
 
 

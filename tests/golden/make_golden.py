@@ -19,6 +19,8 @@ and records, for seeded inputs, what the reference computes:
   ``LayerKVCache``): seeded weights, a prompt, single-token decode steps and
   a 3-token chunk (bottom-right causal mask), fp32;
 * ``kv_cache.json`` -- ``ch02.calculate_kv_cache_size`` over a small grid;
+* ``ffn.npz``      -- ``ch01`` NaiveFFN / SwiGLUFFN / FusedSwiGLUFFN and the
+  ``ch09`` TensorParallelMLP (world 1) with seeded weights, fp32;
 * ``analytic.json`` -- exact values of the reference cost models
   (ch03 roofline / flops / bytes, ch06 memory + flops, ch09 comm models).
 
@@ -178,6 +180,32 @@ def gen_gqa(ref_ch01, ref_ch02, out_dir):
     print("gqa / kv_cache: ok")
 
 
+def gen_ffn(ref_ch01, ref_ch09, out_dir):
+    import importlib
+
+    import torch
+    hidden, inter = 256, 512
+    x = seeded_normal((2, 16, hidden), 51)
+    d = {}
+    for seed, name in ((5, "NaiveFFN"), (6, "SwiGLUFFN"), (7, "FusedSwiGLUFFN")):
+        torch.manual_seed(seed)
+        m = getattr(ref_ch01, name)(hidden, inter)
+        with torch.no_grad():
+            d[name] = m(torch.from_numpy(x)).numpy()
+        d.update({f"{name}_hash_{n}": np.array(array_hash(p.detach().numpy()))
+                  for n, p in m.named_parameters()})
+    torch.manual_seed(8)
+    tpm = importlib.import_module("ch09.tensor_parallel")  # not re-exported by ch09/__init__
+    mlp = tpm.TensorParallelMLP(tpm.TensorParallelConfig(
+        world_size=1, rank=0, hidden_dim=hidden, intermediate_dim=inter))
+    with torch.no_grad():
+        d["TensorParallelMLP"] = mlp(torch.from_numpy(x)).numpy()
+    d.update({f"TensorParallelMLP_hash_{n}": np.array(array_hash(p.detach().numpy()))
+              for n, p in mlp.named_parameters()})
+    np.savez_compressed(os.path.join(out_dir, "ffn.npz"), **d)
+    print("ffn: ok")
+
+
 def gen_tp(ref_ch09, out_dir):
     import torch
     d = {}
@@ -271,6 +299,7 @@ def main():
     gen_mha(ref["ch01"], args.out)
     gen_tp(ref["ch09"], args.out)
     gen_gqa(ref["ch01"], ref["ch02"], args.out)
+    gen_ffn(ref["ch01"], ref["ch09"], args.out)
     gen_analytic(ref, args.out)
 
 

@@ -1,0 +1,82 @@
+"""GPU parity of the fused SwiGLU projection (pli_gemm_swiglu) on every
+route -- skinny (m <= 16), small-M MFMA (m <= 128), 128x128 MFMA tile,
+generic (fp32 / ragged) -- against the f64 oracle, and of the FFN / TP-MLP
+modules that use it.  Bound: |err| <= tol * (|ref| + 1) (the outputs grow
+like sqrt(K)); bf16 1e-2, fp16 4e-3, fp32 1e-4 as for pli_gemm."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+from oracle.linear import swiglu
+from oracle.numerics import seeded_normal
+
+pytestmark = pytest.mark.gpu
+TDT = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}
+TOL = {"fp32": 1e-4, "fp16": 4e-3, "bf16": 1e-2}
+
+CASES = [  # m, n, k, dtype -> route
+    (1, 4096, 4096, "bf16"),     # skinny, decode batch 1
+    (5, 1376, 4096, "bf16"),     # skinny, n % 16 != 0
+    (16, 4096, 1024, "fp16"),    # small-M MFMA
+    (48, 2048, 512, "bf16"),     # small-M MFMA, NBG = 4
+    (128, 1024, 4096, "bf16"),   # small-M MFMA, NBG = 8
+    (200, 1000, 768, "bf16"),    # 128x128 tile, ragged m and n
+    (1024, 2048, 1024, "fp16"),  # 128x128 tile
+    (33, 100, 72, "bf16"),       # generic: n % 8 != 0
+    (64, 96, 40, "fp32"),        # generic fp32
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "m{}n{}k{}_{}".format(*c))
+def test_gemm_swiglu_vs_oracle(case):
+    import pli_hip
+    m, n, k, dt = case
+    x = seeded_normal((m, k), 1, dt) * 0.5
+    wg = seeded_normal((n, k), 2, dt) * k ** -0.5
+    wu = seeded_normal((n, k), 3, dt) * k ** -0.5
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda().to(TDT[dt])
+    h = pli_hip.gemm_swiglu(d(x), d(wg), d(wu))
+    ref = swiglu(x, wg, wu)
+    got = h.float().cpu().numpy().astype(np.float64)
+    bad = np.abs(got - ref) > TOL[dt] * (np.abs(ref) + 1)
+    assert not bad.any(), f"{bad.sum()} beyond tol, max err {np.abs(got - ref).max():.3e}"
+
+
+def test_gemm_swiglu_strided_halves_of_fused_weight():
+    """FusedSwiGLUFFN passes the two row halves of one [2n, k] weight."""
+    import pli_hip
+    m, n, k = 64, 512, 256
+    x = torch.randn(m, k, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(2 * n, k, device="cuda", dtype=torch.bfloat16) * k ** -0.5
+    h = pli_hip.gemm_swiglu(x, w[:n], w[n:])
+    ref = swiglu(x.float().cpu().numpy(), w[:n].float().cpu().numpy(), w[n:].float().cpu().numpy())
+    assert np.abs(h.float().cpu().numpy() - ref).max() <= 1e-2 * (np.abs(ref).max() + 1)
+
+
+@pytest.mark.parametrize("name,seed", [("NaiveFFN", 5), ("SwiGLUFFN", 6), ("FusedSwiGLUFFN", 7)])
+def test_ffn_modules_on_gpu_match_reference(name, seed):
+    import ch01
+    g = load_golden("ffn.npz")
+    torch.manual_seed(seed)
+    m = getattr(ch01, name)(256, 512).cuda()
+    x = torch.from_numpy(seeded_normal((2, 16, 256), 51)).cuda()
+    with torch.no_grad():
+        np.testing.assert_allclose(m(x).cpu().numpy(), g[name], rtol=1e-3, atol=1e-3)
+
+
+def test_tp_mlp_on_gpu_matches_reference_and_bf16_tracks():
+    from ch09 import TensorParallelConfig, TensorParallelMLP
+    g = load_golden("ffn.npz")
+    torch.manual_seed(8)
+    m = TensorParallelMLP(TensorParallelConfig(world_size=1, rank=0, hidden_dim=256,
+                                               intermediate_dim=512))
+    x = torch.from_numpy(seeded_normal((2, 16, 256), 51))
+    with torch.no_grad():
+        np.testing.assert_allclose(m.cuda()(x.cuda()).cpu().numpy(), g["TensorParallelMLP"],
+                                   rtol=1e-3, atol=1e-3)
+        yb = m.bfloat16()(x.cuda().bfloat16()).float().cpu().numpy()
+    rel = np.linalg.norm(yb - g["TensorParallelMLP"]) / np.linalg.norm(g["TensorParallelMLP"])
+    assert rel < 2e-2, rel

@@ -214,6 +214,52 @@ def tune_decode(configs=((1, 32, 8, 32768), (8, 32, 8, 4096), (32, 32, 8, 4096),
         torch.cuda.empty_cache()
 
 
+def tune_swiglu():
+    """Fused SwiGLU (one launch) vs unfused: torch (2 hipBLASLt GEMMs + silu*mul)
+    and HIP (2 pli_gemm + torch silu*mul), at TensorParallelConfig's defaults
+    (hidden 4096, intermediate 14336 = TP1; 1792 = the TP8 shard).  Weights
+    rotated over > 1 GiB for the decode sizes.  Graph-timed."""
+    import math
+    import torch.nn.functional as F
+    H = 4096
+    for inter in (14336, 1792):
+        wbytes = 2 * inter * H * 2
+        copies = max(2, min(12, math.ceil((1 << 30) / wbytes)))
+        wg = [torch.randn(inter, H, device="cuda", dtype=torch.bfloat16) * H ** -0.5 for _ in range(copies)]
+        wu = [torch.randn(inter, H, device="cuda", dtype=torch.bfloat16) * H ** -0.5 for _ in range(copies)]
+        for m in (1, 8, 32, 128, 4096):
+            x = torch.randn(m, H, device="cuda", dtype=torch.bfloat16)
+            out = torch.empty(m, inter, device="cuda", dtype=torch.bfloat16)
+            fns = {"fused": lambda a, b: pli_hip.gemm_swiglu(x, a, b, out=out),
+                   "hip_unfused": lambda a, b: torch.mul(F.silu(pli_hip.gemm(x, a, trans_b=True)),
+                                                         pli_hip.gemm(x, b, trans_b=True), out=out),
+                   "torch": lambda a, b: torch.mul(F.silu(x @ a.t()), x @ b.t(), out=out)}
+            graphs = {}
+            for nm, fn in fns.items():
+                for a, b in zip(wg, wu):
+                    fn(a, b)
+                torch.cuda.synchronize()
+                gr = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gr):
+                    for a, b in zip(wg, wu):
+                        fn(a, b)
+                graphs[nm] = gr
+            t = interleave({nm: g.replay for nm, g in graphs.items()}, 3, 3)
+            fns["torch"](wg[-1], wu[-1])
+            ref = out.float().clone()
+            fns["fused"](wg[-1], wu[-1])
+            err = ((out.float() - ref).abs().max() / (ref.abs().max() + 1e-6)).item()
+            flops = 2 * 2 * m * inter * H
+            nbytes = wbytes + (m * H + m * inter) * 2
+            print(json.dumps({"kernel": "swiglu", "m": m, "inter": inter,
+                              **{f"{nm}_us": t[nm][0] * 1e3 / copies for nm in t},
+                              **{f"{nm}_TFLOP/s": flops / (t[nm][0] * 1e-3 / copies) / 1e12 for nm in t},
+                              **{f"{nm}_GB/s": nbytes / (t[nm][0] * 1e-3 / copies) / 1e9 for nm in t},
+                              "rel_diff_vs_torch": err}), flush=True)
+        del wg, wu
+        torch.cuda.empty_cache()
+
+
 def tune_hbm():
     for nbytes in (1 << 28, 1 << 30):
         n = nbytes // 4
@@ -258,3 +304,5 @@ if __name__ == "__main__":
         tune_gemm()
     if "decode" in what:
         tune_decode()
+    if "swiglu" in what:
+        tune_swiglu()
