@@ -154,6 +154,30 @@ int pli_attn_decode(const void* q, const void* k, const void* v, void* o,
                     int causal, void* workspace, size_t workspace_bytes,
                     int dtype, void* stream);
 
+/* Graph-replayable decode (ch08/cuda_graph.py:18-82 captures the decode step;
+ * a captured launch cannot take the growing cache length as a host value).
+ *
+ * pli_kv_append: write n_new tokens of K and V ([B, n_new, Hkv, D]) into the
+ * caches at rows *pos_dev .. *pos_dev + n_new - 1 (rows >= capacity are
+ * dropped) -- the device-side form of KVCache.update, ch02/kv_cache.py:37-48.
+ * strides[12] in elements: {kn_b, kn_h, kn_n, kc_b, kc_h, kc_n, vc_b, vc_h,
+ * vc_n, vn_b, vn_h, vn_n}.  bf16/fp16, head_dim % 8 == 0.
+ *
+ * pli_attn_decode_dev: pli_attn_decode over n_kv = min(*n_kv_dev + n_kv_add,
+ * n_kv_max) valid cache rows; the split-K grid and the workspace are sized
+ * for n_kv_max (pli_attn_decode_workspace_size(..., n_kv_max, ...)).
+ * Fast-path shapes only (else PLI_EUNSUPPORTED). */
+int pli_kv_append(const void* k_new, const void* v_new, void* k_cache,
+                  void* v_cache, int batch, int n_new, int kv_heads,
+                  int head_dim, int capacity, const int64_t* strides,
+                  const int32_t* pos_dev, int dtype, void* stream);
+int pli_attn_decode_dev(const void* q, const void* k, const void* v, void* o,
+                        int batch, int heads, int kv_heads, int n_q,
+                        int n_kv_max, int head_dim, const int64_t* strides,
+                        float scale, int causal, const int32_t* n_kv_dev,
+                        int n_kv_add, void* workspace, size_t workspace_bytes,
+                        int dtype, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -34,16 +34,26 @@ def _lin(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 
 @dataclass
 class LayerKVCache:
-    """One layer's cache: k, v [batch, max_seq_len, num_kv_heads, head_dim]."""
+    """One layer's cache: k, v [batch, max_seq_len, num_kv_heads, head_dim].
+
+    ``pos`` (optional, this build): an int32 [1] device tensor holding the
+    number of valid rows, shared by all layers of a model and advanced by
+    ``CachedTransformerModel.forward``.  With it the append and the
+    single-token attention read the length on the device, so a decode step
+    can be captured once and replayed (``ch08.DecodeStepGraph``)."""
     k: torch.Tensor
     v: torch.Tensor
     seq_len: int = 0
+    pos: torch.Tensor | None = None
 
     def update(self, k_new: torch.Tensor, v_new: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
         """Append new K/V and return the valid prefixes (``:27-33``)."""
         n = k_new.shape[1]
-        self.k[:, self.seq_len:self.seq_len + n] = k_new
-        self.v[:, self.seq_len:self.seq_len + n] = v_new
+        if self.pos is not None:
+            pli_hip.kv_append(k_new, v_new, self.k, self.v, self.pos)
+        else:
+            self.k[:, self.seq_len:self.seq_len + n] = k_new
+            self.v[:, self.seq_len:self.seq_len + n] = v_new
         self.seq_len += n
         return self.k[:, :self.seq_len], self.v[:, :self.seq_len]
 
@@ -69,11 +79,24 @@ class CachedGQA(nn.Module):
         v = _lin(x, self.v_proj.weight).view(B, S, self.num_kv_heads, self.head_dim)
         if cache is not None:
             cache.update(k, v)
+            if cache.pos is not None and _device_len_ok(q, cache):
+                # length read on the device: replayable inside a captured step
+                o = pli_hip.attn_decode_dev(q, cache.k, cache.v, cache.pos, n_kv_add=S,
+                                            causal=S > 1)
+                return _lin(o.reshape(B, S, self.hidden_dim), self.o_proj.weight)
             k_buf, v_buf, n_kv = cache.k, cache.v, cache.seq_len
         else:
             k_buf, v_buf, n_kv = k, v, S
         o = attend_cached(q, k_buf, v_buf, n_kv).reshape(B, S, self.hidden_dim)
         return _lin(o, self.o_proj.weight)
+
+
+def _device_len_ok(q: torch.Tensor, cache: LayerKVCache) -> bool:
+    """Shapes the device-length decode kernel takes (the prompt, with more
+    query rows per kv head, goes through the host-length path)."""
+    B, S, H, D = q.shape
+    return (q.dtype in (torch.bfloat16, torch.float16) and D in (64, 128)
+            and S * (H // cache.k.shape[2]) <= 16)
 
 
 class RMSNorm(nn.Module):
@@ -140,13 +163,18 @@ class CachedTransformerModel(nn.Module):
         x = self.embed(input_ids)
         for i, layer in enumerate(self.layers):
             x = layer(x, caches[i] if caches is not None else None, start_pos)
+        if caches is not None and caches[0].pos is not None:
+            caches[0].pos.add_(input_ids.shape[1])  # one length shared by every layer
         return _lin(self.norm(x), self.lm_head.weight)
 
     def create_caches(self, batch_size: int, max_seq_len: int, device: torch.device,
-                      dtype: torch.dtype) -> list[LayerKVCache]:
+                      dtype: torch.dtype, device_pos: bool = False) -> list[LayerKVCache]:
+        """Per-layer caches (``:187-201``).  ``device_pos`` (this build) gives them
+        one shared device-resident length for graph-captured decode steps."""
         shape = (batch_size, max_seq_len, self.num_kv_heads, self.head_dim)
+        pos = torch.zeros(1, device=device, dtype=torch.int32) if device_pos else None
         return [LayerKVCache(k=torch.zeros(shape, device=device, dtype=dtype),
-                             v=torch.zeros(shape, device=device, dtype=dtype), seq_len=0)
+                             v=torch.zeros(shape, device=device, dtype=dtype), seq_len=0, pos=pos)
                 for _ in range(self.num_layers)]
 
 

@@ -1,0 +1,163 @@
+"""Graph-captured decode -- mirror of ``ch08/cuda_graph.py``.
+
+``GraphConfig`` / ``CUDAGraphRunner`` keep the reference's API
+(``ch08/cuda_graph.py:7-82``): one captured graph per batch size around a
+``model_fn(static_input)``.  On ROCm ``torch.cuda.CUDAGraph`` is a HIP graph,
+and every libpli_hip entry point is stream-ordered with no host sync or
+allocation, so the HIP kernels capture as they are.
+
+``DecodeStepGraph`` (this build) is what makes that useful for KV-cache
+generation: a decode step whose cache length is a host value cannot be
+replayed (the length is baked into the captured launches).  With caches from
+``CachedTransformerModel.create_caches(..., device_pos=True)`` the append
+(``pli_kv_append``) and the attention (``pli_attn_decode_dev``) read the
+length from one device int that the step itself advances, so ONE capture
+serves every later token: a step is one ``hipGraphLaunch`` instead of
+~(10 x layers) kernel launches from Python.
+"""
+from __future__ import annotations
+
+from collections.abc import Callable
+from dataclasses import dataclass
+
+import torch
+
+
+@dataclass
+class GraphConfig:
+    batch_sizes: list[int] = None
+    max_seq_len: int = 2048
+    warmup_iterations: int = 3
+
+    def __post_init__(self):
+        if self.batch_sizes is None:
+            self.batch_sizes = [1, 2, 4, 8, 16, 32]
+
+
+class CUDAGraphRunner:
+    """Capture ``model_fn`` once per batch size; replay with new inputs copied
+    into the static input buffer (``ch08/cuda_graph.py:18-82``)."""
+
+    def __init__(self, config: GraphConfig, model_fn: Callable | None = None):
+        self.config = config
+        self.model_fn = model_fn
+        self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
+        self.static_inputs: dict[int, dict[str, torch.Tensor]] = {}
+        self.static_outputs: dict[int, torch.Tensor] = {}
+
+    def capture_graph(self, batch_size: int, input_shape: tuple, dtype: torch.dtype = torch.float16,
+                      device: str = "cuda") -> bool:
+        if not torch.cuda.is_available() or self.model_fn is None:
+            return False
+        static_input = torch.zeros(batch_size, *input_shape, dtype=dtype, device=device)
+        for _ in range(self.config.warmup_iterations):
+            self.model_fn(static_input)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            static_output = self.model_fn(static_input)
+        self.graphs[batch_size] = graph
+        self.static_inputs[batch_size] = {"input": static_input}
+        self.static_outputs[batch_size] = static_output
+        return True
+
+    def run_graph(self, batch_size: int, input_tensor: torch.Tensor) -> torch.Tensor | None:
+        if batch_size not in self.graphs:
+            return None
+        self.static_inputs[batch_size]["input"].copy_(input_tensor)
+        self.graphs[batch_size].replay()
+        return self.static_outputs[batch_size].clone()
+
+    def has_graph(self, batch_size: int) -> bool:
+        return batch_size in self.graphs
+
+    def get_captured_batch_sizes(self) -> list[int]:
+        return list(self.graphs.keys())
+
+
+class DecodeStepGraph:
+    """One captured single-token decode step of a ``ch02.CachedTransformerModel``.
+
+        g = DecodeStepGraph(model, batch_size=8, max_seq_len=4096, dtype=torch.bfloat16)
+        logits = g.prefill(prompt_ids)           # eager; fills the caches
+        for _ in range(n):
+            tok = sample(logits[:, -1])
+            logits = g.step(tok)                 # one graph launch per token
+
+    ``step`` returns the static logits buffer [B, 1, vocab] (overwritten by the
+    next step; clone to keep it).
+    """
+
+    def __init__(self, model, batch_size: int, max_seq_len: int, dtype: torch.dtype,
+                 device: torch.device | str = "cuda", warmup: int = 2):
+        self.model = model
+        self.caches = model.create_caches(batch_size, max_seq_len, torch.device(device), dtype,
+                                          device_pos=True)
+        self.pos = self.caches[0].pos
+        self.static_ids = torch.zeros(batch_size, 1, dtype=torch.long, device=device)
+        self.graph: torch.cuda.CUDAGraph | None = None
+        self.static_logits: torch.Tensor | None = None
+        self.warmup = warmup
+
+    @property
+    def seq_len(self) -> int:
+        return self.caches[0].seq_len
+
+    def _set_len(self, n: int) -> None:
+        for c in self.caches:
+            c.seq_len = n
+        self.pos.fill_(n)
+
+    @torch.no_grad()
+    def prefill(self, input_ids: torch.Tensor) -> torch.Tensor:
+        logits = self.model(input_ids, self.caches, start_pos=self.seq_len)
+        if self.graph is None:
+            self._capture()
+        return logits
+
+    @torch.no_grad()
+    def _capture(self) -> None:
+        # warm-up and capture run real steps; they write row `n` of every cache,
+        # which the first replayed step overwrites, and the length is restored
+        n = self.seq_len
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(self.warmup):
+                self.model(self.static_ids, self.caches, start_pos=n)
+                self._set_len(n)
+        torch.cuda.current_stream().wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.static_logits = self.model(self.static_ids, self.caches, start_pos=n)
+        torch.cuda.synchronize()
+        self._set_len(n)
+
+    @torch.no_grad()
+    def step(self, token_ids: torch.Tensor) -> torch.Tensor:
+        if self.graph is None:
+            raise RuntimeError("DecodeStepGraph.step before prefill")
+        if self.seq_len >= self.caches[0].k.shape[1]:
+            raise RuntimeError("KV cache full")
+        self.static_ids.copy_(token_ids.view_as(self.static_ids))
+        self.graph.replay()
+        for c in self.caches:  # host bookkeeping of the device-side append
+            c.seq_len += 1
+        return self.static_logits
+
+
+def explain_cuda_graphs() -> str:
+    return """
+HIP graphs on MI355X (torch.cuda.CUDAGraph on ROCm)
+
+Problem: a decode step is ~10 kernels per layer; from Python each launch
+costs several microseconds of host time, more than the kernels themselves at
+small batch.
+
+Solution: capture the step once, replay it with one launch.
+  - every libpli_hip entry point is stream-ordered, allocation-free and
+    sync-free, so it captures as is;
+  - the KV-cache length lives in device memory (pli_kv_append,
+    pli_attn_decode_dev), so one capture serves every token position;
+  - new tokens are copied into the static input buffer before each replay.
+"""

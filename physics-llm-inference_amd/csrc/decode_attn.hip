@@ -65,7 +65,10 @@ __global__ __launch_bounds__(256, (MODE & 2) ? 3 : 2) void attn_decode_chunk(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
     const uint16_t* __restrict__ v, uint16_t* __restrict__ o, float* __restrict__ part_o,
     float2* __restrict__ part_ml, int Hkv, int G, int Nq, int Nk, int M, DecStrides st, float c,
-    int causal, int chunk, int splits) {
+    int causal, int chunk, int splits, const int* __restrict__ nk_dev, int nk_add) {
+    // graph-replayable form: the valid length lives in device memory (the
+    // grid is planned for the capacity Nk; chunks past the length exit empty)
+    if (nk_dev != nullptr) Nk = max(0, min(Nk, *nk_dev + nk_add));
     constexpr bool RM = (MODE & 8) != 0;
     using L = DecLayout<D, RM>;
     constexpr int KSTEPS = D / 32;  // 32-d k-steps of K.Q^T
@@ -370,9 +373,11 @@ constexpr int kDefaultDecodeMode = 13;
 template <typename T, int D>
 int launch_decode(const void* q, const void* k, const void* v, void* o, int B, int Hkv, int G,
                   int Nq, int Nk, const DecStrides& st, float scale, int causal, float* ws,
-                  hipStream_t stream, int mode, int target) {
+                  hipStream_t stream, int mode, int target, const int* nk_dev = nullptr,
+                  int nk_add = 0) {
     const int64_t bh = (int64_t)B * Hkv;
     const DecPlan p = plan_decode(bh, Nk, target > 0 ? target : kDefaultTargetWgs);
+    if (nk_dev == nullptr && Nk == 0) return PLI_OK;
     const int M = Nq * G;
     PLI_REQUIRE(bh * p.splits < (1ll << 31), "pli_attn_decode: grid too large");
     const float c = scale * 1.4426950408889634f;
@@ -382,7 +387,7 @@ int launch_decode(const void* q, const void* k, const void* v, void* o, int B, i
     hipLaunchKernelGGL((attn_decode_chunk<T, D, MODE>), dim3((unsigned)(bh * p.splits)), dim3(256), \
                        0, stream, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,     \
                        (uint16_t*)o, part_o, part_ml, Hkv, G, Nq, Nk, M, st, c, causal, p.chunk, \
-                       p.splits)
+                       p.splits, nk_dev, nk_add)
     switch (mode < 0 ? kDefaultDecodeMode : mode) {
         case 1: PLI_DEC_LAUNCH(1); break;
         case 2: PLI_DEC_LAUNCH(2); break;
@@ -403,8 +408,64 @@ int launch_decode(const void* q, const void* k, const void* v, void* o, int B, i
     return launch_status("pli_attn_decode");
 }
 
+// Append n_new tokens of K and V to the caches at the device-resident
+// position *pos (+ i); rows past the capacity are dropped.  One thread per
+// 16-byte chunk.
+__global__ __launch_bounds__(256) void kv_append_kernel(
+    const uint16_t* __restrict__ kn, const uint16_t* __restrict__ vn, uint16_t* __restrict__ kc,
+    uint16_t* __restrict__ vc, int B, int T, int Hkv, int D, int cap, DecStrides st,
+    const int* __restrict__ pos) {
+    const int cpr = D / 8;
+    const int64_t total = (int64_t)B * T * Hkv * cpr;
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= total) return;
+    const int ch = idx % cpr;
+    const int h = (idx / cpr) % Hkv;
+    const int t = (idx / ((int64_t)cpr * Hkv)) % T;
+    const int b = idx / ((int64_t)cpr * Hkv * T);
+    const int row = *pos + t;
+    if (row < 0 || row >= cap) return;
+    // strides: q.. slots carry the new tensors, k/v slots the caches
+    const uint16_t* ks = kn + b * st.qb + h * st.qh + (int64_t)t * st.qn + 8 * ch;
+    const uint16_t* vs = vn + b * st.ob + h * st.oh + (int64_t)t * st.on + 8 * ch;
+    uint16_t* kd = kc + b * st.kb + h * st.kh + (int64_t)row * st.kn + 8 * ch;
+    uint16_t* vd = vc + b * st.vb + h * st.vh + (int64_t)row * st.vn + 8 * ch;
+    *reinterpret_cast<i32x4*>(kd) = *reinterpret_cast<const i32x4*>(ks);
+    *reinterpret_cast<i32x4*>(vd) = *reinterpret_cast<const i32x4*>(vs);
+}
+
 }  // namespace
 }  // namespace pli
+
+extern "C" int pli_kv_append(const void* k_new, const void* v_new, void* k_cache, void* v_cache,
+                             int batch, int n_new, int kv_heads, int head_dim, int capacity,
+                             const int64_t* strides, const int32_t* pos_dev, int dtype,
+                             void* stream) {
+    using namespace pli;
+    clear_error();
+    PLI_REQUIRE(k_new && v_new && k_cache && v_cache && strides && pos_dev,
+                "pli_kv_append: null pointer");
+    PLI_REQUIRE(batch >= 0 && n_new >= 0 && kv_heads > 0 && head_dim > 0 && capacity >= 0,
+                "pli_kv_append: bad shape B=%d T=%d Hkv=%d D=%d cap=%d", batch, n_new, kv_heads,
+                head_dim, capacity);
+    PLI_REQUIRE(dtype == PLI_F16 || dtype == PLI_BF16, "pli_kv_append: dtype %d (16-bit caches only)",
+                dtype);
+    PLI_REQUIRE(head_dim % 8 == 0 && aligned16(k_new) && aligned16(v_new) && aligned16(k_cache) &&
+                    aligned16(v_cache),
+                "pli_kv_append: head_dim %% 8 and 16-byte aligned operands required");
+    for (int i = 0; i < 12; ++i)
+        PLI_REQUIRE(strides[i] % 8 == 0, "pli_kv_append: stride %d not a multiple of 8", i);
+    const int64_t total = (int64_t)batch * n_new * kv_heads * (head_dim / 8);
+    if (total == 0) return PLI_OK;
+    // strides[12] = {kn_b, kn_h, kn_n, kc_b, kc_h, kc_n, vc_b, vc_h, vc_n, vn_b, vn_h, vn_n}
+    const DecStrides st{strides[0], strides[1], strides[2], strides[3], strides[4], strides[5],
+                        strides[6], strides[7], strides[8], strides[9], strides[10], strides[11]};
+    hipLaunchKernelGGL(kv_append_kernel, dim3((unsigned)cdiv(total, (int64_t)256)), dim3(256), 0,
+                       (hipStream_t)stream, (const uint16_t*)k_new, (const uint16_t*)v_new,
+                       (uint16_t*)k_cache, (uint16_t*)v_cache, batch, n_new, kv_heads, head_dim,
+                       capacity, st, pos_dev);
+    return launch_status("pli_kv_append");
+}
 
 extern "C" size_t pli_attn_decode_workspace_size(int batch, int heads, int kv_heads, int n_q,
                                                  int n_kv, int head_dim) {
@@ -477,6 +538,45 @@ extern "C" int pli_attn_decode_variant(const void* q, const void* k, const void*
     return head_dim == 128
                ? launch_decode<f16_t, 128>(q, k, v, o, batch, kv_heads, G, n_q, n_kv, st, scale, causal, ws, s, mode, target_wgs)
                : launch_decode<f16_t, 64>(q, k, v, o, batch, kv_heads, G, n_q, n_kv, st, scale, causal, ws, s, mode, target_wgs);
+}
+
+extern "C" int pli_attn_decode_dev(const void* q, const void* k, const void* v, void* o,
+                                   int batch, int heads, int kv_heads, int n_q, int n_kv_max,
+                                   int head_dim, const int64_t* strides, float scale, int causal,
+                                   const int32_t* n_kv_dev, int n_kv_add, void* workspace,
+                                   size_t workspace_bytes, int dtype, void* stream) {
+    using namespace pli;
+    clear_error();
+    PLI_REQUIRE(q && k && v && o && strides && n_kv_dev, "pli_attn_decode_dev: null pointer");
+    PLI_REQUIRE(batch >= 0 && heads > 0 && kv_heads > 0 && n_q >= 0 && n_kv_max >= 0 &&
+                    head_dim > 0 && heads % kv_heads == 0,
+                "pli_attn_decode_dev: bad shape B=%d H=%d Hkv=%d Nq=%d Nmax=%d D=%d", batch, heads,
+                kv_heads, n_q, n_kv_max, head_dim);
+    PLI_REQUIRE(std::isfinite(scale), "pli_attn_decode_dev: non-finite scale");
+    if (batch == 0 || n_q == 0) return PLI_OK;
+    if (!(decode_fast_path(heads, kv_heads, n_q, n_kv_max, head_dim, dtype, strides) &&
+          aligned16(q) && aligned16(k) && aligned16(v) && aligned16(o))) {
+        set_error("pli_attn_decode_dev: needs bf16/fp16, head_dim 64/128, <= 16 rows per kv "
+                  "head, 16-byte aligned operands");
+        return PLI_EUNSUPPORTED;
+    }
+    const size_t need =
+        pli_attn_decode_workspace_size(batch, heads, kv_heads, n_q, n_kv_max, head_dim);
+    PLI_REQUIRE(workspace_bytes >= need && (need == 0 || workspace != nullptr),
+                "pli_attn_decode_dev: workspace of %zu bytes needed, %zu given", need,
+                workspace_bytes);
+    const DecStrides st{strides[0], strides[1], strides[2], strides[3], strides[4], strides[5],
+                        strides[6], strides[7], strides[8], strides[9], strides[10], strides[11]};
+    const int G = heads / kv_heads;
+    hipStream_t s = (hipStream_t)stream;
+    float* ws = (float*)workspace;
+    if (dtype == PLI_BF16)
+        return head_dim == 128
+                   ? launch_decode<bf16_t, 128>(q, k, v, o, batch, kv_heads, G, n_q, n_kv_max, st, scale, causal, ws, s, -1, 0, n_kv_dev, n_kv_add)
+                   : launch_decode<bf16_t, 64>(q, k, v, o, batch, kv_heads, G, n_q, n_kv_max, st, scale, causal, ws, s, -1, 0, n_kv_dev, n_kv_add);
+    return head_dim == 128
+               ? launch_decode<f16_t, 128>(q, k, v, o, batch, kv_heads, G, n_q, n_kv_max, st, scale, causal, ws, s, -1, 0, n_kv_dev, n_kv_add)
+               : launch_decode<f16_t, 64>(q, k, v, o, batch, kv_heads, G, n_q, n_kv_max, st, scale, causal, ws, s, -1, 0, n_kv_dev, n_kv_add);
 }
 
 extern "C" int pli_attn_decode(const void* q, const void* k, const void* v, void* o, int batch,

@@ -42,6 +42,11 @@ _SIGS = {
     "pli_softmax_rows": [_vp, _vp, _c_i64, _c_int, _c_int, _vp],
     "pli_online_softmax_with_output": [_vp, _vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_int, _vp],
     "pli_attn_decode_workspace_size": [_c_int] * 6,
+    "pli_kv_append": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int,
+                      ctypes.POINTER(_c_i64), _vp, _c_int, _vp],
+    "pli_attn_decode_dev": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
+                            ctypes.POINTER(_c_i64), _c_f32, _c_int, _vp, _c_int, _vp,
+                            ctypes.c_size_t, _c_int, _vp],
     "pli_attn_decode": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
                         ctypes.POINTER(_c_i64), _c_f32, _c_int, _vp, ctypes.c_size_t, _c_int, _vp],
     # tuning entry points (not part of include/pli.h): explicit kernel variant
@@ -228,6 +233,55 @@ def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, n
             rc = lib().pli_attn_decode_variant(*args, -1 if variant is None else int(variant),
                                                int(target_wgs))
     _check(rc, "pli_attn_decode")
+    return out
+
+
+def kv_append(k_new: torch.Tensor, v_new: torch.Tensor, k_cache: torch.Tensor,
+              v_cache: torch.Tensor, pos: torch.Tensor) -> None:
+    """Write [B, T, Hkv, D] K/V into [B, S, Hkv, D] caches at rows pos[0] +
+    (0..T-1), pos an int32 device tensor (graph-replayable KVCache.update)."""
+    dev = _require_gpu(k_new, v_new, k_cache, v_cache)
+    if pos.dtype != torch.int32 or not pos.is_cuda:
+        raise PliError("pos must be an int32 device tensor")
+    B, T, Hkv, D = k_new.shape
+    if tuple(v_new.shape) != tuple(k_new.shape) or k_cache.shape[0] != B or \
+            tuple(k_cache.shape[2:]) != (Hkv, D) or tuple(v_cache.shape) != tuple(k_cache.shape):
+        raise PliError(f"kv_append shape mismatch new{tuple(k_new.shape)} cache{tuple(k_cache.shape)}")
+    st = (_c_i64 * 12)(*(int(x) for t in (k_new, k_cache, v_cache, v_new)
+                         for x in (t.stride(0), t.stride(2), t.stride(1))))
+    with _on_device(dev):
+        rc = lib().pli_kv_append(_ptr(k_new), _ptr(v_new), _ptr(k_cache), _ptr(v_cache), B, T, Hkv,
+                                 D, k_cache.shape[1], st, _ptr(pos), _dtype_code(k_new), _stream(dev))
+    _check(rc, "pli_kv_append")
+
+
+def attn_decode_dev(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                    n_kv_dev: torch.Tensor, n_kv_add: int = 0, n_kv_max: int | None = None,
+                    scale: float | None = None, causal: bool = True,
+                    out: torch.Tensor | None = None, workspace: torch.Tensor | None = None
+                    ) -> torch.Tensor:
+    """attn_decode with the valid length n_kv_dev[0] + n_kv_add read on the
+    device (graph-replayable); the grid is planned for n_kv_max (default: the
+    cache capacity)."""
+    dev = _require_gpu(q, k_cache, v_cache)
+    B, Sq, H, D = q.shape
+    Hkv = k_cache.shape[2]
+    n_max = k_cache.shape[1] if n_kv_max is None else int(n_kv_max)
+    if out is None:
+        out = torch.empty((B, Sq, H, D), device=q.device, dtype=q.dtype)
+    if scale is None:
+        scale = D ** -0.5
+    st = (_c_i64 * 12)(*(int(x) for t in (q, k_cache, v_cache, out)
+                         for x in (t.stride(0), t.stride(2), t.stride(1))))
+    ws_bytes = int(lib().pli_attn_decode_workspace_size(B, H, Hkv, Sq, n_max, D))
+    if workspace is None or workspace.numel() * 4 < ws_bytes:
+        workspace = torch.empty(max(ws_bytes // 4, 1), device=q.device, dtype=torch.float32)
+    with _on_device(dev):
+        rc = lib().pli_attn_decode_dev(_ptr(q), _ptr(k_cache), _ptr(v_cache), _ptr(out), B, H, Hkv,
+                                       Sq, n_max, D, st, float(scale), int(bool(causal)),
+                                       _ptr(n_kv_dev), int(n_kv_add), _ptr(workspace), ws_bytes,
+                                       _dtype_code(q), _stream(dev))
+    _check(rc, "pli_attn_decode_dev")
     return out
 
 

@@ -115,3 +115,15 @@ def test_reference_ch02_contracts():
     out, t = cached_generate(model, ids, max_new_tokens=10)
     assert out.shape == (1, 15) and torch.equal(out[:, :5], ids)
     assert len(t["decode_ms"]) == 9 and t["total_ms"] >= t["prefill_ms"]
+
+
+def test_ch08_graph_runner_without_gpu():
+    """The reference's CUDAGraphRunner contract on a host without a device:
+    capture reports False, run_graph None (ch08/cuda_graph.py:37-41, 69-70)."""
+    from ch08 import CUDAGraphRunner, GraphConfig
+    cfg = GraphConfig()
+    assert cfg.batch_sizes == [1, 2, 4, 8, 16, 32] and cfg.max_seq_len == 2048
+    r = CUDAGraphRunner(cfg, model_fn=lambda x: x)
+    if not torch.cuda.is_available():
+        assert r.capture_graph(1, (8,)) is False
+    assert r.run_graph(3, torch.zeros(3, 8)) is None and r.get_captured_batch_sizes() in ([], [1])

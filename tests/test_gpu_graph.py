@@ -1,0 +1,98 @@
+"""GPU checks of graph-replayable decode: pli_kv_append, pli_attn_decode_dev,
+ch08.DecodeStepGraph over ch02.CachedTransformerModel, and the reference's
+CUDAGraphRunner API (ch08/cuda_graph.py:18-82)."""
+from __future__ import annotations
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_kv_append_matches_slice_assignment():
+    import pli_hip
+    B, S, Hkv, D, T = 3, 64, 4, 128, 5
+    kc = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    ref_k, ref_v = kc.clone(), vc.clone()
+    kn = torch.randn(B, T, Hkv, D, device="cuda", dtype=torch.bfloat16)
+    vn = torch.randn_like(kn)
+    pos = torch.tensor([17], device="cuda", dtype=torch.int32)
+    pli_hip.kv_append(kn, vn, kc, vc, pos)
+    ref_k[:, 17:22], ref_v[:, 17:22] = kn, vn
+    assert torch.equal(kc, ref_k) and torch.equal(vc, ref_v)
+    pos.fill_(S - 2)  # rows past the capacity are dropped, not written out of bounds
+    pli_hip.kv_append(kn, vn, kc, vc, pos)
+    ref_k[:, S - 2:], ref_v[:, S - 2:] = kn[:, :2], vn[:, :2]
+    assert torch.equal(kc, ref_k) and torch.equal(vc, ref_v)
+
+
+@pytest.mark.parametrize("n,add", [(1, 0), (300, 1), (4095, 1), (2000, 3)])
+def test_attn_decode_dev_equals_host_length(n, add):
+    import pli_hip
+    B, H, Hkv, D, S = 2, 32, 8, 128, 4096
+    Sq = add if add else 1
+    q = torch.randn(B, Sq, H, D, device="cuda", dtype=torch.bfloat16)
+    kc = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    n_dev = torch.tensor([n], device="cuda", dtype=torch.int32)
+    got = pli_hip.attn_decode_dev(q, kc, vc, n_dev, n_kv_add=add, causal=Sq > 1)
+    ref = pli_hip.attn_decode(q, kc, vc, min(n + add, S), causal=Sq > 1)
+    assert (got.float() - ref.float()).abs().max().item() <= 2 ** -7
+
+
+def _model():
+    from ch02 import CachedTransformerModel
+    torch.manual_seed(0)
+    return CachedTransformerModel(1000, 512, 2, 8, 2, 1024).cuda().bfloat16().eval()
+
+
+def test_decode_step_graph_replays_eager_steps():
+    """Greedy decode: graph replay == eager steps over the same device-length
+    kernels (bitwise), and tracks the host-length eager path."""
+    from ch08 import DecodeStepGraph
+    model = _model()
+    B, P, N = 2, 24, 12
+    ids = torch.randint(0, 1000, (B, P), device="cuda")
+    with torch.no_grad():
+        # eager, device-length caches
+        caches = model.create_caches(B, 64, torch.device("cuda"), torch.bfloat16, device_pos=True)
+        lg = model(ids, caches)
+        eager, tok = [], lg[:, -1:].argmax(-1)
+        for _ in range(N):
+            lg = model(tok, caches, start_pos=caches[0].seq_len)
+            eager.append(lg.float().clone())
+            tok = lg[:, -1:].argmax(-1)
+        # host-length caches (pli_attn_decode with a host n_kv)
+        hc = model.create_caches(B, 64, torch.device("cuda"), torch.bfloat16)
+        lg = model(ids, hc)
+        host, tok = [], lg[:, -1:].argmax(-1)
+        for _ in range(N):
+            lg = model(tok, hc, start_pos=hc[0].seq_len)
+            host.append(lg.float().clone())
+            tok = lg[:, -1:].argmax(-1)
+        # graph
+        g = DecodeStepGraph(model, B, 64, torch.bfloat16)
+        lg = g.prefill(ids)
+        tok = lg[:, -1:].argmax(-1)
+        for i in range(N):
+            lg = g.step(tok)
+            assert torch.equal(lg.float(), eager[i]), f"step {i}"
+            rel = (lg.float() - host[i]).norm() / host[i].norm()
+            assert rel < 1e-2, (i, float(rel))
+            tok = lg[:, -1:].argmax(-1)
+    assert g.seq_len == P + N and int(g.pos.item()) == P + N
+    assert all(c.seq_len == P + N for c in g.caches)
+
+
+def test_cuda_graph_runner_api():
+    from ch08 import CUDAGraphRunner, GraphConfig
+    w = torch.randn(64, 64, device="cuda", dtype=torch.float16)
+    runner = CUDAGraphRunner(GraphConfig(batch_sizes=[1, 4]), model_fn=lambda x: torch.relu(x @ w))
+    for b in (1, 4):
+        assert runner.capture_graph(b, (64,))
+    x = torch.randn(4, 64, device="cuda", dtype=torch.float16)
+    out = runner.run_graph(4, x)
+    torch.testing.assert_close(out, torch.relu(x @ w))
+    assert runner.run_graph(2, x[:2]) is None
+    assert runner.has_graph(1) and sorted(runner.get_captured_batch_sizes()) == [1, 4]

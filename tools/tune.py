@@ -260,6 +260,43 @@ def tune_swiglu():
         torch.cuda.empty_cache()
 
 
+def tune_graph(batches=(1, 8, 32), prompt=512, steps=32):
+    """ch02 decode step of a Llama-shaped model (vocab 32000, hidden 2048,
+    16 layers, 32/8 heads, intermediate 5632, bf16): per-token latency of
+    eager steps (host-length caches) vs one HIP-graph launch per step
+    (ch08.DecodeStepGraph, device-length caches)."""
+    import time
+    from ch02 import CachedTransformerModel
+    from ch08 import DecodeStepGraph
+    torch.manual_seed(0)
+    model = CachedTransformerModel(32000, 2048, 16, 32, 8, 5632).cuda().bfloat16().eval()
+    for B in batches:
+        ids = torch.randint(0, 32000, (B, prompt), device="cuda")
+        tok = torch.randint(0, 32000, (B, 1), device="cuda")
+        res = {}
+        with torch.no_grad():
+            for mode in ("eager", "eager_devlen", "graph"):
+                if mode == "graph":
+                    g = DecodeStepGraph(model, B, prompt + steps + 8, torch.bfloat16)
+                    g.prefill(ids)
+                    fn = lambda: g.step(tok)  # noqa: E731
+                else:
+                    caches = model.create_caches(B, prompt + steps + 8, torch.device("cuda"),
+                                                 torch.bfloat16, device_pos=(mode == "eager_devlen"))
+                    model(ids, caches)
+                    fn = lambda: model(tok, caches, start_pos=caches[0].seq_len)  # noqa: E731
+                fn()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(steps - 1):
+                    fn()
+                torch.cuda.synchronize()
+                res[mode] = (time.perf_counter() - t0) / (steps - 1) * 1e3
+        print(json.dumps({"kernel": "decode_step", "batch": B, "prompt": prompt,
+                          **{f"{k}_ms_per_token": v for k, v in res.items()},
+                          **{f"{k}_tok/s": B / (v * 1e-3) for k, v in res.items()}}), flush=True)
+
+
 def tune_hbm():
     for nbytes in (1 << 28, 1 << 30):
         n = nbytes // 4
@@ -306,3 +343,5 @@ if __name__ == "__main__":
         tune_decode()
     if "swiglu" in what:
         tune_swiglu()
+    if "graph" in what:
+        tune_graph()
