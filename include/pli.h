@@ -154,6 +154,18 @@ int pli_attn_decode(const void* q, const void* k, const void* v, void* o,
                     int causal, void* workspace, size_t workspace_bytes,
                     int dtype, void* stream);
 
+/*
+ * RMSNorm with an optional fused residual add (rows of n elements):
+ *   h = x + residual (stored in dtype, as the torch add would; h = x when
+ *   residual is NULL), y = h / sqrt(mean(h^2) + eps) * weight, fp32 statistics.
+ * Replaces ch02/cached_generation.py:101-109 (RMSNorm.forward) and the
+ * residual adds of CachedTransformerBlock.forward (:143-145).  residual and
+ * h_out may be NULL; h_out must not alias x or residual.
+ */
+int pli_rmsnorm(const void* x, const void* residual, const void* weight, void* y,
+                void* h_out, int64_t rows, int n, int64_t ldx, int64_t ldr,
+                int64_t ldy, int64_t ldh, float eps, int dtype, void* stream);
+
 /* Graph-replayable decode (ch08/cuda_graph.py:18-82 captures the decode step;
  * a captured launch cannot take the growing cache length as a host value).
  *

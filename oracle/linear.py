@@ -62,3 +62,13 @@ def swiglu(x, w_gate, w_up):
 def swiglu_ffn(x, w_gate, w_up, w_down):
     """down(silu(gate(x)) * up(x)), ``SwiGLUFFN.forward`` (``ch01/ffn.py:26-31``)."""
     return swiglu(x, w_gate, w_up) @ np.asarray(w_down, np.float64).T
+
+
+def rms_norm(x, weight, eps=1e-6, residual=None):
+    """x / sqrt(mean(x^2) + eps) * weight over the last dim, float64
+    (``RMSNorm.forward``, ``ch02/cached_generation.py:101-109``); with a
+    residual, of h = x + residual (``CachedTransformerBlock``, ``:143-145``)."""
+    h = np.asarray(x, np.float64)
+    if residual is not None:
+        h = h + np.asarray(residual, np.float64)
+    return h / np.sqrt(np.mean(h * h, axis=-1, keepdims=True) + eps) * np.asarray(weight, np.float64)

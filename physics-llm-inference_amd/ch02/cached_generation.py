@@ -11,8 +11,11 @@ and ``state_dict``s are interchangeable.  On a ROCm device:
 * ``SwiGLUFFN`` runs gate + up + silu·mul as one ``pli_gemm_swiglu`` launch
   and down on ``pli_gemm``;
 * ``CachedTransformerModel``'s ``lm_head`` runs on ``pli_gemm``.
-Embedding lookup, RMSNorm, residual adds and sampling stay in torch (they
-are not on the measured path).  CPU tensors keep the reference math.
+* ``RMSNorm`` is one ``pli_rmsnorm`` launch, and the model folds every
+  residual add into the following norm's launch (2 launches per layer
+  instead of 14 elementwise/reduce kernels).
+Embedding lookup and sampling stay in torch.  CPU tensors keep the
+reference math.
 """
 from __future__ import annotations
 
@@ -106,6 +109,8 @@ class RMSNorm(nn.Module):
         self.eps = eps
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if x.is_cuda:  # one launch (pli_rmsnorm) instead of six elementwise/reduce kernels
+            return pli_hip.rmsnorm(x, self.weight, self.eps)
         return x / torch.sqrt(torch.mean(x ** 2, dim=-1, keepdim=True) + self.eps) * self.weight
 
 
@@ -136,8 +141,24 @@ class CachedTransformerBlock(nn.Module):
 
     def forward(self, x: torch.Tensor, cache: LayerKVCache | None = None, start_pos: int = 0
                 ) -> torch.Tensor:
+        if x.is_cuda:
+            h, n2 = self.attn_half(x, None, cache, start_pos)
+            return h + self.ffn(n2)
         h = x + self.attn(self.input_norm(x), cache, start_pos)
         return h + self.ffn(self.post_attn_norm(h))
+
+    def attn_half(self, x: torch.Tensor, pending: torch.Tensor | None,
+                  cache: LayerKVCache | None, start_pos: int):
+        """Device path: x (+ the previous layer's pending FFN output, added in
+        the input norm's launch) -> attention -> (h, post_attn_norm(h)), the
+        residual add fused into the post-attention norm's launch."""
+        if pending is None:
+            n1 = pli_hip.rmsnorm(x, self.input_norm.weight, self.input_norm.eps)
+        else:
+            x, n1 = pli_hip.rmsnorm(pending, self.input_norm.weight, self.input_norm.eps,
+                                    residual=x)
+        a = self.attn(n1, cache, start_pos)
+        return pli_hip.rmsnorm(a, self.post_attn_norm.weight, self.post_attn_norm.eps, residual=x)
 
 
 class CachedTransformerModel(nn.Module):
@@ -161,10 +182,24 @@ class CachedTransformerModel(nn.Module):
     def forward(self, input_ids: torch.Tensor, caches: list[LayerKVCache] | None = None,
                 start_pos: int = 0) -> torch.Tensor:
         x = self.embed(input_ids)
+        if x.is_cuda:
+            # residual stream with the adds folded into the norms: per layer one
+            # norm(+add) before attention, one after; the FFN output stays
+            # pending until the next layer's (or the final) norm adds it
+            pending = None
+            for i, layer in enumerate(self.layers):
+                x, n2 = layer.attn_half(x, pending, caches[i] if caches is not None else None,
+                                        start_pos)
+                pending = layer.ffn(n2)
+            if caches is not None and caches[0].pos is not None:
+                caches[0].pos.add_(input_ids.shape[1])  # one length shared by every layer
+            if pending is None:  # no layers
+                xn = pli_hip.rmsnorm(x, self.norm.weight, self.norm.eps)
+            else:
+                _, xn = pli_hip.rmsnorm(pending, self.norm.weight, self.norm.eps, residual=x)
+            return _lin(xn, self.lm_head.weight)
         for i, layer in enumerate(self.layers):
             x = layer(x, caches[i] if caches is not None else None, start_pos)
-        if caches is not None and caches[0].pos is not None:
-            caches[0].pos.add_(input_ids.shape[1])  # one length shared by every layer
         return _lin(self.norm(x), self.lm_head.weight)
 
     def create_caches(self, batch_size: int, max_seq_len: int, device: torch.device,

@@ -38,6 +38,8 @@ _SIGS = {
                  _c_int, _vp],
     "pli_gemm_swiglu": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_i64, _c_i64, _c_i64,
                         _c_i64, _c_int, _vp],
+    "pli_rmsnorm": [_vp, _vp, _vp, _vp, _vp, _c_i64, _c_int, _c_i64, _c_i64, _c_i64, _c_i64,
+                    _c_f32, _c_int, _vp],
     "pli_scale_copy": [_vp, _vp, _c_i64, _c_int, _vp],
     "pli_softmax_rows": [_vp, _vp, _c_i64, _c_int, _c_int, _vp],
     "pli_online_softmax_with_output": [_vp, _vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_int, _vp],
@@ -283,6 +285,40 @@ def attn_decode_dev(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
                                        _dtype_code(q), _stream(dev))
     _check(rc, "pli_attn_decode_dev")
     return out
+
+
+# ------------------------------------------------------------------ RMSNorm
+def rmsnorm(x: torch.Tensor, weight: torch.Tensor, eps: float = 1e-6,
+            residual: torch.Tensor | None = None, out: torch.Tensor | None = None):
+    """y = h / sqrt(mean(h^2) + eps) * weight over the last dim, h = x (+ residual).
+    Returns y, or (h, y) when a residual is given (h = x + residual in x.dtype)."""
+    dev = _require_gpu(x, weight)
+    n = x.shape[-1]
+    if weight.shape != (n,):
+        raise PliError(f"weight {tuple(weight.shape)} for rows of {n}")
+    x2 = x.reshape(-1, n)
+    if x2.stride(-1) != 1:
+        x2 = x2.contiguous()
+    r2 = None
+    if residual is not None:
+        _require_gpu(x, residual)
+        if residual.shape != x.shape:
+            raise PliError("residual shape mismatch")
+        r2 = residual.reshape(-1, n)
+        if r2.stride(-1) != 1:
+            r2 = r2.contiguous()
+    weight = weight.contiguous()
+    y = torch.empty_like(x2) if out is None else out.view(-1, n)
+    h = torch.empty_like(x2) if residual is not None else None
+    rows = x2.shape[0]
+    with _on_device(dev):
+        rc = lib().pli_rmsnorm(_ptr(x2), _ptr(r2), _ptr(weight), _ptr(y), _ptr(h), rows, n,
+                               x2.stride(0), r2.stride(0) if r2 is not None else n, y.stride(0),
+                               h.stride(0) if h is not None else n, float(eps), _dtype_code(x),
+                               _stream(dev))
+    _check(rc, "pli_rmsnorm")
+    y = y.view(x.shape)
+    return y if residual is None else (h.view(x.shape), y)
 
 
 # ------------------------------------------------------------ fused SwiGLU
