@@ -226,6 +226,142 @@ __global__ __launch_bounds__(256, 2) void gemm_mfma(const uint16_t* __restrict__
 }
 
 // ---------------------------------------------------------------------------
+// 256x256 tile, 8 waves (2 in M x 4 in N, 128x64 outputs each), BK = 64, on
+// v_mfma_f32_16x16x32 (C^T = B^T A^T, so a lane owns an output row and 4
+// consecutive columns per accumulator).  Operand tiles arrive by LDS-DMA
+// (global_load_lds_dwordx4, 1 KiB per wave-instruction, lane-linear): the
+// swizzles below are applied on the SOURCE address.  K-tile t+1 is in flight
+// (second LDS buffer, 2 x 64 KiB) while t is computed; vmcnt(0) + barrier
+// per K-tile.  One block per CU; 256 blocks at 4096^2.
+//   A, NT B: [256 rows][64 k] (128-B rows), chunk ^= (row >> 1) & 7 --
+//            conflict-free for the 16x16x32 fragment read (16 rows x 16 B
+//            per lane group).
+//   NN B:    [64 k][256 n] (512-B rows), fragment = two ds_read_b64_tr_b16,
+//            chunk ^= 2 * ((k & 3) | ((k >> 3) & 1) << 2) -- each half-wave's
+//            8 rows x 32 B land on 64 distinct banks.
+constexpr int G2M = 256, G2N = 256, G2K = 64;
+
+__device__ __forceinline__ int g2_off_rows(int row, int c) {  // 128-B rows
+    return row * 128 + ((c ^ ((row >> 1) & 7)) << 4);
+}
+__device__ __forceinline__ int g2_fnn(int k) { return 2 * ((k & 3) | (((k >> 3) & 1) << 2)); }
+
+template <typename T, bool TRANS_B, bool BIAS>
+__global__ __launch_bounds__(512, 2) void gemm_256(const uint16_t* __restrict__ A,
+                                                   const uint16_t* __restrict__ Bm,
+                                                   uint16_t* __restrict__ C,
+                                                   const uint16_t* __restrict__ bias, int M, int N,
+                                                   int K, int64_t lda, int64_t ldb, int64_t ldc,
+                                                   int tiles_n, int nblocks) {
+    constexpr int TA = G2M * G2K * 2;  // 32 KiB
+    constexpr int TB = G2N * G2K * 2;  // 32 KiB
+    constexpr int BUF = TA + TB;
+    __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 2, wc = wave & 3;
+    const int l16 = lane & 15, g = lane >> 4;
+    const int lb = xcd_remap(blockIdx.x, nblocks);
+    const int m0 = (lb / tiles_n) * G2M, n0 = (lb % tiles_n) * G2N;
+    const int ktiles = K / G2K;
+
+    // DMA plan: 32 pieces of 1 KiB per operand tile, 4 per wave each.
+    auto dma = [&](int kt, int buf) {
+        char* as = smem + buf * BUF;
+        char* bs = as + TA;
+        const int k0 = kt * G2K;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int piece = wave * 4 + i;          // rows 8*piece .. +7
+            const int row = piece * 8 + (lane >> 3), slot = lane & 7;
+            const int c = slot ^ ((row >> 1) & 7);
+            const int mm = min(m0 + row, M - 1);
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void*)(A + (int64_t)mm * lda + k0 + 8 * c),
+                (__attribute__((address_space(3))) void*)(as + piece * 1024), 16, 0, 0);
+            if constexpr (TRANS_B) {
+                const int nn = min(n0 + row, N - 1);
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(Bm + (int64_t)nn * ldb + k0 + 8 * c),
+                    (__attribute__((address_space(3))) void*)(bs + piece * 1024), 16, 0, 0);
+            } else {
+                // [64 k][256 n]: piece = rows 2*piece, 2*piece+1 (512 B each)
+                const int kr = piece * 2 + (lane >> 5), sl = lane & 31;
+                const int cn = sl ^ g2_fnn(kr);
+                const int ncol = min(n0 + 8 * cn, N - 8);
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(Bm + (int64_t)(k0 + kr) * ldb + ncol),
+                    (__attribute__((address_space(3))) void*)(bs + piece * 1024), 16, 0, 0);
+            }
+        }
+    };
+
+    f32x4 acc[4][8];  // [n-frag][m-frag] of C^T
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int qq = l16 >> 2, pp = lane & 3;
+    dma(0, 0);
+    __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) lgkmcnt(0) expcnt(0)
+    __syncthreads();
+    for (int kt = 0; kt < ktiles; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < ktiles) dma(kt + 1, buf ^ 1);
+        const char* as = smem + buf * BUF;
+        const char* bs = as + TA;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            i32x4 af[8], bf[4];
+#pragma unroll
+            for (int mi = 0; mi < 8; ++mi)
+                af[mi] = lds_read_b128(as, g2_off_rows(wr * 128 + mi * 16 + l16, 4 * s + g));
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) {
+                if constexpr (TRANS_B) {
+                    bf[ni] = lds_read_b128(bs, g2_off_rows(wc * 64 + ni * 16 + l16, 4 * s + g));
+                } else {
+                    // k rows 32s + 8g + qq (+4), n cols wc*64 + ni*16 + 4pp
+                    const int kr = 32 * s + 8 * g + qq;
+                    const int nc = wc * 64 + ni * 16 + 4 * pp;  // element column
+                    const int c = nc >> 3, within = (nc & 7) * 2;
+                    const i32x2 lo = lds_read_tr16(bs, kr * 512 + ((c ^ g2_fnn(kr)) << 4) + within);
+                    const i32x2 hi = lds_read_tr16(bs, (kr + 4) * 512 + ((c ^ g2_fnn(kr + 4)) << 4) + within);
+                    bf[ni] = i32x4{lo.x, lo.y, hi.x, hi.y};
+                }
+            }
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+                for (int mi = 0; mi < 8; ++mi) acc[ni][mi] = mfma16x16x32<T>(bf[ni], af[mi], acc[ni][mi]);
+        }
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+    }
+
+    // epilogue: acc[ni][mi][r] = C[m0 + wr*128 + mi*16 + l16][n0 + wc*64 + ni*16 + 4g + r]
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) {
+        const int m = m0 + wr * 128 + mi * 16 + l16;
+        if (m >= M) continue;
+        uint16_t* crow = C + (int64_t)m * ldc;
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+            const int n = n0 + wc * 64 + ni * 16 + 4 * g;
+            if (n >= N) continue;
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                v[r] = acc[ni][mi][r];
+                if constexpr (BIAS) v[r] += elem<T>::to_f32(T{bias[n + r]});
+            }
+            *reinterpret_cast<i32x2*>(crow + n) = i32x2{(int)pack2<T>(v[0], v[1]), (int)pack2<T>(v[2], v[3])};
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Generic LDS-tiled kernel (any dtype, any shape/stride), fp32 accumulate.
 constexpr int GT = 64, GKT = 16;
 
@@ -541,6 +677,26 @@ int launch_mfma(const void* a, const void* b, void* c, const void* bias, int M, 
 }
 
 template <typename T>
+int launch_256(const void* a, const void* b, void* c, const void* bias, int M, int N, int K,
+               int64_t lda, int64_t ldb, int64_t ldc, int trans_b, hipStream_t s) {
+    const int tm = cdiv(M, G2M), tn = cdiv(N, G2N);
+    const int64_t nb = (int64_t)tm * tn;
+    PLI_REQUIRE(nb < (1ll << 31), "pli_gemm: grid too large");
+    const dim3 grid((unsigned)nb), block(512);
+#define PLI_G256(TB, BI)                                                                          \
+    hipLaunchKernelGGL((gemm_256<T, TB, BI>), grid, block, 0, s, (const uint16_t*)a,             \
+                       (const uint16_t*)b, (uint16_t*)c, (const uint16_t*)bias, M, N, K, lda, ldb, \
+                       ldc, tn, (int)nb)
+    if (trans_b) {
+        if (bias) PLI_G256(true, true); else PLI_G256(true, false);
+    } else {
+        if (bias) PLI_G256(false, true); else PLI_G256(false, false);
+    }
+#undef PLI_G256
+    return launch_status("gemm_256");
+}
+
+template <typename T>
 int launch_generic(const void* a, const void* b, void* c, const void* bias, int M, int N, int K,
                    int64_t lda, int64_t ldb, int64_t ldc, int trans_b, hipStream_t s) {
     const dim3 grid(cdiv(N, GT), cdiv(M, GT)), block(256);
@@ -631,9 +787,11 @@ extern "C" int pli_gemm_swiglu(const void* x, const void* wg, const void* wu, vo
     }
 }
 
-extern "C" int pli_gemm(const void* a, const void* b, void* c, const void* bias, int m, int n,
-                        int k, int64_t lda, int64_t ldb, int64_t ldc, int trans_b, int dtype,
-                        void* stream) {
+// variant: 0 = default routing, 1 = force the 128x128 MFMA tile, 2 = force
+// the 256x256 LDS-DMA tile (where its shape conditions hold)
+extern "C" int pli_gemm_variant(const void* a, const void* b, void* c, const void* bias, int m,
+                                int n, int k, int64_t lda, int64_t ldb, int64_t ldc, int trans_b,
+                                int dtype, void* stream, int variant) {
     using namespace pli;
     clear_error();
     PLI_REQUIRE(a && b && c, "pli_gemm: null pointer");
@@ -671,6 +829,14 @@ extern "C" int pli_gemm(const void* a, const void* b, void* c, const void* bias,
             return launch_skinny<bf16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, s);
         return launch_skinny<f16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, s);
     }
+    // large problems: 256x256 LDS-DMA tile (K a multiple of 64; at least a 2x2
+    // grid of tiles so the block count is not tiny)
+    const bool big = vec && k % G2K == 0 && m >= 2 * G2M && n >= 2 * G2N && variant != 1;
+    if (big || (vec && variant == 2 && k % G2K == 0 && n >= 8)) {
+        if (dtype == PLI_BF16)
+            return launch_256<bf16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, s);
+        return launch_256<f16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, s);
+    }
     if (vec) {
         if (dtype == PLI_BF16)
             return launch_mfma<bf16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, s);
@@ -682,4 +848,10 @@ extern "C" int pli_gemm(const void* a, const void* b, void* c, const void* bias,
         case PLI_BF16: return launch_generic<bf16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, s);
         default: set_error("pli_gemm: bad dtype %d", dtype); return PLI_EINVAL;
     }
+}
+
+extern "C" int pli_gemm(const void* a, const void* b, void* c, const void* bias, int m, int n,
+                        int k, int64_t lda, int64_t ldb, int64_t ldc, int trans_b, int dtype,
+                        void* stream) {
+    return pli_gemm_variant(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, dtype, stream, 0);
 }

@@ -56,6 +56,8 @@ _SIGS = {
                                    _c_int, ctypes.POINTER(_c_i64), _c_f32, _c_int, _c_int, _vp,
                                    _c_int],
     "pli_gemv_variant": [_vp, _vp, _vp, _c_int, _c_int, _c_i64, _c_int, _vp, _c_int],
+    "pli_gemm_variant": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_i64, _c_i64, _c_i64,
+                         _c_int, _c_int, _vp, _c_int],
     "pli_attn_decode_variant": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
                                 ctypes.POINTER(_c_i64), _c_f32, _c_int, _vp, ctypes.c_size_t,
                                 _c_int, _vp, _c_int, _c_int],
@@ -373,7 +375,8 @@ def gemv(w: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None,
 
 # ---------------------------------------------------------------------- GEMM
 def gemm(a: torch.Tensor, b: torch.Tensor, trans_b: bool = False,
-         bias: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+         bias: torch.Tensor | None = None, out: torch.Tensor | None = None,
+         variant: int | None = None) -> torch.Tensor:
     """C = A B (trans_b=False, torch.mm) or A B^T (+ bias) (trans_b=True, F.linear)."""
     ts = (a, b) if bias is None else (a, b, bias)
     dev = _require_gpu(*ts)
@@ -395,10 +398,13 @@ def gemm(a: torch.Tensor, b: torch.Tensor, trans_b: bool = False,
         out = torch.empty((m, n), dtype=a.dtype, device=dev)
     lda = a.stride(0) if m > 1 else k
     ldb = b.stride(0) if b.shape[0] > 1 else b.shape[1]
+    args = (_ptr(a), _ptr(b), _ptr(out), _ptr(bias), m, n, k, max(lda, 1), max(ldb, 1),
+            max(out.stride(0), n), int(bool(trans_b)), _dtype_code(a), _stream(dev))
     with _on_device(dev):
-        rc = lib().pli_gemm(_ptr(a), _ptr(b), _ptr(out), _ptr(bias), m, n, k, max(lda, 1),
-                            max(ldb, 1), max(out.stride(0), n), int(bool(trans_b)),
-                            _dtype_code(a), _stream(dev))
+        if variant is None:
+            rc = lib().pli_gemm(*args)
+        else:
+            rc = lib().pli_gemm_variant(*args, int(variant))
     _check(rc, "pli_gemm")
     return out
 

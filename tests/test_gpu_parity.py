@@ -234,6 +234,30 @@ def test_gemm_vs_oracle(m, n, k, dt, tb):
     assert_lin_close(c, ref, dt, f"gemm {m}x{n}x{k} {dt} tb={tb}")
 
 
+@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("m,n,k,tb,bias", [
+    (512, 512, 512, False, False),
+    (512, 512, 512, True, True),
+    (600, 520, 256, False, False),    # ragged M and N in the last tiles
+    (520, 600, 128, True, False),
+    (1024, 768, 1024, False, True),   # tiles_n = 3 (XCD remap with nwg % 8 != 0)
+    (256, 4096, 64, True, False),     # one K-tile
+])
+def test_gemm_tile_variants(m, n, k, tb, bias, variant):
+    """The 128x128 register-staged tile (1) and the 256x256 LDS-DMA tile (2)."""
+    import pli_hip
+    dt = "bf16"
+    a = seeded_normal((m, k), 3, dt)
+    b = seeded_normal((n, k) if tb else (k, n), 4, dt)
+    bb = seeded_normal((n,), 5, dt) if bias else None
+    out = pli_hip.gemm(dev(a, dt), dev(b, dt), trans_b=tb, bias=dev(bb, dt) if bias else None,
+                       variant=variant)
+    ref = olin.gemm(a, b.T if tb else b)
+    if bias:
+        ref = ref + bb.astype(np.float64)
+    assert_lin_close(out, ref, dt, f"variant {variant}")
+
+
 @pytest.mark.parametrize("m", [192, 4, 48])
 def test_gemm_bias_epilogue(m):
     import pli_hip

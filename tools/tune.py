@@ -313,8 +313,10 @@ def tune_gemm():
         a = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
         b = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
         c = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
-        fns = {"hip_nn": lambda: pli_hip.gemm(a, b, out=c),
-               "hip_nt": lambda: pli_hip.gemm(a, b, trans_b=True, out=c),
+        fns = {"hip_nn_128": lambda: pli_hip.gemm(a, b, out=c, variant=1),
+               "hip_nn_256": lambda: pli_hip.gemm(a, b, out=c, variant=2),
+               "hip_nt_128": lambda: pli_hip.gemm(a, b, trans_b=True, out=c, variant=1),
+               "hip_nt_256": lambda: pli_hip.gemm(a, b, trans_b=True, out=c, variant=2),
                "torch_nn": lambda: torch.mm(a, b)}
         t = interleave(fns, 5, 3)
         for kname, (med, mn) in t.items():
