@@ -362,6 +362,199 @@ __global__ __launch_bounds__(512, 2) void gemm_256(const uint16_t* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
+// gemm_256p: the 256x256 tile with a phased pipeline (4 phases per K-tile,
+// 16 MFMAs each; after the guide's 8-phase template, schedule derived here).
+// Each half-tile (A rows 0-127 "At", 128-255 "Ab", B rows/cols likewise "Bt",
+// "Bb"; 16 KiB) is one LDS-DMA unit.  A wave owns 64 rows of each A half and
+// 32 columns of each B half, so phase p reads only:
+//   P1: At + Bt fragments  -> C(At, Bt)      P2: Bb -> C(At, Bb)
+//   P3: Ab -> C(Ab, Bb)                       P4: (registers) -> C(Ab, Bt)
+// One half-tile is DMA'd per phase, 5-6 phases ahead of its first read:
+//   P1(t): Bb(t+1)  P2(t): Ab(t+1)  P3(t): At(t+2)  P4(t): Bt(t+2)
+// into buffer kt & 1; every restage is >= 2 phases after the last read of the
+// old contents, so one barrier per phase orders it.  A half read in phase p is
+// retired by a counted vmcnt in phase p-1 before that phase's barrier
+// (vmcnt(8): the 4 half-tiles issued after it may stay in flight; vmcnt(0)
+// once the issue stream has run out).  All LDS in one __shared__ array, raw
+// s_barrier, sched_barrier at the phase edges so hipcc keeps the order.
+template <typename T, bool TRANS_B, bool BIAS>
+__global__ __launch_bounds__(512, 2) void gemm_256p(const uint16_t* __restrict__ A,
+                                                    const uint16_t* __restrict__ Bm,
+                                                    uint16_t* __restrict__ C,
+                                                    const uint16_t* __restrict__ bias, int M, int N,
+                                                    int K, int64_t lda, int64_t ldb, int64_t ldc,
+                                                    int tiles_n, int nblocks) {
+    constexpr int HT = 16384, BUF = 4 * HT;
+    constexpr int AT = 0, AB = 1, BT = 2, BB = 3;
+    __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 2, wc = wave & 3;
+    const int l16 = lane & 15, g = lane >> 4, qq = l16 >> 2, pp = lane & 3;
+    const int lb = xcd_remap(blockIdx.x, nblocks);
+    const int m0 = (lb / tiles_n) * G2M, n0 = (lb % tiles_n) * G2N;
+    const int ktiles = K / G2K;
+
+    auto issue = [&](int half, int kt) {
+        if (kt >= ktiles) return;
+        char* dst = smem + (kt & 1) * BUF + half * HT;
+        const int k0 = kt * G2K;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int piece = wave * 2 + i;
+            if (half == AT || half == AB || TRANS_B) {
+                const int row = piece * 8 + (lane >> 3), slot = lane & 7;
+                const int c = slot ^ ((row >> 1) & 7);
+                const uint16_t* src;
+                if (half == AT || half == AB)
+                    src = A + (int64_t)min(m0 + (half == AB ? 128 : 0) + row, M - 1) * lda;
+                else
+                    src = Bm + (int64_t)min(n0 + (half == BB ? 128 : 0) + row, N - 1) * ldb;
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(src + k0 + 8 * c),
+                    (__attribute__((address_space(3))) void*)(dst + piece * 1024), 16, 0, 0);
+            } else {  // NN B half: [64 k][128 n], 256-B rows, 4 rows per piece
+                const int row = piece * 4 + (lane >> 4), slot = lane & 15;
+                const int c = slot ^ g2_fnn(row);
+                const int ncol = min(n0 + (half == BB ? 128 : 0) + 8 * c, N - 8);
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(Bm + (int64_t)(k0 + row) * ldb + ncol),
+                    (__attribute__((address_space(3))) void*)(dst + piece * 1024), 16, 0, 0);
+            }
+        }
+    };
+    auto read_a = [&](const char* half, int mi, int s) {
+        return lds_read_b128(half, g2_off_rows(wr * 64 + mi * 16 + l16, 4 * s + g));
+    };
+    auto read_b = [&](const char* half, int ni, int s) {
+        if constexpr (TRANS_B) {
+            return lds_read_b128(half, g2_off_rows(wc * 32 + ni * 16 + l16, 4 * s + g));
+        } else {
+            const int kr = 32 * s + 8 * g + qq;
+            const int nc = wc * 32 + ni * 16 + 4 * pp;
+            const int c = nc >> 3, within = (nc & 7) * 2;
+            const i32x2 lo = lds_read_tr16(half, kr * 256 + ((c ^ g2_fnn(kr)) << 4) + within);
+            const i32x2 hi = lds_read_tr16(half, (kr + 4) * 256 + ((c ^ g2_fnn(kr + 4)) << 4) + within);
+            return i32x4{lo.x, lo.y, hi.x, hi.y};
+        }
+    };
+    auto wait_vm = [&](bool drain) {
+        if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    };
+    auto sync = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    f32x4 acc[4][8];  // [n-frag: 0,1 = Bt, 2,3 = Bb][m-frag: 0-3 = At, 4-7 = Ab]
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // prologue: K-tile 0 complete-able, At/Bt of K-tile 1 in flight
+    issue(AT, 0);
+    issue(BT, 0);
+    issue(BB, 0);
+    issue(AB, 0);
+    issue(AT, 1);
+    issue(BT, 1);
+    wait_vm(ktiles < 2);  // retires At(0), Bt(0)
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+
+    i32x4 fat[4][2], fab[4][2], fbt[2][2], fbb[2][2];
+    for (int kt = 0; kt < ktiles; ++kt) {
+        const char* base = smem + (kt & 1) * BUF;
+        const bool drain = kt + 2 >= ktiles;
+        // ---- P1: At + Bt -> C(At, Bt)
+        issue(BB, kt + 1);
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) fat[mi][s2] = read_a(base + AT * HT, mi, s2);
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) fbt[ni][s2] = read_b(base + BT * HT, ni, s2);
+        wait_vm(drain);  // retires Bb(kt), read in P2
+        sync();
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+                    acc[ni][mi] = mfma16x16x32<T>(fbt[ni][s2], fat[mi][s2], acc[ni][mi]);
+        // ---- P2: Bb -> C(At, Bb)
+        issue(AB, kt + 1);
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) fbb[ni][s2] = read_b(base + BB * HT, ni, s2);
+        wait_vm(drain);  // retires Ab(kt), read in P3
+        sync();
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+                    acc[2 + ni][mi] = mfma16x16x32<T>(fbb[ni][s2], fat[mi][s2], acc[2 + ni][mi]);
+        // ---- P3: Ab -> C(Ab, Bb)
+        issue(AT, kt + 2);
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) fab[mi][s2] = read_a(base + AB * HT, mi, s2);
+        sync();
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+                    acc[2 + ni][4 + mi] = mfma16x16x32<T>(fbb[ni][s2], fab[mi][s2], acc[2 + ni][4 + mi]);
+        // ---- P4: registers -> C(Ab, Bt)
+        issue(BT, kt + 2);
+        wait_vm(drain);  // retires At(kt+1), Bt(kt+1), read in the next P1
+        sync();
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+                    acc[ni][4 + mi] = mfma16x16x32<T>(fbt[ni][s2], fab[mi][s2], acc[ni][4 + mi]);
+    }
+
+    // epilogue: acc[ni][mi][r] = C[m][n], m = m0 + (mi>>2)*128 + wr*64 + (mi&3)*16 + l16,
+    //                                     n = n0 + (ni>>1)*128 + wc*32 + (ni&1)*16 + 4g + r
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) {
+        const int m = m0 + (mi >> 2) * 128 + wr * 64 + (mi & 3) * 16 + l16;
+        if (m >= M) continue;
+        uint16_t* crow = C + (int64_t)m * ldc;
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+            const int n = n0 + (ni >> 1) * 128 + wc * 32 + (ni & 1) * 16 + 4 * g;
+            if (n >= N) continue;
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                v[r] = acc[ni][mi][r];
+                if constexpr (BIAS) v[r] += elem<T>::to_f32(T{bias[n + r]});
+            }
+            *reinterpret_cast<i32x2*>(crow + n) = i32x2{(int)pack2<T>(v[0], v[1]), (int)pack2<T>(v[2], v[3])};
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Generic LDS-tiled kernel (any dtype, any shape/stride), fp32 accumulate.
 constexpr int GT = 64, GKT = 16;
 
@@ -678,15 +871,22 @@ int launch_mfma(const void* a, const void* b, void* c, const void* bias, int M, 
 
 template <typename T>
 int launch_256(const void* a, const void* b, void* c, const void* bias, int M, int N, int K,
-               int64_t lda, int64_t ldb, int64_t ldc, int trans_b, hipStream_t s) {
+               int64_t lda, int64_t ldb, int64_t ldc, int trans_b, hipStream_t s, bool phased) {
     const int tm = cdiv(M, G2M), tn = cdiv(N, G2N);
     const int64_t nb = (int64_t)tm * tn;
     PLI_REQUIRE(nb < (1ll << 31), "pli_gemm: grid too large");
     const dim3 grid((unsigned)nb), block(512);
 #define PLI_G256(TB, BI)                                                                          \
-    hipLaunchKernelGGL((gemm_256<T, TB, BI>), grid, block, 0, s, (const uint16_t*)a,             \
-                       (const uint16_t*)b, (uint16_t*)c, (const uint16_t*)bias, M, N, K, lda, ldb, \
-                       ldc, tn, (int)nb)
+    do {                                                                                          \
+        if (phased)                                                                               \
+            hipLaunchKernelGGL((gemm_256p<T, TB, BI>), grid, block, 0, s, (const uint16_t*)a,     \
+                               (const uint16_t*)b, (uint16_t*)c, (const uint16_t*)bias, M, N, K,  \
+                               lda, ldb, ldc, tn, (int)nb);                                       \
+        else                                                                                      \
+            hipLaunchKernelGGL((gemm_256<T, TB, BI>), grid, block, 0, s, (const uint16_t*)a,      \
+                               (const uint16_t*)b, (uint16_t*)c, (const uint16_t*)bias, M, N, K,  \
+                               lda, ldb, ldc, tn, (int)nb);                                       \
+    } while (0)
     if (trans_b) {
         if (bias) PLI_G256(true, true); else PLI_G256(true, false);
     } else {
@@ -788,7 +988,8 @@ extern "C" int pli_gemm_swiglu(const void* x, const void* wg, const void* wu, vo
 }
 
 // variant: 0 = default routing, 1 = force the 128x128 MFMA tile, 2 = force
-// the 256x256 LDS-DMA tile (where its shape conditions hold)
+// the 256x256 LDS-DMA tile, 3 = force the phased 256x256 tile (where their
+// shape conditions hold)
 extern "C" int pli_gemm_variant(const void* a, const void* b, void* c, const void* bias, int m,
                                 int n, int k, int64_t lda, int64_t ldb, int64_t ldc, int trans_b,
                                 int dtype, void* stream, int variant) {
@@ -832,10 +1033,11 @@ extern "C" int pli_gemm_variant(const void* a, const void* b, void* c, const voi
     // large problems: 256x256 LDS-DMA tile (K a multiple of 64; at least a 2x2
     // grid of tiles so the block count is not tiny)
     const bool big = vec && k % G2K == 0 && m >= 2 * G2M && n >= 2 * G2N && variant != 1;
-    if (big || (vec && variant == 2 && k % G2K == 0 && n >= 8)) {
+    if (big || (vec && variant >= 2 && k % G2K == 0 && n >= 8)) {
+        const bool phased = variant == 3;
         if (dtype == PLI_BF16)
-            return launch_256<bf16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, s);
-        return launch_256<f16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, s);
+            return launch_256<bf16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, s, phased);
+        return launch_256<f16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, s, phased);
     }
     if (vec) {
         if (dtype == PLI_BF16)

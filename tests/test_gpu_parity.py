@@ -234,7 +234,7 @@ def test_gemm_vs_oracle(m, n, k, dt, tb):
     assert_lin_close(c, ref, dt, f"gemm {m}x{n}x{k} {dt} tb={tb}")
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3])
 @pytest.mark.parametrize("m,n,k,tb,bias", [
     (512, 512, 512, False, False),
     (512, 512, 512, True, True),
@@ -242,9 +242,14 @@ def test_gemm_vs_oracle(m, n, k, dt, tb):
     (520, 600, 128, True, False),
     (1024, 768, 1024, False, True),   # tiles_n = 3 (XCD remap with nwg % 8 != 0)
     (256, 4096, 64, True, False),     # one K-tile
+    (512, 512, 128, False, False),    # two K-tiles: pipeline drain from the start
+    (768, 1024, 192, True, True),     # three K-tiles
+    (2048, 2048, 4096, False, False), # long K: the steady-state vmcnt(8) path
+    (2048, 2048, 4096, True, False),
 ])
 def test_gemm_tile_variants(m, n, k, tb, bias, variant):
-    """The 128x128 register-staged tile (1) and the 256x256 LDS-DMA tile (2)."""
+    """The 128x128 register-staged tile (1), the 256x256 LDS-DMA tile (2) and
+    its phased pipeline (3)."""
     import pli_hip
     dt = "bf16"
     a = seeded_normal((m, k), 3, dt)

@@ -315,8 +315,10 @@ def tune_gemm():
         c = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
         fns = {"hip_nn_128": lambda: pli_hip.gemm(a, b, out=c, variant=1),
                "hip_nn_256": lambda: pli_hip.gemm(a, b, out=c, variant=2),
+               "hip_nn_256p": lambda: pli_hip.gemm(a, b, out=c, variant=3),
                "hip_nt_128": lambda: pli_hip.gemm(a, b, trans_b=True, out=c, variant=1),
                "hip_nt_256": lambda: pli_hip.gemm(a, b, trans_b=True, out=c, variant=2),
+               "hip_nt_256p": lambda: pli_hip.gemm(a, b, trans_b=True, out=c, variant=3),
                "torch_nn": lambda: torch.mm(a, b)}
         t = interleave(fns, 5, 3)
         for kname, (med, mn) in t.items():
