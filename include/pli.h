@@ -166,6 +166,36 @@ int pli_rmsnorm(const void* x, const void* residual, const void* weight, void* y
                 void* h_out, int64_t rows, int n, int64_t ldx, int64_t ldr,
                 int64_t ldy, int64_t ldh, float eps, int dtype, void* stream);
 
+/*
+ * Mixture of experts (ch09/moe_layer.py:18-83: Router softmax/topk/renorm and
+ * the per-expert masked loop).
+ *
+ * pli_moe_route: logits [tokens, experts] (ld_logits) -> per (token, k):
+ *   weights (fp32; renormalised over the k when normalize), expert_idx,
+ *   pos (row of the expert-sorted activation matrix); gather[row] = token;
+ *   offsets[experts + 1] = each expert's row range.  experts <= 64, top_k <= 8.
+ *   workspace: int32 [experts + tokens * top_k].
+ * pli_gemm_grouped: for every expert e, rows r in [offsets[e], offsets[e+1]):
+ *   c[r] = x[gather[r]] W_e^T  (gather NULL = identity), or with wu_ptrs
+ *   silu(x W1_e^T) * (x W3_e^T); w_ptrs / wu_ptrs are DEVICE arrays of the
+ *   experts' [n, k] weight pointers; rows_bound >= every expert's row count.
+ *   bf16/fp16, k % 128 == 0, n % 16 == 0.
+ * pli_moe_combine: out[t] = sum_k weights[t, k] * y[pos[t, k]] (fp32 sum in k
+ *   order).
+ */
+int pli_moe_route(const void* logits, int64_t ld_logits, int tokens, int experts,
+                  int top_k, int normalize, int dtype, float* weights,
+                  int32_t* expert_idx, int32_t* pos, int32_t* gather,
+                  int32_t* offsets, int32_t* workspace, void* stream);
+int pli_gemm_grouped(const void* x, const int32_t* gather,
+                     const void* const* w_ptrs, const void* const* wu_ptrs,
+                     void* c, const int32_t* offsets, int experts, int rows_bound,
+                     int n, int k, int64_t ldx, int64_t ldw, int64_t ldc,
+                     int dtype, void* stream);
+int pli_moe_combine(const void* y, int64_t ldy, const int32_t* pos,
+                    const float* weights, void* out, int64_t ldo, int tokens,
+                    int top_k, int hidden, int dtype, void* stream);
+
 /* Graph-replayable decode (ch08/cuda_graph.py:18-82 captures the decode step;
  * a captured launch cannot take the growing cache length as a host value).
  *

@@ -72,3 +72,30 @@ def rms_norm(x, weight, eps=1e-6, residual=None):
     if residual is not None:
         h = h + np.asarray(residual, np.float64)
     return h / np.sqrt(np.mean(h * h, axis=-1, keepdims=True) + eps) * np.asarray(weight, np.float64)
+
+
+def moe_route(logits, top_k, normalize=True):
+    """Router of ``ch09/moe_layer.py:24-33`` in float64: softmax, top-k
+    (descending, ties to the lower index), optional renormalisation."""
+    lg = np.asarray(logits, np.float64)
+    p = np.exp(lg - lg.max(-1, keepdims=True))
+    p /= p.sum(-1, keepdims=True)
+    idx = np.argsort(-p, axis=-1, kind="stable")[:, :top_k]
+    w = np.take_along_axis(p, idx, -1)
+    if normalize:
+        w = w / w.sum(-1, keepdims=True)
+    return w, idx
+
+
+def moe_layer(x, gate_w, experts, top_k, normalize=True):
+    """``MoELayer.forward`` (``ch09/moe_layer.py:58-83``) in float64:
+    out[t] = sum_k w[t,k] * W2_e (silu(W1_e x) * W3_e x), e = idx[t,k];
+    experts = [(w1, w2, w3), ...] as nn.Linear weights."""
+    x = np.asarray(x, np.float64)
+    w, idx = moe_route(x @ np.asarray(gate_w, np.float64).T, top_k, normalize)
+    out = np.zeros_like(x)
+    for t in range(x.shape[0]):
+        for j in range(top_k):
+            w1, w2, w3 = experts[idx[t, j]]
+            out[t] += w[t, j] * swiglu_ffn(x[t:t + 1], w1, w3, w2)[0]
+    return out

@@ -1,6 +1,16 @@
 """Chapter 09 on MI355X: tensor-parallel linear layers on the HIP GEMM with a
-real RCCL all-reduce, and the collective cost models (MoE is out of scope)."""
+real RCCL all-reduce, the collective cost models, and the MoE layer on the
+grouped expert GEMM (the expert-offloading engine of moe_inference.py is
+control plane and not mirrored)."""
 
+from .moe_layer import (
+    ExpertLayer,
+    MoEConfig,
+    MoELayer,
+    Router,
+    expert_load_balance_loss,
+    explain_moe,
+)
 from .nccl_primitives import (
     AllGatherConfig,
     AllReduceConfig,
@@ -20,6 +30,12 @@ from .tensor_parallel import (
 )
 
 __all__ = [
+    "MoEConfig",
+    "Router",
+    "ExpertLayer",
+    "MoELayer",
+    "expert_load_balance_loss",
+    "explain_moe",
     "TensorParallelConfig",
     "ColumnParallelLinear",
     "RowParallelLinear",

@@ -826,6 +826,103 @@ __global__ __launch_bounds__(256) void gemm_smallm_nt(const uint16_t* __restrict
     }
 }
 
+// Grouped (MoE expert) form of the small-M kernel: workgroup = (expert e,
+// 16 output columns).  Expert e owns rows offsets[e] .. offsets[e+1]-1 of the
+// permuted activation matrix; its X rows are read through `gather` (token
+// index per permuted row, or identity when null), its weights through the
+// device pointer table `w_ptrs[e]` (the reference keeps one nn.Linear per
+// expert, ch09/moe_layer.py:36-45), and the rows are processed 16*NBG at a
+// time (NBG sized on the host from the row bound, so decode batches run
+// NBG = 1).  SWIGLU: w_ptrs / wu_ptrs are W1 / W3 and the output is
+// silu(x W1^T) * (x W3^T).
+template <typename T, int NBG, bool SWIGLU>
+__global__ __launch_bounds__(256) void gemm_grouped_nt(
+    const uint16_t* __restrict__ X, const int* __restrict__ gather,
+    const uint16_t* const* __restrict__ w_ptrs, const uint16_t* const* __restrict__ wu_ptrs,
+    uint16_t* __restrict__ C, const int* __restrict__ offsets, int N, int K, int64_t ldx,
+    int64_t ldw, int64_t ldc, int nblk) {
+    constexpr int NW = SWIGLU ? 2 : 1;
+    constexpr int U = SWIGLU ? 4 : 8;
+    __shared__ __attribute__((aligned(16))) float part[4][NBG][NW][4][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int e = blockIdx.x / nblk, n0 = (blockIdx.x % nblk) * 16;
+    const int r0 = offsets[e], Me = offsets[e + 1] - r0;
+    if (Me <= 0) return;
+    const int r16 = lane & 15, kq = 8 * (lane >> 4);
+    const int kw = K / 4;
+    const uint16_t* wp[NW];
+    wp[0] = w_ptrs[e] + (int64_t)min(n0 + r16, N - 1) * ldw + wave * kw + kq;
+    if constexpr (SWIGLU) wp[NW - 1] = wu_ptrs[e] + (int64_t)min(n0 + r16, N - 1) * ldw + wave * kw + kq;
+    for (int c0 = 0; c0 < Me; c0 += 16 * NBG) {
+        const int M = min(16 * NBG, Me - c0);
+        const uint16_t* xp[NBG];
+#pragma unroll
+        for (int gi = 0; gi < NBG; ++gi) {
+            const int pr = r0 + c0 + min(gi * 16 + r16, M - 1);
+            const int tok = gather ? gather[pr] : pr;
+            xp[gi] = X + (int64_t)tok * ldx + wave * kw + kq;
+        }
+        f32x4 acc[NW][NBG];
+#pragma unroll
+        for (int w = 0; w < NW; ++w)
+#pragma unroll
+            for (int gi = 0; gi < NBG; ++gi) acc[w][gi] = f32x4{0.f, 0.f, 0.f, 0.f};
+        int k0 = 0;
+        for (; k0 + 32 * U <= kw; k0 += 32 * U) {
+            i32x4 wf[NW][U], xf[U][NBG];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+#pragma unroll
+                for (int w = 0; w < NW; ++w)
+                    wf[w][u] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wp[w] + k0 + 32 * u));
+#pragma unroll
+                for (int gi = 0; gi < NBG; ++gi)
+                    xf[u][gi] = *reinterpret_cast<const i32x4*>(xp[gi] + k0 + 32 * u);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int w = 0; w < NW; ++w)
+#pragma unroll
+                    for (int gi = 0; gi < NBG; ++gi)
+                        acc[w][gi] = mfma16x16x32<T>(wf[w][u], xf[u][gi], acc[w][gi]);
+        }
+        for (; k0 < kw; k0 += 32) {
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+                const i32x4 wf = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wp[w] + k0));
+#pragma unroll
+                for (int gi = 0; gi < NBG; ++gi)
+                    acc[w][gi] = mfma16x16x32<T>(wf, *reinterpret_cast<const i32x4*>(xp[gi] + k0), acc[w][gi]);
+            }
+        }
+        __syncthreads();  // part[] of the previous chunk fully consumed
+#pragma unroll
+        for (int w = 0; w < NW; ++w)
+#pragma unroll
+            for (int gi = 0; gi < NBG; ++gi)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) part[wave][gi][w][r][lane] = acc[w][gi][r];
+        __syncthreads();
+        for (int gi = wave; gi < NBG; gi += 4) {
+            const int bt = gi * 16 + r16;
+            const int nr = n0 + 4 * (lane >> 4);
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                v[r] = part[0][gi][0][r][lane] + part[1][gi][0][r][lane] + part[2][gi][0][r][lane] +
+                       part[3][gi][0][r][lane];
+                if constexpr (SWIGLU)
+                    v[r] = silu_mul(v[r], part[0][gi][NW - 1][r][lane] + part[1][gi][NW - 1][r][lane] +
+                                              part[2][gi][NW - 1][r][lane] + part[3][gi][NW - 1][r][lane]);
+            }
+            if (bt < M && nr < N)
+                *reinterpret_cast<i32x2*>(C + (int64_t)(r0 + c0 + bt) * ldc + nr) =
+                    i32x2{(int)pack2<T>(v[0], v[1]), (int)pack2<T>(v[2], v[3])};
+        }
+    }
+}
+
 template <typename T>
 int launch_smallm(const void* a, const void* b, void* c, const void* bias, int M, int N, int K,
                   int64_t lda, int64_t ldb, int64_t ldc, hipStream_t s) {
@@ -1056,4 +1153,51 @@ extern "C" int pli_gemm(const void* a, const void* b, void* c, const void* bias,
                         int k, int64_t lda, int64_t ldb, int64_t ldc, int trans_b, int dtype,
                         void* stream) {
     return pli_gemm_variant(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, dtype, stream, 0);
+}
+
+// Grouped NT GEMM over experts (see gemm_grouped_nt): C[r] = X[gather[r]] W_e^T
+// (or silu(. W1_e^T) * (. W3_e^T) when wu_ptrs != NULL) for r in expert e's
+// row range [offsets[e], offsets[e+1]).  rows_bound (host) bounds every
+// expert's row count and sizes the per-workgroup batch groups.
+extern "C" int pli_gemm_grouped(const void* x, const int32_t* gather, const void* const* w_ptrs,
+                                const void* const* wu_ptrs, void* c, const int32_t* offsets,
+                                int experts, int rows_bound, int n, int k, int64_t ldx,
+                                int64_t ldw, int64_t ldc, int dtype, void* stream) {
+    using namespace pli;
+    clear_error();
+    PLI_REQUIRE(x && w_ptrs && c && offsets, "pli_gemm_grouped: null pointer");
+    PLI_REQUIRE(experts > 0 && rows_bound >= 0 && n > 0 && k > 0,
+                "pli_gemm_grouped: bad shape E=%d rows=%d n=%d k=%d", experts, rows_bound, n, k);
+    PLI_REQUIRE(dtype == PLI_BF16 || dtype == PLI_F16, "pli_gemm_grouped: bf16/fp16 only");
+    PLI_REQUIRE(k % 128 == 0 && n % 16 == 0 && ldx % 8 == 0 && ldw % 8 == 0 && ldc % 8 == 0 &&
+                    al16(x) && al16(c),
+                "pli_gemm_grouped: needs k %% 128 == 0, n %% 16 == 0, 16-byte aligned rows");
+    PLI_REQUIRE(ldx >= k && ldw >= k && ldc >= n, "pli_gemm_grouped: leading dimension too small");
+    if (rows_bound == 0) return PLI_OK;
+    const int nblk = n / 16;
+    PLI_REQUIRE((int64_t)experts * nblk < (1ll << 31), "pli_gemm_grouped: grid too large");
+    const dim3 grid((unsigned)(experts * nblk)), block(256);
+    hipStream_t s = (hipStream_t)stream;
+    const auto* X = (const uint16_t*)x;
+    const auto* const* W = (const uint16_t* const*)w_ptrs;
+    const auto* const* Wu = (const uint16_t* const*)wu_ptrs;
+    auto* Cc = (uint16_t*)c;
+#define PLI_GRP(TT, NBG, SW)                                                                      \
+    hipLaunchKernelGGL((gemm_grouped_nt<TT, NBG, SW>), grid, block, 0, s, X, gather, W, Wu, Cc, \
+                       offsets, n, k, ldx, ldw, ldc, nblk)
+#define PLI_GRP_NBG(TT, SW)                                                                       \
+    do {                                                                                          \
+        if (rows_bound <= 16) PLI_GRP(TT, 1, SW);                                                 \
+        else if (rows_bound <= 32) PLI_GRP(TT, 2, SW);                                            \
+        else if (rows_bound <= 64) PLI_GRP(TT, 4, SW);                                            \
+        else PLI_GRP(TT, 8, SW);                                                                  \
+    } while (0)
+    if (dtype == PLI_BF16) {
+        if (wu_ptrs) PLI_GRP_NBG(bf16_t, true); else PLI_GRP_NBG(bf16_t, false);
+    } else {
+        if (wu_ptrs) PLI_GRP_NBG(f16_t, true); else PLI_GRP_NBG(f16_t, false);
+    }
+#undef PLI_GRP_NBG
+#undef PLI_GRP
+    return launch_status("pli_gemm_grouped");
 }

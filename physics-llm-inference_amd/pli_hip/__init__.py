@@ -40,6 +40,11 @@ _SIGS = {
                         _c_i64, _c_int, _vp],
     "pli_rmsnorm": [_vp, _vp, _vp, _vp, _vp, _c_i64, _c_int, _c_i64, _c_i64, _c_i64, _c_i64,
                     _c_f32, _c_int, _vp],
+    "pli_moe_route": [_vp, _c_i64, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp,
+                      _vp, _vp, _vp],
+    "pli_gemm_grouped": [_vp, _vp, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_i64,
+                         _c_i64, _c_i64, _c_int, _vp],
+    "pli_moe_combine": [_vp, _c_i64, _vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_int, _c_int, _vp],
     "pli_scale_copy": [_vp, _vp, _c_i64, _c_int, _vp],
     "pli_softmax_rows": [_vp, _vp, _c_i64, _c_int, _c_int, _vp],
     "pli_online_softmax_with_output": [_vp, _vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_int, _vp],
@@ -286,6 +291,66 @@ def attn_decode_dev(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
                                        _ptr(n_kv_dev), int(n_kv_add), _ptr(workspace), ws_bytes,
                                        _dtype_code(q), _stream(dev))
     _check(rc, "pli_attn_decode_dev")
+    return out
+
+
+# ---------------------------------------------------------------------- MoE
+def moe_route(logits: torch.Tensor, top_k: int, normalize: bool = True):
+    """Router tail of ch09/moe_layer.py:24-33 on the device: returns
+    (weights [T, k] fp32, expert_idx [T, k] int32, pos [T, k] int32,
+    gather [T*k] int32, offsets [E+1] int32)."""
+    dev = _require_gpu(logits)
+    T, E = logits.shape
+    if logits.stride(1) != 1:
+        logits = logits.contiguous()
+    i32 = dict(device=logits.device, dtype=torch.int32)
+    weights = torch.empty(T, top_k, device=logits.device, dtype=torch.float32)
+    idx = torch.empty(T, top_k, **i32)
+    pos = torch.empty(T, top_k, **i32)
+    gather = torch.empty(max(T * top_k, 1), **i32)
+    offsets = torch.empty(E + 1, **i32)
+    ws = torch.empty(E + T * top_k, **i32)
+    with _on_device(dev):
+        rc = lib().pli_moe_route(_ptr(logits), logits.stride(0), T, E, int(top_k), int(bool(normalize)),
+                                 _dtype_code(logits), _ptr(weights), _ptr(idx), _ptr(pos),
+                                 _ptr(gather), _ptr(offsets), _ptr(ws), _stream(dev))
+    _check(rc, "pli_moe_route")
+    return weights, idx, pos, gather, offsets
+
+
+def weight_table(weights: list[torch.Tensor]) -> torch.Tensor:
+    """Device int64 array of the weights' data pointers (for pli_gemm_grouped)."""
+    return torch.tensor([w.data_ptr() for w in weights], dtype=torch.int64,
+                        device=weights[0].device)
+
+
+def gemm_grouped(x: torch.Tensor, gather: torch.Tensor | None, w_table: torch.Tensor,
+                 offsets: torch.Tensor, rows: int, n: int, k: int, ldw: int,
+                 wu_table: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Per-expert NT GEMM over expert-sorted rows (see include/pli.h)."""
+    dev = _require_gpu(x)
+    E = offsets.numel() - 1
+    if out is None:
+        out = torch.empty(max(rows, 1), n, device=x.device, dtype=x.dtype)
+    with _on_device(dev):
+        rc = lib().pli_gemm_grouped(_ptr(x), _ptr(gather), _ptr(w_table), _ptr(wu_table), _ptr(out),
+                                    _ptr(offsets), E, int(rows), int(n), int(k), x.stride(0),
+                                    int(ldw), out.stride(0), _dtype_code(x), _stream(dev))
+    _check(rc, "pli_gemm_grouped")
+    return out
+
+
+def moe_combine(y: torch.Tensor, pos: torch.Tensor, weights: torch.Tensor, tokens: int,
+                out: torch.Tensor | None = None) -> torch.Tensor:
+    dev = _require_gpu(y)
+    H = y.shape[1]
+    k = pos.shape[1]
+    if out is None:
+        out = torch.empty(tokens, H, device=y.device, dtype=y.dtype)
+    with _on_device(dev):
+        rc = lib().pli_moe_combine(_ptr(y), y.stride(0), _ptr(pos), _ptr(weights), _ptr(out),
+                                   out.stride(0), tokens, k, H, _dtype_code(y), _stream(dev))
+    _check(rc, "pli_moe_combine")
     return out
 
 

@@ -19,6 +19,8 @@ and records, for seeded inputs, what the reference computes:
   ``LayerKVCache``): seeded weights, a prompt, single-token decode steps and
   a 3-token chunk (bottom-right causal mask), fp32;
 * ``kv_cache.json`` -- ``ch02.calculate_kv_cache_size`` over a small grid;
+* ``moe.npz``      -- ``ch09`` MoELayer (hidden 256, experts 8 x 512, top-2)
+  and its Router with seeded weights, fp32;
 * ``ffn.npz``      -- ``ch01`` NaiveFFN / SwiGLUFFN / FusedSwiGLUFFN and the
   ``ch09`` TensorParallelMLP (world 1) with seeded weights, fp32;
 * ``analytic.json`` -- exact values of the reference cost models
@@ -206,6 +208,24 @@ def gen_ffn(ref_ch01, ref_ch09, out_dir):
     print("ffn: ok")
 
 
+def gen_moe(out_dir):
+    import importlib
+
+    import torch
+    ml = importlib.import_module("ch09.moe_layer")
+    cfg = ml.MoEConfig(hidden_dim=256, expert_dim=512, num_experts=8, num_experts_per_tok=2)
+    torch.manual_seed(9)
+    moe = ml.MoELayer(cfg)
+    x = seeded_normal((2, 8, 256), 61)
+    with torch.no_grad():
+        y = moe(torch.from_numpy(x)).numpy()
+        w, idx, logits = moe.router(torch.from_numpy(x).view(-1, 256))
+    d = {"y": y, "router_w": w.numpy(), "router_idx": idx.numpy(), "router_logits": logits.numpy()}
+    d.update({f"hash_{n}": np.array(array_hash(p.detach().numpy())) for n, p in moe.named_parameters()})
+    np.savez_compressed(os.path.join(out_dir, "moe.npz"), **d)
+    print("moe: ok")
+
+
 def gen_tp(ref_ch09, out_dir):
     import torch
     d = {}
@@ -300,6 +320,7 @@ def main():
     gen_tp(ref["ch09"], args.out)
     gen_gqa(ref["ch01"], ref["ch02"], args.out)
     gen_ffn(ref["ch01"], ref["ch09"], args.out)
+    gen_moe(args.out)
     gen_analytic(ref, args.out)
 
 

@@ -297,6 +297,61 @@ def tune_graph(batches=(1, 8, 32), prompt=512, steps=32):
                           **{f"{k}_tok/s": B / (v * 1e-3) for k, v in res.items()}}), flush=True)
 
 
+def tune_moe(tokens=(1, 8, 32, 128)):
+    """ch09 MoE layer at MoEConfig's defaults (hidden 4096, 8 experts x 14336,
+    top-2), bf16: the HIP path (route + 2 grouped GEMMs + combine) vs the
+    reference's masked per-expert loop, same device and weights.  GB/s over
+    the weights of the experts actually selected."""
+    import time
+    from ch09 import MoEConfig, MoELayer
+    torch.manual_seed(0)
+    cfg = MoEConfig()
+    moe = MoELayer(cfg).cuda().bfloat16().eval()
+
+    def ref_forward(x):  # ch09/moe_layer.py:58-83 on the same weights (torch ops)
+        x_flat = x.view(-1, cfg.hidden_dim)
+        logits = (x_flat @ moe.router.gate.weight.t()).float()  # fp32 routing: no bf16 top-k flips
+        w = torch.softmax(logits, dim=-1)
+        tw, ti = torch.topk(w, cfg.num_experts_per_tok, dim=-1)
+        tw = tw / tw.sum(-1, keepdim=True)
+        out = torch.zeros_like(x_flat)
+        for e in range(cfg.num_experts):
+            mask = (ti == e).any(dim=-1)
+            if not mask.any():
+                continue
+            ex = moe.experts[e]
+            xe = x_flat[mask]
+            ye = (torch.nn.functional.silu(xe @ ex.w1.weight.t()) * (xe @ ex.w3.weight.t())) @ ex.w2.weight.t()
+            for kk in range(cfg.num_experts_per_tok):
+                em = ti[:, kk] == e
+                cm = mask & em
+                if cm.any():
+                    out[cm] += tw[cm, kk].unsqueeze(-1).to(x.dtype) * ye[em[mask]]
+        return out.view_as(x)
+
+    per_expert = 3 * cfg.hidden_dim * cfg.expert_dim * 2
+    for T in tokens:
+        x = torch.randn(1, T, cfg.hidden_dim, device="cuda", dtype=torch.bfloat16)
+        with torch.no_grad():
+            y = moe(x)
+            yr = ref_forward(x)
+            active = int(torch.unique(moe.router(x.view(-1, cfg.hidden_dim))[1]).numel())
+            res = {}
+            for name, fn in (("hip", lambda: moe(x)), ("reference", lambda: ref_forward(x))):
+                fn()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(10):
+                    fn()
+                torch.cuda.synchronize()
+                res[name] = (time.perf_counter() - t0) / 10 * 1e3
+        err = ((y.float() - yr.float()).norm() / yr.float().norm()).item()
+        print(json.dumps({"kernel": "moe_layer", "tokens": T, "active_experts": active,
+                          **{f"{k}_us": v * 1e3 for k, v in res.items()},
+                          **{f"{k}_GB/s": active * per_expert / (v * 1e-3) / 1e9 for k, v in res.items()},
+                          "rel_diff": err}), flush=True)
+
+
 def tune_hbm():
     for nbytes in (1 << 28, 1 << 30):
         n = nbytes // 4
@@ -349,3 +404,5 @@ if __name__ == "__main__":
         tune_swiglu()
     if "graph" in what:
         tune_graph()
+    if "moe" in what:
+        tune_moe()
