@@ -275,10 +275,10 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_mfma(
 // (A software-pipelined variant that issued QK^T(t+1) beside softmax(t) with
 // LDS-DMA staging spilled at D=128 and ran 1.5-2.5x slower: every spill
 // reload's vmcnt(0) also drained the in-flight DMA.  See DESIGN.md.)
-template <int D> struct PadLayout {
+template <int D, int KTL = KT> struct PadLayout {
     static constexpr int KS = 2 * D + 16;  // K row stride (bytes)
     static constexpr int VS = 2 * D + 64;  // V row stride (bytes)
-    static constexpr int KSZ = KT * KS, VSZ = KT * VS, BUF = KSZ + VSZ;
+    static constexpr int KSZ = KTL * KS, VSZ = KTL * VS, BUF = KSZ + VSZ;
 };
 
 // OPT bits (A/B levers on the v2 body, variants 16-20):
@@ -292,7 +292,13 @@ template <int D> struct PadLayout {
 //     uncorrected (measured 1.05e-2 on the spike test without it).
 // 16: epilogue: pair the two half-waves' 8-byte pieces of a row with
 //     v_permlane32_swap so each lane stores 16 B (8 dwordx4 instead of 16 dwordx2)
-constexpr int kOptPermlane = 1, kOptPrio = 2, kOptDefer = 4, kOptRoundedSum = 8, kOptWideStore = 16;
+// 32 / 64: __builtin_amdgcn_iglp_opt(0) / (1) in the tile loop (the compiler's
+//     MFMA + DS interleave strategies)
+// 128: batched fragment reads (all K fragments of the tile, V^T one block
+//     ahead) so LDS latency overlaps the MFMAs instead of pairing each read
+//     with the MFMA that consumes it
+constexpr int kOptPermlane = 1, kOptPrio = 2, kOptDefer = 4, kOptRoundedSum = 8, kOptWideStore = 16,
+              kOptIglp0 = 32, kOptIglp1 = 64, kOptBatchReads = 128;
 constexpr float kDeferThr = 8.f;
 
 __device__ __forceinline__ float xor32_max(float x) {
@@ -304,18 +310,19 @@ __device__ __forceinline__ float xor32_sum(float x) {
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-template <typename T, int D, int NW, bool LAZY, int OPT = 0>
+template <typename T, int D, int NW, bool LAZY, int OPT = 0, int KTL = KT>
 __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_v2(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
     const uint16_t* __restrict__ v, uint16_t* __restrict__ o, int H, int group,
     int Nq, int Nk, AttnStrides st, float c, int causal, int qblocks,
     int nblocks) {
-    using L = PadLayout<D>;
+    using L = PadLayout<D, KTL>;
+    constexpr int NS = KTL / 32;        // 32-key sub-tiles per tile
     constexpr int NT = NW * 64;
     constexpr int CPR = D / 8;          // 16-byte chunks per row
     constexpr int RPI = NT / CPR;       // rows covered by one staging step
-    constexpr int CPT = KT / RPI;       // staging steps per tile
-    static_assert(NT % CPR == 0 && KT % RPI == 0, "staging must tile evenly");
+    constexpr int CPT = KTL / RPI;      // staging steps per tile
+    static_assert(NT % CPR == 0 && KTL % RPI == 0, "staging must tile evenly");
     __shared__ __attribute__((aligned(16))) char smem[2 * L::BUF];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -348,10 +355,10 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_v2(
 
     int kv_end = Nk;
     if (causal) kv_end = min(Nk, qbase + NW * QW + off_diag);
-    const int nt = kv_end > 0 ? cdiv(kv_end, KT) : 0;
-    const int t_full = Nk / KT;  // tiles [0, t_full) need no row clamp
+    const int nt = kv_end > 0 ? cdiv(kv_end, KTL) : 0;
+    const int t_full = Nk / KTL;  // tiles [0, t_full) need no row clamp
     int t_mask = t_full;         // first tile this wave must mask
-    if (causal) t_mask = min(t_mask, max(0, (q0 + off_diag + 1) / KT));
+    if (causal) t_mask = min(t_mask, max(0, (q0 + off_diag + 1) / KTL));
 
     // staging: thread owns chunk `sch` of rows srow + i*RPI
     const int srow = tid / CPR, sch = tid % CPR;
@@ -363,14 +370,14 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_v2(
         if (t < t_full) {
 #pragma unroll
             for (int i = 0; i < CPT; ++i) {
-                const int64_t r = (int64_t)t * KT + i * RPI;
+                const int64_t r = (int64_t)t * KTL + i * RPI;
                 kst[i] = *reinterpret_cast<const i32x4*>(kg + r * st.kn);
                 vst[i] = *reinterpret_cast<const i32x4*>(vg + r * st.vn);
             }
         } else {
 #pragma unroll
             for (int i = 0; i < CPT; ++i) {
-                const int key = t * KT + i * RPI + srow;
+                const int key = t * KTL + i * RPI + srow;
                 const int64_t r = min(key, Nk - 1) - srow;
                 const i32x4 kx = *reinterpret_cast<const i32x4*>(kg + r * st.kn);
                 const i32x4 vx = *reinterpret_cast<const i32x4*>(vg + r * st.vn);
@@ -410,13 +417,31 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_v2(
     }
 
     for (int t = 0; t < nt; ++t) {
+        if constexpr ((OPT & kOptIglp0) != 0) __builtin_amdgcn_iglp_opt(0);
+        if constexpr ((OPT & kOptIglp1) != 0) __builtin_amdgcn_iglp_opt(1);
         if (t + 1 < nt) load_tile(t + 1);
         const char* kb = smem + (t & 1) * L::BUF + kr;
         const char* vb = smem + (t & 1) * L::BUF + vr;
 
-        f32x16 s[2];
+        f32x16 s[NS];
+        if constexpr ((OPT & kOptBatchReads) != 0) {
+            // every K fragment of the tile in flight before the first MFMA
+            i32x4 kfr[NS][D / 16];
 #pragma unroll
-        for (int tt = 0; tt < 2; ++tt) {
+            for (int tt = 0; tt < NS; ++tt)
+#pragma unroll
+                for (int kk = 0; kk < D / 16; ++kk) kfr[tt][kk] = lds_read_b128(kb, tt * 32 * L::KS + kk * 32);
+            __builtin_amdgcn_sched_barrier(0);  // keep the batch ahead of the MFMAs
+#pragma unroll
+            for (int tt = 0; tt < NS; ++tt) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) s[tt][r] = 0.f;
+#pragma unroll
+                for (int kk = 0; kk < D / 16; ++kk) s[tt] = mfma32x32x16<T>(kfr[tt][kk], qf[kk], s[tt]);
+            }
+        } else {
+#pragma unroll
+        for (int tt = 0; tt < NS; ++tt) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) s[tt][r] = 0.f;
 #pragma unroll
@@ -425,26 +450,39 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_v2(
                 s[tt] = mfma32x32x16<T>(kf, qf[kk], s[tt]);
             }
         }
+        }
 
         if (t >= t_mask) {
             const int lim = causal ? q0 + l32 + off_diag : Nk;
 #pragma unroll
-            for (int tt = 0; tt < 2; ++tt)
+            for (int tt = 0; tt < NS; ++tt)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    const int key = t * KT + tt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
+                    const int key = t * KTL + tt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
                     if (key >= Nk || key > lim) s[tt][r] = -INFINITY;
                 }
         }
 
-        float mx = max3(s[0][0], s[1][0], s[0][1]);
-        float my = max3(s[1][1], s[0][2], s[1][2]);
+        float mx, my;
+        if constexpr (NS == 2) {
+            mx = max3(s[0][0], s[1][0], s[0][1]);
+            my = max3(s[1][1], s[0][2], s[1][2]);
 #pragma unroll
-        for (int r = 3; r < 15; r += 2) {
-            mx = max3(mx, s[0][r], s[1][r]);
-            my = max3(my, s[0][r + 1], s[1][r + 1]);
+            for (int r = 3; r < 15; r += 2) {
+                mx = max3(mx, s[0][r], s[1][r]);
+                my = max3(my, s[0][r + 1], s[1][r + 1]);
+            }
+            mx = max3(mx, my, max3(s[0][15], s[1][15], mx));
+        } else {
+            mx = max3(s[0][0], s[0][1], s[0][2]);
+            my = max3(s[0][3], s[0][4], s[0][5]);
+#pragma unroll
+            for (int i = 6; i + 3 < NS * 16; i += 4) {
+                mx = max3(mx, s[i / 16][i % 16], s[(i + 1) / 16][(i + 1) % 16]);
+                my = max3(my, s[(i + 2) / 16][(i + 2) % 16], s[(i + 3) / 16][(i + 3) % 16]);
+            }
+            mx = max3(mx, my, max3(s[NS - 1][14], s[NS - 1][15], mx));
         }
-        mx = max3(mx, my, max3(s[0][15], s[1][15], mx));
         if constexpr ((OPT & kOptPermlane) != 0) mx = xor32_max(mx);
         else mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
         float m_new = fmaxf(m_run, mx * c);
@@ -453,7 +491,7 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_v2(
         m_run = m_new;
         float rs = 0.f;
 #pragma unroll
-        for (int tt = 0; tt < 2; ++tt)
+        for (int tt = 0; tt < NS; ++tt)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const float p = __builtin_amdgcn_exp2f(fmaf(s[tt][r], c, -m_new));
@@ -468,9 +506,9 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_v2(
                 for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
         }
 
-        i32x4 pb[2][2];
+        i32x4 pb[NS][2];
 #pragma unroll
-        for (int tt = 0; tt < 2; ++tt)
+        for (int tt = 0; tt < NS; ++tt)
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) {
                 const int r0 = 8 * s2;
@@ -482,7 +520,7 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_v2(
         if constexpr ((OPT & kOptRoundedSum) != 0) {
             float r0 = 0.f, r1 = 0.f;
 #pragma unroll
-            for (int tt = 0; tt < 2; ++tt)
+            for (int tt = 0; tt < NS; ++tt)
 #pragma unroll
                 for (int s2 = 0; s2 < 2; ++s2) {
                     r0 = add_pair<T>((uint32_t)pb[tt][s2][0], r0);
@@ -492,10 +530,38 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_v2(
                 }
             l_run = fmaf(l_run, alpha, r0 + r1);
         }
+        if constexpr ((OPT & kOptBatchReads) != 0) {
+            // V^T fragments of one 32-column block read as a batch, the next
+            // block's batch issued before this block's MFMAs
+            i32x4 vf[2][NS][2];
+            auto read_v = [&](int dblk, i32x4 (&dst)[NS][2]) {
+#pragma unroll
+                for (int tt = 0; tt < NS; ++tt)
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2) {
+                        const int ro = (tt * 32 + 16 * s2) * L::VS + dblk * 64;
+                        const i32x2 lo = lds_read_tr16(vb, ro);
+                        const i32x2 hi = lds_read_tr16(vb, ro + 8 * L::VS);
+                        dst[tt][s2] = i32x4{lo.x, lo.y, hi.x, hi.y};
+                    }
+            };
+            read_v(0, vf[0]);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int dblk = 0; dblk < D / 32; ++dblk) {
+                if (dblk + 1 < D / 32) read_v(dblk + 1, vf[(dblk + 1) & 1]);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int tt = 0; tt < NS; ++tt)
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2)
+                        oacc[dblk] = mfma32x32x16<T>(vf[dblk & 1][tt][s2], pb[tt][s2], oacc[dblk]);
+            }
+        } else {
 #pragma unroll
         for (int dblk = 0; dblk < D / 32; ++dblk)
 #pragma unroll
-            for (int tt = 0; tt < 2; ++tt)
+            for (int tt = 0; tt < NS; ++tt)
 #pragma unroll
                 for (int s2 = 0; s2 < 2; ++s2) {
                     const int ro = (tt * 32 + 16 * s2) * L::VS + dblk * 64;
@@ -503,6 +569,7 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_v2(
                     const i32x2 hi = lds_read_tr16(vb, ro + 8 * L::VS);
                     oacc[dblk] = mfma32x32x16<T>(i32x4{lo.x, lo.y, hi.x, hi.y}, pb[tt][s2], oacc[dblk]);
                 }
+        }
 
         if (t + 1 < nt) store_tile((t + 1) & 1);
         __syncthreads();
@@ -545,6 +612,233 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_v2(
                     *reinterpret_cast<i32x2*>(op + d) = w;
                 }
         }
+    }
+}
+
+// --------------------------------------------------------------------------
+// attn_fwd_pp: variant 21's body split into two barrier phases per tile,
+//   X(t) = S = K.Q^T, mask, softmax -> P(t)      Y(t) = O rescale + P(t).V(t)
+// with waves 4..7 one barrier behind waves 0..3 (one extra s_barrier at the
+// start).  The two waves a SIMD holds (one from each half) then ping-pong:
+// while one runs X (MFMA + the whole VALU softmax) the other runs Y (MFMA),
+// instead of both entering QK^T, softmax and PV together after every
+// barrier (in lockstep the softmax VALU of both waves serialises between
+// the MFMA blocks).  Staging of tile t+1: the leading half stores its rows
+// at the end of Y(t), the lagging half at the end of X(t) -- both after
+// every read of tile t-1 and before the first read of t+1 (X(t+1) of the
+// leading half); each thread then issues its loads for t+2.  The leading
+// half ends with one extra barrier so both halves execute the same count.
+template <typename T, int D>
+__global__ __launch_bounds__(512, 2) void attn_fwd_pp(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
+    const uint16_t* __restrict__ v, uint16_t* __restrict__ o, int H, int group,
+    int Nq, int Nk, AttnStrides st, float c, int causal, int qblocks,
+    int nblocks) {
+    using L = PadLayout<D>;
+    constexpr int NW = 8, NT = 512;
+    constexpr int CPR = D / 8;
+    constexpr int RPI = NT / CPR;
+    constexpr int CPT = KT / RPI;
+    static_assert(NT % CPR == 0 && KT % RPI == 0, "staging must tile evenly");
+    __shared__ __attribute__((aligned(16))) char smem[2 * L::BUF];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const bool lag = wave >= NW / 2;
+    const int h32 = lane >> 5, l32 = lane & 31;
+    const int lb = xcd_remap(blockIdx.x, nblocks);
+    const int bh = lb / qblocks;
+    const int qblk = causal ? qblocks - 1 - lb % qblocks : lb % qblocks;
+    const int b = bh / H, hq = bh % H, hk = hq / group;
+    const int qbase = qblk * (NW * QW);
+    const int q0 = qbase + wave * QW;
+    const int off_diag = Nk - Nq;
+
+    const uint16_t* qp = q + b * st.qb + hq * st.qh;
+    const uint16_t* kp = k + b * st.kb + hk * st.kh;
+    const uint16_t* vp = v + b * st.vb + hk * st.vh;
+
+    i32x4 qf[D / 16];
+    {
+        const int qr = q0 + l32;
+        const bool ok = qr < Nq;
+        const uint16_t* src = qp + (int64_t)(ok ? qr : 0) * st.qn + 8 * h32;
+#pragma unroll
+        for (int kk = 0; kk < D / 16; ++kk) {
+            const i32x4 x = *reinterpret_cast<const i32x4*>(src + 16 * kk);
+            qf[kk] = ok ? x : i32x4{0, 0, 0, 0};
+        }
+    }
+
+    int kv_end = Nk;
+    if (causal) kv_end = min(Nk, qbase + NW * QW + off_diag);
+    const int nt = kv_end > 0 ? cdiv(kv_end, KT) : 0;
+    const int t_full = Nk / KT;
+    int t_mask = t_full;
+    if (causal) t_mask = min(t_mask, max(0, (q0 + off_diag + 1) / KT));
+
+    const int srow = tid / CPR, sch = tid % CPR;
+    const uint16_t* kg = kp + (int64_t)srow * st.kn + sch * 8;
+    const uint16_t* vg = vp + (int64_t)srow * st.vn + sch * 8;
+    const int kw = srow * L::KS + sch * 16, vw = L::KSZ + srow * L::VS + sch * 16;
+    i32x4 kst[CPT], vst[CPT];
+    auto load_tile = [&](int t) {
+        if (t < t_full) {
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) {
+                const int64_t r = (int64_t)t * KT + i * RPI;
+                kst[i] = *reinterpret_cast<const i32x4*>(kg + r * st.kn);
+                vst[i] = *reinterpret_cast<const i32x4*>(vg + r * st.vn);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) {
+                const int key = t * KT + i * RPI + srow;
+                const int64_t r = min(key, Nk - 1) - srow;
+                const i32x4 kx = *reinterpret_cast<const i32x4*>(kg + r * st.kn);
+                const i32x4 vx = *reinterpret_cast<const i32x4*>(vg + r * st.vn);
+                kst[i] = key < Nk ? kx : i32x4{0, 0, 0, 0};
+                vst[i] = key < Nk ? vx : i32x4{0, 0, 0, 0};
+            }
+        }
+    };
+    auto store_tile = [&](int buf) {
+        char* base = smem + buf * L::BUF;
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+            lds_write_b128(base, kw + i * RPI * L::KS, kst[i]);
+            lds_write_b128(base, vw + i * RPI * L::VS, vst[i]);
+        }
+    };
+
+    const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+    const int kr = l32 * L::KS + h32 * 16;
+    const int vr = L::KSZ + (4 * h32 + qq) * L::VS + (2 * (g & 1) + (pp >> 1)) * 16 + 8 * (pp & 1);
+
+    f32x16 oacc[D / 32];
+#pragma unroll
+    for (int d = 0; d < D / 32; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[d][r] = 0.f;
+    float m_run = -1e30f, l_run = 0.f;
+
+    if (nt > 0) {
+        load_tile(0);
+        store_tile(0);
+    }
+    __syncthreads();
+    if (nt > 1) load_tile(1);
+    if (lag) __builtin_amdgcn_s_barrier();  // the lagging half runs one phase behind
+
+    for (int t = 0; t < nt; ++t) {
+        const char* kb = smem + (t & 1) * L::BUF + kr;
+        const char* vb = smem + (t & 1) * L::BUF + vr;
+        // ------------------------------------------------------------ X(t)
+        f32x16 s[2];
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[tt][r] = 0.f;
+#pragma unroll
+            for (int kk = 0; kk < D / 16; ++kk) {
+                const i32x4 kf = lds_read_b128(kb, tt * 32 * L::KS + kk * 32);
+                s[tt] = mfma32x32x16<T>(kf, qf[kk], s[tt]);
+            }
+        }
+        if (t >= t_mask) {
+            const int lim = causal ? q0 + l32 + off_diag : Nk;
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int key = t * KT + tt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
+                    if (key >= Nk || key > lim) s[tt][r] = -INFINITY;
+                }
+        }
+        float mx = max3(s[0][0], s[1][0], s[0][1]);
+        float my = max3(s[1][1], s[0][2], s[1][2]);
+#pragma unroll
+        for (int r = 3; r < 15; r += 2) {
+            mx = max3(mx, s[0][r], s[1][r]);
+            my = max3(my, s[0][r + 1], s[1][r + 1]);
+        }
+        mx = xor32_max(max3(mx, my, max3(s[0][15], s[1][15], mx)));
+        float m_new = fmaxf(m_run, mx * c);
+        m_new = mx * c > m_run + kDeferThr ? m_new : m_run;
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+        m_run = m_new;
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[tt][r] = __builtin_amdgcn_exp2f(fmaf(s[tt][r], c, -m_new));
+        i32x4 pb[2][2];
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const int r0 = 8 * s2;
+                pb[tt][s2] = i32x4{(int)pack2<T>(s[tt][r0 + 0], s[tt][r0 + 1]),
+                                   (int)pack2<T>(s[tt][r0 + 2], s[tt][r0 + 3]),
+                                   (int)pack2<T>(s[tt][r0 + 4], s[tt][r0 + 5]),
+                                   (int)pack2<T>(s[tt][r0 + 6], s[tt][r0 + 7])};
+            }
+        {
+            float r0 = 0.f, r1 = 0.f;
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    r0 = add_pair<T>((uint32_t)pb[tt][s2][0], r0);
+                    r1 = add_pair<T>((uint32_t)pb[tt][s2][1], r1);
+                    r0 = add_pair<T>((uint32_t)pb[tt][s2][2], r0);
+                    r1 = add_pair<T>((uint32_t)pb[tt][s2][3], r1);
+                }
+            l_run = fmaf(l_run, alpha, r0 + r1);
+        }
+        if (lag && t + 1 < nt) {
+            store_tile((t + 1) & 1);
+            if (t + 2 < nt) load_tile(t + 2);
+        }
+        __syncthreads();
+        // ------------------------------------------------------------ Y(t)
+        if (__ballot(alpha != 1.f)) {
+#pragma unroll
+            for (int d = 0; d < D / 32; ++d)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
+        }
+#pragma unroll
+        for (int dblk = 0; dblk < D / 32; ++dblk)
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    const int ro = (tt * 32 + 16 * s2) * L::VS + dblk * 64;
+                    const i32x2 lo = lds_read_tr16(vb, ro);
+                    const i32x2 hi = lds_read_tr16(vb, ro + 8 * L::VS);
+                    oacc[dblk] = mfma32x32x16<T>(i32x4{lo.x, lo.y, hi.x, hi.y}, pb[tt][s2], oacc[dblk]);
+                }
+        if (!lag && t + 1 < nt) {
+            store_tile((t + 1) & 1);
+            if (t + 2 < nt) load_tile(t + 2);
+        }
+        __syncthreads();
+    }
+    if (!lag) __builtin_amdgcn_s_barrier();  // match the lagging half's extra barrier
+
+    const float l = xor32_sum(l_run);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const int qr = q0 + l32;
+    if (qr < Nq) {
+        uint16_t* op = o + b * st.ob + hq * st.oh + (int64_t)qr * st.on;
+#pragma unroll
+        for (int dblk = 0; dblk < D / 32; ++dblk)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int d = dblk * 32 + 8 * i + 4 * h32;
+                const i32x2 w = {(int)pack2<T>(oacc[dblk][4 * i] * inv, oacc[dblk][4 * i + 1] * inv),
+                                 (int)pack2<T>(oacc[dblk][4 * i + 2] * inv, oacc[dblk][4 * i + 3] * inv)};
+                *reinterpret_cast<i32x2*>(op + d) = w;
+            }
     }
 }
 
@@ -1853,6 +2147,10 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
 //         sum), 9 (permlane + rounded sum)
 //  24: variant 21 + epilogue stores widened to dwordx4 (OPT 16)
 //  (16 waves x 32 rows was tried: needs <= 128 VGPRs and spills 296 B/lane)
+//  25: variant 21 with 128-key tiles (one barrier per 128 keys; 148 KiB LDS)
+//  27: attn_fwd_pp -- variant 21 split in two phases, waves 4-7 one phase
+//      behind (ping-pong of the two waves on each SIMD)
+//  28: variant 21 + iglp_opt(0)      29: variant 21 + batched fragment reads
 // default: v2 NW8 + permlane row max + defer-max (THR 8, log2) + rounded-P row sum
 // (1057 TF vs 983 for plain v2 at B8 H32 S4096 D128; spike + variant parity green)
 constexpr int kDefaultVariant = 21;
@@ -1902,6 +2200,10 @@ int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int
         case 22: PLI_ATTN_LAUNCH((attn_fwd_v2<T, D, 8, true, 12>)); break;
         case 23: PLI_ATTN_LAUNCH((attn_fwd_v2<T, D, 8, true, 9>)); break;
         case 24: PLI_ATTN_LAUNCH((attn_fwd_v2<T, D, 8, true, 29>)); break;
+        case 25: PLI_ATTN_LAUNCH((attn_fwd_v2<T, D, 8, true, 13, 128>)); break;
+        case 27: PLI_ATTN_LAUNCH((attn_fwd_pp<T, D>)); break;
+        case 28: PLI_ATTN_LAUNCH((attn_fwd_v2<T, D, 8, true, 13 | 32>)); break;
+        case 29: PLI_ATTN_LAUNCH((attn_fwd_v2<T, D, 8, true, 13 | 128>)); break;
         case 15: hipLaunchKernelGGL((attn_fwd_v6<T, D>), grid, dim3(512), 0, stream, qq, kk, vv, oo,
                                     H, group, Nq, Nk, st, c, causal, qblocks, (int)nb); break;
         case 14: PLI_ATTN_V5(1, true); break;

@@ -39,7 +39,7 @@ def interleave(fns: dict, iters: int, rounds: int):
     return {k: (float(np.median(v)), float(np.min(v))) for k, v in res.items()}
 
 
-def tune_flash(variants=(21, 24, 2), causal=False, B=8, H=32, S=4096, D=128):
+def tune_flash(variants=(21, 28, 29), causal=False, B=8, H=32, S=4096, D=128):
     from oracle.attention import naive_attention
     g = torch.Generator(device="cuda").manual_seed(0)
     q, k, v = (torch.randn(B, H, S, D, device="cuda", dtype=torch.bfloat16, generator=g) for _ in range(3))
@@ -50,7 +50,7 @@ def tune_flash(variants=(21, 24, 2), causal=False, B=8, H=32, S=4096, D=128):
     ref = naive_attention(*(t[0:1, 0:1].float().cpu().numpy() for t in (q, k, v)), causal=causal)
     fns = {vv: (lambda vv=vv: pli_hip.flash_attn_fwd(q, k, v, causal=causal, out=outs[vv], variant=vv))
            for vv in variants}
-    t = interleave(fns, 5, 3)
+    t = interleave(fns, 5, int(os.environ.get("PLI_TUNE_ROUNDS", "3")))
     flops = 4 * B * H * S * S * D * (0.5 if causal else 1.0)
     for vv in variants:
         diff = (outs[vv].float() - outs[variants[0]].float()).abs().max().item()
