@@ -246,7 +246,7 @@ __device__ __forceinline__ int g2_off_rows(int row, int c) {  // 128-B rows
 }
 __device__ __forceinline__ int g2_fnn(int k) { return 2 * ((k & 3) | (((k >> 3) & 1) << 2)); }
 
-template <typename T, bool TRANS_B, bool BIAS>
+template <typename T, bool TRANS_B, bool BIAS, bool PRIO = false>
 __global__ __launch_bounds__(512, 2) void gemm_256(const uint16_t* __restrict__ A,
                                                    const uint16_t* __restrict__ Bm,
                                                    uint16_t* __restrict__ C,
@@ -331,10 +331,12 @@ __global__ __launch_bounds__(512, 2) void gemm_256(const uint16_t* __restrict__ 
                     bf[ni] = i32x4{lo.x, lo.y, hi.x, hi.y};
                 }
             }
+            if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
                 for (int mi = 0; mi < 8; ++mi) acc[ni][mi] = mfma16x16x32<T>(bf[ni], af[mi], acc[ni][mi]);
+            if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
         }
         __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();
@@ -968,7 +970,8 @@ int launch_mfma(const void* a, const void* b, void* c, const void* bias, int M, 
 
 template <typename T>
 int launch_256(const void* a, const void* b, void* c, const void* bias, int M, int N, int K,
-               int64_t lda, int64_t ldb, int64_t ldc, int trans_b, hipStream_t s, bool phased) {
+               int64_t lda, int64_t ldb, int64_t ldc, int trans_b, hipStream_t s, bool phased,
+               bool prio = false) {
     const int tm = cdiv(M, G2M), tn = cdiv(N, G2N);
     const int64_t nb = (int64_t)tm * tn;
     PLI_REQUIRE(nb < (1ll << 31), "pli_gemm: grid too large");
@@ -977,6 +980,10 @@ int launch_256(const void* a, const void* b, void* c, const void* bias, int M, i
     do {                                                                                          \
         if (phased)                                                                               \
             hipLaunchKernelGGL((gemm_256p<T, TB, BI>), grid, block, 0, s, (const uint16_t*)a,     \
+                               (const uint16_t*)b, (uint16_t*)c, (const uint16_t*)bias, M, N, K,  \
+                               lda, ldb, ldc, tn, (int)nb);                                       \
+        else if (prio)                                                                            \
+            hipLaunchKernelGGL((gemm_256<T, TB, BI, true>), grid, block, 0, s, (const uint16_t*)a, \
                                (const uint16_t*)b, (uint16_t*)c, (const uint16_t*)bias, M, N, K,  \
                                lda, ldb, ldc, tn, (int)nb);                                       \
         else                                                                                      \
@@ -1085,8 +1092,9 @@ extern "C" int pli_gemm_swiglu(const void* x, const void* wg, const void* wu, vo
 }
 
 // variant: 0 = default routing, 1 = force the 128x128 MFMA tile, 2 = force
-// the 256x256 LDS-DMA tile, 3 = force the phased 256x256 tile (where their
-// shape conditions hold)
+// the 256x256 LDS-DMA tile, 3 = force the phased 256x256 tile, 4 = the
+// 256x256 tile with s_setprio(1) around its MFMA clusters (where their shape
+// conditions hold)
 extern "C" int pli_gemm_variant(const void* a, const void* b, void* c, const void* bias, int m,
                                 int n, int k, int64_t lda, int64_t ldb, int64_t ldc, int trans_b,
                                 int dtype, void* stream, int variant) {
@@ -1131,10 +1139,10 @@ extern "C" int pli_gemm_variant(const void* a, const void* b, void* c, const voi
     // grid of tiles so the block count is not tiny)
     const bool big = vec && k % G2K == 0 && m >= 2 * G2M && n >= 2 * G2N && variant != 1;
     if (big || (vec && variant >= 2 && k % G2K == 0 && n >= 8)) {
-        const bool phased = variant == 3;
+        const bool phased = variant == 3, prio = variant == 4;
         if (dtype == PLI_BF16)
-            return launch_256<bf16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, s, phased);
-        return launch_256<f16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, s, phased);
+            return launch_256<bf16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, s, phased, prio);
+        return launch_256<f16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, s, phased, prio);
     }
     if (vec) {
         if (dtype == PLI_BF16)

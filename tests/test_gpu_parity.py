@@ -234,7 +234,7 @@ def test_gemm_vs_oracle(m, n, k, dt, tb):
     assert_lin_close(c, ref, dt, f"gemm {m}x{n}x{k} {dt} tb={tb}")
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4])
 @pytest.mark.parametrize("m,n,k,tb,bias", [
     (512, 512, 512, False, False),
     (512, 512, 512, True, True),

@@ -368,14 +368,12 @@ def tune_gemm():
         a = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
         b = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
         c = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
-        fns = {"hip_nn_128": lambda: pli_hip.gemm(a, b, out=c, variant=1),
-               "hip_nn_256": lambda: pli_hip.gemm(a, b, out=c, variant=2),
-               "hip_nn_256p": lambda: pli_hip.gemm(a, b, out=c, variant=3),
-               "hip_nt_128": lambda: pli_hip.gemm(a, b, trans_b=True, out=c, variant=1),
+        fns = {"hip_nn_256": lambda: pli_hip.gemm(a, b, out=c, variant=2),
+               "hip_nn_256prio": lambda: pli_hip.gemm(a, b, out=c, variant=4),
                "hip_nt_256": lambda: pli_hip.gemm(a, b, trans_b=True, out=c, variant=2),
-               "hip_nt_256p": lambda: pli_hip.gemm(a, b, trans_b=True, out=c, variant=3),
+               "hip_nt_256prio": lambda: pli_hip.gemm(a, b, trans_b=True, out=c, variant=4),
                "torch_nn": lambda: torch.mm(a, b)}
-        t = interleave(fns, 5, 3)
+        t = interleave(fns, 5, int(os.environ.get("PLI_TUNE_ROUNDS", "3")))
         for kname, (med, mn) in t.items():
             print(json.dumps({"kernel": "gemm", "n": n, "impl": kname, "ms_med": med,
                               "TFLOP/s": 2 * n ** 3 / med / 1e9}), flush=True)
