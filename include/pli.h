@@ -213,6 +213,20 @@ int pli_kv_append(const void* k_new, const void* v_new, void* k_cache,
                   void* v_cache, int batch, int n_new, int kv_heads,
                   int head_dim, int capacity, const int64_t* strides,
                   const int32_t* pos_dev, int dtype, void* stream);
+/* pli_gemm_multi_nt: the q, k and v projections of a decode step in one
+ * launch, k / v written straight into the caches (fuses pli_kv_append).
+ * Up to 3 groups share x [m, k] (m <= 16 rows = batch x tokens_per_batch);
+ * group g computes x W_g^T ([n_g, k] weights, ldw_g) and stores row
+ * r = b * tokens_per_batch + s at
+ *   c_g + b * stride_batch_g + (s + *row_offset_g) * stride_token_g (+ col),
+ * row_offset_g a device int32 or NULL (= 0); rows >= capacity_g are dropped.
+ * bf16/fp16, k % 8 == 0. */
+int pli_gemm_multi_nt(const void* x, int64_t ldx, int m, int k,
+                      int tokens_per_batch, const void* const* w,
+                      void* const* c, const int* n, const int64_t* ldw,
+                      const int64_t* stride_batch, const int64_t* stride_token,
+                      const int32_t* const* row_offset, const int* capacity,
+                      int ngroups, int dtype, void* stream);
 int pli_attn_decode_dev(const void* q, const void* k, const void* v, void* o,
                         int batch, int heads, int kv_heads, int n_q,
                         int n_kv_max, int head_dim, const int64_t* strides,

@@ -77,6 +77,17 @@ class CachedGQA(nn.Module):
     def forward(self, x: torch.Tensor, cache: LayerKVCache | None = None, start_pos: int = 0
                 ) -> torch.Tensor:
         B, S, _ = x.shape
+        if (cache is not None and cache.pos is not None and x.is_cuda and B * S <= 16
+                and _device_len_ok_shape(x, S, self.num_heads, self.num_kv_heads, self.head_dim)):
+            # decode step, device-resident length: q/k/v projections in one
+            # launch with k/v written straight into the cache rows at pos
+            q = torch.empty(B, S, self.num_heads * self.head_dim, device=x.device, dtype=x.dtype)
+            pli_hip.qkv_into_cache(x, self.q_proj.weight, self.k_proj.weight, self.v_proj.weight,
+                                   q, cache.k, cache.v, cache.pos)
+            cache.seq_len += S
+            o = pli_hip.attn_decode_dev(q.view(B, S, self.num_heads, self.head_dim), cache.k,
+                                        cache.v, cache.pos, n_kv_add=S, causal=S > 1)
+            return _lin(o.reshape(B, S, self.hidden_dim), self.o_proj.weight)
         q = _lin(x, self.q_proj.weight).view(B, S, self.num_heads, self.head_dim)
         k = _lin(x, self.k_proj.weight).view(B, S, self.num_kv_heads, self.head_dim)
         v = _lin(x, self.v_proj.weight).view(B, S, self.num_kv_heads, self.head_dim)
@@ -92,6 +103,11 @@ class CachedGQA(nn.Module):
             k_buf, v_buf, n_kv = k, v, S
         o = attend_cached(q, k_buf, v_buf, n_kv).reshape(B, S, self.hidden_dim)
         return _lin(o, self.o_proj.weight)
+
+
+def _device_len_ok_shape(x: torch.Tensor, S: int, H: int, Hkv: int, D: int) -> bool:
+    return (x.dtype in (torch.bfloat16, torch.float16) and D in (64, 128)
+            and S * (H // Hkv) <= 16 and x.shape[-1] % 8 == 0)
 
 
 def _device_len_ok(q: torch.Tensor, cache: LayerKVCache) -> bool:

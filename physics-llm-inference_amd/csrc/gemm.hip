@@ -713,6 +713,84 @@ __global__ __launch_bounds__(128) void gemm_skinny_nt(const uint16_t* __restrict
     }
 }
 
+// Multi-output skinny NT GEMM for the decode step: up to 3 weight matrices
+// (e.g. the q, k and v projections) against the same M <= 16 rows of X in
+// ONE launch, each output with its own row addressing so the k / v rows can
+// be written straight into a [B, S_max, Hkv, D] cache at a device-resident
+// position: row r = b * S + s of group g goes to
+//   c + b * stride_batch + (s + *row_offset) * stride_token   (+ column n),
+// and is dropped when s + *row_offset >= capacity.  One wave per output
+// column, as gemm_skinny_nt; waves are assigned to groups by column range.
+struct MultiGroup {
+    const uint16_t* w;
+    uint16_t* c;
+    int n;
+    int64_t ldw, stride_batch, stride_token;
+    const int* row_offset;
+    int capacity;
+};
+struct MultiArgs {
+    MultiGroup g[3];
+    int ngroups;
+};
+
+template <typename T, int NB>
+__global__ __launch_bounds__(128) void gemm_skinny_multi(const uint16_t* __restrict__ X, int M,
+                                                         int S, int nchunks, int64_t ldx,
+                                                         MultiArgs args) {
+    constexpr int CPL = 8;
+    const int lane = threadIdx.x & 63;
+    int n = blockIdx.x * 2 + (threadIdx.x >> 6);
+    int gi = 0;
+    while (gi < args.ngroups && n >= args.g[gi].n) n -= args.g[gi++].n;
+    if (gi >= args.ngroups) return;
+    const MultiGroup& G = args.g[gi];
+    const uint16_t* wrow = G.w + (int64_t)n * G.ldw;
+    float acc[NB];
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb) acc[bb] = 0.f;
+    for (int c0 = 0; c0 < nchunks; c0 += 64 * CPL) {
+        i32x4 wv[CPL];
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) {
+            const int cc = min(c0 + lane + 64 * u, nchunks - 1);
+            wv[u] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wrow + cc * 8));
+        }
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) {
+            const int cc = c0 + lane + 64 * u;
+            if (cc < nchunks) {
+#pragma unroll
+                for (int bb = 0; bb < NB; ++bb) {
+                    if (bb < M) {
+                        const i32x4 xv = *reinterpret_cast<const i32x4*>(X + bb * ldx + cc * 8);
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const int wi = wv[u][i], xi = xv[i];
+                            const float w0 = elem<T>::to_f32(T{(uint16_t)(wi & 0xffff)});
+                            const float w1 = elem<T>::to_f32(T{(uint16_t)((uint32_t)wi >> 16)});
+                            const float x0 = elem<T>::to_f32(T{(uint16_t)(xi & 0xffff)});
+                            const float x1 = elem<T>::to_f32(T{(uint16_t)((uint32_t)xi >> 16)});
+                            acc[bb] = fmaf(w1, x1, fmaf(w0, x0, acc[bb]));
+                        }
+                    }
+                }
+            }
+        }
+    }
+    const int off = G.row_offset ? *G.row_offset : 0;
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb) {
+        if (bb < M) {
+            const float r = wave_sum(acc[bb]);
+            const int b = bb / S, srow = bb % S + off;
+            if (lane == 0 && srow < G.capacity)
+                G.c[b * G.stride_batch + (int64_t)srow * G.stride_token + n] =
+                    __builtin_bit_cast(uint16_t, elem<T>::from_f32(r));
+        }
+    }
+}
+
 template <typename T>
 int launch_skinny(const void* a, const void* b, void* c, const void* bias, int M, int N, int K,
                   int64_t lda, int64_t ldb, int64_t ldc, hipStream_t s) {
@@ -1208,4 +1286,53 @@ extern "C" int pli_gemm_grouped(const void* x, const int32_t* gather, const void
 #undef PLI_GRP_NBG
 #undef PLI_GRP
     return launch_status("pli_gemm_grouped");
+}
+
+// Multi-output decode projection (see gemm_skinny_multi): up to 3 groups
+// sharing X [m, k] (m <= 16 rows = batch x tokens_per_batch); each group g
+// writes c_g[b * stride_batch + (s + *row_offset) * stride_token + n] for
+// row r = b * tokens_per_batch + s (row_offset may be NULL = 0; rows at or
+// past `capacity` are dropped).
+extern "C" int pli_gemm_multi_nt(const void* x, int64_t ldx, int m, int k, int tokens_per_batch,
+                                 const void* const* w, void* const* c, const int* n,
+                                 const int64_t* ldw, const int64_t* stride_batch,
+                                 const int64_t* stride_token, const int32_t* const* row_offset,
+                                 const int* capacity, int ngroups, int dtype, void* stream) {
+    using namespace pli;
+    clear_error();
+    PLI_REQUIRE(x && w && c && n && ldw && stride_batch && stride_token && row_offset && capacity,
+                "pli_gemm_multi_nt: null pointer");
+    PLI_REQUIRE(ngroups >= 1 && ngroups <= 3, "pli_gemm_multi_nt: 1..3 groups, got %d", ngroups);
+    PLI_REQUIRE(m >= 1 && m <= 16 && k > 0 && k % 8 == 0 && ldx >= k && ldx % 8 == 0 &&
+                    tokens_per_batch >= 1 && m % tokens_per_batch == 0 && al16(x),
+                "pli_gemm_multi_nt: needs 1 <= m <= 16 rows (whole batches), k %% 8 == 0, aligned x");
+    PLI_REQUIRE(dtype == PLI_BF16 || dtype == PLI_F16, "pli_gemm_multi_nt: bf16/fp16 only");
+    MultiArgs args{};
+    int ntot = 0;
+    for (int g = 0; g < ngroups; ++g) {
+        PLI_REQUIRE(w[g] && c[g] && n[g] > 0 && ldw[g] >= k && ldw[g] % 8 == 0 && al16(w[g]),
+                    "pli_gemm_multi_nt: bad group %d", g);
+        args.g[g] = MultiGroup{(const uint16_t*)w[g], (uint16_t*)c[g], n[g], ldw[g],
+                               stride_batch[g], stride_token[g], row_offset[g], capacity[g]};
+        ntot += n[g];
+    }
+    args.ngroups = ngroups;
+    const dim3 grid(cdiv(ntot, 2)), block(128);
+    hipStream_t s = (hipStream_t)stream;
+    const auto* X = (const uint16_t*)x;
+    const int nch = k / 8;
+#define PLI_MULTI(TT, NB) \
+    hipLaunchKernelGGL((gemm_skinny_multi<TT, NB>), grid, block, 0, s, X, m, tokens_per_batch, nch, ldx, args)
+#define PLI_MULTI_NB(TT)                  \
+    do {                                  \
+        if (m <= 1) PLI_MULTI(TT, 1);     \
+        else if (m <= 2) PLI_MULTI(TT, 2);\
+        else if (m <= 4) PLI_MULTI(TT, 4);\
+        else if (m <= 8) PLI_MULTI(TT, 8);\
+        else PLI_MULTI(TT, 16);           \
+    } while (0)
+    if (dtype == PLI_BF16) PLI_MULTI_NB(bf16_t); else PLI_MULTI_NB(f16_t);
+#undef PLI_MULTI_NB
+#undef PLI_MULTI
+    return launch_status("pli_gemm_multi_nt");
 }

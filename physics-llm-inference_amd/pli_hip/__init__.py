@@ -40,6 +40,8 @@ _SIGS = {
                         _c_i64, _c_int, _vp],
     "pli_rmsnorm": [_vp, _vp, _vp, _vp, _vp, _c_i64, _c_int, _c_i64, _c_i64, _c_i64, _c_i64,
                     _c_f32, _c_int, _vp],
+    "pli_gemm_multi_nt": [_vp, _c_i64, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                          _vp, _c_int, _c_int, _vp],
     "pli_moe_route": [_vp, _c_i64, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp,
                       _vp, _vp, _vp],
     "pli_gemm_grouped": [_vp, _vp, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_i64,
@@ -386,6 +388,47 @@ def rmsnorm(x: torch.Tensor, weight: torch.Tensor, eps: float = 1e-6,
     _check(rc, "pli_rmsnorm")
     y = y.view(x.shape)
     return y if residual is None else (h.view(x.shape), y)
+
+
+def qkv_into_cache(x: torch.Tensor, wq: torch.Tensor, wk: torch.Tensor, wv: torch.Tensor,
+                   q_out: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                   pos: torch.Tensor) -> torch.Tensor:
+    """Decode-step projections in one launch (pli_gemm_multi_nt): x [B, S, hidden]
+    (B*S <= 16) -> q_out [B, S, Hq*D]; k / v rows written into [B, S_max, Hkv, D]
+    caches at rows pos[0] + s.  Returns q_out."""
+    dev = _require_gpu(x, wq, wk, wv, q_out, k_cache, v_cache)
+    B, S, hidden = x.shape
+    x2 = x.reshape(B * S, hidden)
+    if x2.stride(1) != 1:
+        x2 = x2.contiguous()
+    S_max, Hkv, D = k_cache.shape[1:]
+    if pos.dtype != torch.int32 or not pos.is_cuda:
+        raise PliError("pos must be an int32 device tensor")
+    for name, t in (("k_cache", k_cache), ("v_cache", v_cache)):
+        if t.shape[0] != B or t.stride(3) != 1 or t.stride(2) != D:
+            raise PliError(f"{name} must be [B, S_max, Hkv, D] with contiguous (Hkv, D) rows")
+    if tuple(v_cache.shape) != tuple(k_cache.shape):
+        raise PliError("k_cache / v_cache shape mismatch")
+    if wk.shape[0] != Hkv * D or wv.shape[0] != Hkv * D or q_out.shape[-1] != wq.shape[0]:
+        raise PliError("projection widths do not match the cache / output")
+    if q_out.dim() != 3 or tuple(q_out.shape[:2]) != (B, S) or q_out.stride(2) != 1:
+        raise PliError("q_out must be [B, S, Hq*D] with unit inner stride")
+    if any(w.stride(1) != 1 or w.shape[1] != hidden for w in (wq, wk, wv)):
+        raise PliError("weights must be [n, hidden] with unit inner stride")
+    P = ctypes.c_void_p
+    w = (P * 3)(*(t.data_ptr() for t in (wq, wk, wv)))
+    c = (P * 3)(q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr())
+    n = (_c_int * 3)(wq.shape[0], wk.shape[0], wv.shape[0])
+    ldw = (_c_i64 * 3)(wq.stride(0), wk.stride(0), wv.stride(0))
+    sb = (_c_i64 * 3)(q_out.stride(0), k_cache.stride(0), v_cache.stride(0))
+    stok = (_c_i64 * 3)(q_out.stride(1), k_cache.stride(1), v_cache.stride(1))
+    ro = (P * 3)(None, pos.data_ptr(), pos.data_ptr())
+    cap = (_c_int * 3)(S, S_max, S_max)
+    with _on_device(dev):
+        rc = lib().pli_gemm_multi_nt(_ptr(x2), x2.stride(0), B * S, hidden, S, w, c, n, ldw, sb, stok,
+                                     ro, cap, 3, _dtype_code(x), _stream(dev))
+    _check(rc, "pli_gemm_multi_nt")
+    return q_out
 
 
 # ------------------------------------------------------------ fused SwiGLU

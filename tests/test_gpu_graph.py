@@ -41,6 +41,39 @@ def test_attn_decode_dev_equals_host_length(n, add):
     assert (got.float() - ref.float()).abs().max().item() <= 2 ** -7
 
 
+@pytest.mark.parametrize("B,S", [(1, 1), (2, 1), (4, 4), (16, 1), (3, 5)])
+def test_qkv_into_cache_matches_separate_projections(B, S):
+    """pli_gemm_multi_nt: q plus k/v rows written into the caches at pos ==
+    three pli_gemm calls + pli_kv_append; rows past the capacity dropped."""
+    import pli_hip
+    torch.manual_seed(B * 10 + S)
+    hidden, H, Hkv, D, S_max = 1024, 16, 4, 64, 40
+    x = torch.randn(B, S, hidden, device="cuda", dtype=torch.bfloat16)
+    wq = torch.randn(H * D, hidden, device="cuda", dtype=torch.bfloat16) * 0.03
+    wk = torch.randn(Hkv * D, hidden, device="cuda", dtype=torch.bfloat16) * 0.03
+    wv = torch.randn(Hkv * D, hidden, device="cuda", dtype=torch.bfloat16) * 0.03
+    for p0 in (7, S_max - 2):
+        kc = torch.randn(B, S_max, Hkv, D, device="cuda", dtype=torch.bfloat16)
+        vc = torch.randn_like(kc)
+        rk, rv = kc.clone(), vc.clone()
+        pos = torch.tensor([p0], device="cuda", dtype=torch.int32)
+        q = torch.empty(B, S, H * D, device="cuda", dtype=torch.bfloat16)
+        pli_hip.qkv_into_cache(x, wq, wk, wv, q, kc, vc, pos)
+        x2 = x.reshape(B * S, hidden)
+        ref_q = pli_hip.gemm(x2, wq, trans_b=True).view(B, S, -1)
+        kn = pli_hip.gemm(x2, wk, trans_b=True).view(B, S, Hkv, D)
+        vn = pli_hip.gemm(x2, wv, trans_b=True).view(B, S, Hkv, D)
+        pli_hip.kv_append(kn, vn, rk, rv, pos)
+        tol = 2 ** -7
+        assert (q.float() - ref_q.float()).abs().max().item() <= tol * ref_q.float().abs().max().item()
+        assert (kc.float() - rk.float()).abs().max().item() <= tol * rk.float().abs().max().item()
+        assert (vc.float() - rv.float()).abs().max().item() <= tol * rv.float().abs().max().item()
+        n_in = min(S, S_max - p0)  # untouched rows stay bitwise
+        assert torch.equal(kc[:, :p0], rk[:, :p0]) and torch.equal(vc[:, p0 + n_in:], rv[:, p0 + n_in:])
+        fp = (x2.float() @ wk.float().t()).view(B, S, Hkv, D)[:, :n_in]
+        assert (kc[:, p0:p0 + n_in].float() - fp).abs().max().item() <= 2 ** -6 * fp.abs().max().item()
+
+
 def _model():
     from ch02 import CachedTransformerModel
     torch.manual_seed(0)
