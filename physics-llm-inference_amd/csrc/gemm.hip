@@ -246,13 +246,33 @@ __device__ __forceinline__ int g2_off_rows(int row, int c) {  // 128-B rows
 }
 __device__ __forceinline__ int g2_fnn(int k) { return 2 * ((k & 3) | (((k >> 3) & 1) << 2)); }
 
+// Logical tile index -> output tile.  group_m == 0: row-major.  Otherwise
+// bands of group_m tile rows are swept column by column, so the ~32 blocks an
+// XCD runs at once (consecutive indices after xcd_remap) cover a
+// group_m x (32 / group_m) patch: group_m A panels and 32 / group_m B panels
+// per K-step instead of 1 A panel and 32 B panels.
+__device__ __forceinline__ void g2_tile(int lb, int tiles_m, int tiles_n, int group_m, int& tm,
+                                        int& tn) {
+    if (group_m <= 0) {
+        tm = lb / tiles_n;
+        tn = lb % tiles_n;
+        return;
+    }
+    const int width = group_m * tiles_n;
+    const int first = (lb / width) * group_m;
+    const int rows = min(tiles_m - first, group_m);
+    const int r = lb % width;
+    tm = first + r % rows;
+    tn = r / rows;
+}
+
 template <typename T, bool TRANS_B, bool BIAS, bool PRIO = false>
 __global__ __launch_bounds__(512, 2) void gemm_256(const uint16_t* __restrict__ A,
                                                    const uint16_t* __restrict__ Bm,
                                                    uint16_t* __restrict__ C,
                                                    const uint16_t* __restrict__ bias, int M, int N,
                                                    int K, int64_t lda, int64_t ldb, int64_t ldc,
-                                                   int tiles_n, int nblocks) {
+                                                   int tiles_n, int nblocks, int group_m) {
     constexpr int TA = G2M * G2K * 2;  // 32 KiB
     constexpr int TB = G2N * G2K * 2;  // 32 KiB
     constexpr int BUF = TA + TB;
@@ -262,7 +282,9 @@ __global__ __launch_bounds__(512, 2) void gemm_256(const uint16_t* __restrict__ 
     const int wr = wave >> 2, wc = wave & 3;
     const int l16 = lane & 15, g = lane >> 4;
     const int lb = xcd_remap(blockIdx.x, nblocks);
-    const int m0 = (lb / tiles_n) * G2M, n0 = (lb % tiles_n) * G2N;
+    int tmi, tni;
+    g2_tile(lb, cdiv(M, G2M), tiles_n, group_m, tmi, tni);
+    const int m0 = tmi * G2M, n0 = tni * G2N;
     const int ktiles = K / G2K;
 
     // DMA plan: 32 pieces of 1 KiB per operand tile, 4 per wave each.
@@ -379,13 +401,24 @@ __global__ __launch_bounds__(512, 2) void gemm_256(const uint16_t* __restrict__ 
 // (vmcnt(8): the 4 half-tiles issued after it may stay in flight; vmcnt(0)
 // once the issue stream has run out).  All LDS in one __shared__ array, raw
 // s_barrier, sched_barrier at the phase edges so hipcc keeps the order.
-template <typename T, bool TRANS_B, bool BIAS>
+//
+// SCHED bits (A/B; 0 = the schedule above):
+//  1: the guide's two barriers per phase with waves 4-7 (wr = 1) one barrier
+//     behind: a phase is {reads + DMA issue} barrier {MFMAs} barrier, so the
+//     two waves on each SIMD alternate a read segment with an MFMA segment.
+//     With the stagger, all reads of phase p are retired by the barrier that
+//     ends the lagging half's MFMA segment of phase p; the restage points
+//     above are >= 2 phases later and the counted waits stay one phase
+//     ahead of the first read, so the same issue plan is race-free.
+//  2: s_setprio(1) around each MFMA cluster
+//  4: the phase's fragment reads issued before its DMA (template order)
+template <typename T, bool TRANS_B, bool BIAS, int SCHED = 0>
 __global__ __launch_bounds__(512, 2) void gemm_256p(const uint16_t* __restrict__ A,
                                                     const uint16_t* __restrict__ Bm,
                                                     uint16_t* __restrict__ C,
                                                     const uint16_t* __restrict__ bias, int M, int N,
                                                     int K, int64_t lda, int64_t ldb, int64_t ldc,
-                                                    int tiles_n, int nblocks) {
+                                                    int tiles_n, int nblocks, int group_m) {
     constexpr int HT = 16384, BUF = 4 * HT;
     constexpr int AT = 0, AB = 1, BT = 2, BB = 3;
     __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
@@ -394,7 +427,9 @@ __global__ __launch_bounds__(512, 2) void gemm_256p(const uint16_t* __restrict__
     const int wr = wave >> 2, wc = wave & 3;
     const int l16 = lane & 15, g = lane >> 4, qq = l16 >> 2, pp = lane & 3;
     const int lb = xcd_remap(blockIdx.x, nblocks);
-    const int m0 = (lb / tiles_n) * G2M, n0 = (lb % tiles_n) * G2N;
+    int tmi, tni;
+    g2_tile(lb, cdiv(M, G2M), tiles_n, group_m, tmi, tni);
+    const int m0 = tmi * G2M, n0 = tni * G2N;
     const int ktiles = K / G2K;
 
     auto issue = [&](int half, int kt) {
@@ -448,8 +483,18 @@ __global__ __launch_bounds__(512, 2) void gemm_256p(const uint16_t* __restrict__
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr ((SCHED & 2) != 0) __builtin_amdgcn_s_setprio(1);
         __builtin_amdgcn_sched_barrier(0);
     };
+    auto sync_end = [&]() {  // end of a phase's MFMA cluster
+        if constexpr ((SCHED & 3) != 0) {
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr ((SCHED & 2) != 0) __builtin_amdgcn_s_setprio(0);
+            if constexpr ((SCHED & 1) != 0) __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    constexpr bool kReadFirst = (SCHED & 4) != 0;
 
     f32x4 acc[4][8];  // [n-frag: 0,1 = Bt, 2,3 = Bb][m-frag: 0-3 = At, 4-7 = Ab]
 #pragma unroll
@@ -467,6 +512,9 @@ __global__ __launch_bounds__(512, 2) void gemm_256p(const uint16_t* __restrict__
     wait_vm(ktiles < 2);  // retires At(0), Bt(0)
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
+    if constexpr ((SCHED & 1) != 0) {
+        if (wr == 1) __builtin_amdgcn_s_barrier();  // the lagging half
+    }
     __builtin_amdgcn_sched_barrier(0);
 
     i32x4 fat[4][2], fab[4][2], fbt[2][2], fbb[2][2];
@@ -474,15 +522,16 @@ __global__ __launch_bounds__(512, 2) void gemm_256p(const uint16_t* __restrict__
         const char* base = smem + (kt & 1) * BUF;
         const bool drain = kt + 2 >= ktiles;
         // ---- P1: At + Bt -> C(At, Bt)
-        issue(BB, kt + 1);
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) fat[mi][s2] = read_a(base + AT * HT, mi, s2);
+        if constexpr (!kReadFirst) issue(BB, kt + 1);
 #pragma unroll
         for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) fbt[ni][s2] = read_b(base + BT * HT, ni, s2);
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) fat[mi][s2] = read_a(base + AT * HT, mi, s2);
+        if constexpr (kReadFirst) issue(BB, kt + 1);
         wait_vm(drain);  // retires Bb(kt), read in P2
         sync();
 #pragma unroll
@@ -492,12 +541,14 @@ __global__ __launch_bounds__(512, 2) void gemm_256p(const uint16_t* __restrict__
 #pragma unroll
                 for (int mi = 0; mi < 4; ++mi)
                     acc[ni][mi] = mfma16x16x32<T>(fbt[ni][s2], fat[mi][s2], acc[ni][mi]);
+        sync_end();
         // ---- P2: Bb -> C(At, Bb)
-        issue(AB, kt + 1);
+        if constexpr (!kReadFirst) issue(AB, kt + 1);
 #pragma unroll
         for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) fbb[ni][s2] = read_b(base + BB * HT, ni, s2);
+        if constexpr (kReadFirst) issue(AB, kt + 1);
         wait_vm(drain);  // retires Ab(kt), read in P3
         sync();
 #pragma unroll
@@ -507,12 +558,14 @@ __global__ __launch_bounds__(512, 2) void gemm_256p(const uint16_t* __restrict__
 #pragma unroll
                 for (int mi = 0; mi < 4; ++mi)
                     acc[2 + ni][mi] = mfma16x16x32<T>(fbb[ni][s2], fat[mi][s2], acc[2 + ni][mi]);
+        sync_end();
         // ---- P3: Ab -> C(Ab, Bb)
-        issue(AT, kt + 2);
+        if constexpr (!kReadFirst) issue(AT, kt + 2);
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) fab[mi][s2] = read_a(base + AB * HT, mi, s2);
+        if constexpr (kReadFirst) issue(AT, kt + 2);
         sync();
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2)
@@ -521,6 +574,7 @@ __global__ __launch_bounds__(512, 2) void gemm_256p(const uint16_t* __restrict__
 #pragma unroll
                 for (int mi = 0; mi < 4; ++mi)
                     acc[2 + ni][4 + mi] = mfma16x16x32<T>(fbb[ni][s2], fab[mi][s2], acc[2 + ni][4 + mi]);
+        sync_end();
         // ---- P4: registers -> C(Ab, Bt)
         issue(BT, kt + 2);
         wait_vm(drain);  // retires At(kt+1), Bt(kt+1), read in the next P1
@@ -532,6 +586,10 @@ __global__ __launch_bounds__(512, 2) void gemm_256p(const uint16_t* __restrict__
 #pragma unroll
                 for (int mi = 0; mi < 4; ++mi)
                     acc[ni][4 + mi] = mfma16x16x32<T>(fbt[ni][s2], fab[mi][s2], acc[ni][4 + mi]);
+        sync_end();
+    }
+    if constexpr ((SCHED & 1) != 0) {
+        if (wr == 0) __builtin_amdgcn_s_barrier();  // equal barrier counts
     }
 
     // epilogue: acc[ni][mi][r] = C[m][n], m = m0 + (mi>>2)*128 + wr*64 + (mi&3)*16 + l16,
@@ -1046,28 +1104,46 @@ int launch_mfma(const void* a, const void* b, void* c, const void* bias, int M, 
     return launch_status("gemm_mfma");
 }
 
+template <typename T, bool TB, bool BI>
+void launch_256p(int sched, dim3 grid, dim3 block, hipStream_t s, const void* a, const void* b,
+                 void* c, const void* bias, int M, int N, int K, int64_t lda, int64_t ldb,
+                 int64_t ldc, int tn, int nb, int group_m) {
+#define PLI_G256P(SC)                                                                           \
+    hipLaunchKernelGGL((gemm_256p<T, TB, BI, SC>), grid, block, 0, s, (const uint16_t*)a,       \
+                       (const uint16_t*)b, (uint16_t*)c, (const uint16_t*)bias, M, N, K, lda, ldb, \
+                       ldc, tn, nb, group_m)
+    switch (sched) {
+        case 1: PLI_G256P(1); break;
+        case 3: PLI_G256P(3); break;
+        case 5: PLI_G256P(5); break;
+        case 7: PLI_G256P(7); break;
+        default: PLI_G256P(0);
+    }
+#undef PLI_G256P
+}
+
 template <typename T>
 int launch_256(const void* a, const void* b, void* c, const void* bias, int M, int N, int K,
-               int64_t lda, int64_t ldb, int64_t ldc, int trans_b, hipStream_t s, bool phased,
-               bool prio = false) {
+               int64_t lda, int64_t ldb, int64_t ldc, int trans_b, hipStream_t s, int phased,
+               bool prio = false, int group_m = 0) {
+    // phased: -1 = gemm_256 (one phase per K-tile), else gemm_256p's SCHED bits
     const int tm = cdiv(M, G2M), tn = cdiv(N, G2N);
     const int64_t nb = (int64_t)tm * tn;
     PLI_REQUIRE(nb < (1ll << 31), "pli_gemm: grid too large");
     const dim3 grid((unsigned)nb), block(512);
 #define PLI_G256(TB, BI)                                                                          \
     do {                                                                                          \
-        if (phased)                                                                               \
-            hipLaunchKernelGGL((gemm_256p<T, TB, BI>), grid, block, 0, s, (const uint16_t*)a,     \
-                               (const uint16_t*)b, (uint16_t*)c, (const uint16_t*)bias, M, N, K,  \
-                               lda, ldb, ldc, tn, (int)nb);                                       \
+        if (phased >= 0)                                                                          \
+            launch_256p<T, TB, BI>(phased, grid, block, s, a, b, c, bias, M, N, K, lda, ldb, ldc, \
+                                   tn, (int)nb, group_m);                                         \
         else if (prio)                                                                            \
             hipLaunchKernelGGL((gemm_256<T, TB, BI, true>), grid, block, 0, s, (const uint16_t*)a, \
                                (const uint16_t*)b, (uint16_t*)c, (const uint16_t*)bias, M, N, K,  \
-                               lda, ldb, ldc, tn, (int)nb);                                       \
+                               lda, ldb, ldc, tn, (int)nb, group_m);                              \
         else                                                                                      \
             hipLaunchKernelGGL((gemm_256<T, TB, BI>), grid, block, 0, s, (const uint16_t*)a,      \
                                (const uint16_t*)b, (uint16_t*)c, (const uint16_t*)bias, M, N, K,  \
-                               lda, ldb, ldc, tn, (int)nb);                                       \
+                               lda, ldb, ldc, tn, (int)nb, group_m);                              \
     } while (0)
     if (trans_b) {
         if (bias) PLI_G256(true, true); else PLI_G256(true, false);
@@ -1169,10 +1245,13 @@ extern "C" int pli_gemm_swiglu(const void* x, const void* wg, const void* wu, vo
     }
 }
 
-// variant: 0 = default routing, 1 = force the 128x128 MFMA tile, 2 = force
-// the 256x256 LDS-DMA tile, 3 = force the phased 256x256 tile, 4 = the
-// 256x256 tile with s_setprio(1) around its MFMA clusters (where their shape
-// conditions hold)
+// variant: 0 = default routing (large shapes: phased 256x256 tile, staggered
+// two-barrier schedule, grouped rasterization), 1 = force the 128x128 MFMA
+// tile, 2 = force the one-phase 256x256 LDS-DMA tile, 3 = the phased tile
+// with one barrier per phase, 4 = the one-phase tile with s_setprio(1) around
+// its MFMA clusters, 5-8 = phased SCHED 1/3/5/7, 9-11 = one-phase with
+// group_m 4/8/16, 12-15 = phased SCHED 7 with group_m 8/4/2/16 (where their
+// shape conditions hold)
 extern "C" int pli_gemm_variant(const void* a, const void* b, void* c, const void* bias, int m,
                                 int n, int k, int64_t lda, int64_t ldb, int64_t ldc, int trans_b,
                                 int dtype, void* stream, int variant) {
@@ -1217,10 +1296,30 @@ extern "C" int pli_gemm_variant(const void* a, const void* b, void* c, const voi
     // grid of tiles so the block count is not tiny)
     const bool big = vec && k % G2K == 0 && m >= 2 * G2M && n >= 2 * G2N && variant != 1;
     if (big || (vec && variant >= 2 && k % G2K == 0 && n >= 8)) {
-        const bool phased = variant == 3, prio = variant == 4;
+        // variant 3: phased (SCHED 0); 5-8: phased with SCHED 1, 3, 5, 7;
+        // 9-11: one-phase tile with grouped rasterization (group_m 4, 8, 16);
+        // 12-15: phased SCHED 7 with group_m 8, 4, 2, 16
+        // default (0): phased SCHED 7 with group_m 4 (= variant 13; NT 8192^3
+        // 1371-1414 vs 1145-1185 TF for the one-phase tile, NN 4096^3 1104 vs 935)
+        int phased = variant == 3 ? 0 : (variant >= 5 && variant <= 8) ? 2 * (variant - 5) + 1 : -1;
+        int group_m = 0;
+        if (variant == 0) {
+            phased = 7;
+            group_m = 4;
+        }
+        if (variant >= 9 && variant <= 11) group_m = 4 << (variant - 9);
+        if (variant == 12 || variant == 13) {
+            phased = 7;
+            group_m = variant == 12 ? 8 : 4;
+        }
+        if (variant == 14 || variant == 15) {  // phased SCHED 7 with group_m 2, 16
+            phased = 7;
+            group_m = variant == 14 ? 2 : 16;
+        }
+        const bool prio = variant == 4;
         if (dtype == PLI_BF16)
-            return launch_256<bf16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, s, phased, prio);
-        return launch_256<f16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, s, phased, prio);
+            return launch_256<bf16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, s, phased, prio, group_m);
+        return launch_256<f16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, s, phased, prio, group_m);
     }
     if (vec) {
         if (dtype == PLI_BF16)

@@ -234,7 +234,7 @@ def test_gemm_vs_oracle(m, n, k, dt, tb):
     assert_lin_close(c, ref, dt, f"gemm {m}x{n}x{k} {dt} tb={tb}")
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15])
 @pytest.mark.parametrize("m,n,k,tb,bias", [
     (512, 512, 512, False, False),
     (512, 512, 512, True, True),
@@ -248,8 +248,9 @@ def test_gemm_vs_oracle(m, n, k, dt, tb):
     (2048, 2048, 4096, True, False),
 ])
 def test_gemm_tile_variants(m, n, k, tb, bias, variant):
-    """The 128x128 register-staged tile (1), the 256x256 LDS-DMA tile (2) and
-    its phased pipeline (3)."""
+    """The 128x128 register-staged tile (1), the 256x256 LDS-DMA tile (2), its
+    s_setprio form (4), its phased pipeline (3) and the phased pipeline with
+    the staggered two-barrier schedule (5-8: SCHED 1, 3, 5, 7)."""
     import pli_hip
     dt = "bf16"
     a = seeded_normal((m, k), 3, dt)

@@ -368,15 +368,39 @@ def tune_gemm():
         a = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
         b = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
         c = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
-        fns = {"hip_nn_256": lambda: pli_hip.gemm(a, b, out=c, variant=2),
-               "hip_nn_256prio": lambda: pli_hip.gemm(a, b, out=c, variant=4),
-               "hip_nt_256": lambda: pli_hip.gemm(a, b, trans_b=True, out=c, variant=2),
-               "hip_nt_256prio": lambda: pli_hip.gemm(a, b, trans_b=True, out=c, variant=4),
-               "torch_nn": lambda: torch.mm(a, b)}
+        vs = [int(v) for v in os.environ.get("PLI_GEMM_VARIANTS", "2,5,6,7,8").split(",")]
+        fns = {}
+        for v in vs:
+            fns[f"hip_nn_v{v}"] = (lambda v=v: pli_hip.gemm(a, b, out=c, variant=v))
+            fns[f"hip_nt_v{v}"] = (lambda v=v: pli_hip.gemm(a, b, trans_b=True, out=c, variant=v))
+        fns["torch_nn"] = lambda: torch.mm(a, b)
+        fns["torch_nt"] = lambda: torch.mm(a, b.t())
         t = interleave(fns, 5, int(os.environ.get("PLI_TUNE_ROUNDS", "3")))
         for kname, (med, mn) in t.items():
             print(json.dumps({"kernel": "gemm", "n": n, "impl": kname, "ms_med": med,
                               "TFLOP/s": 2 * n ** 3 / med / 1e9}), flush=True)
+
+
+def tune_gemm_shapes():
+    """256-tile schedule / rasterization variants over the callers' shapes."""
+    shapes = [(4096, 4096, 4096), (8192, 8192, 8192), (16384, 4096, 4096), (4096, 14336, 4096),
+              (4096, 4096, 14336), (8192, 1024, 8192), (8192, 8192, 1024), (2048, 2048, 2048),
+              (1024, 1024, 1024), (512, 4096, 4096), (4096, 512, 4096), (1024, 8192, 8192)]
+    vs = [int(v) for v in os.environ.get("PLI_GEMM_VARIANTS", "2,13,12,14").split(",")]
+    for (m, n, k) in shapes:
+        a = torch.randn(m, k, device="cuda", dtype=torch.bfloat16)
+        bt = torch.randn(n, k, device="cuda", dtype=torch.bfloat16)
+        bn = torch.randn(k, n, device="cuda", dtype=torch.bfloat16)
+        c = torch.empty(m, n, device="cuda", dtype=torch.bfloat16)
+        fns = {}
+        for v in vs:
+            fns[f"nt_v{v}"] = (lambda v=v: pli_hip.gemm(a, bt, trans_b=True, out=c, variant=v))
+            fns[f"nn_v{v}"] = (lambda v=v: pli_hip.gemm(a, bn, out=c, variant=v))
+        fns["nt_torch"] = lambda: torch.mm(a, bt.t())
+        fns["nn_torch"] = lambda: torch.mm(a, bn)
+        t = interleave(fns, 5, int(os.environ.get("PLI_TUNE_ROUNDS", "3")))
+        row = {kname: round(2 * m * n * k / med / 1e9, 1) for kname, (med, mn) in t.items()}
+        print(json.dumps({"kernel": "gemm_shapes", "m": m, "n": n, "k": k, "TFLOP/s": row}), flush=True)
 
 
 if __name__ == "__main__":
@@ -396,6 +420,8 @@ if __name__ == "__main__":
         tune_flash(D=64, H=64)
     if "gemm" in what:
         tune_gemm()
+    if "gemmshapes" in what:
+        tune_gemm_shapes()
     if "decode" in what:
         tune_decode()
     if "swiglu" in what:
