@@ -39,6 +39,11 @@ struct AttnStrides {
     int64_t qb, qh, qn, kb, kh, kn, vb, vh, vn, ob, oh, on;
 };
 
+// 32-bit LDS byte address of a __shared__ pointer (for M0)
+__device__ __forceinline__ uint32_t lds_addr(const char* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
 constexpr int KT = 64;  // keys per LDS tile
 constexpr int QW = 32;  // query rows per wave
 
@@ -2129,6 +2134,316 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
     }
 }
 
+// --------------------------------------------------------------------------
+// attn_fwd_seg: segmented 8-wave structure (D = 128).  Each 64-key tile is
+// four barrier-separated segments per wave,
+//   S1 load:    K(t) fragments LDS -> registers (16 ds_read_b128) + LDS-DMA of K(t+2)
+//   S2 compute: S(t) = K(t) Q^T (16 MFMAs, registers only)
+//   S3 load:    V(t-1)^T fragments -> the same registers (32 ds_read_b64_tr_b16)
+//               + LDS-DMA of V(t+1)
+//   S4 compute: O += P(t-1) V(t-1) (16 MFMAs) beside softmax(t): mask, row
+//               max, deferred running max, exp2, bf16 pack -> P(t), rounded
+//               row sum (P double-buffered in registers, S(t) lives S2-S4)
+// and waves 4-7 run one segment behind waves 0-3, so the two waves of every
+// SIMD pair a compute segment with a load segment.  K and V tiles arrive by
+// LDS-DMA (global_load_lds, 1 KiB lane-linear pieces, two per wave per tile)
+// into 3-deep rings of XOR-swizzled [64][256 B] images (chunk ^= (row&3)<<2 |
+// (row>>2)&3, applied on the DMA source address): a buffer is restaged >= 4
+// segments after its last read, and the counted vmcnt(4) at the end of S2
+// (retires K(t+1)) and S4 (retires V(t)) precedes, for both halves, the
+// barrier before the first read.  Softmax as variant 21 (defer-max, rounded
+// row sum, permlane row max).  SGB: sched_group_barrier interleave of the
+// compute segments.
+template <typename T, int SGB>
+__global__ __launch_bounds__(512, 2) void attn_fwd_seg(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
+    const uint16_t* __restrict__ v, uint16_t* __restrict__ o, int H, int group,
+    int Nq, int Nk, AttnStrides st, float c, int causal, int qblocks,
+    int nblocks) {
+    constexpr int D = 128, NW = 8, TB = KT * 256;  // one 16 KiB tile image
+    __shared__ __attribute__((aligned(1024))) char smem[6 * TB];  // K ring 0-2, V ring 3-5
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: DMA destinations in SGPRs
+    const int h32 = lane >> 5, l32 = lane & 31;
+    const int lag = wave >> 2;  // 1: the half that runs one segment behind
+    const int lb = xcd_remap(blockIdx.x, nblocks);
+    const int bh = lb / qblocks;
+    const int qblk = causal ? qblocks - 1 - lb % qblocks : lb % qblocks;
+    const int b = bh / H, hq = bh % H, hk = hq / group;
+    const int qbase = qblk * (NW * QW);
+    const int q0 = qbase + wave * QW;
+    const int off_diag = Nk - Nq;
+
+    const uint16_t* qp = q + b * st.qb + hq * st.qh;
+    const uint16_t* kp = k + b * st.kb + hk * st.kh;
+    const uint16_t* vp = v + b * st.vb + hk * st.vh;
+
+    int kv_end = Nk;
+    if (causal) kv_end = min(Nk, qbase + NW * QW + off_diag);
+    const int nt = kv_end > 0 ? cdiv(kv_end, KT) : 0;
+    int t_mask = Nk / KT;
+    if (causal) t_mask = min(t_mask, max(0, (q0 + off_diag + 1) / KT));
+
+    // LDS-DMA plan: piece 2*wave+i of a tile image = rows 4*piece .. +3;
+    // lane -> row 4*piece + (lane>>4), physical chunk lane&15 = logical chunk
+    // (lane&15) ^ f(row)
+    auto fsw = [](int row) { return ((row & 3) << 2) | ((row >> 2) & 3); };
+    // per-lane element offsets of the two pieces inside a tile (32-bit: the
+    // tile's own offset t*KT*stride is scalar)
+    int drow[2], koff[2], voff[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        drow[i] = 4 * (2 * wave + i) + (lane >> 4);
+        const int ch = (lane & 15) ^ fsw(drow[i]);
+        koff[i] = drow[i] * (int)st.kn + 8 * ch;
+        voff[i] = drow[i] * (int)st.vn + 8 * ch;
+    }
+    auto dma = [&](const uint16_t* base, int64_t sn, const int (&off)[2], int t, char* img) {
+        const uint16_t* tb = base + (int64_t)t * KT * sn;
+        const bool ragged = t * KT + KT > Nk;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            int o = off[i];
+            if (ragged && t * KT + drow[i] >= Nk)  // rows past Nk re-read row Nk-1 (masked / P = 0)
+                o += (Nk - 1 - t * KT - drow[i]) * (int)sn;
+            // inline asm: hipcc's waitcnt pass does not see it, so it does not
+            // drain it with vmcnt(0) before the (alias-unknown) tr_b16 reads;
+            // the counted vmcnt(4) waits below order every use
+            const uint32_t m0v = lds_addr(img + (2 * wave + i) * 1024);
+            asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+                         :: "s"(m0v), "v"(tb + o) : "memory", "m0");
+        }
+    };
+    auto kimg = [&](int t) { return smem + (t % 3) * TB; };
+    auto vimg = [&](int t) { return smem + (3 + t % 3) * TB; };
+
+    // fragment addresses (see the derivation in DESIGN.md §3.1):
+    //   K: row tt*32 + l32, chunk 2kk + h32  -> (A0 ^ (kk << 5)) + tt * 8192
+    //   V^T: rows tt*32 + 16*s2 + 4*h32 + qq (+8), chunk 4*dblk + c0
+    //        -> (B0 ^ (dblk << 6) [^ 32]) + (tt*32 + 16*s2) * 256 [+ 2048]
+    const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+    int A0 = l32 * 256 + ((h32 ^ fsw(l32)) << 4);
+    const int c0 = 2 * (g & 1) + (pp >> 1);
+    int B0 = (4 * h32 + qq) * 256 + ((c0 ^ ((qq << 2) | h32)) << 4) + 8 * (pp & 1);
+
+    i32x4 qf[D / 16];
+    {
+        const int qr = q0 + l32;
+        const bool ok = qr < Nq;
+        const uint16_t* src = qp + (int64_t)(ok ? qr : 0) * st.qn + 8 * h32;
+#pragma unroll
+        for (int kk = 0; kk < D / 16; ++kk) {
+            const i32x4 x = *reinterpret_cast<const i32x4*>(src + 16 * kk);
+            qf[kk] = ok ? x : i32x4{0, 0, 0, 0};
+        }
+    }
+
+    f32x16 oacc[D / 32];
+#pragma unroll
+    for (int d = 0; d < D / 32; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[d][r] = 0.f;
+    float m_run = -1e30f, l_run = 0.f, alpha_p = 1.f;
+
+    // prologue: K(0), K(1), V(0); K(0) retired before the first barrier
+    if (nt > 0) {
+        dma(kp, st.kn, koff, 0, kimg(0));
+        if (nt > 1) dma(kp, st.kn, koff, 1, kimg(1));
+        dma(vp, st.vn, voff, 0, vimg(0));
+    }
+    if (nt > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    auto seg_barrier = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    seg_barrier();
+    if (lag) seg_barrier();
+
+    i32x4 fr[16];  // K(t) fragments [tt*8 + kk] in S1-S2, V^T fragments in S3-S4
+    f32x16 sc[2];  // S(t), S2 -> S4
+    // HC: tile t exists (S1 K reads, S2 QK^T, S4 softmax(t));
+    // HP: tile t-1 exists (S3 V reads, S4 PV(t-1) with pkp = P(t-1));
+    // pkc receives P(t)
+    auto iter = [&](auto HC_, auto HP_, int t, i32x4 (&pkc)[2][2], i32x4 (&pkp)[2][2]) {
+        constexpr bool HC = decltype(HC_)::value, HP = decltype(HP_)::value;
+        // opaque per iteration: the compiler recomputes the few VALU of
+        // address math instead of keeping dozens of hoisted addresses live
+        asm volatile("" : "+v"(A0), "+v"(B0), "+v"(koff[0]), "+v"(koff[1]), "+v"(voff[0]), "+v"(voff[1]),
+                     "+v"(drow[0]), "+v"(drow[1]));
+        // ---- S1: K(t) fragments; DMA K(t+2)
+        if constexpr (HC) {
+            const int ab = (int)(kimg(t) - smem) + A0;  // image base is 16 KiB aligned
+#pragma unroll
+            for (int kk = 0; kk < 8; ++kk) {
+                const int a = ab ^ (kk << 5);
+                fr[kk] = lds_read_b128(smem, a);
+                fr[8 + kk] = lds_read_b128(smem, a + 8192);
+            }
+        }
+        if (t + 2 < nt) dma(kp, st.kn, koff, t + 2, kimg(t + 2));
+        seg_barrier();
+        // ---- S2: S(t) = K Q^T (registers only)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (HC) {
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) sc[tt][r] = 0.f;
+#pragma unroll
+                for (int kk = 0; kk < 8; ++kk) sc[tt] = mfma32x32x16<T>(fr[tt * 8 + kk], qf[kk], sc[tt]);
+            }
+            asm volatile("" : "+v"(sc[0]), "+v"(sc[1]));  // keep QK^T in S2
+        }
+        if (t + 2 < nt) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // K(t+1) landed
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        seg_barrier();
+        // ---- S3: V(t-1)^T fragments; DMA V(t+1)
+        if constexpr (HP) {
+            const int bb = (int)(vimg(t - 1) - smem) + B0;
+#pragma unroll
+            for (int dblk = 0; dblk < 4; ++dblk) {
+                const int alo = bb ^ (dblk << 6), ahi = (alo ^ 32) + 2048;
+#pragma unroll
+                for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2) {
+                        const int ro = (tt * 32 + 16 * s2) * 256;
+                        const i32x2 lo = lds_read_tr16(smem, alo + ro);
+                        const i32x2 hi = lds_read_tr16(smem, ahi + ro);
+                        fr[dblk * 4 + tt * 2 + s2] = i32x4{lo.x, lo.y, hi.x, hi.y};
+                    }
+            }
+        }
+        if (t + 1 < nt) dma(vp, st.vn, voff, t + 1, vimg(t + 1));
+        seg_barrier();
+        // ---- S4: O += P(t-1) V(t-1)  ||  softmax(t) -> P(t)
+        if (HP && __ballot(alpha_p != 1.f)) {
+#pragma unroll
+            for (int d = 0; d < D / 32; ++d)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha_p;
+        }
+        if (HC && t >= t_mask) {
+            // key t*KT + 4*h32 + kr(tt, r) is valid iff kr <= thr (one per-lane
+            // threshold against constants: nothing per register to hoist)
+            const int last = causal ? min(q0 + l32 + off_diag, Nk - 1) : Nk - 1;
+            const int thr = last - t * KT - 4 * h32;
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if (tt * 32 + (r & 3) + 8 * (r >> 2) > thr) sc[tt][r] = -INFINITY;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (HP) {
+#pragma unroll
+            for (int dblk = 0; dblk < 4; ++dblk)
+#pragma unroll
+                for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2)
+                        oacc[dblk] = mfma32x32x16<T>(fr[dblk * 4 + tt * 2 + s2], pkp[tt][s2], oacc[dblk]);
+        }
+        if constexpr (HC) {
+            float mx = max3(sc[0][0], sc[1][0], sc[0][1]);
+            float my = max3(sc[1][1], sc[0][2], sc[1][2]);
+#pragma unroll
+            for (int r = 3; r < 15; r += 2) {
+                mx = max3(mx, sc[0][r], sc[1][r]);
+                my = max3(my, sc[0][r + 1], sc[1][r + 1]);
+            }
+            mx = max3(mx, my, max3(sc[0][15], sc[1][15], mx));
+            mx = xor32_max(mx);
+            float m_new = fmaxf(m_run, mx * c);
+            m_new = mx * c > m_run + kDeferThr ? m_new : m_run;
+            const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+            m_run = m_new;
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) sc[tt][r] = __builtin_amdgcn_exp2f(fmaf(sc[tt][r], c, -m_new));
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    const int r0 = 8 * s2;
+                    pkc[tt][s2] = i32x4{(int)pack2<T>(sc[tt][r0 + 0], sc[tt][r0 + 1]),
+                                        (int)pack2<T>(sc[tt][r0 + 2], sc[tt][r0 + 3]),
+                                        (int)pack2<T>(sc[tt][r0 + 4], sc[tt][r0 + 5]),
+                                        (int)pack2<T>(sc[tt][r0 + 6], sc[tt][r0 + 7])};
+                }
+            float r0 = 0.f, r1 = 0.f;
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    r0 = add_pair<T>((uint32_t)pkc[tt][s2][0], r0);
+                    r1 = add_pair<T>((uint32_t)pkc[tt][s2][1], r1);
+                    r0 = add_pair<T>((uint32_t)pkc[tt][s2][2], r0);
+                    r1 = add_pair<T>((uint32_t)pkc[tt][s2][3], r1);
+                }
+            l_run = fmaf(l_run, alpha, r0 + r1);
+            alpha_p = alpha;  // O rescale before PV(t), in the next S4
+            // pin: without it the softmax sinks past the barriers to its use in
+            // the next tile's S4 (sched_barrier does not stop IR-level sinking)
+            asm volatile("" : "+v"(pkc[0][0]), "+v"(pkc[0][1]), "+v"(pkc[1][0]), "+v"(pkc[1][1]),
+                         "+v"(l_run), "+v"(alpha_p), "+v"(m_run));
+        }
+        if constexpr (SGB != 0 && HC && HP) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);  // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x002, 8, 1);  // VALU
+            }
+        }
+        if (t + 2 < nt) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // V(t) landed
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        seg_barrier();
+    };
+
+    // tiles 0 .. nt-1 plus one drain step (t = nt: PV of the last tile);
+    // even t packs P(t) into pa, odd t into pb
+    const std::true_type Y{};
+    const std::false_type N{};
+    i32x4 pa[2][2], pb[2][2];
+    if (nt > 0) {
+        iter(Y, N, 0, pa, pb);
+        int t = 1;
+        for (; t + 1 < nt; t += 2) {
+            iter(Y, Y, t, pb, pa);
+            iter(Y, Y, t + 1, pa, pb);
+        }
+        if (t < nt) {
+            iter(Y, Y, t, pb, pa);
+            iter(N, Y, t + 1, pa, pb);
+        } else {
+            iter(N, Y, t, pb, pa);
+        }
+    }
+    if (!lag) seg_barrier();  // equal barrier counts for both halves
+
+    const float l = xor32_sum(l_run);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const int qr = q0 + l32;
+    if (qr < Nq) {
+        uint16_t* op = o + b * st.ob + hq * st.oh + (int64_t)qr * st.on;
+#pragma unroll
+        for (int dblk = 0; dblk < D / 32; ++dblk)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int d = dblk * 32 + 8 * i + 4 * h32;
+                const i32x2 w = {(int)pack2<T>(oacc[dblk][4 * i] * inv, oacc[dblk][4 * i + 1] * inv),
+                                 (int)pack2<T>(oacc[dblk][4 * i + 2] * inv, oacc[dblk][4 * i + 3] * inv)};
+                *reinterpret_cast<i32x2*>(op + d) = w;
+            }
+    }
+}
+
 // Kernel variants behind the same ABI (A/B-able via pli_flash_attn_fwd_variant):
 //   0: attn_fwd_mfma (XOR-swizzled LDS), 4 waves
 //   1: attn_fwd_v2, 4 waves, lazy rescale    2: attn_fwd_v2, 8 waves, lazy rescale
@@ -2151,6 +2466,9 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
 //  27: attn_fwd_pp -- variant 21 split in two phases, waves 4-7 one phase
 //      behind (ping-pong of the two waves on each SIMD)
 //  28: variant 21 + iglp_opt(0)      29: variant 21 + batched fragment reads
+//  30: attn_fwd_seg (four barrier-separated load / compute segments per tile,
+//      waves 4-7 one segment behind, LDS-DMA into 3-deep rings; D=128, else 21)
+//  31: attn_fwd_seg + sched_group_barrier interleave of the compute segments
 // default: v2 NW8 + permlane row max + defer-max (THR 8, log2) + rounded-P row sum
 // (1057 TF vs 983 for plain v2 at B8 H32 S4096 D128; spike + variant parity green)
 constexpr int kDefaultVariant = 21;
@@ -2204,6 +2522,15 @@ int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int
         case 27: PLI_ATTN_LAUNCH((attn_fwd_pp<T, D>)); break;
         case 28: PLI_ATTN_LAUNCH((attn_fwd_v2<T, D, 8, true, 13 | 32>)); break;
         case 29: PLI_ATTN_LAUNCH((attn_fwd_v2<T, D, 8, true, 13 | 128>)); break;
+        case 30:
+        case 31:
+            if constexpr (D == 128) {
+                if (variant == 30) PLI_ATTN_LAUNCH((attn_fwd_seg<T, 0>));
+                else PLI_ATTN_LAUNCH((attn_fwd_seg<T, 1>));
+            } else {
+                PLI_ATTN_LAUNCH((attn_fwd_v2<T, D, 8, true, 13>));
+            }
+            break;
         case 15: hipLaunchKernelGGL((attn_fwd_v6<T, D>), grid, dim3(512), 0, stream, qq, kk, vv, oo,
                                     H, group, Nq, Nk, st, c, causal, qblocks, (int)nb); break;
         case 14: PLI_ATTN_V5(1, true); break;

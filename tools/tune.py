@@ -39,8 +39,10 @@ def interleave(fns: dict, iters: int, rounds: int):
     return {k: (float(np.median(v)), float(np.min(v))) for k, v in res.items()}
 
 
-def tune_flash(variants=(21, 28, 29), causal=False, B=8, H=32, S=4096, D=128):
+def tune_flash(variants=None, causal=False, B=8, H=32, S=4096, D=128):
     from oracle.attention import naive_attention
+    if variants is None:
+        variants = tuple(int(x) for x in os.environ.get("PLI_FLASH_VARIANTS", "21,30,31").split(","))
     g = torch.Generator(device="cuda").manual_seed(0)
     q, k, v = (torch.randn(B, H, S, D, device="cuda", dtype=torch.bfloat16, generator=g) for _ in range(3))
     outs = {vv: torch.empty_like(q) for vv in variants}
