@@ -412,13 +412,19 @@ __global__ __launch_bounds__(512, 2) void gemm_256(const uint16_t* __restrict__ 
 //     ahead of the first read, so the same issue plan is race-free.
 //  2: s_setprio(1) around each MFMA cluster
 //  4: the phase's fragment reads issued before its DMA (template order)
-template <typename T, bool TRANS_B, bool BIAS, int SCHED = 0>
+// SWIGLU (NT): C[m, n] = silu(A Bg^T) * (A Bu^T) on a 256 x 128 output tile:
+// the Bt half-tile holds Bg rows n0..n0+127 and Bb the same rows of Bu, so a
+// lane's acc[ni] (gate) and acc[ni + 2] (up) are the same (m, n).
+template <typename T, bool TRANS_B, bool BIAS, int SCHED = 0, bool SWIGLU = false>
 __global__ __launch_bounds__(512, 2) void gemm_256p(const uint16_t* __restrict__ A,
                                                     const uint16_t* __restrict__ Bm,
                                                     uint16_t* __restrict__ C,
                                                     const uint16_t* __restrict__ bias, int M, int N,
                                                     int K, int64_t lda, int64_t ldb, int64_t ldc,
-                                                    int tiles_n, int nblocks, int group_m) {
+                                                    int tiles_n, int nblocks, int group_m,
+                                                    const uint16_t* __restrict__ Bu, int64_t ldbu) {
+    static_assert(!SWIGLU || (TRANS_B && !BIAS), "SwiGLU tile: NT, no bias");
+    constexpr int TN = SWIGLU ? 128 : G2N;  // output columns per tile
     constexpr int HT = 16384, BUF = 4 * HT;
     constexpr int AT = 0, AB = 1, BT = 2, BB = 3;
     __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
@@ -429,7 +435,7 @@ __global__ __launch_bounds__(512, 2) void gemm_256p(const uint16_t* __restrict__
     const int lb = xcd_remap(blockIdx.x, nblocks);
     int tmi, tni;
     g2_tile(lb, cdiv(M, G2M), tiles_n, group_m, tmi, tni);
-    const int m0 = tmi * G2M, n0 = tni * G2N;
+    const int m0 = tmi * G2M, n0 = tni * TN;
     const int ktiles = K / G2K;
 
     auto issue = [&](int half, int kt) {
@@ -445,6 +451,9 @@ __global__ __launch_bounds__(512, 2) void gemm_256p(const uint16_t* __restrict__
                 const uint16_t* src;
                 if (half == AT || half == AB)
                     src = A + (int64_t)min(m0 + (half == AB ? 128 : 0) + row, M - 1) * lda;
+                else if constexpr (SWIGLU)
+                    src = half == BB ? Bu + (int64_t)min(n0 + row, N - 1) * ldbu
+                                     : Bm + (int64_t)min(n0 + row, N - 1) * ldb;
                 else
                     src = Bm + (int64_t)min(n0 + (half == BB ? 128 : 0) + row, N - 1) * ldb;
                 __builtin_amdgcn_global_load_lds(
@@ -594,6 +603,24 @@ __global__ __launch_bounds__(512, 2) void gemm_256p(const uint16_t* __restrict__
 
     // epilogue: acc[ni][mi][r] = C[m][n], m = m0 + (mi>>2)*128 + wr*64 + (mi&3)*16 + l16,
     //                                     n = n0 + (ni>>1)*128 + wc*32 + (ni&1)*16 + 4g + r
+    if constexpr (SWIGLU) {  // gate acc[ni], up acc[ni + 2] of column n0 + wc*32 + ni*16 + 4g + r
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) {
+            const int m = m0 + (mi >> 2) * 128 + wr * 64 + (mi & 3) * 16 + l16;
+            if (m >= M) continue;
+            uint16_t* crow = C + (int64_t)m * ldc;
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni) {
+                const int n = n0 + wc * 32 + ni * 16 + 4 * g;
+                if (n >= N) continue;
+                float v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = silu_mul(acc[ni][mi][r], acc[ni + 2][mi][r]);
+                *reinterpret_cast<i32x2*>(crow + n) = i32x2{(int)pack2<T>(v[0], v[1]), (int)pack2<T>(v[2], v[3])};
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi) {
         const int m = m0 + (mi >> 2) * 128 + wr * 64 + (mi & 3) * 16 + l16;
@@ -1111,7 +1138,7 @@ void launch_256p(int sched, dim3 grid, dim3 block, hipStream_t s, const void* a,
 #define PLI_G256P(SC)                                                                           \
     hipLaunchKernelGGL((gemm_256p<T, TB, BI, SC>), grid, block, 0, s, (const uint16_t*)a,       \
                        (const uint16_t*)b, (uint16_t*)c, (const uint16_t*)bias, M, N, K, lda, ldb, \
-                       ldc, tn, nb, group_m)
+                       ldc, tn, nb, group_m, nullptr, 0)
     switch (sched) {
         case 1: PLI_G256P(1); break;
         case 3: PLI_G256P(3); break;
@@ -1202,6 +1229,15 @@ int launch_swiglu(const void* x, const void* wg, const void* wu, void* h, int M,
         else PLI_SMALLM_SW(8);
 #undef PLI_SMALLM_SW
         return launch_status("gemm_smallm_nt<swiglu>");
+    }
+    if (vec && M >= G2M && N >= 256 && K % G2K == 0 && (int64_t)cdiv(M, G2M) * cdiv(N, 128) >= 96) {
+        // prefill sizes: the phased 256 x 128 tile (staggered schedule, grouped rasterization)
+        const int tm = cdiv(M, G2M), tn = cdiv(N, 128);
+        const int64_t nb = (int64_t)tm * tn;
+        PLI_REQUIRE(nb < (1ll << 31), "pli_gemm_swiglu: grid too large");
+        hipLaunchKernelGGL((gemm_256p<T, true, false, 7, true>), dim3((unsigned)nb), dim3(512), 0, s,
+                           X, G, Hh, nullptr, M, N, K, ldx, ldwg, ldh, tn, (int)nb, 4, U, ldwu);
+        return launch_status("gemm_256p<swiglu>");
     }
     if (vec) {
         const int tm = cdiv(M, BM), tn = cdiv(N, BN / 2);
@@ -1294,7 +1330,10 @@ extern "C" int pli_gemm_variant(const void* a, const void* b, void* c, const voi
     }
     // large problems: 256x256 LDS-DMA tile (K a multiple of 64; at least a 2x2
     // grid of tiles so the block count is not tiny)
-    const bool big = vec && k % G2K == 0 && m >= 2 * G2M && n >= 2 * G2N && variant != 1;
+    // (fewer than 128 tiles of 256^2 leave CUs idle: the 128^2 tile's 4x grid
+    // wins there, +20-60 % at 16-64 tiles, profiles/r01/gemm/tune_few_tiles.log)
+    const bool big = vec && k % G2K == 0 && m >= 2 * G2M && n >= 2 * G2N && variant != 1 &&
+                     (variant != 0 || (int64_t)cdiv(m, G2M) * cdiv(n, G2N) >= 128);
     if (big || (vec && variant >= 2 && k % G2K == 0 && n >= 8)) {
         // variant 3: phased (SCHED 0); 5-8: phased with SCHED 1, 3, 5, 7;
         // 9-11: one-phase tile with grouped rasterization (group_m 4, 8, 16);

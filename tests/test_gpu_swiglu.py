@@ -1,6 +1,7 @@
 """GPU parity of the fused SwiGLU projection (pli_gemm_swiglu) on every
 route -- skinny (m <= 16), small-M MFMA (m <= 128), 128x128 MFMA tile,
-generic (fp32 / ragged) -- against the f64 oracle, and of the FFN / TP-MLP
+phased 256x128 tile (m, n >= 256, k % 64 == 0), generic (fp32 / ragged) --
+against the f64 oracle, and of the FFN / TP-MLP
 modules that use it.  Bound: |err| <= tol * (|ref| + 1) (the outputs grow
 like sqrt(K)); bf16 1e-2, fp16 4e-3, fp32 1e-4 as for pli_gemm."""
 from __future__ import annotations
@@ -24,7 +25,11 @@ CASES = [  # m, n, k, dtype -> route
     (48, 2048, 512, "bf16"),     # small-M MFMA, NBG = 4
     (128, 1024, 4096, "bf16"),   # small-M MFMA, NBG = 8
     (200, 1000, 768, "bf16"),    # 128x128 tile, ragged m and n
-    (1024, 2048, 1024, "fp16"),  # 128x128 tile
+    (1024, 2048, 1024, "fp16"),  # 128x128 tile (64 tiles of 256x128: too few for the phased tile)
+    (2304, 1376, 256, "bf16"),   # phased 256x128 tile (>= 96 tiles), ragged n (10.75 column tiles)
+    (2100, 1536, 640, "fp16"),   # phased tile, ragged m, 10 K-tiles
+    (2048, 5632, 2048, "bf16"),  # phased tile, Llama-shaped MLP
+    (3072, 1024, 64, "bf16"),    # phased tile, one K-tile
     (33, 100, 72, "bf16"),       # generic: n % 8 != 0
     (64, 96, 40, "fp32"),        # generic fp32
 ]
@@ -45,10 +50,12 @@ def test_gemm_swiglu_vs_oracle(case):
     assert not bad.any(), f"{bad.sum()} beyond tol, max err {np.abs(got - ref).max():.3e}"
 
 
-def test_gemm_swiglu_strided_halves_of_fused_weight():
-    """FusedSwiGLUFFN passes the two row halves of one [2n, k] weight."""
+@pytest.mark.parametrize("m", [64, 3072])
+def test_gemm_swiglu_strided_halves_of_fused_weight(m):
+    """FusedSwiGLUFFN passes the two row halves of one [2n, k] weight (m = 3072:
+    the phased tile, 96 tiles)."""
     import pli_hip
-    m, n, k = 64, 512, 256
+    n, k = 1024, 256
     x = torch.randn(m, k, device="cuda", dtype=torch.bfloat16)
     w = torch.randn(2 * n, k, device="cuda", dtype=torch.bfloat16) * k ** -0.5
     h = pli_hip.gemm_swiglu(x, w[:n], w[n:])

@@ -229,7 +229,7 @@ def tune_swiglu():
         copies = max(2, min(12, math.ceil((1 << 30) / wbytes)))
         wg = [torch.randn(inter, H, device="cuda", dtype=torch.bfloat16) * H ** -0.5 for _ in range(copies)]
         wu = [torch.randn(inter, H, device="cuda", dtype=torch.bfloat16) * H ** -0.5 for _ in range(copies)]
-        for m in (1, 8, 32, 128, 4096):
+        for m in tuple(int(v) for v in os.environ.get("PLI_SWIGLU_M", "1,8,32,128,4096").split(",")):
             x = torch.randn(m, H, device="cuda", dtype=torch.bfloat16)
             out = torch.empty(m, inter, device="cuda", dtype=torch.bfloat16)
             fns = {"fused": lambda a, b: pli_hip.gemm_swiglu(x, a, b, out=out),
@@ -388,6 +388,8 @@ def tune_gemm_shapes():
     shapes = [(4096, 4096, 4096), (8192, 8192, 8192), (16384, 4096, 4096), (4096, 14336, 4096),
               (4096, 4096, 14336), (8192, 1024, 8192), (8192, 8192, 1024), (2048, 2048, 2048),
               (1024, 1024, 1024), (512, 4096, 4096), (4096, 512, 4096), (1024, 8192, 8192)]
+    if os.environ.get("PLI_GEMM_SHAPES"):
+        shapes = [tuple(int(x) for x in sh.split("x")) for sh in os.environ["PLI_GEMM_SHAPES"].split(",")]
     vs = [int(v) for v in os.environ.get("PLI_GEMM_VARIANTS", "2,13,12,14").split(",")]
     for (m, n, k) in shapes:
         a = torch.randn(m, k, device="cuda", dtype=torch.bfloat16)
