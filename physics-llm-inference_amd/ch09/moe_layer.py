@@ -18,7 +18,8 @@ call and masked ``+=`` per expert and per top-k slot) with five launches:
 5. ``pli_moe_combine``: out[t] = sum_k w[t,k] * y[row(t,k)], fixed order.
 
 Each active expert's weights are streamed once per call, whatever its token
-count.  Shapes the grouped kernel does not take (K % 128, N % 16) run every
+count (decode sizes: a weight-streaming kernel; >= 16 rows per expert: the
+phased 256-row MFMA tile per (expert, slot), rows gathered by LDS-DMA).  Shapes the grouped kernel does not take (K % 128, N % 16) run every
 expert densely on the HIP GEMMs and mask by the routing weights (slow, only
 for toy sizes).  CPU tensors keep the reference math.
 """

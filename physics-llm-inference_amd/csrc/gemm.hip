@@ -415,28 +415,39 @@ __global__ __launch_bounds__(512, 2) void gemm_256(const uint16_t* __restrict__ 
 // SWIGLU (NT): C[m, n] = silu(A Bg^T) * (A Bu^T) on a 256 x 128 output tile:
 // the Bt half-tile holds Bg rows n0..n0+127 and Bb the same rows of Bu, so a
 // lane's acc[ni] (gate) and acc[ni + 2] (up) are the same (m, n).
-template <typename T, bool TRANS_B, bool BIAS, int SCHED = 0, bool SWIGLU = false>
-__global__ __launch_bounds__(512, 2) void gemm_256p(const uint16_t* __restrict__ A,
-                                                    const uint16_t* __restrict__ Bm,
-                                                    uint16_t* __restrict__ C,
-                                                    const uint16_t* __restrict__ bias, int M, int N,
-                                                    int K, int64_t lda, int64_t ldb, int64_t ldc,
-                                                    int tiles_n, int nblocks, int group_m,
-                                                    const uint16_t* __restrict__ Bu, int64_t ldbu) {
+//
+// The tile body is shared by the dense kernel (gemm_256p) and the grouped MoE
+// kernel (gemm_256g): output rows m0 .. min(m0 + 256, mend) - 1, A row r read
+// from A[amap ? amap[r] : r] (the per-lane source rows are loaded once before
+// the first DMA: a gather load inside the pipeline would make hipcc drain the
+// LDS-DMA queue with vmcnt(0) at its use).
+constexpr int G2P_LDS = 2 * 4 * 16384;
+
+template <typename T, bool TRANS_B, bool BIAS, int SCHED, bool SWIGLU>
+__device__ __forceinline__ void g256p_body(char* __restrict__ smem, const uint16_t* __restrict__ A,
+                                           int64_t lda, const int* __restrict__ amap, int m0,
+                                           int mend, const uint16_t* __restrict__ Bm, int64_t ldb,
+                                           const uint16_t* __restrict__ Bu, int64_t ldbu, int n0,
+                                           int N, int K, uint16_t* __restrict__ C, int64_t ldc,
+                                           const uint16_t* __restrict__ bias) {
     static_assert(!SWIGLU || (TRANS_B && !BIAS), "SwiGLU tile: NT, no bias");
-    constexpr int TN = SWIGLU ? 128 : G2N;  // output columns per tile
     constexpr int HT = 16384, BUF = 4 * HT;
     constexpr int AT = 0, AB = 1, BT = 2, BB = 3;
-    __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = wave >> 2, wc = wave & 3;
     const int l16 = lane & 15, g = lane >> 4, qq = l16 >> 2, pp = lane & 3;
-    const int lb = xcd_remap(blockIdx.x, nblocks);
-    int tmi, tni;
-    g2_tile(lb, cdiv(M, G2M), tiles_n, group_m, tmi, tni);
-    const int m0 = tmi * G2M, n0 = tni * TN;
+    const int M = mend;
     const int ktiles = K / G2K;
+    // source rows of this lane's A pieces: [half AT/AB][piece i]
+    int arow[2][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int r = min(m0 + 128 * h + (wave * 2 + i) * 8 + (lane >> 3), mend - 1);
+            arow[h][i] = amap ? amap[r] : r;
+        }
 
     auto issue = [&](int half, int kt) {
         if (kt >= ktiles) return;
@@ -450,7 +461,7 @@ __global__ __launch_bounds__(512, 2) void gemm_256p(const uint16_t* __restrict__
                 const int c = slot ^ ((row >> 1) & 7);
                 const uint16_t* src;
                 if (half == AT || half == AB)
-                    src = A + (int64_t)min(m0 + (half == AB ? 128 : 0) + row, M - 1) * lda;
+                    src = A + (int64_t)arow[half == AB ? 1 : 0][i] * lda;
                 else if constexpr (SWIGLU)
                     src = half == BB ? Bu + (int64_t)min(n0 + row, N - 1) * ldbu
                                      : Bm + (int64_t)min(n0 + row, N - 1) * ldb;
@@ -639,6 +650,63 @@ __global__ __launch_bounds__(512, 2) void gemm_256p(const uint16_t* __restrict__
             *reinterpret_cast<i32x2*>(crow + n) = i32x2{(int)pack2<T>(v[0], v[1]), (int)pack2<T>(v[2], v[3])};
         }
     }
+}
+
+
+template <typename T, bool TRANS_B, bool BIAS, int SCHED = 0, bool SWIGLU = false>
+__global__ __launch_bounds__(512, 2) void gemm_256p(const uint16_t* __restrict__ A,
+                                                    const uint16_t* __restrict__ Bm,
+                                                    uint16_t* __restrict__ C,
+                                                    const uint16_t* __restrict__ bias, int M, int N,
+                                                    int K, int64_t lda, int64_t ldb, int64_t ldc,
+                                                    int tiles_n, int nblocks, int group_m,
+                                                    const uint16_t* __restrict__ Bu, int64_t ldbu) {
+    constexpr int TN = SWIGLU ? 128 : G2N;  // output columns per tile
+    __shared__ __attribute__((aligned(16))) char smem[G2P_LDS];
+    const int lb = xcd_remap(blockIdx.x, nblocks);
+    int tmi, tni;
+    g2_tile(lb, cdiv(M, G2M), tiles_n, group_m, tmi, tni);
+    g256p_body<T, TRANS_B, BIAS, SCHED, SWIGLU>(smem, A, lda, nullptr, tmi * G2M, M, Bm, ldb, Bu,
+                                                ldbu, tni * TN, N, K, C, ldc, bias);
+}
+
+// Grouped MoE GEMM on the phased tile: expert e owns the expert-sorted rows
+// offsets[e] .. offsets[e+1]-1 (device table, pli_moe_route); its rows are cut
+// into 256-row slots, slot s of the launch (slots_bound = cdiv(rows, 256) + E,
+// an upper bound) is found by a scalar scan of the offsets, and blocks past
+// the real slot count exit before any barrier.  A rows are read through
+// `gather` (row -> token of x; NULL: A is already expert-sorted), B is expert
+// e's weight (W[e], for SWIGLU gate W[e] / up Wu[e]), C rows are the sorted rows.
+template <typename T, bool SWIGLU>
+__global__ __launch_bounds__(512, 2) void gemm_256g(const uint16_t* __restrict__ X, int64_t ldx,
+                                                    const int* __restrict__ gather,
+                                                    const uint16_t* const* __restrict__ W,
+                                                    const uint16_t* const* __restrict__ Wu,
+                                                    int64_t ldw, uint16_t* __restrict__ C,
+                                                    int64_t ldc, const int* __restrict__ offsets,
+                                                    int E, int N, int K, int slots, int tiles_n,
+                                                    int nblocks) {
+    constexpr int TN = SWIGLU ? 128 : G2N;
+    __shared__ __attribute__((aligned(16))) char smem[G2P_LDS];
+    const int lb = xcd_remap(blockIdx.x, nblocks);
+    int slot, tni;
+    g2_tile(lb, slots, tiles_n, 4, slot, tni);
+    int e = -1, rbeg = 0, rend = 0, acc = 0;
+    for (int j = 0; j < E; ++j) {
+        const int b0 = offsets[j], b1 = offsets[j + 1];
+        const int nt = (b1 - b0 + G2M - 1) / G2M;
+        if (slot < acc + nt) {
+            e = j;
+            rbeg = b0 + (slot - acc) * G2M;
+            rend = b1;
+            break;
+        }
+        acc += nt;
+    }
+    if (e < 0) return;  // whole block: before any barrier
+    g256p_body<T, true, false, 7, SWIGLU>(smem, X, ldx, gather, rbeg, rend, W[e], ldw,
+                                          SWIGLU ? Wu[e] : nullptr, ldw, tni * TN, N, K, C, ldc,
+                                          nullptr);
 }
 
 // ---------------------------------------------------------------------------
@@ -1398,6 +1466,30 @@ extern "C" int pli_gemm_grouped(const void* x, const int32_t* gather, const void
                 "pli_gemm_grouped: needs k %% 128 == 0, n %% 16 == 0, 16-byte aligned rows");
     PLI_REQUIRE(ldx >= k && ldw >= k && ldc >= n, "pli_gemm_grouped: leading dimension too small");
     if (rows_bound == 0) return PLI_OK;
+    hipStream_t st = (hipStream_t)stream;
+    if (rows_bound >= 16 * experts) {
+        // prefill-sized routing (>= 16 rows per expert on average): the phased
+        // 256-row tile per (expert, slot); decode sizes stay on the
+        // weight-streaming kernel below
+        const bool sw = wu_ptrs != nullptr;
+        const int slots = cdiv(rows_bound, G2M) + experts;
+        const int tn = cdiv(n, sw ? 128 : G2N);
+        const int64_t nb = (int64_t)slots * tn;
+        PLI_REQUIRE(nb < (1ll << 31), "pli_gemm_grouped: grid too large");
+        const auto* Xg = (const uint16_t*)x;
+        const auto* const* Wg = (const uint16_t* const*)w_ptrs;
+        const auto* const* Wug = (const uint16_t* const*)wu_ptrs;
+#define PLI_G256G(TT, SW)                                                                          \
+    hipLaunchKernelGGL((gemm_256g<TT, SW>), dim3((unsigned)nb), dim3(512), 0, st, Xg, ldx, gather, \
+                       Wg, Wug, ldw, (uint16_t*)c, ldc, offsets, experts, n, k, slots, tn, (int)nb)
+        if (dtype == PLI_BF16) {
+            if (sw) PLI_G256G(bf16_t, true); else PLI_G256G(bf16_t, false);
+        } else {
+            if (sw) PLI_G256G(f16_t, true); else PLI_G256G(f16_t, false);
+        }
+#undef PLI_G256G
+        return launch_status("gemm_256g");
+    }
     const int nblk = n / 16;
     PLI_REQUIRE((int64_t)experts * nblk < (1ll << 31), "pli_gemm_grouped: grid too large");
     const dim3 grid((unsigned)(experts * nblk)), block(256);

@@ -33,12 +33,19 @@ def test_moe_route_vs_oracle(T, E, k):
             assert off[e] <= p[t, j] < off[e + 1] and gth[p[t, j]] == t
 
 
-@pytest.mark.parametrize("T,E,k,H,I", [(4, 8, 2, 256, 512), (64, 8, 2, 512, 1024),
-                                       (300, 8, 2, 256, 256)])
-def test_grouped_gemm_and_combine_vs_oracle(T, E, k, H, I):
+@pytest.mark.parametrize("T,E,k,H,I,dead", [
+    (4, 8, 2, 256, 512, ()),         # decode sizes: weight-streaming grouped kernel
+    (64, 8, 2, 512, 1024, ()),       # 16 rows / expert: the phased 256-row tile (gemm_256g)
+    (300, 8, 2, 256, 256, ()),
+    (1200, 4, 2, 384, 640, ()),      # ~600 rows / expert = 3 slots each; ragged n on both GEMMs
+    (600, 16, 1, 256, 512, (3, 7, 11)),  # experts with no rows: their slots are skipped
+])
+def test_grouped_gemm_and_combine_vs_oracle(T, E, k, H, I, dead):
     import pli_hip
     x = torch.from_numpy(seeded_normal((T, H), 1, "bf16")).cuda().bfloat16()
     logits = torch.from_numpy(seeded_normal((T, E), 2)).cuda()
+    for e in dead:
+        logits[:, e] -= 100.0
     ws = [[torch.from_numpy(seeded_normal(s, 10 * e + i, "bf16") * s[1] ** -0.5).cuda().bfloat16()
            for i, s in enumerate(((I, H), (H, I), (I, H)))] for e in range(E)]
     w, idx, pos, gather, offsets = pli_hip.moe_route(logits, k)
@@ -59,6 +66,8 @@ def test_grouped_gemm_and_combine_vs_oracle(T, E, k, H, I):
         ref = swiglu(xn[gth[list(rows)]], ws[e][0].double().cpu().numpy(), ws[e][2].double().cpu().numpy())
         assert np.abs(hn[list(rows)] - ref).max() <= 1e-2 * (np.abs(ref).max() + 1)
     # end to end vs the f64 layer with the same routing
+    if dead:
+        assert all(off[e] == off[e + 1] for e in dead)
     rw, ridx = moe_route(logits.double().cpu().numpy(), k)
     exp = np.zeros((T, H))
     for t in range(T):

@@ -332,6 +332,8 @@ def tune_moe(tokens=(1, 8, 32, 128)):
         return out.view_as(x)
 
     per_expert = 3 * cfg.hidden_dim * cfg.expert_dim * 2
+    if os.environ.get("PLI_MOE_T"):
+        tokens = tuple(int(v) for v in os.environ["PLI_MOE_T"].split(","))
     for T in tokens:
         x = torch.randn(1, T, cfg.hidden_dim, device="cuda", dtype=torch.bfloat16)
         with torch.no_grad():
@@ -351,6 +353,8 @@ def tune_moe(tokens=(1, 8, 32, 128)):
         print(json.dumps({"kernel": "moe_layer", "tokens": T, "active_experts": active,
                           **{f"{k}_us": v * 1e3 for k, v in res.items()},
                           **{f"{k}_GB/s": active * per_expert / (v * 1e-3) / 1e9 for k, v in res.items()},
+                          **{f"{k}_TFLOP/s": 2 * T * cfg.num_experts_per_tok * 3 * cfg.hidden_dim
+                             * cfg.expert_dim / (v * 1e-3) / 1e12 for k, v in res.items()},
                           "rel_diff": err}), flush=True)
 
 
