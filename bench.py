@@ -18,6 +18,9 @@ The same JSON line carries, as sub-objects, the other hot-path rows:
           xGMI when N > 1 (compute / all-reduce / total / bus bandwidth)
   cpu_baseline  the reference tile loop restated on torch CPU (oracle, kind
           "port"), rank 0, N=1 only, on a bounded sample of the workload.
+  cpu_other     torch.mv / torch.mm / one TP8 shard F.linear on the host cores
+  tp_gemm.small_m  the TP shard GEMM at M = 1 and 128
+  flash_wallclock_ms  the reference's timing style (sync per call) beside the events
 
 All device times are HIP events recorded on the stream the kernels run on.
 """
@@ -197,6 +200,17 @@ def bench_tp(stream, world: int, rank: int, iters: int) -> dict:
     ms_gemm = event_time_ms(gemm, iters, stream)
     out = {"workload": f"ch09 RowParallel 8192x8192 TP={world}, M={M}, bf16",
            "gemm_us": ms_gemm * 1e3, "gemm_TFLOP/s": 2 * M * N * kl / (ms_gemm * 1e-3) / 1e12}
+    # also M in {1, 128} (decode batches; W streamed from HBM)
+    small = {}
+    for m in (1, 128):
+        xs = torch.randn(m, kl, device="cuda", dtype=torch.bfloat16)
+        ys = torch.empty(m, N, device="cuda", dtype=torch.bfloat16)
+        fs = lambda: pli_hip.gemm(xs, w, trans_b=True, out=ys)  # noqa: E731
+        fs()
+        ms = event_time_ms(fs, 20, stream)
+        small[str(m)] = {"gemm_us": ms * 1e3, "weight_GB/s": N * kl * 2 / (ms * 1e-3) / 1e9,
+                         "TFLOP/s": 2 * m * N * kl / (ms * 1e-3) / 1e12}
+    out["small_m"] = small
     if world > 1:
         def ar():
             dist.all_reduce(y)
@@ -239,6 +253,39 @@ def cpu_baseline(seconds: float = 15.0) -> dict:
             "sample": f"reference tile loop (ch06/flash_attention.py:14-74 restated, oracle/attention.py) "
                       f"on torch CPU bf16, B=1 H=32 S=4096 D=128 = 1/8 of the workload, "
                       f"best of {len(times)} runs ({sec:.2f} s each)"}
+
+
+def cpu_other() -> dict:
+    """SURVEY 8(d)'s other CPU baselines, torch CPU on the box's host cores
+    (bounded: a few seconds in all): torch.mv 4096^2 (ch03 GEMV, 10 + 100),
+    torch.mm 4096^3 NN (ch03 GEMM, 2 + 5), one TP8 row shard F.linear
+    ([8192, 1024] x [8192, 1024]^T, 2 + 5)."""
+    import torch.nn.functional as F
+    g = torch.Generator().manual_seed(0)
+    out = {"cores": torch.get_num_threads(), "dtype": "bf16", "kind": "reference ops (torch CPU)"}
+
+    def tmin(fn, warm, iters):
+        for _ in range(warm):
+            fn()
+        best = float("inf")
+        for _ in range(iters):
+            t0 = time.perf_counter()
+            fn()
+            best = min(best, time.perf_counter() - t0)
+        return best
+
+    w = torch.randn(4096, 4096, generator=g).bfloat16()
+    x = torch.randn(4096, generator=g).bfloat16()
+    t = tmin(lambda: torch.mv(w, x), 10, 100)
+    out["gemv_torch.mv"] = {"us": t * 1e6, "GB/s": 33570816 / t / 1e9}
+    a = torch.randn(4096, 4096, generator=g).bfloat16()
+    t = tmin(lambda: torch.mm(a, w), 2, 5)
+    out["gemm_torch.mm_4096"] = {"ms": t * 1e3, "TFLOP/s": 2 * 4096 ** 3 / t / 1e12}
+    xs = torch.randn(8192, 1024, generator=g).bfloat16()
+    ws = torch.randn(8192, 1024, generator=g).bfloat16()
+    t = tmin(lambda: F.linear(xs, ws), 2, 5)
+    out["tp8_shard_F.linear"] = {"ms": t * 1e3, "TFLOP/s": 2 * 8192 * 8192 * 1024 / t / 1e12}
+    return out
 
 
 def main():
@@ -302,6 +349,16 @@ def main():
     for _ in range(2 if not args.flash_only else 0):
         pli_hip.flash_attn_fwd(q, k, v, causal=True, out=o)
     if not args.flash_only:
+        # the reference's own timing style (sync per call, wall clock), next to the events
+        wc = []
+        for _ in range(5):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            step()
+            torch.cuda.synchronize()
+            wc.append(time.perf_counter() - t1)
+        extra["flash_wallclock_ms"] = {"mean": sum(wc) / len(wc) * 1e3, "min": min(wc) * 1e3,
+                                       "timing": "sync + perf_counter per call, 5 calls"}
         ms_c = event_time_ms(lambda: pli_hip.flash_attn_fwd(q, k, v, causal=True, out=o), 5, stream)
         extra["flash_causal"] = {"ms": ms_c,
                                  "TFLOP/s": 4 * B * H * D * (S * (S + 1) // 2) / (ms_c * 1e-3) / 1e12}
@@ -343,6 +400,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.quick:
         result["cpu_baseline"] = cpu_baseline()
+        result["cpu_other"] = cpu_other()
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
