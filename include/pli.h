@@ -227,6 +227,21 @@ int pli_gemm_multi_nt(const void* x, int64_t ldx, int m, int k,
                       const int64_t* stride_batch, const int64_t* stride_token,
                       const int32_t* const* row_offset, const int* capacity,
                       int ngroups, int dtype, void* stream);
+/* pli_rms_gemm_nt: a decode-step RMSNorm fused into the projection that
+ * consumes it (ch02/cached_generation.py:112-120 RMSNorm -> :58-69 q/k/v,
+ * :136-140 gate/up, :180-185 final norm -> lm_head).  Rows: h = a (+ residual)
+ * (written to h_out if not NULL), y = h * rsqrt(mean(h^2) + eps) * norm_weight
+ * -- bitwise the row pli_rmsnorm writes -- kept on chip; then the groups of
+ * pli_gemm_multi_nt on y (w_up non-NULL: every group is SwiGLU,
+ * silu(y.w) * (y.w_up), w_up rows with the same ldw).  1 <= m <= 4 rows,
+ * k % 8 == 0, k <= 8192, bf16/fp16. */
+int pli_rms_gemm_nt(const void* a, int64_t lda, const void* residual, int64_t ldr,
+                    const void* norm_weight, float eps, void* h_out, int64_t ldh, int m, int k,
+                    int tokens_per_batch, const void* const* w, const void* const* w_up,
+                    void* const* c, const int* n, const int64_t* ldw,
+                    const int64_t* stride_batch, const int64_t* stride_token,
+                    const int32_t* const* row_offset, const int* capacity, int ngroups,
+                    int dtype, void* stream);
 int pli_attn_decode_dev(const void* q, const void* k, const void* v, void* o,
                         int batch, int heads, int kv_heads, int n_q,
                         int n_kv_max, int head_dim, const int64_t* strides,

@@ -163,6 +163,36 @@ class CachedTransformerBlock(nn.Module):
         h = x + self.attn(self.input_norm(x), cache, start_pos)
         return h + self.ffn(self.post_attn_norm(h))
 
+    def decode_fused(self, x: torch.Tensor, pending: torch.Tensor | None, cache: LayerKVCache
+                     ) -> tuple[torch.Tensor, torch.Tensor]:
+        """Decode step of the layer in 5 launches: input norm (+ the pending
+        residual add) fused into q/k/v (k/v straight into the cache at the
+        device position), attention, o_proj, post-attention norm (+ residual)
+        fused into gate/up/silu*mul, down_proj.  Returns (residual stream,
+        pending FFN output)."""
+        B, S, hd = x.shape
+        at = self.attn
+        q = torch.empty(B, S, at.num_heads * at.head_dim, device=x.device, dtype=x.dtype)
+        if pending is None:
+            pli_hip.rms_qkv_into_cache(x, self.input_norm.weight, self.input_norm.eps,
+                                       at.q_proj.weight, at.k_proj.weight, at.v_proj.weight, q,
+                                       cache.k, cache.v, cache.pos)
+        else:
+            h = torch.empty_like(x)
+            pli_hip.rms_qkv_into_cache(pending, self.input_norm.weight, self.input_norm.eps,
+                                       at.q_proj.weight, at.k_proj.weight, at.v_proj.weight, q,
+                                       cache.k, cache.v, cache.pos, residual=x, h_out=h)
+            x = h
+        cache.seq_len += S
+        o = pli_hip.attn_decode_dev(q.view(B, S, at.num_heads, at.head_dim), cache.k, cache.v,
+                                    cache.pos, n_kv_add=S, causal=S > 1)
+        a = _lin(o.reshape(B, S, hd), at.o_proj.weight)
+        h2 = torch.empty_like(x)
+        f = self.ffn
+        g = pli_hip.rms_swiglu(a, self.post_attn_norm.weight, self.post_attn_norm.eps,
+                               f.gate_proj.weight, f.up_proj.weight, residual=x, h_out=h2)
+        return h2, _lin(g, f.down_proj.weight)
+
     def attn_half(self, x: torch.Tensor, pending: torch.Tensor | None,
                   cache: LayerKVCache | None, start_pos: int):
         """Device path: x (+ the previous layer's pending FFN output, added in
@@ -175,6 +205,12 @@ class CachedTransformerBlock(nn.Module):
                                     residual=x)
         a = self.attn(n1, cache, start_pos)
         return pli_hip.rmsnorm(a, self.post_attn_norm.weight, self.post_attn_norm.eps, residual=x)
+
+
+# decode steps (<= 4 rows, device-resident cache length): every RMSNorm fused
+# into the projection that consumes it (pli_rms_gemm_nt); tests flip it off
+# to compare with the unfused launches
+FUSED_DECODE = True
 
 
 class CachedTransformerModel(nn.Module):
@@ -198,6 +234,13 @@ class CachedTransformerModel(nn.Module):
     def forward(self, input_ids: torch.Tensor, caches: list[LayerKVCache] | None = None,
                 start_pos: int = 0) -> torch.Tensor:
         x = self.embed(input_ids)
+        if x.is_cuda and self._fused_decode_ok(x, caches):
+            pending = None
+            for i, layer in enumerate(self.layers):
+                x, pending = layer.decode_fused(x, pending, caches[i])
+            caches[0].pos.add_(input_ids.shape[1])
+            return pli_hip.rms_linear(pending, self.norm.weight, self.norm.eps, self.lm_head.weight,
+                                      residual=x)
         if x.is_cuda:
             # residual stream with the adds folded into the norms: per layer one
             # norm(+add) before attention, one after; the FFN output stays
@@ -217,6 +260,14 @@ class CachedTransformerModel(nn.Module):
         for i, layer in enumerate(self.layers):
             x = layer(x, caches[i] if caches is not None else None, start_pos)
         return _lin(self.norm(x), self.lm_head.weight)
+
+    def _fused_decode_ok(self, x: torch.Tensor, caches) -> bool:
+        if not FUSED_DECODE or caches is None or caches[0].pos is None or not self.layers:
+            return False
+        B, S, hd = x.shape
+        at = self.layers[0].attn
+        return (B * S <= 4 and hd % 8 == 0 and hd <= 8192 and B * S * hd * 2 <= 65536
+                and _device_len_ok_shape(x, S, at.num_heads, at.num_kv_heads, at.head_dim))
 
     def create_caches(self, batch_size: int, max_seq_len: int, device: torch.device,
                       dtype: torch.dtype, device_pos: bool = False) -> list[LayerKVCache]:

@@ -42,6 +42,8 @@ _SIGS = {
                     _c_f32, _c_int, _vp],
     "pli_gemm_multi_nt": [_vp, _c_i64, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                           _vp, _c_int, _c_int, _vp],
+    "pli_rms_gemm_nt": [_vp, _c_i64, _vp, _c_i64, _vp, _c_f32, _vp, _c_i64, _c_int, _c_int, _c_int,
+                        _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _c_int, _vp],
     "pli_moe_route": [_vp, _c_i64, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp,
                       _vp, _vp, _vp],
     "pli_gemm_grouped": [_vp, _vp, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_i64,
@@ -428,6 +430,92 @@ def qkv_into_cache(x: torch.Tensor, wq: torch.Tensor, wk: torch.Tensor, wv: torc
         rc = lib().pli_gemm_multi_nt(_ptr(x2), x2.stride(0), B * S, hidden, S, w, c, n, ldw, sb, stok,
                                      ro, cap, 3, _dtype_code(x), _stream(dev))
     _check(rc, "pli_gemm_multi_nt")
+    return q_out
+
+
+def _rows(t: torch.Tensor) -> torch.Tensor:
+    t2 = t.reshape(-1, t.shape[-1])
+    return t2 if t2.stride(1) == 1 and t2.stride(0) % 8 == 0 else t2.contiguous()
+
+
+def _rms_gemm(a: torch.Tensor, norm_weight: torch.Tensor, eps: float, groups: list,
+              residual: torch.Tensor | None, h_out: torch.Tensor | None, tokens_per_batch: int,
+              swiglu: bool) -> None:
+    """pli_rms_gemm_nt.  groups: (w, w_up | None, c, n, stride_batch, stride_token,
+    pos | None, capacity) with c the output base tensor."""
+    dev = _require_gpu(a, norm_weight, *(g[0] for g in groups))
+    a2 = _rows(a)
+    r2 = _rows(residual) if residual is not None else None
+    if h_out is not None and (h_out.stride(-1) != 1 or tuple(h_out.shape[-1:]) != (a2.shape[1],)):
+        raise PliError("h_out must have unit inner stride and the hidden width")
+    h2 = h_out.view(-1, h_out.shape[-1]) if h_out is not None else None
+    m, k = a2.shape
+    ng = len(groups)
+    P = ctypes.c_void_p
+    w = (P * ng)(*(g[0].data_ptr() for g in groups))
+    wu = (P * ng)(*(g[1].data_ptr() for g in groups)) if swiglu else None
+    c = (P * ng)(*(g[2].data_ptr() for g in groups))
+    n = (_c_int * ng)(*(int(g[3]) for g in groups))
+    ldw = (_c_i64 * ng)(*(g[0].stride(0) for g in groups))
+    sb = (_c_i64 * ng)(*(int(g[4]) for g in groups))
+    stok = (_c_i64 * ng)(*(int(g[5]) for g in groups))
+    ro = (P * ng)(*((g[6].data_ptr() if g[6] is not None else None) for g in groups))
+    cap = (_c_int * ng)(*(int(g[7]) for g in groups))
+    for g in groups:
+        if g[0].stride(1) != 1 or (g[1] is not None and (g[1].stride(1) != 1 or g[1].stride(0) != g[0].stride(0))):
+            raise PliError("weights must be [n, k] with unit inner stride (up weight: same ldw)")
+    with _on_device(dev):
+        rc = lib().pli_rms_gemm_nt(_ptr(a2), a2.stride(0), _ptr(r2), r2.stride(0) if r2 is not None else 0,
+                                   _ptr(norm_weight), float(eps), _ptr(h2),
+                                   h2.stride(0) if h2 is not None else 0, m, k, int(tokens_per_batch),
+                                   w, wu, c, n, ldw, sb, stok, ro, cap, ng, _dtype_code(a), _stream(dev))
+    _check(rc, "pli_rms_gemm_nt")
+
+
+def rms_linear(a: torch.Tensor, norm_weight: torch.Tensor, eps: float, w: torch.Tensor,
+               residual: torch.Tensor | None = None, h_out: torch.Tensor | None = None,
+               out: torch.Tensor | None = None) -> torch.Tensor:
+    """rmsnorm(a (+ residual)) @ w^T in one launch (decode: <= 4 rows)."""
+    a2 = a.reshape(-1, a.shape[-1])
+    if out is None:
+        out = torch.empty(a2.shape[0], w.shape[0], device=a.device, dtype=a.dtype)
+    # one token per "batch": row bb lands at out + bb * stride(0)
+    _rms_gemm(a, norm_weight, eps, [(w, None, out, w.shape[0], out.stride(0), 0, None, 1 << 30)],
+              residual, h_out, 1, False)
+    return out.view(*a.shape[:-1], w.shape[0])
+
+
+def rms_swiglu(a: torch.Tensor, norm_weight: torch.Tensor, eps: float, wg: torch.Tensor,
+               wu: torch.Tensor, residual: torch.Tensor | None = None,
+               h_out: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """silu(y wg^T) * (y wu^T) with y = rmsnorm(a (+ residual)), one launch."""
+    a2 = a.reshape(-1, a.shape[-1])
+    if out is None:
+        out = torch.empty(a2.shape[0], wg.shape[0], device=a.device, dtype=a.dtype)
+    _rms_gemm(a, norm_weight, eps, [(wg, wu, out, wg.shape[0], out.stride(0), 0, None, 1 << 30)],
+              residual, h_out, 1, True)
+    return out.view(*a.shape[:-1], wg.shape[0])
+
+
+def rms_qkv_into_cache(a: torch.Tensor, norm_weight: torch.Tensor, eps: float,
+                       wq: torch.Tensor, wk: torch.Tensor, wv: torch.Tensor, q_out: torch.Tensor,
+                       k_cache: torch.Tensor, v_cache: torch.Tensor, pos: torch.Tensor,
+                       residual: torch.Tensor | None = None,
+                       h_out: torch.Tensor | None = None) -> torch.Tensor:
+    """qkv_into_cache on rmsnorm(a (+ residual)), one launch; a [B, S, hidden]."""
+    B, S, _ = a.shape
+    S_max, Hkv, D = k_cache.shape[1:]
+    if pos.dtype != torch.int32 or not pos.is_cuda:
+        raise PliError("pos must be an int32 device tensor")
+    for t in (k_cache, v_cache):
+        if t.shape[0] != B or t.stride(3) != 1 or t.stride(2) != D:
+            raise PliError("caches must be [B, S_max, Hkv, D] with contiguous (Hkv, D) rows")
+    if q_out.dim() != 3 or tuple(q_out.shape[:2]) != (B, S) or q_out.stride(2) != 1:
+        raise PliError("q_out must be [B, S, Hq*D] with unit inner stride")
+    groups = [(wq, None, q_out, wq.shape[0], q_out.stride(0), q_out.stride(1), None, S),
+              (wk, None, k_cache, wk.shape[0], k_cache.stride(0), k_cache.stride(1), pos, S_max),
+              (wv, None, v_cache, wv.shape[0], v_cache.stride(0), v_cache.stride(1), pos, S_max)]
+    _rms_gemm(a, norm_weight, eps, groups, residual, h_out, S, False)
     return q_out
 
 

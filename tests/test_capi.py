@@ -78,6 +78,11 @@ def test_argument_validation_without_gpu(built_lib):
     assert multi(17, 1, 3) == EINVAL and b"m <= 16" in L.pli_last_error()
     assert multi(6, 4, 3) == EINVAL  # 6 rows are not whole batches of 4
     assert multi(4, 1, 4) == EINVAL and b"groups" in L.pli_last_error()
+    # fused norm + projection: <= 4 rows, k <= 8192
+    rms = lambda m, k: L.pli_rms_gemm_nt(p, 8192, None, 0, p, 1e-6, None, 0, m, k, 1, w3, None, w3,
+                                         n3, ld3, ld3, ld3, P3(None, None, None), I3(9, 9, 9), 3, 2, None)
+    assert rms(5, 64) == EINVAL and b"m <= 4" in L.pli_last_error()
+    assert rms(1, 16384) == EINVAL and b"k <= 8192" in L.pli_last_error()
 
 
 def test_decode_workspace_plan(built_lib):

@@ -129,3 +129,85 @@ def test_cuda_graph_runner_api():
     torch.testing.assert_close(out, torch.relu(x @ w))
     assert runner.run_graph(2, x[:2]) is None
     assert runner.has_graph(1) and sorted(runner.get_captured_batch_sizes()) == [1, 4]
+
+
+@pytest.mark.parametrize("M", [1, 3])
+def test_rms_gemm_matches_norm_then_gemm(M):
+    """pli_rms_gemm_nt == pli_rmsnorm (+ residual) followed by the unfused
+    projection: bitwise at one row (same reduction and dot orders), within
+    bf16 rounding at more rows (the unfused GEMM is then the MFMA small-M
+    kernel)."""
+    import pli_hip
+    torch.manual_seed(M)
+    hd, N, I = 2048, 1536, 2816
+    a = torch.randn(M, hd, device="cuda", dtype=torch.bfloat16)
+    res = torch.randn(M, hd, device="cuda", dtype=torch.bfloat16)
+    g = (1 + 0.1 * torch.randn(hd, device="cuda")).bfloat16()
+    w = torch.randn(N, hd, device="cuda", dtype=torch.bfloat16) * hd ** -0.5
+    wg = torch.randn(I, hd, device="cuda", dtype=torch.bfloat16) * hd ** -0.5
+    wu = torch.randn(I, hd, device="cuda", dtype=torch.bfloat16) * hd ** -0.5
+    h_ref, y = pli_hip.rmsnorm(a, g, 1e-6, residual=res)
+    h = torch.empty_like(a)
+
+    def same(x, ref):
+        if M == 1:
+            assert torch.equal(x, ref)
+        else:
+            assert (x.float() - ref.float()).abs().max().item() <= 2 ** -7 * (ref.float().abs().max().item() + 1)
+
+    out = pli_hip.rms_linear(a, g, 1e-6, w, residual=res, h_out=h)
+    assert torch.equal(h, h_ref)
+    same(out, pli_hip.gemm(y, w, trans_b=True))
+    same(pli_hip.rms_swiglu(a, g, 1e-6, wg, wu, residual=res), pli_hip.gemm_swiglu(y, wg, wu))
+    # no residual: h_out untouched, y = rmsnorm(a)
+    y0 = pli_hip.rmsnorm(a, g, 1e-6)
+    same(pli_hip.rms_linear(a, g, 1e-6, w), pli_hip.gemm(y0, w, trans_b=True))
+    # q/k/v into the caches at the device position
+    B, S = (M, 1)
+    H, Hkv, D, S_max = 16, 4, 64, 24
+    wq = torch.randn(H * D, hd, device="cuda", dtype=torch.bfloat16) * hd ** -0.5
+    wk = torch.randn(Hkv * D, hd, device="cuda", dtype=torch.bfloat16) * hd ** -0.5
+    wv = torch.randn(Hkv * D, hd, device="cuda", dtype=torch.bfloat16) * hd ** -0.5
+    kc = torch.zeros(B, S_max, Hkv, D, device="cuda", dtype=torch.bfloat16)
+    vc, kr, vr = torch.zeros_like(kc), torch.zeros_like(kc), torch.zeros_like(kc)
+    pos = torch.tensor([5], device="cuda", dtype=torch.int32)
+    q = torch.empty(B, S, H * D, device="cuda", dtype=torch.bfloat16)
+    qr = torch.empty_like(q)
+    pli_hip.rms_qkv_into_cache(a.view(B, S, hd), g, 1e-6, wq, wk, wv, q, kc, vc, pos,
+                               residual=res.view(B, S, hd))
+    pli_hip.qkv_into_cache(y.view(B, S, hd), wq, wk, wv, qr, kr, vr, pos)
+    assert torch.equal(q, qr) and torch.equal(kc, kr) and torch.equal(vc, vr)
+
+
+@pytest.mark.parametrize("B", [1, 2])
+def test_fused_decode_step_matches_unfused(B):
+    """The model's fused decode path (5 launches per layer) against the
+    unfused launches over the same caches: bitwise at batch 1, close at 2."""
+    import ch02.cached_generation as cg
+    model = _model()
+    ids = torch.randint(0, 1000, (B, 20), device="cuda")
+    outs = {}
+    try:
+        for fused in (True, False):
+            cg.FUSED_DECODE = fused
+            with torch.no_grad():
+                caches = model.create_caches(B, 48, torch.device("cuda"), torch.bfloat16, device_pos=True)
+                lg = model(ids, caches)
+                tok = lg[:, -1:].argmax(-1)
+                steps = []
+                for _ in range(6):
+                    lg = model(tok, caches, start_pos=caches[0].seq_len)
+                    steps.append(lg.float().clone())
+                    tok = lg[:, -1:].argmax(-1)
+            outs[fused] = (steps, caches[0].k.clone(), int(caches[0].pos.item()))
+    finally:
+        cg.FUSED_DECODE = True
+    (sf, kf, pf), (su, ku, pu) = outs[True], outs[False]
+    assert pf == pu == 26
+    for a, b in zip(sf, su):
+        if B == 1:
+            assert torch.equal(a, b)
+        else:
+            assert ((a - b).norm() / b.norm()).item() < 1e-2
+    if B == 1:
+        assert torch.equal(kf, ku)
