@@ -151,9 +151,13 @@ def test_cpu_tp_layers_match_reference():
     assert tuple(row.weight.shape) == tuple(g["row_w_shape"])
     assert array_hash(col.weight.detach().numpy()) == str(g["col_w_hash"])
     assert array_hash(row.weight.detach().numpy()) == str(g["row_w_hash"])
+    # Same F.linear as the reference; the last bits depend on the host BLAS
+    # kernel (AVX2 vs AVX-512 summation order), so not bit-exact across CPUs.
     with torch.no_grad():
-        np.testing.assert_array_equal(col(torch.from_numpy(seeded_normal((8, 256), 41))).numpy(), g["col_y"])
-        np.testing.assert_array_equal(row(torch.from_numpy(seeded_normal((8, 256), 42))).numpy(), g["row_y"])
+        np.testing.assert_allclose(col(torch.from_numpy(seeded_normal((8, 256), 41))).numpy(), g["col_y"],
+                                   rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(row(torch.from_numpy(seeded_normal((8, 256), 42))).numpy(), g["row_y"],
+                                   rtol=1e-5, atol=1e-5)
 
 
 def test_cpu_online_softmax_vs_golden():
