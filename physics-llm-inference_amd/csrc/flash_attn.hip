@@ -30,6 +30,7 @@
 #include <cmath>
 #include <type_traits>
 
+#include "flash_w4.h"
 #include "pli_common.h"
 
 namespace pli {
@@ -2469,6 +2470,18 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_seg(
 //  30: attn_fwd_seg (four barrier-separated load / compute segments per tile,
 //      waves 4-7 one segment behind, LDS-DMA into 3-deep rings; D=128, else 21)
 //  31: attn_fwd_seg + sched_group_barrier interleave of the compute segments
+//  40-42: attn_fwd_w4 (flash_w4.hip: 4 waves x 64 rows, one wave per SIMD,
+//      two-slot software pipeline; LDS reads 3 / 2 / 4 MFMAs ahead); D=64 -> 21
+//  43-45: attn_fwd_w4p (two phases of 32 MFMAs per tile, each K / V fragment
+//      feeding both row blocks; fragments 2 / 3 / 4 ahead; ragged Nk -> w4)
+//  46: attn_fwd_w4p fragments 3 ahead + s_memtime stamps (diagnostic)
+//  47-49: w4p, DMA offsets recomputed per piece; DMA pieces K in phase 1 /
+//      V in phase 2 (47), all in phase 2 (48), all in phase 1 (49); 57-59 = the
+//      same with stamps
+//  50/51: 49/47 + softmax chunks pinned on entry (INPIN); 60/61 stamped
+//  52: 50 with fragments 5 ahead; 53/54: timing-only experiments (WRONG
+//      results: f32 row sums of unrounded P / no DMA in the loop); 62-64 stamped
+//  55: 52 with sched_barrier entry fences (INPIN 2); 65 stamped
 // default: v2 NW8 + permlane row max + defer-max (THR 8, log2) + rounded-P row sum
 // (1057 TF vs 983 for plain v2 at B8 H32 S4096 D128; spike + variant parity green)
 constexpr int kDefaultVariant = 21;
@@ -2527,6 +2540,40 @@ int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int
             if constexpr (D == 128) {
                 if (variant == 30) PLI_ATTN_LAUNCH((attn_fwd_seg<T, 0>));
                 else PLI_ATTN_LAUNCH((attn_fwd_seg<T, 1>));
+            } else {
+                PLI_ATTN_LAUNCH((attn_fwd_v2<T, D, 8, true, 13>));
+            }
+            break;
+        case 40:
+        case 41:
+        case 42:
+        case 43:
+        case 44:
+        case 45:
+        case 46:
+        case 47:
+        case 48:
+        case 49:
+        case 50:
+        case 51:
+        case 52:
+        case 53:
+        case 54:
+        case 55:
+        case 65:
+        case 60:
+        case 61:
+        case 62:
+        case 63:
+        case 64:
+        case 57:
+        case 58:
+        case 59:
+            if constexpr (D == 128) {
+                const W4Strides w4{st.qb, st.qh, st.qn, st.kb, st.kh, st.kn,
+                                   st.vb, st.vh, st.vn, st.ob, st.oh, st.on};
+                return launch_attn_w4(q, k, v, o, B, H, group, Nq, Nk, w4, scale, causal,
+                                      std::is_same<T, bf16_t>::value ? 1 : 0, stream, variant - 40);
             } else {
                 PLI_ATTN_LAUNCH((attn_fwd_v2<T, D, 8, true, 13>));
             }

@@ -105,7 +105,7 @@ def test_flash_vs_oracle(case):
 
 
 # every MFMA variant (alternates A/B-tested by tools/tune.py) on the MFMA-eligible cases
-MFMA_VARIANTS = (0, 1, 2, 3, 8, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 27, 28, 29, 30, 31)
+MFMA_VARIANTS = (0, 1, 2, 3, 8, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 27, 28, 29, 30, 31, 40, 41, 42, 43, 44, 45)
 
 
 
@@ -136,7 +136,7 @@ def test_flash_strided_views_and_out_param():
     assert_attn_close(o.transpose(1, 2), ref, "bf16", "strided")
 
 
-@pytest.mark.parametrize("variant", [2, 21, 22, 23, 27, 30, 31])
+@pytest.mark.parametrize("variant", [2, 21, 22, 23, 27, 30, 31, 40, 41, 42, 43, 44, 45])
 def test_flash_forced_rescale_spike(variant):
     """A key spike in a late tile forces the online max to jump past the
     defer-max threshold (variants 18/19), exercising the rescale branch."""
