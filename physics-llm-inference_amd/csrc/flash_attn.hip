@@ -2474,14 +2474,8 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_seg(
 //      two-slot software pipeline; LDS reads 3 / 2 / 4 MFMAs ahead); D=64 -> 21
 //  43-45: attn_fwd_w4p (two phases of 32 MFMAs per tile, each K / V fragment
 //      feeding both row blocks; fragments 2 / 3 / 4 ahead; ragged Nk -> w4)
-//  46: attn_fwd_w4p fragments 3 ahead + s_memtime stamps (diagnostic)
-//  47-49: w4p, DMA offsets recomputed per piece; DMA pieces K in phase 1 /
-//      V in phase 2 (47), all in phase 2 (48), all in phase 1 (49); 57-59 = the
-//      same with stamps
-//  50/51: 49/47 + softmax chunks pinned on entry (INPIN); 60/61 stamped
-//  52: 50 with fragments 5 ahead; 53/54: timing-only experiments (WRONG
-//      results: f32 row sums of unrounded P / no DMA in the loop); 62-64 stamped
-//  55: 52 with sched_barrier entry fences (INPIN 2); 65 stamped
+//  46: attn_fwd_w4p fragments 3 ahead + s_memtime stamps (diagnostic; cycle
+//      anatomy in DESIGN.md 3.1, tools/w4_stamps.py)
 // default: v2 NW8 + permlane row max + defer-max (THR 8, log2) + rounded-P row sum
 // (1057 TF vs 983 for plain v2 at B8 H32 S4096 D128; spike + variant parity green)
 constexpr int kDefaultVariant = 21;
@@ -2551,24 +2545,6 @@ int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int
         case 44:
         case 45:
         case 46:
-        case 47:
-        case 48:
-        case 49:
-        case 50:
-        case 51:
-        case 52:
-        case 53:
-        case 54:
-        case 55:
-        case 65:
-        case 60:
-        case 61:
-        case 62:
-        case 63:
-        case 64:
-        case 57:
-        case 58:
-        case 59:
             if constexpr (D == 128) {
                 const W4Strides w4{st.qb, st.qh, st.qn, st.kb, st.kh, st.kn,
                                    st.vb, st.vh, st.vn, st.ob, st.oh, st.on};

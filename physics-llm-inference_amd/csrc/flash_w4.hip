@@ -373,6 +373,10 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_w4(
         }
         if (0 >= t_mask) slot(Y, N, Y, Y, DN, 1, 0, 0, 0, 0, 0, 0);
         else slot(Y, N, Y, N, DN, 1, 0, 0, 0, 0, 0, 0);
+        // every wave has read K(0) (image 0) before iteration 0 DMAs K(2) into it
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_barrier" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
         // straight-line phases (no per-iteration mask switch: one loop body
         // per phase keeps the register assignment of O / S / P stable)
         const int t_a = max(0, min(nt - 1, t_mask - 1));  // iterations [0, t_a) need no mask
@@ -427,22 +431,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_w4(
 // and the number of waves, read back by pli_debug_w4_stamps
 __device__ unsigned long long g_w4_stamps[8];
 
-// DMAPH: where the 8 LDS-DMA pieces of a tile go (0: all in phase 1, 1: K in
-// phase 1 / V in phase 2, 2: all in phase 2).  RECOMP: the per-lane DMA
-// offsets are recomputed per piece from two opaque registers instead of being
-// held (8 VGPRs that the full register file otherwise spills).
-// INPIN: each softmax chunk also pins its INPUTS on entry (empty volatile asm
-// after the preceding MFMA), so hipcc cannot hoist the chunk above that MFMA
-// and issue two MFMAs back to back (the second one then blocks the wave's
-// issue for a whole MFMA slot with no filler beside it).
-// DIAG (timing experiments only, wrong results): 1 = row sums as f32 adds of
-// the unrounded P (no v_dot2c), 2 = no K/V DMA inside the tile loop.
-// INPIN 2: the entry fence is __builtin_amdgcn_sched_barrier(0) instead of an
-// empty asm that (re)defines the inputs -- hipcc pads every VALU that reads a
-// register defined by the inline asm just before it with s_nop 0 (its
-// dst-forwarding hazard rule assumes any asm may be a 16-bit dst-sel write).
-template <typename T, int PD, bool STAMP = false, int DMAPH = 0, bool RECOMP = false,
-          int INPIN = 0, int DIAG = 0>
+template <typename T, int PD, bool STAMP = false>
 __global__ __launch_bounds__(256, 1) void attn_fwd_w4p(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
     const uint16_t* __restrict__ v, uint16_t* __restrict__ o, int H, int group,
@@ -497,22 +486,8 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_w4p(
         koff[i] = (uint32_t)(drow * (int)st.kn + 8 * ch) * 2u;
         voff[i] = (uint32_t)(drow * (int)st.vn + 8 * ch) * 2u;
     }
-    // RECOMP: drow = 16 wave + 4 i + (lane >> 4) gives w4_fsw(drow) =
-    // ((lane >> 4) << 2) | i, so chunk = cb ^ i with cb = (lane & 15) ^
-    // ((lane >> 4) << 2); row 4 i moves into the (scalar) tile base
-    uint32_t rk = (uint32_t)((16 * wave + (lane >> 4)) * (int)st.kn) * 2u;
-    uint32_t rv = (uint32_t)((16 * wave + (lane >> 4)) * (int)st.vn) * 2u;
-    uint32_t cb = (uint32_t)((lane & 15) ^ ((lane >> 4) << 2));
     auto dma_piece = [&](bool is_v, int i, int t, int img) {
         const int64_t sn = is_v ? st.vn : st.kn;
-        if constexpr (RECOMP) {
-            const uint16_t* tb = (is_v ? vp : kp) + ((int64_t)t * KT + 4 * i) * sn;
-            const uint32_t ob = (is_v ? rv : rk) + ((cb ^ (uint32_t)i) << 4);
-            const uint32_t m0v = w4_lds_addr(smem + img * W4_IMG + (4 * wave + i) * 1024);
-            asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
-                         :: "s"(m0v), "v"(ob), "s"(tb) : "memory", "m0");
-            return;
-        }
         const uint16_t* tb = (is_v ? vp : kp) + (int64_t)t * KT * sn;
         const uint32_t ob = is_v ? voff[i] : koff[i];
         const uint32_t m0v = w4_lds_addr(smem + img * W4_IMG + (4 * wave + i) * 1024);
@@ -558,14 +533,6 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_w4p(
         constexpr bool MASK = decltype(mask_tag)::value;
         constexpr int X = decltype(set_tag)::value;
         f32x16 (&s)[2] = sc[X][r];
-        if constexpr (INPIN == 2) {
-            __builtin_amdgcn_sched_barrier(0);
-        } else if constexpr (INPIN) {
-            if (k == 0) w4_pin(s[0], s[1]);
-            else if (k < 5) w4_pin(ch[r][0], ch[r][1], ch[r][2], ch[r][3]);
-            else if (k == 5) w4_pin(mxv[r]);
-            else w4_pin(s[0]);
-        }
         if (k == 0) {
             if constexpr (MASK) {
                 const int last = causal ? min(q0 + 32 * r + l32 + off_diag, Nk - 1) : Nk - 1;
@@ -611,13 +578,6 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_w4p(
     auto finish_chunk = [&](auto set_tag, int r, int k) {
         constexpr int X = decltype(set_tag)::value;
         f32x16 (&s)[2] = sc[X][r];
-        if constexpr (INPIN == 2) {
-            __builtin_amdgcn_sched_barrier(0);
-        } else if constexpr (INPIN) {
-            if (k < 8) w4_pin(s[1]);
-            else if (k == 8) w4_pin(s[0]);
-            else w4_pin(s[(k - 8) >> 2], rsa[r], rsb[r]);
-        }
         if (k < 8) {  // exps of scores 16 + 2k, +1 (tt = 1), in place
             const int e0 = 2 * k;
             s[1][e0] = __builtin_amdgcn_exp2f(fmaf(s[1][e0], c, -m_run[r]));
@@ -632,13 +592,8 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_w4p(
                 const int w = w0 + u, cpn = w & 3, e = 2 * (w & 7);
                 const uint32_t pw = pack2<T>(s[tt][e], s[tt][e + 1]);
                 pk[r][tt][s2][cpn] = (int)pw;
-                if constexpr (DIAG == 1) {
-                    if (u == 0) rsa[r] = rsa[r] + s[tt][e] + s[tt][e + 1];
-                    else rsb[r] = rsb[r] + s[tt][e] + s[tt][e + 1];
-                } else {
-                    if (u == 0) rsa[r] = add_pair<T>(pw, rsa[r]);
-                    else rsb[r] = add_pair<T>(pw, rsb[r]);
-                }
+                if (u == 0) rsa[r] = add_pair<T>(pw, rsa[r]);
+                else rsb[r] = add_pair<T>(pw, rsb[r]);
             }
             asm volatile("" : "+v"(pk[r][tt][s2]), "+v"(rsa[r]), "+v"(rsb[r]));
             if (k == 15) l_run[r] = fmaf(l_run[r], alpha[r], rsa[r] + rsb[r]);
@@ -650,18 +605,20 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_w4p(
         constexpr int Y = decltype(set_tag)::value;
         const int kab = kimg * W4_IMG + A0;
         i32x4 fr[16];
+        auto ftt = [](int f) { return f >> 3; };
+        auto fkk = [](int f) { return f & 7; };
 #pragma unroll
         for (int f = 0; f < 16; ++f) {
             if (f == 0) {
 #pragma unroll
                 for (int p2 = 0; p2 < PD; ++p2)
-                    fr[p2] = lds_read_b128(smem, (kab ^ ((p2 & 7) << 5)) + (p2 >> 3) * 8192);
+                    fr[p2] = lds_read_b128(smem, (kab ^ (fkk(p2) << 5)) + ftt(p2) * 8192);
             }
             if (f + PD < 16) {
                 const int fn = f + PD;
-                fr[fn] = lds_read_b128(smem, (kab ^ ((fn & 7) << 5)) + (fn >> 3) * 8192);
+                fr[fn] = lds_read_b128(smem, (kab ^ (fkk(fn) << 5)) + ftt(fn) * 8192);
             }
-            const int tt = f >> 3, kk = f & 7;
+            const int tt = ftt(f), kk = fkk(f);
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
                 if (kk == 0) w4_mfma_v0<T>(sc[Y][r][tt], fr[f], qf[r][kk]);
@@ -726,23 +683,17 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_w4p(
         // opaque per iteration: recompute addresses instead of holding hoisted
         // 64-bit pointers (the register file is full)
         asm volatile("" : "+v"(A0), "+v"(B0));
-        if constexpr (RECOMP) asm volatile("" : "+v"(rk), "+v"(rv), "+v"(cb));
         // K(t+2) -> image t&1 (held K(t)), V(t+1) -> image 2+((t+1)&1) (held
         // V(t-1)); past the last tile the source is clamped (a harmless refill
         // of an image nobody reads again)
         const int tk = min(t + 2, tl), tv = min(t + 1, tl);
         // phase 1: QK^T(t+1) || finish(t); DMA pieces one every 4 MFMAs
         auto piece = [&](int pc) {  // 0-3 K(t+2), 4-7 V(t+1)
-            if constexpr (DIAG == 2) return;
             dma_piece(pc >= 4, pc & 3, pc >= 4 ? tv : tk, pc >= 4 ? 2 + ((t + 1) & 1) : (t & 1));
         };
         auto w1 = [&](int j) {
             finish_chunk(set_x, j & 1, j >> 1);
-            if constexpr (DMAPH == 0) {
-                if ((j & 3) == 1) piece(j >> 2);
-            } else if constexpr (DMAPH == 1) {
-                if ((j & 7) == 1) piece(j >> 3);
-            }
+            if ((j & 3) == 1) piece(j >> 2);
         };
         stamp(3);
         if constexpr (NEXT) {
@@ -772,11 +723,6 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_w4p(
         auto w2 = [&](int j) {
             if constexpr (NEXT) {
                 if (j < 28) start_chunk(mask_tag, set_y, j & 1, j >> 1, t + 1);
-            }
-            if constexpr (DMAPH == 1) {
-                if ((j & 7) == 3) piece(4 + (j >> 3));
-            } else if constexpr (DMAPH == 2) {
-                if ((j & 3) == 3) piece(j >> 2);
             }
         };
         phase_pv(2 + (t & 1), w2);
@@ -811,6 +757,10 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_w4p(
 #pragma unroll
             for (int j = 0; j < 28; ++j) start_chunk(N, S0, j & 1, j >> 1, 0);
         }
+        // every wave has read K(0) (image 0) before iteration 0 DMAs K(2) into it
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_barrier" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
         stamp(4);
         // iterations: pairs (even t: X = 0, odd t: X = 1); the mask-free phase first
         const int t_a = max(0, min(nt - 1, t_mask - 1));
@@ -888,28 +838,10 @@ int launch_attn_w4(const void* q, const void* k, const void* v, void* o, int B, 
     do {                                                                                          \
         if (Nk % W4_KT) PLI_W4(TT, 3);                                                            \
         else if (sub == 6) PLI_W4P_L(TT, 3, true);                                                \
-        else if (sub == 7) PLI_W4P_L(TT, 3, false, 1, true);                                      \
-        else if (sub == 8) PLI_W4P_L(TT, 3, false, 2, true);                                      \
-        else if (sub == 9) PLI_W4P_L(TT, 3, false, 0, true);                                      \
-        else if (sub == 17) PLI_W4P_L(TT, 3, true, 1, true);                                      \
-        else if (sub == 18) PLI_W4P_L(TT, 3, true, 2, true);                                      \
-        else if (sub == 19) PLI_W4P_L(TT, 3, true, 0, true);                                      \
-        else if (sub == 10) PLI_W4P_L(TT, 3, false, 0, true, true);                               \
-        else if (sub == 12) PLI_W4P_L(TT, 5, false, 0, true, true);                               \
-        else if (sub == 15) PLI_W4P_L(TT, 5, false, 0, true, 2);                                  \
-        else if (sub == 25) PLI_W4P_L(TT, 5, true, 0, true, 2);                                   \
-        else if (sub == 13) PLI_W4P_L(TT, 3, false, 0, true, true, 1);                            \
-        else if (sub == 14) PLI_W4P_L(TT, 3, false, 0, true, true, 2);                            \
-        else if (sub == 22) PLI_W4P_L(TT, 5, true, 0, true, true);                                \
-        else if (sub == 23) PLI_W4P_L(TT, 3, true, 0, true, true, 1);                             \
-        else if (sub == 24) PLI_W4P_L(TT, 3, true, 0, true, true, 2);                             \
-        else if (sub == 11) PLI_W4P_L(TT, 3, false, 1, true, true);                               \
-        else if (sub == 20) PLI_W4P_L(TT, 3, true, 0, true, true);                                \
-        else if (sub == 21) PLI_W4P_L(TT, 3, true, 1, true, true);                                \
         else PLI_W4P_L(TT, PD);                                                                   \
     } while (0)
     if (sub >= 3) {  // two-phase shared-fragment form, fragments 2 / 3 / 4 ahead (6: 3 + stamps)
-        const int pd = sub >= 6 ? 3 : sub - 1;
+        const int pd = sub == 6 ? 3 : sub - 1;
         if (is_bf16) {
             if (pd == 2) PLI_W4P(bf16_t, 2);
             else if (pd == 3) PLI_W4P(bf16_t, 3);

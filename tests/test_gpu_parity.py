@@ -105,7 +105,8 @@ def test_flash_vs_oracle(case):
 
 
 # every MFMA variant (alternates A/B-tested by tools/tune.py) on the MFMA-eligible cases
-MFMA_VARIANTS = (0, 1, 2, 3, 8, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 27, 28, 29, 30, 31, 40, 41, 42, 43, 44, 45)
+MFMA_VARIANTS = (0, 1, 2, 3, 8, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 27, 28, 29, 30, 31, 40, 41, 42, 43, 44,
+                 45, 46)
 
 
 

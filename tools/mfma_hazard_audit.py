@@ -11,6 +11,7 @@ hipcc does not model an MFMA written as inline asm (cdna_hip_programming.md
          NPASS+4 instructions (8-pass 32x32x16: 12 wait states)
   * WAW  non-MFMA write of an MFMA dest within the same window
   * WAR  non-MFMA write of an MFMA C (accumulator) operand within the window
+  * WAR  non-MFMA write of an MFMA A/B operand within WINDOW_AB states
 
 Branches break the linear order, so this is a heuristic: it is conservative
 inside straight-line code (every wait state is counted as one instruction;
@@ -25,6 +26,7 @@ import sys
 
 REG = re.compile(r"\b([va])\[(\d+):(\d+)\]|\b([va])(\d+)\b")
 WINDOW_D = 12
+WINDOW_AB = 8  # A/B operand reads of an 8-pass MFMA assumed spread over its first passes
 
 
 def regs(tok: str) -> set:
@@ -110,6 +112,9 @@ def audit(lines, name):
                 issues.append((i, f"WAW {op} D -> {pop} {ws} states"))
             if w & c and not (w & d):
                 issues.append((i, f"WAR {op} C <- {pop} {ws} states"))
+            ab = set().union(*(regs(o) for o in ops[1:3])) if len(ops) > 2 else set()
+            if w & ab and ws < WINDOW_AB:
+                issues.append((i, f"WAR {op} A/B <- {pop} ({sorted(w & ab)[:2]}) {ws} states"))
             ws += states(pop, pops)
     for i, msg in issues:
         print(f"{name}: line {lineno[i]} (kernel-relative): {msg}")

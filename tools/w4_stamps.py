@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Cycle anatomy of attn_fwd_w4p from its s_memtime-stamped build (flash
-variants 46, 57-59) at the bench config: per wave, per 64-key tile, the shader cycles
+variant 46) at the bench config: per wave, per 64-key tile, the shader cycles
 of phase 1 (QK^T || softmax finish), between phases (rescale + hazard pad),
 phase 2 (PV || softmax start) and the barrier (vmcnt(0) + s_barrier), plus
 prologue / epilogue per wave.  Also times variants 44 and 46 with events."""
@@ -21,7 +21,7 @@ B, H, S, D = 8, 32, 4096, 128
 q, k, v = (torch.randn(B, H, S, D, device="cuda", dtype=torch.bfloat16, generator=g) for _ in range(3))
 o = torch.empty_like(q)
 buf = (ctypes.c_ulonglong * 8)()
-STAMPED = {46, 57, 58, 59, 60, 61, 62, 63, 64, 65}
+STAMPED = {46}
 for var in [int(a) for a in sys.argv[1:]] or [44, 46]:
     for _ in range(3):
         pli_hip.flash_attn_fwd(q, k, v, out=o, variant=var)
