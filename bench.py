@@ -304,8 +304,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # PLI_BENCH_BACKEND=gloo rehearses the multi-rank path on a box with
+        # fewer GPUs than ranks (ranks share devices round-robin); the driver's
+        # runs use the default, RCCL ("nccl") with one rank per GPU
+        backend = os.environ.get("PLI_BENCH_BACKEND", "nccl")
+        dev = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group(backend, device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
     import pli_hip
     assert pli_hip.available(), "libpli_hip.so must be built and a ROCm device visible"
 
