@@ -94,6 +94,19 @@ int pli_gemm(const void* a, const void* b, void* c, const void* bias, int m,
              int dtype, void* stream);
 
 /*
+ * pli_gemm with a caller-owned device workspace (16-byte aligned) of at least
+ * pli_gemm_workspace_size(m, n, k, trans_b, dtype) bytes (0: none needed, the
+ * call is pli_gemm).  Decode-batch / TP-shard NT shapes (16 < m <= 256) then
+ * split K over workgroups and sum the fp32 slices in a fixed order (the
+ * ch09/tensor_parallel.py:67 row shard at M = 128, ch03/batching_benchmark.py
+ * batches).  The workspace is scratch: nothing persists between calls.
+ */
+size_t pli_gemm_workspace_size(int m, int n, int k, int trans_b, int dtype);
+int pli_gemm_ws(const void* a, const void* b, void* c, const void* bias, int m,
+                int n, int k, int64_t lda, int64_t ldb, int64_t ldc, int trans_b,
+                int dtype, void* workspace, size_t workspace_bytes, void* stream);
+
+/*
  * Fused SwiGLU projection  h[m, n] = silu(x Wg^T)[m, n] * (x Wu^T)[m, n]
  * (fp32 accumulate, silu(g) = g / (1 + e^-g)).
  * Replaces gate_proj -> silu, up_proj, multiply of

@@ -1179,6 +1179,406 @@ int launch_smallm(const void* a, const void* b, void* c, const void* bias, int M
     return launch_status("gemm_smallm_nt");
 }
 
+// ---------------------------------------------------------------------------
+// Mid-M NT path (batched decode / TP shards at M ~ 32-256: the ch09 row shard
+// at M = 128): C^T[32 W rows][<= 128 X rows] per workgroup on
+// v_mfma_f32_32x32x16.  The workgroup's 32 weight rows are streamed from HBM
+// exactly once (non-temporal), split over the 4 waves in K; every lane loads
+// its MFMA fragments straight from global memory (W row n0 + l%32, X row
+// m + l%32, 16 B at k + 8(l/32)), two 64-k steps in flight per wave, and the
+// four K partials are summed through LDS.  N/32 workgroups (256 at N = 8192):
+// X (the small operand) is re-read from L2 once per workgroup, half the L2
+// traffic of the 16-row small-M kernel, which is what bounds that kernel at
+// M = 128.  grid.y walks 128-row slabs of X for M > 128.
+template <typename T, int MC, bool BIAS>
+__global__ __launch_bounds__(256) void gemm_midm_nt(const uint16_t* __restrict__ X,
+                                                    const uint16_t* __restrict__ W,
+                                                    uint16_t* __restrict__ C,
+                                                    const uint16_t* __restrict__ bias, int M,
+                                                    int N, int K, int64_t ldx, int64_t ldw,
+                                                    int64_t ldc) {
+    __shared__ __attribute__((aligned(16))) float part[4][MC][16][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int l32 = lane & 31, h32 = lane >> 5;
+    const int n0 = blockIdx.x * 32, m0 = blockIdx.y * 128;
+    const int kw = K / 4;  // this wave's K range: [wave * kw, (wave + 1) * kw)
+    const uint16_t* wp = W + (int64_t)min(n0 + l32, N - 1) * ldw + wave * kw + 8 * h32;
+    const uint16_t* xp[MC];
+#pragma unroll
+    for (int mc = 0; mc < MC; ++mc)
+        xp[mc] = X + (int64_t)min(m0 + 32 * mc + l32, M - 1) * ldx + wave * kw + 8 * h32;
+    f32x16 acc[MC];
+#pragma unroll
+    for (int mc = 0; mc < MC; ++mc)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[mc][e] = 0.f;
+
+    i32x4 wf[2][4], xf[2][MC][4];
+    auto load = [&](int b, int k0) {
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+            wf[b][s2] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wp + k0 + 16 * s2));
+#pragma unroll
+            for (int mc = 0; mc < MC; ++mc)
+                xf[b][mc][s2] = *reinterpret_cast<const i32x4*>(xp[mc] + k0 + 16 * s2);
+        }
+    };
+    auto compute = [&](int b) {
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+            for (int mc = 0; mc < MC; ++mc)
+                acc[mc] = mfma32x32x16<T>(wf[b][s2], xf[b][mc][s2], acc[mc]);
+    };
+    const int steps = kw / 64;  // host guarantees K % 256 == 0, steps >= 1
+    load(0, 0);
+    int st = 0;
+    for (; st + 2 <= steps; st += 2) {
+        load(1, (st + 1) * 64);
+        compute(0);
+        if (st + 2 < steps) load(0, (st + 2) * 64);
+        compute(1);
+    }
+    if (st < steps) compute(0);
+
+    // acc[mc][r] = C[m][n]: m = m0 + 32 mc + l32, n = n0 + 8 (r >> 2) + 4 h32 + (r & 3)
+#pragma unroll
+    for (int mc = 0; mc < MC; ++mc)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) part[wave][mc][r][lane] = acc[mc][r];
+    __syncthreads();
+    for (int mc = wave; mc < MC; mc += 4) {
+        const int m = m0 + 32 * mc + l32;
+        if (m >= M) continue;
+        uint16_t* crow = C + (int64_t)m * ldc;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int n = n0 + 8 * q + 4 * h32;
+            if (n >= N) continue;
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = 4 * q + r;
+                v[r] = part[0][mc][i][lane] + part[1][mc][i][lane] + part[2][mc][i][lane] +
+                       part[3][mc][i][lane];
+                if constexpr (BIAS) v[r] += elem<T>::to_f32(T{bias[n + r]});
+            }
+            *reinterpret_cast<i32x2*>(crow + n) = i32x2{(int)pack2<T>(v[0], v[1]), (int)pack2<T>(v[2], v[3])};
+        }
+    }
+}
+
+template <typename T>
+int launch_midm(const void* a, const void* b, void* c, const void* bias, int M, int N, int K,
+                int64_t lda, int64_t ldb, int64_t ldc, hipStream_t s) {
+    const dim3 grid(cdiv(N, 32), cdiv(M, 128)), block(256);
+    const int mc = cdiv(min(M, 128), 32);
+#define PLI_MIDM(MCC)                                                                          \
+    do {                                                                                       \
+        if (bias)                                                                              \
+            hipLaunchKernelGGL((gemm_midm_nt<T, MCC, true>), grid, block, 0, s,                \
+                               (const uint16_t*)a, (const uint16_t*)b, (uint16_t*)c,           \
+                               (const uint16_t*)bias, M, N, K, lda, ldb, ldc);                 \
+        else                                                                                   \
+            hipLaunchKernelGGL((gemm_midm_nt<T, MCC, false>), grid, block, 0, s,               \
+                               (const uint16_t*)a, (const uint16_t*)b, (uint16_t*)c,           \
+                               (const uint16_t*)bias, M, N, K, lda, ldb, ldc);                 \
+    } while (0)
+    if (mc == 1) PLI_MIDM(1);
+    else if (mc == 2) PLI_MIDM(2);
+    else if (mc == 3) PLI_MIDM(3);
+    else PLI_MIDM(4);
+#undef PLI_MIDM
+    return launch_status("gemm_midm_nt");
+}
+
+// ---------------------------------------------------------------------------
+// Split-K mid-M NT path (caller workspace; pli_gemm_ws): workgroup = (128
+// weight rows, one K slice, one 128-row slab of X).  Wave w streams weight
+// rows n0 + 32 w .. +31 over the slice (non-temporal, exactly once) and all
+// MC 32-row chunks of X; the four waves load the SAME X fragments, so X is
+// fetched from L2 once per workgroup and shared through the CU's L1 -- a
+// quarter of the X traffic of gemm_midm_nt, which is what bounds the M ~ 128
+// shapes.  KS slices fill the chip (N/128 x KS ~ 256 workgroups); each slice
+// writes an fp32 partial C tile (16-B stores) to ws[ks][m][n] and
+// gemm_splitk_reduce sums them in fixed order (deterministic) into C (+ bias).
+// KS == 1 writes C directly.
+template <typename T, int MC, bool PARTIAL, bool BIAS>
+__global__ __launch_bounds__(256) void gemm_splitk_nt(const uint16_t* __restrict__ X,
+                                                      const uint16_t* __restrict__ W,
+                                                      uint16_t* __restrict__ C,
+                                                      float* __restrict__ ws,
+                                                      const uint16_t* __restrict__ bias, int M,
+                                                      int N, int K, int kslice, int64_t ldx,
+                                                      int64_t ldw, int64_t ldc) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int l32 = lane & 31, h32 = lane >> 5;
+    const int nw = blockIdx.x * 128 + wave * 32;  // this wave's first weight row
+    const int ks = blockIdx.y, m0 = blockIdx.z * 128;
+    const int kb = ks * kslice;
+    const uint16_t* wp = W + (int64_t)min(nw + l32, N - 1) * ldw + kb + 8 * h32;
+    const uint16_t* xp[MC];
+#pragma unroll
+    for (int mc = 0; mc < MC; ++mc)
+        xp[mc] = X + (int64_t)min(m0 + 32 * mc + l32, M - 1) * ldx + kb + 8 * h32;
+    f32x16 acc[MC];
+#pragma unroll
+    for (int mc = 0; mc < MC; ++mc)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[mc][e] = 0.f;
+
+    i32x4 wf[2][4], xf[2][MC][4];
+    auto load = [&](int b, int k0) {
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+            wf[b][s2] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wp + k0 + 16 * s2));
+#pragma unroll
+            for (int mc = 0; mc < MC; ++mc)
+                xf[b][mc][s2] = *reinterpret_cast<const i32x4*>(xp[mc] + k0 + 16 * s2);
+        }
+    };
+    auto compute = [&](int b) {
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+            for (int mc = 0; mc < MC; ++mc)
+                acc[mc] = mfma32x32x16<T>(wf[b][s2], xf[b][mc][s2], acc[mc]);
+    };
+    const int steps = kslice / 64;  // host: kslice % 64 == 0, >= 64
+    load(0, 0);
+    int st = 0;
+    for (; st + 2 <= steps; st += 2) {
+        load(1, (st + 1) * 64);
+        compute(0);
+        if (st + 2 < steps) load(0, (st + 2) * 64);
+        compute(1);
+    }
+    if (st < steps) compute(0);
+
+    // acc[mc][4q + r] = C[m][n]: m = m0 + 32 mc + l32, n = nw + 8 q + 4 h32 + r
+    if (nw >= N) return;
+#pragma unroll
+    for (int mc = 0; mc < MC; ++mc) {
+        const int m = m0 + 32 * mc + l32;
+        if (m >= M) continue;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int n = nw + 8 * q + 4 * h32;
+            if constexpr (PARTIAL) {
+                *reinterpret_cast<f32x4*>(ws + ((int64_t)ks * M + m) * N + n) =
+                    f32x4{acc[mc][4 * q], acc[mc][4 * q + 1], acc[mc][4 * q + 2], acc[mc][4 * q + 3]};
+            } else {
+                float v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    v[r] = acc[mc][4 * q + r];
+                    if constexpr (BIAS) v[r] += elem<T>::to_f32(T{bias[n + r]});
+                }
+                *reinterpret_cast<i32x2*>(C + (int64_t)m * ldc + n) =
+                    i32x2{(int)pack2<T>(v[0], v[1]), (int)pack2<T>(v[2], v[3])};
+            }
+        }
+    }
+}
+
+// C[m][n] = sum_ks ws[ks][m][n] (+ bias): 8 consecutive n per thread
+template <typename T, bool BIAS>
+__global__ __launch_bounds__(256) void gemm_splitk_reduce(const float* __restrict__ ws,
+                                                          uint16_t* __restrict__ C,
+                                                          const uint16_t* __restrict__ bias,
+                                                          int M, int N, int KS, int64_t ldc) {
+    const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+    const int64_t MN = (int64_t)M * N;
+    if (i >= MN) return;
+    const int m = (int)(i / N), n = (int)(i % N);
+    float v[8];
+    {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(ws + i);
+        const f32x4 b = *reinterpret_cast<const f32x4*>(ws + i + 4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { v[r] = a[r]; v[4 + r] = b[r]; }
+    }
+    for (int ks = 1; ks < KS; ++ks) {
+        const f32x4 a = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(ws + ks * MN + i));
+        const f32x4 b = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(ws + ks * MN + i + 4));
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { v[r] += a[r]; v[4 + r] += b[r]; }
+    }
+    if constexpr (BIAS) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) v[r] += elem<T>::to_f32(T{bias[n + r]});
+    }
+    *reinterpret_cast<i32x4*>(C + (int64_t)m * ldc + n) =
+        i32x4{(int)pack2<T>(v[0], v[1]), (int)pack2<T>(v[2], v[3]), (int)pack2<T>(v[4], v[5]),
+              (int)pack2<T>(v[6], v[7])};
+}
+
+// LDS-staged form of gemm_splitk_nt (variant 25): each 64-k step of the
+// workgroup's 128 weight rows and MC*32 X rows arrives by LDS-DMA as whole
+// 128-B row segments (1 KiB = 8 rows per wave-instruction, chunk XOR-swizzled
+// on the source address, g2_off_rows), double-buffered, and the MFMA
+// fragments come back by ds_read_b128 -- the direct-load kernel touches 32
+// half-lines per load instruction, which caps it far below HBM rate.
+template <typename T, int MC, bool PARTIAL, bool BIAS>
+__global__ __launch_bounds__(256) void gemm_splitk_lds_nt(const uint16_t* __restrict__ X,
+                                                          const uint16_t* __restrict__ W,
+                                                          uint16_t* __restrict__ C,
+                                                          float* __restrict__ ws,
+                                                          const uint16_t* __restrict__ bias, int M,
+                                                          int N, int K, int kslice, int64_t ldx,
+                                                          int64_t ldw, int64_t ldc) {
+    constexpr int WIMG = 128 * 128, XIMG = MC * 32 * 128, BUF = WIMG + XIMG;
+    __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int l32 = lane & 31, h32 = lane >> 5;
+    const int n0 = blockIdx.x * 128, nw = n0 + wave * 32;
+    const int ks = blockIdx.y, m0 = blockIdx.z * 128;
+    const int kb = ks * kslice;
+    // DMA pieces of this wave: W rows 32 w + 8 i + (lane >> 3), i < 4; X rows
+    // 8 j + (lane >> 3) for pieces j = w, w + 4, .. < 4 MC
+    const int prow = lane >> 3, slot = lane & 7;
+    const uint16_t* wsrc[4];
+    int wdst[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int row = wave * 32 + 8 * i + prow;
+        wsrc[i] = W + (int64_t)min(n0 + row, N - 1) * ldw + kb + 8 * (slot ^ ((row >> 1) & 7));
+        wdst[i] = (wave * 4 + i) * 1024;
+    }
+    const uint16_t* xsrc[MC];
+    int xdst[MC];
+#pragma unroll
+    for (int j = 0; j < MC; ++j) {
+        const int piece = wave + 4 * j, row = 8 * piece + prow;
+        xsrc[j] = X + (int64_t)min(m0 + row, M - 1) * ldx + kb + 8 * (slot ^ ((row >> 1) & 7));
+        xdst[j] = WIMG + piece * 1024;
+    }
+    auto issue = [&](int buf, int k0) {
+        char* base = smem + buf * BUF;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(wsrc[i] + k0),
+                                             (__attribute__((address_space(3))) void*)(base + wdst[i]), 16, 0, 0);
+#pragma unroll
+        for (int j = 0; j < MC; ++j)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(xsrc[j] + k0),
+                                             (__attribute__((address_space(3))) void*)(base + xdst[j]), 16, 0, 0);
+    };
+    f32x16 acc[MC];
+#pragma unroll
+    for (int mc = 0; mc < MC; ++mc)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[mc][e] = 0.f;
+
+    const int steps = kslice / 64;
+    issue(0, 0);
+    for (int st = 0; st < steps; ++st) {
+        const int buf = st & 1;
+        if (st + 1 < steps) {
+            issue(buf ^ 1, (st + 1) * 64);
+            if constexpr (MC == 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+            else if constexpr (MC == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+            else if constexpr (MC == 3) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();  // every wave's pieces of step st have landed
+        const char* base = smem + buf * BUF;
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+            const i32x4 wfr = lds_read_b128(base, g2_off_rows(wave * 32 + l32, 2 * s2 + h32));
+#pragma unroll
+            for (int mc = 0; mc < MC; ++mc) {
+                const i32x4 xfr = lds_read_b128(base + WIMG, g2_off_rows(mc * 32 + l32, 2 * s2 + h32));
+                acc[mc] = mfma32x32x16<T>(wfr, xfr, acc[mc]);
+            }
+        }
+        __syncthreads();  // buffer buf is refilled by the DMA issued next step
+    }
+
+    if (nw >= N) return;
+#pragma unroll
+    for (int mc = 0; mc < MC; ++mc) {
+        const int m = m0 + 32 * mc + l32;
+        if (m >= M) continue;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int n = nw + 8 * q + 4 * h32;
+            if constexpr (PARTIAL) {
+                *reinterpret_cast<f32x4*>(ws + ((int64_t)ks * M + m) * N + n) =
+                    f32x4{acc[mc][4 * q], acc[mc][4 * q + 1], acc[mc][4 * q + 2], acc[mc][4 * q + 3]};
+            } else {
+                float v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    v[r] = acc[mc][4 * q + r];
+                    if constexpr (BIAS) v[r] += elem<T>::to_f32(T{bias[n + r]});
+                }
+                *reinterpret_cast<i32x2*>(C + (int64_t)m * ldc + n) =
+                    i32x2{(int)pack2<T>(v[0], v[1]), (int)pack2<T>(v[2], v[3])};
+            }
+        }
+    }
+}
+
+// K slices for the split-K mid-M path: the largest power of two with
+// cdiv(N,128) * cdiv(M,128) * KS <= target workgroups, slices of >= 256 and a
+// multiple of 64.  0: the path does not apply.
+inline int splitk_slices(int M, int N, int K, int target) {
+    if (M <= 16 || M > 256 || N % 32 != 0 || K % 64 != 0 || K < 64) return 0;
+    const int64_t tiles = (int64_t)cdiv(N, 128) * cdiv(M, 128);
+    int ks = 1;
+    while (tiles * ks * 2 <= target && K % (ks * 2 * 64) == 0 && K / (ks * 2) >= 256) ks *= 2;
+    return ks;
+}
+
+template <typename T>
+int launch_splitk(const void* a, const void* b, void* c, const void* bias, int M, int N, int K,
+                  int64_t lda, int64_t ldb, int64_t ldc, int ks, float* ws, hipStream_t s,
+                  bool lds = false) {
+    const dim3 grid(cdiv(N, 128), ks, cdiv(M, 128)), block(256);
+    const int mc = cdiv(min(M, 128), 32);
+    const int kslice = K / ks;
+#define PLI_SK(MCC, PA, BI)                                                                     \
+    do {                                                                                        \
+        if (lds)                                                                                \
+            hipLaunchKernelGGL((gemm_splitk_lds_nt<T, MCC, PA, BI>), grid, block, 0, s,           \
+                               (const uint16_t*)a, (const uint16_t*)b, (uint16_t*)c, ws,        \
+                               (const uint16_t*)bias, M, N, K, kslice, lda, ldb, ldc);          \
+        else                                                                                    \
+            hipLaunchKernelGGL((gemm_splitk_nt<T, MCC, PA, BI>), grid, block, 0, s,               \
+                               (const uint16_t*)a, (const uint16_t*)b, (uint16_t*)c, ws,        \
+                               (const uint16_t*)bias, M, N, K, kslice, lda, ldb, ldc);          \
+    } while (0)
+#define PLI_SK_MC(PA, BI)                   \
+    do {                                    \
+        if (mc == 1) PLI_SK(1, PA, BI);     \
+        else if (mc == 2) PLI_SK(2, PA, BI); \
+        else if (mc == 3) PLI_SK(3, PA, BI); \
+        else PLI_SK(4, PA, BI);             \
+    } while (0)
+    if (ks > 1) {
+        PLI_SK_MC(true, false);
+        const int rc = launch_status("gemm_splitk_nt");
+        if (rc) return rc;
+        const int64_t groups = ((int64_t)M * N) / 8;
+        const dim3 rgrid((unsigned)cdiv((int)((groups + 255) / 256 * 256), 256));
+        if (bias)
+            hipLaunchKernelGGL((gemm_splitk_reduce<T, true>), rgrid, dim3(256), 0, s, ws, (uint16_t*)c,
+                               (const uint16_t*)bias, M, N, ks, ldc);
+        else
+            hipLaunchKernelGGL((gemm_splitk_reduce<T, false>), rgrid, dim3(256), 0, s, ws, (uint16_t*)c,
+                               (const uint16_t*)bias, M, N, ks, ldc);
+        return launch_status("gemm_splitk_reduce");
+    }
+    if (bias) PLI_SK_MC(false, true);
+    else PLI_SK_MC(false, false);
+#undef PLI_SK_MC
+#undef PLI_SK
+    return launch_status("gemm_splitk_nt");
+}
+
 template <typename T>
 int launch_mfma(const void* a, const void* b, void* c, const void* bias, int M, int N, int K,
                 int64_t lda, int64_t ldb, int64_t ldc, int trans_b, hipStream_t s) {
@@ -1356,9 +1756,54 @@ extern "C" int pli_gemm_swiglu(const void* x, const void* wg, const void* wu, vo
 // its MFMA clusters, 5-8 = phased SCHED 1/3/5/7, 9-11 = one-phase with
 // group_m 4/8/16, 12-15 = phased SCHED 7 with group_m 8/4/2/16 (where their
 // shape conditions hold)
+namespace pli {
+namespace {
+// split-K target workgroups by variant (0: default 256; 22: 512; 24: 128)
+inline int splitk_target(int variant) {
+    return (variant == 0 || variant == 22 || variant == 26) ? 512
+           : (variant == 24 || variant == 27)             ? 128
+                                                          : 256;
+}
+inline bool splitk_variant(int v) { return v == 0 || v == 22 || v == 24 || (v >= 25 && v <= 27); }
+}  // namespace
+}  // namespace pli
+
+extern "C" size_t pli_gemm_workspace_size(int m, int n, int k, int trans_b, int dtype) {
+    using namespace pli;
+    if (!trans_b || (dtype != PLI_BF16 && dtype != PLI_F16) || m <= 0 || n <= 0 || k <= 0) return 0;
+    const int ks = splitk_slices(m, n, k, splitk_target(22));  // the largest any variant uses
+    return ks > 1 ? (size_t)ks * m * n * sizeof(float) : 0;
+}
+
+static int gemm_dispatch(const void* a, const void* b, void* c, const void* bias, int m, int n,
+                         int k, int64_t lda, int64_t ldb, int64_t ldc, int trans_b, int dtype,
+                         void* stream, int variant, void* ws, size_t ws_bytes);
+
 extern "C" int pli_gemm_variant(const void* a, const void* b, void* c, const void* bias, int m,
                                 int n, int k, int64_t lda, int64_t ldb, int64_t ldc, int trans_b,
                                 int dtype, void* stream, int variant) {
+    return gemm_dispatch(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, dtype, stream, variant,
+                         nullptr, 0);
+}
+
+extern "C" int pli_gemm_ws(const void* a, const void* b, void* c, const void* bias, int m, int n,
+                           int k, int64_t lda, int64_t ldb, int64_t ldc, int trans_b, int dtype,
+                           void* workspace, size_t workspace_bytes, void* stream) {
+    return gemm_dispatch(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, dtype, stream, 0,
+                         workspace, workspace_bytes);
+}
+
+extern "C" int pli_gemm_ws_variant(const void* a, const void* b, void* c, const void* bias, int m,
+                                   int n, int k, int64_t lda, int64_t ldb, int64_t ldc, int trans_b,
+                                   int dtype, void* workspace, size_t workspace_bytes, void* stream,
+                                   int variant) {
+    return gemm_dispatch(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, dtype, stream, variant,
+                         workspace, workspace_bytes);
+}
+
+static int gemm_dispatch(const void* a, const void* b, void* c, const void* bias, int m, int n,
+                         int k, int64_t lda, int64_t ldb, int64_t ldc, int trans_b, int dtype,
+                         void* stream, int variant, void* ws, size_t ws_bytes) {
     using namespace pli;
     clear_error();
     PLI_REQUIRE(a && b && c, "pli_gemm: null pointer");
@@ -1385,6 +1830,31 @@ extern "C" int pli_gemm_variant(const void* a, const void* b, void* c, const voi
         if (dtype == PLI_BF16)
             return launch_skinny<bf16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, s);
         return launch_skinny<f16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, s);
+    }
+    // Decode-batch / TP-shard NT shapes, 16 < M <= 256 (tools/tune.py midm,
+    // profiles/r01/gemm/tune_midm.log).  With a workspace: the LDS-staged
+    // split-K kernel (~ hipBLASLt at M 17-256 for K >= 4096: M 128 x 8192^2
+    // 38.6 us vs 146 on the small-M kernel); short K (<= 2048) at M <= 128 is
+    // better served without splitting: the mid-M kernel for M > 32 (also the
+    // no-workspace route), the small-M kernel below that.
+    // A/B: 22/24 direct-load split-K (512/128 target workgroups), 25/26/27
+    // LDS split-K (256/512/128), 20 mid-M, 21 small-M.
+    const bool short_k = k <= 2048 && m <= 128;
+    if (vec && trans_b && splitk_variant(variant) && ws != nullptr && !(variant == 0 && short_k)) {
+        const int ks = splitk_slices(m, n, k, splitk_target(variant));
+        if (ks >= 1 && (ks == 1 || ws_bytes >= (size_t)ks * m * n * sizeof(float))) {
+            PLI_REQUIRE(((uintptr_t)ws & 15) == 0, "pli_gemm_ws: workspace must be 16-byte aligned");
+            const bool lds = variant == 0 || variant >= 25;
+            if (dtype == PLI_BF16)
+                return launch_splitk<bf16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, ks, (float*)ws, s, lds);
+            return launch_splitk<f16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, ks, (float*)ws, s, lds);
+        }
+    }
+    if (vec && trans_b && k % 256 == 0 &&
+        ((variant == 20 && m <= 256) || (variant == 0 && m > 32 && m <= 128))) {
+        if (dtype == PLI_BF16)
+            return launch_midm<bf16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, s);
+        return launch_midm<f16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, s);
     }
     if (vec && trans_b && m <= 128 && k % 128 == 0 && n % 16 == 0) {
         if (dtype == PLI_BF16)

@@ -36,6 +36,9 @@ _SIGS = {
     "pli_gemv": [_vp, _vp, _vp, _c_int, _c_int, _c_i64, _c_int, _vp],
     "pli_gemm": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_i64, _c_i64, _c_i64, _c_int,
                  _c_int, _vp],
+    "pli_gemm_workspace_size": [_c_int, _c_int, _c_int, _c_int, _c_int],
+    "pli_gemm_ws": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_i64, _c_i64, _c_i64, _c_int,
+                    _c_int, _vp, ctypes.c_size_t, _vp],
     "pli_gemm_swiglu": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_i64, _c_i64, _c_i64,
                         _c_i64, _c_int, _vp],
     "pli_rmsnorm": [_vp, _vp, _vp, _vp, _vp, _c_i64, _c_int, _c_i64, _c_i64, _c_i64, _c_i64,
@@ -67,6 +70,8 @@ _SIGS = {
     "pli_gemv_variant": [_vp, _vp, _vp, _c_int, _c_int, _c_i64, _c_int, _vp, _c_int],
     "pli_gemm_variant": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_i64, _c_i64, _c_i64,
                          _c_int, _c_int, _vp, _c_int],
+    "pli_gemm_ws_variant": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_i64, _c_i64, _c_i64,
+                            _c_int, _c_int, _vp, ctypes.c_size_t, _vp, _c_int],
     "pli_attn_decode_variant": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
                                 ctypes.POINTER(_c_i64), _c_f32, _c_int, _vp, ctypes.c_size_t,
                                 _c_int, _vp, _c_int, _c_int],
@@ -594,13 +599,23 @@ def gemm(a: torch.Tensor, b: torch.Tensor, trans_b: bool = False,
         out = torch.empty((m, n), dtype=a.dtype, device=dev)
     lda = a.stride(0) if m > 1 else k
     ldb = b.stride(0) if b.shape[0] > 1 else b.shape[1]
-    args = (_ptr(a), _ptr(b), _ptr(out), _ptr(bias), m, n, k, max(lda, 1), max(ldb, 1),
-            max(out.stride(0), n), int(bool(trans_b)), _dtype_code(a), _stream(dev))
+    head = (_ptr(a), _ptr(b), _ptr(out), _ptr(bias), m, n, k, max(lda, 1), max(ldb, 1),
+            max(out.stride(0), n), int(bool(trans_b)), _dtype_code(a))
     with _on_device(dev):
-        if variant is None:
-            rc = lib().pli_gemm(*args)
+        # decode-batch NT shapes split K over workgroups through a scratch
+        # workspace from torch's caching allocator (pli_gemm_ws)
+        wsb = lib().pli_gemm_workspace_size(m, n, k, int(bool(trans_b)), _dtype_code(a)) \
+            if variant in (None, 0, 22, 24, 25, 26, 27) else 0
+        if wsb:
+            ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+            if variant is None:
+                rc = lib().pli_gemm_ws(*head, _ptr(ws), wsb, _stream(dev))
+            else:
+                rc = lib().pli_gemm_ws_variant(*head, _ptr(ws), wsb, _stream(dev), int(variant))
+        elif variant is None:
+            rc = lib().pli_gemm(*head, _stream(dev))
         else:
-            rc = lib().pli_gemm_variant(*args, int(variant))
+            rc = lib().pli_gemm_variant(*head, _stream(dev), int(variant))
     _check(rc, "pli_gemm")
     return out
 

@@ -265,6 +265,50 @@ def test_gemm_tile_variants(m, n, k, tb, bias, variant):
     assert_lin_close(out, ref, dt, f"variant {variant}")
 
 
+# decode-batch / TP-shard NT paths, 16 < M <= 256: default route (workspace
+# from the wrapper: LDS split-K, or mid-M / small-M for short K), direct-load
+# split-K (22, 24), LDS split-K (25-27), mid-M (20), small-M (21)
+@pytest.mark.parametrize("variant", [None, 20, 21, 22, 24, 25, 26, 27])
+@pytest.mark.parametrize("m,n,k,dt,bias", [
+    (17, 1024, 4096, "bf16", False),   # one 32-row chunk, 8 n-tiles x 8 slices
+    (64, 512, 8192, "bf16", True),     # long K slices
+    (100, 288, 4096, "fp16", False),   # ragged M chunk, N % 128 != 0 (last tile half empty)
+    (128, 256, 1024, "bf16", True),    # short K: mid-M route by default
+    (200, 640, 2048, "bf16", False),   # two 128-row slabs of X, the second partial
+    (256, 128, 512, "fp16", True),     # one n-tile: slices fill the grid
+])
+def test_gemm_decode_batch_paths(m, n, k, dt, bias, variant):
+    import pli_hip
+    a = seeded_normal((m, k), 7 + m, dt)
+    w = seeded_normal((n, k), 8 + n, dt)
+    bb = seeded_normal((n,), 9, dt) if bias else None
+    out = pli_hip.gemm(dev(a, dt), dev(w, dt), trans_b=True, bias=dev(bb, dt) if bias else None,
+                       variant=variant)
+    assert_lin_close(out, olin.linear(a, w, bb), dt, f"decode-batch gemm {m}x{n}x{k} v{variant}")
+
+
+def test_gemm_ws_abi_direct():
+    """pli_gemm_ws through the C ABI: undersized workspace falls back, a
+    sized one takes the split-K path; both match the oracle."""
+    import ctypes
+    import pli_hip
+    m, n, k = 96, 512, 4096
+    a, w = seeded_normal((m, k), 1, "bf16"), seeded_normal((n, k), 2, "bf16")
+    at, wt = dev(a, "bf16"), dev(w, "bf16")
+    ref = olin.linear(a, w)
+    lib = pli_hip.lib()
+    need = lib.pli_gemm_workspace_size(m, n, k, 1, 2)
+    assert need > 0 and lib.pli_gemm_workspace_size(m, n, k, 0, 2) == 0
+    stream = torch.cuda.current_stream().cuda_stream
+    for wsb in (16, need):
+        ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=DEV)
+        out = torch.empty(m, n, dtype=torch.bfloat16, device=DEV)
+        rc = lib.pli_gemm_ws(at.data_ptr(), wt.data_ptr(), out.data_ptr(), None, m, n, k, k, k, n, 1, 2,
+                             ws.data_ptr(), wsb, ctypes.c_void_p(stream))
+        assert rc == 0, pli_hip.lib().pli_last_error()
+        assert_lin_close(out, ref, "bf16", f"pli_gemm_ws ws={wsb}")
+
+
 @pytest.mark.parametrize("m", [192, 4, 48])
 def test_gemm_bias_epilogue(m):
     import pli_hip

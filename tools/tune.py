@@ -411,6 +411,32 @@ def tune_gemm_shapes():
         print(json.dumps({"kernel": "gemm_shapes", "m": m, "n": n, "k": k, "TFLOP/s": row}), flush=True)
 
 
+def tune_midm():
+    """Decode-batch / TP-shard NT GEMMs at M = 17..256: the split-K path with
+    256 / 512 / 128 target workgroups (0 / 22 / 24, workspace from the
+    wrapper), the mid-M kernel (20), the small-M kernel (21), torch F.linear."""
+    shapes = [(m, n, k) for (n, k) in ((8192, 8192), (4096, 4096), (8192, 1024), (14336, 4096))
+              for m in (17, 32, 64, 128, 256)]
+    if os.environ.get("PLI_GEMM_SHAPES"):
+        shapes = [tuple(int(x) for x in sh.split("x")) for sh in os.environ["PLI_GEMM_SHAPES"].split(",")]
+    for (m, n, k) in shapes:
+        x = torch.randn(m, k, device="cuda", dtype=torch.bfloat16)
+        w = torch.randn(n, k, device="cuda", dtype=torch.bfloat16) * k ** -0.5
+        ref = torch.nn.functional.linear(x.float(), w.float())
+        outs = {v: torch.empty(m, n, device="cuda", dtype=torch.bfloat16) for v in (0, 20, 21, 25, 26, 27)}
+        fns = {f"v{v}": (lambda v=v: pli_hip.gemm(x, w, trans_b=True, out=outs[v], variant=v)) for v in outs}
+        fns["torch"] = lambda: torch.nn.functional.linear(x, w)
+        errs = {}
+        for v in outs:
+            fns[f"v{v}"]()
+            errs[f"v{v}"] = round(((outs[v].float() - ref).abs() / (ref.abs() + 1)).max().item(), 4)
+        t = interleave(fns, 10, int(os.environ.get("PLI_TUNE_ROUNDS", "3")))
+        print(json.dumps({"kernel": "midm", "m": m, "n": n, "k": k,
+                          "us": {kk: round(med * 1e3, 1) for kk, (med, mn) in t.items()},
+                          "weight_TB/s": {kk: round(n * k * 2 / med / 1e9, 2) for kk, (med, mn) in t.items()},
+                          "err": errs}), flush=True)
+
+
 if __name__ == "__main__":
     what = sys.argv[1:] or ["hbm", "gemv", "flash", "gemm"]
     if "hbm" in what:
@@ -428,6 +454,8 @@ if __name__ == "__main__":
         tune_flash(D=64, H=64)
     if "gemm" in what:
         tune_gemm()
+    if "midm" in what:
+        tune_midm()
     if "gemmshapes" in what:
         tune_gemm_shapes()
     if "decode" in what:
