@@ -1525,8 +1525,8 @@ __global__ __launch_bounds__(256) void gemm_splitk_lds_nt(const uint16_t* __rest
 // K slices for the split-K mid-M path: the largest power of two with
 // cdiv(N,128) * cdiv(M,128) * KS <= target workgroups, slices of >= 256 and a
 // multiple of 64.  0: the path does not apply.
-inline int splitk_slices(int M, int N, int K, int target) {
-    if (M <= 16 || M > 256 || N % 32 != 0 || K % 64 != 0 || K < 64) return 0;
+inline int splitk_slices(int M, int N, int K, int target, int max_m = 256) {
+    if (M <= 16 || M > max_m || N % 32 != 0 || K % 64 != 0 || K < 64) return 0;
     const int64_t tiles = (int64_t)cdiv(N, 128) * cdiv(M, 128);
     int ks = 1;
     while (tiles * ks * 2 <= target && K % (ks * 2 * 64) == 0 && K / (ks * 2) >= 256) ks *= 2;
@@ -1771,7 +1771,7 @@ inline bool splitk_variant(int v) { return v == 0 || v == 22 || v == 24 || (v >=
 extern "C" size_t pli_gemm_workspace_size(int m, int n, int k, int trans_b, int dtype) {
     using namespace pli;
     if (!trans_b || (dtype != PLI_BF16 && dtype != PLI_F16) || m <= 0 || n <= 0 || k <= 0) return 0;
-    const int ks = splitk_slices(m, n, k, splitk_target(22));  // the largest any variant uses
+    const int ks = splitk_slices(m, n, k, splitk_target(22), 2048);  // the largest any variant uses
     return ks > 1 ? (size_t)ks * m * n * sizeof(float) : 0;
 }
 
@@ -1839,9 +1839,16 @@ static int gemm_dispatch(const void* a, const void* b, void* c, const void* bias
     // no-workspace route), the small-M kernel below that.
     // A/B: 22/24 direct-load split-K (512/128 target workgroups), 25/26/27
     // LDS split-K (256/512/128), 20 mid-M, 21 small-M.
+    // Few-tile NT shapes above that (256 < M <= 2048, fewer than 128 tiles of
+    // 256^2) take the same split-K kernel with 128-row slabs: 512 x 4096 x
+    // 4096 220 -> 476 TF, 1024 x 4096^2 417 -> 645, 2048^3 400 -> 469
+    // (hipBLASLt 571 / 897 / 716).
     const bool short_k = k <= 2048 && m <= 128;
-    if (vec && trans_b && splitk_variant(variant) && ws != nullptr && !(variant == 0 && short_k)) {
-        const int ks = splitk_slices(m, n, k, splitk_target(variant));
+    const bool few_tiles = m > 256 && m <= 2048 && (int64_t)cdiv(m, G2M) * cdiv(n, G2N) < 128;
+    if (vec && trans_b && splitk_variant(variant) && ws != nullptr && !(variant == 0 && short_k) &&
+        (variant != 0 || m <= 256 || few_tiles)) {
+        const int target = (variant == 0 && m > 256 && k < 4096) ? 128 : splitk_target(variant);
+        const int ks = splitk_slices(m, n, k, target, (variant == 0 || variant >= 25) ? 2048 : 256);
         if (ks >= 1 && (ks == 1 || ws_bytes >= (size_t)ks * m * n * sizeof(float))) {
             PLI_REQUIRE(((uintptr_t)ws & 15) == 0, "pli_gemm_ws: workspace must be 16-byte aligned");
             const bool lds = variant == 0 || variant >= 25;

@@ -276,6 +276,8 @@ def test_gemm_tile_variants(m, n, k, tb, bias, variant):
     (128, 256, 1024, "bf16", True),    # short K: mid-M route by default
     (200, 640, 2048, "bf16", False),   # two 128-row slabs of X, the second partial
     (256, 128, 512, "fp16", True),     # one n-tile: slices fill the grid
+    (520, 384, 1024, "bf16", True),    # few-tile route: 5 slabs, the last one 8 rows
+    (1024, 512, 4096, "fp16", False),
 ])
 def test_gemm_decode_batch_paths(m, n, k, dt, bias, variant):
     import pli_hip
