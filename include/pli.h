@@ -120,6 +120,14 @@ int pli_gemm_ws(const void* a, const void* b, void* c, const void* bias, int m,
 int pli_gemm_swiglu(const void* x, const void* wg, const void* wu, void* h,
                     int m, int n, int k, int64_t ldx, int64_t ldwg,
                     int64_t ldwu, int64_t ldh, int dtype, void* stream);
+/* pli_gemm_swiglu with a caller workspace of pli_gemm_swiglu_workspace_size
+ * bytes (0: none needed): decode batches (16 < m <= 256) split K over
+ * workgroups for gate and up and apply silu(g) * u in a fixed-order reduce. */
+size_t pli_gemm_swiglu_workspace_size(int m, int n, int k, int dtype);
+int pli_gemm_swiglu_ws(const void* x, const void* wg, const void* wu, void* h,
+                       int m, int n, int k, int64_t ldx, int64_t ldwg,
+                       int64_t ldwu, int64_t ldh, int dtype, void* workspace,
+                       size_t workspace_bytes, void* stream);
 
 /*
  * HBM calibration kernels of ch05/coalescing.cu:7-20 (fp32):

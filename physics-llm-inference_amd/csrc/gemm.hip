@@ -1419,6 +1419,8 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(const float* __restric
 // on the source address, g2_off_rows), double-buffered, and the MFMA
 // fragments come back by ds_read_b128 -- the direct-load kernel touches 32
 // half-lines per load instruction, which caps it far below HBM rate.
+// W2 (SwiGLU, PARTIAL only): grid.y = 2 x the slices, slices y >= nks2 read
+// the up weights W2 and write partial planes nks2 .. 2 nks2 - 1.
 template <typename T, int MC, bool PARTIAL, bool BIAS>
 __global__ __launch_bounds__(256) void gemm_splitk_lds_nt(const uint16_t* __restrict__ X,
                                                           const uint16_t* __restrict__ W,
@@ -1426,14 +1428,21 @@ __global__ __launch_bounds__(256) void gemm_splitk_lds_nt(const uint16_t* __rest
                                                           float* __restrict__ ws,
                                                           const uint16_t* __restrict__ bias, int M,
                                                           int N, int K, int kslice, int64_t ldx,
-                                                          int64_t ldw, int64_t ldc) {
+                                                          int64_t ldw, int64_t ldc,
+                                                          const uint16_t* __restrict__ W2 = nullptr,
+                                                          int64_t ldw2 = 0, int nks2 = 0) {
     constexpr int WIMG = 128 * 128, XIMG = MC * 32 * 128, BUF = WIMG + XIMG;
     __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int l32 = lane & 31, h32 = lane >> 5;
     const int n0 = blockIdx.x * 128, nw = n0 + wave * 32;
-    const int ks = blockIdx.y, m0 = blockIdx.z * 128;
-    const int kb = ks * kslice;
+    const int ks = blockIdx.y, m0 = blockIdx.z * 128;  // ks = output plane
+    const bool up = W2 != nullptr && ks >= nks2;
+    if (up) {
+        W = W2;
+        ldw = ldw2;
+    }
+    const int kb = (up ? ks - nks2 : ks) * kslice;
     // DMA pieces of this wave: W rows 32 w + 8 i + (lane >> 3), i < 4; X rows
     // 8 j + (lane >> 3) for pieces j = w, w + 4, .. < 4 MC
     const int prow = lane >> 3, slot = lane & 7;
@@ -1522,6 +1531,38 @@ __global__ __launch_bounds__(256) void gemm_splitk_lds_nt(const uint16_t* __rest
     }
 }
 
+// h[m][n] = silu(sum_s g_s) * (sum_s u_s) over the 2 x KS partial planes of
+// the SwiGLU split-K launch (gate planes 0..KS-1, up planes KS..2KS-1)
+template <typename T>
+__global__ __launch_bounds__(256) void gemm_splitk_reduce_swiglu(const float* __restrict__ ws,
+                                                                 uint16_t* __restrict__ H, int M,
+                                                                 int N, int KS, int64_t ldh) {
+    const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+    const int64_t MN = (int64_t)M * N;
+    if (i >= MN) return;
+    const int m = (int)(i / N), n = (int)(i % N);
+    float g[8], u[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) g[r] = u[r] = 0.f;
+    for (int ks = 0; ks < KS; ++ks) {
+        const f32x4 g0 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(ws + ks * MN + i));
+        const f32x4 g1 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(ws + ks * MN + i + 4));
+        const f32x4 u0 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(ws + (KS + ks) * MN + i));
+        const f32x4 u1 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(ws + (KS + ks) * MN + i + 4));
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            g[r] += g0[r]; g[4 + r] += g1[r];
+            u[r] += u0[r]; u[4 + r] += u1[r];
+        }
+    }
+    float v[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = silu_mul(g[r], u[r]);
+    *reinterpret_cast<i32x4*>(H + (int64_t)m * ldh + n) =
+        i32x4{(int)pack2<T>(v[0], v[1]), (int)pack2<T>(v[2], v[3]), (int)pack2<T>(v[4], v[5]),
+              (int)pack2<T>(v[6], v[7])};
+}
+
 // K slices for the split-K mid-M path: the largest power of two with
 // cdiv(N,128) * cdiv(M,128) * KS <= target workgroups, slices of >= 256 and a
 // multiple of 64.  0: the path does not apply.
@@ -1577,6 +1618,30 @@ int launch_splitk(const void* a, const void* b, void* c, const void* bias, int M
 #undef PLI_SK_MC
 #undef PLI_SK
     return launch_status("gemm_splitk_nt");
+}
+
+template <typename T>
+int launch_splitk_swiglu(const void* x, const void* wg, const void* wu, void* h, int M, int N,
+                         int K, int64_t ldx, int64_t ldwg, int64_t ldwu, int64_t ldh, int ks,
+                         float* ws, hipStream_t s) {
+    const dim3 grid(cdiv(N, 128), 2 * ks, cdiv(M, 128)), block(256);
+    const int mc = cdiv(min(M, 128), 32);
+    const int kslice = K / ks;
+#define PLI_SKS(MCC)                                                                              \
+    hipLaunchKernelGGL((gemm_splitk_lds_nt<T, MCC, true, false>), grid, block, 0, s,               \
+                       (const uint16_t*)x, (const uint16_t*)wg, (uint16_t*)h, ws, nullptr, M, N, K, \
+                       kslice, ldx, ldwg, ldh, (const uint16_t*)wu, ldwu, ks)
+    if (mc == 1) PLI_SKS(1);
+    else if (mc == 2) PLI_SKS(2);
+    else if (mc == 3) PLI_SKS(3);
+    else PLI_SKS(4);
+#undef PLI_SKS
+    const int rc = launch_status("gemm_splitk_nt<swiglu>");
+    if (rc) return rc;
+    const int64_t groups = ((int64_t)M * N) / 8;
+    hipLaunchKernelGGL((gemm_splitk_reduce_swiglu<T>), dim3((unsigned)((groups + 255) / 256)),
+                       dim3(256), 0, s, ws, (uint16_t*)h, M, N, ks, ldh);
+    return launch_status("gemm_splitk_reduce_swiglu");
 }
 
 template <typename T>
@@ -1725,9 +1790,42 @@ int launch_swiglu(const void* x, const void* wg, const void* wu, void* h, int M,
 }  // namespace
 }  // namespace pli
 
+static int swiglu_dispatch(const void* x, const void* wg, const void* wu, void* h, int m, int n,
+                           int k, int64_t ldx, int64_t ldwg, int64_t ldwu, int64_t ldh, int dtype,
+                           void* stream, void* ws, size_t ws_bytes);
+
+// split-K slices of the SwiGLU decode-batch route (0: not taken)
+static int swiglu_slices(int m, int n, int k) {
+    if (m <= 16 || m > 256 || (k <= 2048 && m <= 128)) return 0;
+    // the phased 256 x 128 SwiGLU tile has enough tiles here (M 256 x 14336:
+    // 104.5 vs 126 us split)
+    if (m >= 256 && (int64_t)pli::cdiv(m, 256) * pli::cdiv(n, 128) >= 96) return 0;
+    return pli::splitk_slices(m, n, k, 512);
+}
+
+extern "C" size_t pli_gemm_swiglu_workspace_size(int m, int n, int k, int dtype) {
+    if ((dtype != PLI_BF16 && dtype != PLI_F16) || m <= 0 || n <= 0 || k <= 0) return 0;
+    const int ks = swiglu_slices(m, n, k);
+    return ks > 0 ? (size_t)2 * ks * m * n * sizeof(float) : 0;
+}
+
 extern "C" int pli_gemm_swiglu(const void* x, const void* wg, const void* wu, void* h, int m,
                                int n, int k, int64_t ldx, int64_t ldwg, int64_t ldwu, int64_t ldh,
                                int dtype, void* stream) {
+    return swiglu_dispatch(x, wg, wu, h, m, n, k, ldx, ldwg, ldwu, ldh, dtype, stream, nullptr, 0);
+}
+
+extern "C" int pli_gemm_swiglu_ws(const void* x, const void* wg, const void* wu, void* h, int m,
+                                  int n, int k, int64_t ldx, int64_t ldwg, int64_t ldwu,
+                                  int64_t ldh, int dtype, void* workspace, size_t workspace_bytes,
+                                  void* stream) {
+    return swiglu_dispatch(x, wg, wu, h, m, n, k, ldx, ldwg, ldwu, ldh, dtype, stream, workspace,
+                           workspace_bytes);
+}
+
+static int swiglu_dispatch(const void* x, const void* wg, const void* wu, void* h, int m, int n,
+                           int k, int64_t ldx, int64_t ldwg, int64_t ldwu, int64_t ldh, int dtype,
+                           void* stream, void* ws, size_t ws_bytes) {
     using namespace pli;
     clear_error();
     PLI_REQUIRE(x && wg && wu && h, "pli_gemm_swiglu: null pointer");
@@ -1742,6 +1840,16 @@ extern "C" int pli_gemm_swiglu(const void* x, const void* wg, const void* wu, vo
     const bool vec = (dtype == PLI_BF16 || dtype == PLI_F16) && k > 0 && k % 8 == 0 &&
                      n % 8 == 0 && ldx % 8 == 0 && ldwg % 8 == 0 && ldwu % 8 == 0 && ldh % 8 == 0 &&
                      al16(x) && al16(wg) && al16(wu) && al16(h);
+    // decode batches (16 < m <= 256, K > 2048 or m > 128) with a workspace:
+    // gate and up split-K planes in one LDS-staged launch, silu(g) * u in the
+    // fixed-order reduce (profiles/r01/gemm/tune_swiglu_splitk.log)
+    const int ks = vec ? swiglu_slices(m, n, k) : 0;
+    if (ks > 0 && ws != nullptr && ws_bytes >= (size_t)2 * ks * m * n * sizeof(float)) {
+        PLI_REQUIRE(((uintptr_t)ws & 15) == 0, "pli_gemm_swiglu_ws: workspace must be 16-byte aligned");
+        if (dtype == PLI_BF16)
+            return launch_splitk_swiglu<bf16_t>(x, wg, wu, h, m, n, k, ldx, ldwg, ldwu, ldh, ks, (float*)ws, s);
+        return launch_splitk_swiglu<f16_t>(x, wg, wu, h, m, n, k, ldx, ldwg, ldwu, ldh, ks, (float*)ws, s);
+    }
     switch (dtype) {
         case PLI_BF16: return launch_swiglu<bf16_t>(x, wg, wu, h, m, n, k, ldx, ldwg, ldwu, ldh, vec, s);
         case PLI_F16: return launch_swiglu<f16_t>(x, wg, wu, h, m, n, k, ldx, ldwg, ldwu, ldh, vec, s);

@@ -50,6 +50,27 @@ def test_gemm_swiglu_vs_oracle(case):
     assert not bad.any(), f"{bad.sum()} beyond tol, max err {np.abs(got - ref).max():.3e}"
 
 
+@pytest.mark.parametrize("split_k", [True, False])
+@pytest.mark.parametrize("case", [(32, 1024, 4096, "bf16"), (100, 416, 8192, "bf16"),
+                                  (200, 384, 4096, "fp16"), (256, 512, 2048, "bf16"),
+                                  (64, 4096, 1024, "bf16")],
+                         ids=lambda c: "m{}n{}k{}_{}".format(*c))
+def test_gemm_swiglu_decode_batch_split_k(case, split_k):
+    """Decode batches 16 < m <= 256: gate and up split-K planes through the
+    wrapper's workspace + the silu(g) * u reduce, and the no-workspace routes."""
+    import pli_hip
+    m, n, k, dt = case
+    x = seeded_normal((m, k), 4, dt) * 0.5
+    wg = seeded_normal((n, k), 5, dt) * k ** -0.5
+    wu = seeded_normal((n, k), 6, dt) * k ** -0.5
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda().to(TDT[dt])
+    h = pli_hip.gemm_swiglu(d(x), d(wg), d(wu), split_k=split_k)
+    ref = swiglu(x, wg, wu)
+    got = h.float().cpu().numpy().astype(np.float64)
+    bad = np.abs(got - ref) > TOL[dt] * (np.abs(ref) + 1)
+    assert not bad.any(), f"{bad.sum()} beyond tol, max err {np.abs(got - ref).max():.3e}"
+
+
 @pytest.mark.parametrize("m", [64, 3072])
 def test_gemm_swiglu_strided_halves_of_fused_weight(m):
     """FusedSwiGLUFFN passes the two row halves of one [2n, k] weight (m = 3072:

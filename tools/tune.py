@@ -233,6 +233,7 @@ def tune_swiglu():
             x = torch.randn(m, H, device="cuda", dtype=torch.bfloat16)
             out = torch.empty(m, inter, device="cuda", dtype=torch.bfloat16)
             fns = {"fused": lambda a, b: pli_hip.gemm_swiglu(x, a, b, out=out),
+                   "fused_nosplit": lambda a, b: pli_hip.gemm_swiglu(x, a, b, out=out, split_k=False),
                    "hip_unfused": lambda a, b: torch.mul(F.silu(pli_hip.gemm(x, a, trans_b=True)),
                                                          pli_hip.gemm(x, b, trans_b=True), out=out),
                    "torch": lambda a, b: torch.mul(F.silu(x @ a.t()), x @ b.t(), out=out)}
