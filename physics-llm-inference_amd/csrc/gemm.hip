@@ -1421,7 +1421,7 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(const float* __restric
 // half-lines per load instruction, which caps it far below HBM rate.
 // W2 (SwiGLU, PARTIAL only): grid.y = 2 x the slices, slices y >= nks2 read
 // the up weights W2 and write partial planes nks2 .. 2 nks2 - 1.
-template <typename T, int MC, bool PARTIAL, bool BIAS>
+template <typename T, int MC, bool PARTIAL, bool BIAS, int NB = 2>
 __global__ __launch_bounds__(256) void gemm_splitk_lds_nt(const uint16_t* __restrict__ X,
                                                           const uint16_t* __restrict__ W,
                                                           uint16_t* __restrict__ C,
@@ -1432,7 +1432,7 @@ __global__ __launch_bounds__(256) void gemm_splitk_lds_nt(const uint16_t* __rest
                                                           const uint16_t* __restrict__ W2 = nullptr,
                                                           int64_t ldw2 = 0, int nks2 = 0) {
     constexpr int WIMG = 128 * 128, XIMG = MC * 32 * 128, BUF = WIMG + XIMG;
-    __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];
+    __shared__ __attribute__((aligned(1024))) char smem[NB * BUF];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int l32 = lane & 31, h32 = lane >> 5;
     const int n0 = blockIdx.x * 128, nw = n0 + wave * 32;
@@ -1480,6 +1480,37 @@ __global__ __launch_bounds__(256) void gemm_splitk_lds_nt(const uint16_t* __rest
         for (int e = 0; e < 16; ++e) acc[mc][e] = 0.f;
 
     const int steps = kslice / 64;
+    auto mma_step = [&](const char* base) {
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+            const i32x4 wfr = lds_read_b128(base, g2_off_rows(wave * 32 + l32, 2 * s2 + h32));
+#pragma unroll
+            for (int mc = 0; mc < MC; ++mc) {
+                const i32x4 xfr = lds_read_b128(base + WIMG, g2_off_rows(mc * 32 + l32, 2 * s2 + h32));
+                acc[mc] = mfma32x32x16<T>(wfr, xfr, acc[mc]);
+            }
+        }
+    };
+    if constexpr (NB == 3) {
+        // 3-deep ring, one barrier per step: wait for step st, barrier (every
+        // wave is also done with step st-1, whose buffer the next issue refills),
+        // issue step st+2, compute step st
+        issue(0, 0);
+        if (steps > 1) issue(1, 64);
+        for (int st = 0; st < steps; ++st) {
+            if (st + 1 < steps) {
+                if constexpr (MC == 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+                else if constexpr (MC == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                else if constexpr (MC == 3) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __syncthreads();
+            if (st + 2 < steps) issue((st + 2) % 3, (st + 2) * 64);
+            mma_step(smem + (st % 3) * BUF);
+        }
+    } else {
     issue(0, 0);
     for (int st = 0; st < steps; ++st) {
         const int buf = st & 1;
@@ -1493,17 +1524,9 @@ __global__ __launch_bounds__(256) void gemm_splitk_lds_nt(const uint16_t* __rest
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         __syncthreads();  // every wave's pieces of step st have landed
-        const char* base = smem + buf * BUF;
-#pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2) {
-            const i32x4 wfr = lds_read_b128(base, g2_off_rows(wave * 32 + l32, 2 * s2 + h32));
-#pragma unroll
-            for (int mc = 0; mc < MC; ++mc) {
-                const i32x4 xfr = lds_read_b128(base + WIMG, g2_off_rows(mc * 32 + l32, 2 * s2 + h32));
-                acc[mc] = mfma32x32x16<T>(wfr, xfr, acc[mc]);
-            }
-        }
+        mma_step(smem + buf * BUF);
         __syncthreads();  // buffer buf is refilled by the DMA issued next step
+    }
     }
 
     if (nw >= N) return;
@@ -1577,13 +1600,17 @@ inline int splitk_slices(int M, int N, int K, int target, int max_m = 256) {
 template <typename T>
 int launch_splitk(const void* a, const void* b, void* c, const void* bias, int M, int N, int K,
                   int64_t lda, int64_t ldb, int64_t ldc, int ks, float* ws, hipStream_t s,
-                  bool lds = false) {
+                  bool lds = false, bool nb3 = false) {
     const dim3 grid(cdiv(N, 128), ks, cdiv(M, 128)), block(256);
     const int mc = cdiv(min(M, 128), 32);
     const int kslice = K / ks;
 #define PLI_SK(MCC, PA, BI)                                                                     \
     do {                                                                                        \
-        if (lds)                                                                                \
+        if (lds && nb3)                                                                         \
+            hipLaunchKernelGGL((gemm_splitk_lds_nt<T, MCC, PA, BI, 3>), grid, block, 0, s,        \
+                               (const uint16_t*)a, (const uint16_t*)b, (uint16_t*)c, ws,        \
+                               (const uint16_t*)bias, M, N, K, kslice, lda, ldb, ldc);          \
+        else if (lds)                                                                           \
             hipLaunchKernelGGL((gemm_splitk_lds_nt<T, MCC, PA, BI>), grid, block, 0, s,           \
                                (const uint16_t*)a, (const uint16_t*)b, (uint16_t*)c, ws,        \
                                (const uint16_t*)bias, M, N, K, kslice, lda, ldb, ldc);          \
@@ -1868,11 +1895,11 @@ namespace pli {
 namespace {
 // split-K target workgroups by variant (0: default 256; 22: 512; 24: 128)
 inline int splitk_target(int variant) {
-    return (variant == 0 || variant == 22 || variant == 26) ? 512
-           : (variant == 24 || variant == 27)             ? 128
+    return (variant == 0 || variant == 22 || variant == 26 || variant == 28) ? 512
+           : (variant == 24 || variant == 27 || variant == 29) ? 128
                                                           : 256;
 }
-inline bool splitk_variant(int v) { return v == 0 || v == 22 || v == 24 || (v >= 25 && v <= 27); }
+inline bool splitk_variant(int v) { return v == 0 || v == 22 || v == 24 || (v >= 25 && v <= 29); }
 }  // namespace
 }  // namespace pli
 
@@ -1960,9 +1987,10 @@ static int gemm_dispatch(const void* a, const void* b, void* c, const void* bias
         if (ks >= 1 && (ks == 1 || ws_bytes >= (size_t)ks * m * n * sizeof(float))) {
             PLI_REQUIRE(((uintptr_t)ws & 15) == 0, "pli_gemm_ws: workspace must be 16-byte aligned");
             const bool lds = variant == 0 || variant >= 25;
+            const bool nb3 = variant == 28 || variant == 29;
             if (dtype == PLI_BF16)
-                return launch_splitk<bf16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, ks, (float*)ws, s, lds);
-            return launch_splitk<f16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, ks, (float*)ws, s, lds);
+                return launch_splitk<bf16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, ks, (float*)ws, s, lds, nb3);
+            return launch_splitk<f16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, ks, (float*)ws, s, lds, nb3);
         }
     }
     if (vec && trans_b && k % 256 == 0 &&

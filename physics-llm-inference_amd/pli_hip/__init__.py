@@ -613,7 +613,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, trans_b: bool = False,
         # decode-batch NT shapes split K over workgroups through a scratch
         # workspace from torch's caching allocator (pli_gemm_ws)
         wsb = lib().pli_gemm_workspace_size(m, n, k, int(bool(trans_b)), _dtype_code(a)) \
-            if variant in (None, 0, 22, 24, 25, 26, 27) else 0
+            if variant in (None, 0, 22, 24, 25, 26, 27, 28, 29) else 0
         if wsb:
             ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
             if variant is None:

@@ -268,7 +268,7 @@ def test_gemm_tile_variants(m, n, k, tb, bias, variant):
 # decode-batch / TP-shard NT paths, 16 < M <= 256: default route (workspace
 # from the wrapper: LDS split-K, or mid-M / small-M for short K), direct-load
 # split-K (22, 24), LDS split-K (25-27), mid-M (20), small-M (21)
-@pytest.mark.parametrize("variant", [None, 20, 21, 22, 24, 25, 26, 27])
+@pytest.mark.parametrize("variant", [None, 20, 21, 22, 24, 25, 26, 27, 28, 29])
 @pytest.mark.parametrize("m,n,k,dt,bias", [
     (17, 1024, 4096, "bf16", False),   # one 32-row chunk, 8 n-tiles x 8 slices
     (64, 512, 8192, "bf16", True),     # long K slices
