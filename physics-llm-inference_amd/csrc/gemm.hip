@@ -1586,6 +1586,133 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_swiglu(const float* __
               (int)pack2<T>(v[6], v[7])};
 }
 
+// Grouped (MoE) form of the LDS-staged kernel for decode-sized routing
+// (rows_bound <= 1024): workgroup = (output tile, 128-row slab of expert e's
+// rows, expert e).  Expert e's weights come from the device pointer table;
+// its X rows through `gather` (per-lane LDS-DMA source rows); one K pass (the
+// experts x tiles already fill the chip).  SW (W1/W3): the W image is 64 gate
+// rows (waves 0-1) + the same 64 up rows (waves 2-3); the up waves hand their
+// accumulators over through LDS and waves 0-1 write silu(g) * u, so neither
+// activation reaches HBM.  Slabs past an expert's rows exit before any barrier.
+template <typename T, int MC, bool SW>
+__global__ __launch_bounds__(256) void gemm_grouped_lds_nt(
+    const uint16_t* __restrict__ X, int64_t ldx, const int32_t* __restrict__ gather,
+    const uint16_t* const* __restrict__ wtab, const uint16_t* const* __restrict__ wutab,
+    int64_t ldw, uint16_t* __restrict__ C, int64_t ldc, const int32_t* __restrict__ offsets, int N,
+    int K) {
+    constexpr int WIMG = 128 * 128, XIMG = MC * 32 * 128, BUF = WIMG + XIMG;
+    constexpr int TN = SW ? 64 : 128;  // output columns per workgroup
+    __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int l32 = lane & 31, h32 = lane >> 5;
+    const int e = blockIdx.z;
+    const int r0 = offsets[e] + blockIdx.y * 128, r1 = offsets[e + 1];
+    if (r0 >= r1) return;  // uniform over the workgroup
+    const int n0 = blockIdx.x * TN;
+    const uint16_t* We = wtab[e];
+    const uint16_t* Wue = SW ? wutab[e] : nullptr;
+    const int prow = lane >> 3, slot = lane & 7;
+    const uint16_t* wsrc[4];
+    int wdst[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int row = wave * 32 + 8 * i + prow;  // W image row
+        const uint16_t* base = We;
+        int nr = n0 + row;
+        if constexpr (SW) {
+            if (row >= 64) { base = Wue; nr = n0 + row - 64; }
+        }
+        wsrc[i] = base + (int64_t)min(nr, N - 1) * ldw + 8 * (slot ^ ((row >> 1) & 7));
+        wdst[i] = (wave * 4 + i) * 1024;
+    }
+    const uint16_t* xsrc[MC];
+    int xdst[MC];
+#pragma unroll
+    for (int j = 0; j < MC; ++j) {
+        const int piece = wave + 4 * j, row = 8 * piece + prow;
+        const int r = min(r0 + row, r1 - 1);
+        const int src = gather ? gather[r] : r;
+        xsrc[j] = X + (int64_t)src * ldx + 8 * (slot ^ ((row >> 1) & 7));
+        xdst[j] = WIMG + piece * 1024;
+    }
+    auto issue = [&](int buf, int k0) {
+        char* b = smem + buf * BUF;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(wsrc[i] + k0),
+                                             (__attribute__((address_space(3))) void*)(b + wdst[i]), 16, 0, 0);
+#pragma unroll
+        for (int j = 0; j < MC; ++j)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(xsrc[j] + k0),
+                                             (__attribute__((address_space(3))) void*)(b + xdst[j]), 16, 0, 0);
+    };
+    f32x16 acc[MC];
+#pragma unroll
+    for (int mc = 0; mc < MC; ++mc)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[mc][q] = 0.f;
+    const int steps = K / 64;
+    issue(0, 0);
+    for (int st = 0; st < steps; ++st) {
+        const int buf = st & 1;
+        if (st + 1 < steps) {
+            issue(buf ^ 1, (st + 1) * 64);
+            if constexpr (MC == 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+            else if constexpr (MC == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+            else if constexpr (MC == 3) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        const char* b = smem + buf * BUF;
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+            const i32x4 wfr = lds_read_b128(b, g2_off_rows(wave * 32 + l32, 2 * s2 + h32));
+#pragma unroll
+            for (int mc = 0; mc < MC; ++mc) {
+                const i32x4 xfr = lds_read_b128(b + WIMG, g2_off_rows(mc * 32 + l32, 2 * s2 + h32));
+                acc[mc] = mfma32x32x16<T>(wfr, xfr, acc[mc]);
+            }
+        }
+        __syncthreads();
+    }
+    // acc[mc][4q + r]: row r0 + 32 mc + l32, column (image row) 32 w' + 8 q + 4 h32 + r
+    if constexpr (SW) {
+        float* part = reinterpret_cast<float*>(smem);  // [2 waves][MC][16][64], after the last barrier
+        if (wave >= 2) {
+#pragma unroll
+            for (int mc = 0; mc < MC; ++mc)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) part[(((wave - 2) * MC + mc) * 16 + q) * 64 + lane] = acc[mc][q];
+        }
+        __syncthreads();
+        if (wave >= 2) return;
+    }
+    const int nw = n0 + wave * 32;
+    if (nw >= N) return;
+#pragma unroll
+    for (int mc = 0; mc < MC; ++mc) {
+        const int m = r0 + 32 * mc + l32;
+        if (m >= r1) continue;
+        uint16_t* crow = C + (int64_t)m * ldc;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int n = nw + 8 * q + 4 * h32;
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                v[r] = acc[mc][4 * q + r];
+                if constexpr (SW) {
+                    const float* part = reinterpret_cast<const float*>(smem);
+                    v[r] = silu_mul(v[r], part[((wave * MC + mc) * 16 + 4 * q + r) * 64 + lane]);
+                }
+            }
+            *reinterpret_cast<i32x2*>(crow + n) = i32x2{(int)pack2<T>(v[0], v[1]), (int)pack2<T>(v[2], v[3])};
+        }
+    }
+}
+
 // K slices for the split-K mid-M path: the largest power of two with
 // cdiv(N,128) * cdiv(M,128) * KS <= target workgroups, slices of >= 256 and a
 // multiple of 64.  0: the path does not apply.
@@ -2064,10 +2191,34 @@ extern "C" int pli_gemm(const void* a, const void* b, void* c, const void* bias,
 // (or silu(. W1_e^T) * (. W3_e^T) when wu_ptrs != NULL) for r in expert e's
 // row range [offsets[e], offsets[e+1]).  rows_bound (host) bounds every
 // expert's row count and sizes the per-workgroup batch groups.
+static int grouped_dispatch(const void* x, const int32_t* gather, const void* const* w_ptrs,
+                            const void* const* wu_ptrs, void* c, const int32_t* offsets,
+                            int experts, int rows_bound, int n, int k, int64_t ldx, int64_t ldw,
+                            int64_t ldc, int dtype, void* stream, int variant);
+
 extern "C" int pli_gemm_grouped(const void* x, const int32_t* gather, const void* const* w_ptrs,
                                 const void* const* wu_ptrs, void* c, const int32_t* offsets,
                                 int experts, int rows_bound, int n, int k, int64_t ldx,
                                 int64_t ldw, int64_t ldc, int dtype, void* stream) {
+    return grouped_dispatch(x, gather, w_ptrs, wu_ptrs, c, offsets, experts, rows_bound, n, k, ldx,
+                            ldw, ldc, dtype, stream, 0);
+}
+
+// Not in pli.h: variant 1 = the weight-streaming / 256-row-tile routes only,
+// 2 = the LDS-staged grouped kernel wherever it applies.
+extern "C" int pli_gemm_grouped_variant(const void* x, const int32_t* gather,
+                                        const void* const* w_ptrs, const void* const* wu_ptrs,
+                                        void* c, const int32_t* offsets, int experts,
+                                        int rows_bound, int n, int k, int64_t ldx, int64_t ldw,
+                                        int64_t ldc, int dtype, void* stream, int variant) {
+    return grouped_dispatch(x, gather, w_ptrs, wu_ptrs, c, offsets, experts, rows_bound, n, k, ldx,
+                            ldw, ldc, dtype, stream, variant);
+}
+
+static int grouped_dispatch(const void* x, const int32_t* gather, const void* const* w_ptrs,
+                            const void* const* wu_ptrs, void* c, const int32_t* offsets,
+                            int experts, int rows_bound, int n, int k, int64_t ldx, int64_t ldw,
+                            int64_t ldc, int dtype, void* stream, int variant) {
     using namespace pli;
     clear_error();
     PLI_REQUIRE(x && w_ptrs && c && offsets, "pli_gemm_grouped: null pointer");
@@ -2080,7 +2231,40 @@ extern "C" int pli_gemm_grouped(const void* x, const int32_t* gather, const void
     PLI_REQUIRE(ldx >= k && ldw >= k && ldc >= n, "pli_gemm_grouped: leading dimension too small");
     if (rows_bound == 0) return PLI_OK;
     hipStream_t st = (hipStream_t)stream;
-    if (rows_bound >= 16 * experts) {
+    // decode-sized routing, 16 < rows <= 1024: the LDS-staged grouped kernel
+    // (n % 64 for the SwiGLU form, n % 128 plain; k % 128 holds).  MoEConfig
+    // defaults, both grouped GEMMs (profiles/r01/gemm/tune_moe_grouped.log):
+    // 32 tokens 717 -> 599 us (4.7 TB/s of expert weights), 128 tokens 734 ->
+    // 682, 256 tokens 791 -> 701; 1-8 tokens keep the weight-streaming kernel
+    // (1 token: 140 vs 312 us).
+    const bool sw = wu_ptrs != nullptr;
+    const bool lds_ok = rows_bound <= 1024 && n % (sw ? 64 : 128) == 0;
+    if (lds_ok && variant != 1 && (variant == 2 || rows_bound > 16)) {
+        const int mc = cdiv(min(rows_bound, 128), 32);
+        const dim3 grid((unsigned)(n / (sw ? 64 : 128)), (unsigned)cdiv(rows_bound, 128), (unsigned)experts);
+        const auto* Xg = (const uint16_t*)x;
+        const auto* const* Wg = (const uint16_t* const*)w_ptrs;
+        const auto* const* Wug = (const uint16_t* const*)wu_ptrs;
+#define PLI_GLDS(TT, MCC, SWW)                                                                   \
+    hipLaunchKernelGGL((gemm_grouped_lds_nt<TT, MCC, SWW>), grid, dim3(256), 0, st, Xg, ldx, gather, \
+                       Wg, Wug, ldw, (uint16_t*)c, ldc, offsets, n, k)
+#define PLI_GLDS_MC(TT, SWW)                  \
+    do {                                      \
+        if (mc == 1) PLI_GLDS(TT, 1, SWW);    \
+        else if (mc == 2) PLI_GLDS(TT, 2, SWW); \
+        else if (mc == 3) PLI_GLDS(TT, 3, SWW); \
+        else PLI_GLDS(TT, 4, SWW);            \
+    } while (0)
+        if (dtype == PLI_BF16) {
+            if (sw) PLI_GLDS_MC(bf16_t, true); else PLI_GLDS_MC(bf16_t, false);
+        } else {
+            if (sw) PLI_GLDS_MC(f16_t, true); else PLI_GLDS_MC(f16_t, false);
+        }
+#undef PLI_GLDS_MC
+#undef PLI_GLDS
+        return launch_status("gemm_grouped_lds_nt");
+    }
+    if (variant != 2 && rows_bound >= 16 * experts) {
         // prefill-sized routing (>= 16 rows per expert on average): the phased
         // 256-row tile per (expert, slot); decode sizes stay on the
         // weight-streaming kernel below

@@ -54,6 +54,8 @@ _SIGS = {
                       _vp, _vp, _vp],
     "pli_gemm_grouped": [_vp, _vp, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_i64,
                          _c_i64, _c_i64, _c_int, _vp],
+    "pli_gemm_grouped_variant": [_vp, _vp, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int,
+                                 _c_i64, _c_i64, _c_i64, _c_int, _vp, _c_int],
     "pli_moe_combine": [_vp, _c_i64, _vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_int, _c_int, _vp],
     "pli_scale_copy": [_vp, _vp, _c_i64, _c_int, _vp],
     "pli_softmax_rows": [_vp, _vp, _c_i64, _c_int, _c_int, _vp],
@@ -338,16 +340,20 @@ def weight_table(weights: list[torch.Tensor]) -> torch.Tensor:
 
 def gemm_grouped(x: torch.Tensor, gather: torch.Tensor | None, w_table: torch.Tensor,
                  offsets: torch.Tensor, rows: int, n: int, k: int, ldw: int,
-                 wu_table: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+                 wu_table: torch.Tensor | None = None, out: torch.Tensor | None = None,
+                 variant: int | None = None) -> torch.Tensor:
     """Per-expert NT GEMM over expert-sorted rows (see include/pli.h)."""
     dev = _require_gpu(x)
     E = offsets.numel() - 1
     if out is None:
         out = torch.empty(max(rows, 1), n, device=x.device, dtype=x.dtype)
+    args = (_ptr(x), _ptr(gather), _ptr(w_table), _ptr(wu_table), _ptr(out), _ptr(offsets), E,
+            int(rows), int(n), int(k), x.stride(0), int(ldw), out.stride(0), _dtype_code(x), _stream(dev))
     with _on_device(dev):
-        rc = lib().pli_gemm_grouped(_ptr(x), _ptr(gather), _ptr(w_table), _ptr(wu_table), _ptr(out),
-                                    _ptr(offsets), E, int(rows), int(n), int(k), x.stride(0),
-                                    int(ldw), out.stride(0), _dtype_code(x), _stream(dev))
+        if variant is None:
+            rc = lib().pli_gemm_grouped(*args)
+        else:
+            rc = lib().pli_gemm_grouped_variant(*args, int(variant))
     _check(rc, "pli_gemm_grouped")
     return out
 

@@ -33,14 +33,16 @@ def test_moe_route_vs_oracle(T, E, k):
             assert off[e] <= p[t, j] < off[e + 1] and gth[p[t, j]] == t
 
 
+@pytest.mark.parametrize("variant", [None, 1, 2])
 @pytest.mark.parametrize("T,E,k,H,I,dead", [
     (4, 8, 2, 256, 512, ()),         # decode sizes: weight-streaming grouped kernel
-    (64, 8, 2, 512, 1024, ()),       # 16 rows / expert: the phased 256-row tile (gemm_256g)
-    (300, 8, 2, 256, 256, ()),
+    (24, 8, 2, 256, 512, ()),        # 48 rows: the LDS-staged grouped kernel (default)
+    (64, 8, 2, 512, 1024, ()),       # 16 rows / expert: LDS kernel (default) / phased 256-row tile (1)
+    (300, 8, 2, 256, 256, ()),       # 600 rows: experts span several 128-row slabs
     (1200, 4, 2, 384, 640, ()),      # ~600 rows / expert = 3 slots each; ragged n on both GEMMs
-    (600, 16, 1, 256, 512, (3, 7, 11)),  # experts with no rows: their slots are skipped
+    (600, 16, 1, 256, 512, (3, 7, 11)),  # experts with no rows: their slots / slabs are skipped
 ])
-def test_grouped_gemm_and_combine_vs_oracle(T, E, k, H, I, dead):
+def test_grouped_gemm_and_combine_vs_oracle(T, E, k, H, I, dead, variant):
     import pli_hip
     x = torch.from_numpy(seeded_normal((T, H), 1, "bf16")).cuda().bfloat16()
     logits = torch.from_numpy(seeded_normal((T, E), 2)).cuda()
@@ -52,8 +54,8 @@ def test_grouped_gemm_and_combine_vs_oracle(T, E, k, H, I, dead):
     t1 = pli_hip.weight_table([e[0] for e in ws])
     t2 = pli_hip.weight_table([e[1] for e in ws])
     t3 = pli_hip.weight_table([e[2] for e in ws])
-    h = pli_hip.gemm_grouped(x, gather, t1, offsets, T * k, I, H, H, wu_table=t3)
-    y = pli_hip.gemm_grouped(h, None, t2, offsets, T * k, H, I, I)
+    h = pli_hip.gemm_grouped(x, gather, t1, offsets, T * k, I, H, H, wu_table=t3, variant=variant)
+    y = pli_hip.gemm_grouped(h, None, t2, offsets, T * k, H, I, I, variant=variant)
     out = pli_hip.moe_combine(y, pos, w, T)
     # per-row check of the grouped SwiGLU against the oracle
     xn, gth = x.double().cpu().numpy(), gather.cpu().numpy()

@@ -438,6 +438,41 @@ def tune_midm():
                           "err": errs}), flush=True)
 
 
+def tune_moe_grouped():
+    """The two grouped expert GEMMs of the ch09 MoE layer (MoEConfig defaults)
+    on the same routing: variant 1 (weight-streaming / 256-row tile routes)
+    vs 2 (LDS-staged grouped kernel); GB/s over the active experts' weights."""
+    from ch09 import MoEConfig, MoELayer
+    torch.manual_seed(0)
+    cfg = MoEConfig()
+    moe = MoELayer(cfg).cuda().bfloat16().eval()
+    t1, t3, t2 = moe._weight_tables()
+    H, I = cfg.hidden_dim, cfg.expert_dim
+    tokens = tuple(int(v) for v in os.environ.get("PLI_MOE_T", "1,8,32,64,128,256,512").split(","))
+    for T in tokens:
+        x = torch.randn(T, H, device="cuda", dtype=torch.bfloat16)
+        with torch.no_grad():
+            logits = pli_hip.gemm(x, moe.router.gate.weight, trans_b=True)
+            w, _, pos, gather, offsets = pli_hip.moe_route(logits, cfg.num_experts_per_tok,
+                                                           cfg.normalize_expert_weights)
+        rows = T * cfg.num_experts_per_tok
+        active = int((offsets[1:] - offsets[:-1] > 0).sum().item())
+        outs = {}
+
+        def run(v):
+            h = pli_hip.gemm_grouped(x, gather, t1, offsets, rows, I, H, H, wu_table=t3, variant=v)
+            return pli_hip.gemm_grouped(h, None, t2, offsets, rows, H, I, I, variant=v)
+        for v in (1, 2):
+            outs[v] = run(v).float()
+        diff = (outs[1] - outs[2]).abs().max().item() / (outs[1].abs().max().item() + 1e-6)
+        t = interleave({v: (lambda v=v: run(v)) for v in (1, 2)}, 5, 3)
+        wbytes = active * 3 * H * I * 2
+        print(json.dumps({"kernel": "moe_grouped", "tokens": T, "active_experts": active,
+                          "us": {f"v{v}": round(t[v][0] * 1e3, 1) for v in t},
+                          "weight_TB/s": {f"v{v}": round(wbytes / t[v][0] / 1e9, 2) for v in t},
+                          "rel_diff_v1_v2": diff}), flush=True)
+
+
 if __name__ == "__main__":
     what = sys.argv[1:] or ["hbm", "gemv", "flash", "gemm"]
     if "hbm" in what:
@@ -457,6 +492,8 @@ if __name__ == "__main__":
         tune_gemm()
     if "midm" in what:
         tune_midm()
+    if "moeg" in what:
+        tune_moe_grouped()
     if "gemmshapes" in what:
         tune_gemm_shapes()
     if "decode" in what:
