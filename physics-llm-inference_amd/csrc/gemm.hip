@@ -2105,7 +2105,12 @@ static int gemm_dispatch(const void* a, const void* b, void* c, const void* bias
     // 256^2) take the same split-K kernel with 128-row slabs: 512 x 4096 x
     // 4096 220 -> 476 TF, 1024 x 4096^2 417 -> 645, 2048^3 400 -> 469
     // (hipBLASLt 571 / 897 / 716).
-    const bool short_k = k <= 2048 && m <= 128;
+    // short K keeps the unsplit kernels only where they win: a wide N (the TP-8
+    // row shard 8192 x 1024: mid-M 14.1 vs split 16.5-19 us at M 128) below
+    // 16384 columns (an lm_head 32 x 32000 x 2048: split 26 vs 56 us), or
+    // M <= 32 with few columns (32 x 2048 x 2048: small-M 8.3 vs 11.3 us);
+    // M 33-128 with few columns splits (64 x 2048 x 2048: 11.8 vs 16.7 us)
+    const bool short_k = k <= 2048 && m <= 128 && n < 16384 && (m <= 32 || n / 128 >= 64);
     const bool few_tiles = m > 256 && m <= 2048 && (int64_t)cdiv(m, G2M) * cdiv(n, G2N) < 128;
     if (vec && trans_b && splitk_variant(variant) && ws != nullptr && !(variant == 0 && short_k) &&
         (variant != 0 || m <= 256 || few_tiles)) {
