@@ -88,9 +88,18 @@ class CachedGQA(nn.Module):
             o = pli_hip.attn_decode_dev(q.view(B, S, self.num_heads, self.head_dim), cache.k,
                                         cache.v, cache.pos, n_kv_add=S, causal=S > 1)
             return _lin(o.reshape(B, S, self.hidden_dim), self.o_proj.weight)
-        q = _lin(x, self.q_proj.weight).view(B, S, self.num_heads, self.head_dim)
-        k = _lin(x, self.k_proj.weight).view(B, S, self.num_kv_heads, self.head_dim)
-        v = _lin(x, self.v_proj.weight).view(B, S, self.num_kv_heads, self.head_dim)
+        if x.is_cuda:
+            # q, k and v from one GEMM over the packed [Wq; Wk; Wv] (views of
+            # the output columns feed the cache append and attention in place)
+            nq, nk = self.num_heads * self.head_dim, self.num_kv_heads * self.head_dim
+            qkv = _lin(x, self._packed_qkv())
+            q = qkv[..., :nq].unflatten(-1, (self.num_heads, self.head_dim))
+            k = qkv[..., nq:nq + nk].unflatten(-1, (self.num_kv_heads, self.head_dim))
+            v = qkv[..., nq + nk:].unflatten(-1, (self.num_kv_heads, self.head_dim))
+        else:
+            q = _lin(x, self.q_proj.weight).view(B, S, self.num_heads, self.head_dim)
+            k = _lin(x, self.k_proj.weight).view(B, S, self.num_kv_heads, self.head_dim)
+            v = _lin(x, self.v_proj.weight).view(B, S, self.num_kv_heads, self.head_dim)
         if cache is not None:
             cache.update(k, v)
             if cache.pos is not None and _device_len_ok(q, cache):
@@ -103,6 +112,26 @@ class CachedGQA(nn.Module):
             k_buf, v_buf, n_kv = k, v, S
         o = attend_cached(q, k_buf, v_buf, n_kv).reshape(B, S, self.hidden_dim)
         return _lin(o, self.o_proj.weight)
+
+
+    def _packed_qkv(self) -> torch.Tensor:
+        """[Wq; Wk; Wv] as one contiguous [(H + 2 Hkv) hd, hidden] tensor whose
+        row blocks ARE the three projections' weights: the first call packs
+        them and re-points the parameters' data at the blocks (no second
+        copy is kept); a parameter replaced later (load, dtype / device move)
+        is detected by address and packed again."""
+        wq, wk, wv = self.q_proj.weight, self.k_proj.weight, self.v_proj.weight
+        buf = getattr(self, "_qkv_buf", None)
+        nq, nk = wq.shape[0], wk.shape[0]
+        if (buf is not None and buf.device == wq.device and buf.dtype == wq.dtype
+                and wq.data_ptr() == buf.data_ptr() and wk.data_ptr() == buf[nq].data_ptr()
+                and wv.data_ptr() == buf[nq + nk].data_ptr()):
+            return buf
+        with torch.no_grad():
+            buf = torch.cat([wq.data, wk.data, wv.data]).contiguous()
+            wq.data, wk.data, wv.data = buf[:nq], buf[nq:nq + nk], buf[nq + nk:]
+        self._qkv_buf = buf
+        return buf
 
 
 def _device_len_ok_shape(x: torch.Tensor, S: int, H: int, Hkv: int, D: int) -> bool:
