@@ -1946,11 +1946,16 @@ int launch_swiglu(const void* x, const void* wg, const void* wu, void* h, int M,
 
 static int swiglu_dispatch(const void* x, const void* wg, const void* wu, void* h, int m, int n,
                            int k, int64_t ldx, int64_t ldwg, int64_t ldwu, int64_t ldh, int dtype,
-                           void* stream, void* ws, size_t ws_bytes);
+                           void* stream, void* ws, size_t ws_bytes, int variant = 0);
 
-// split-K slices of the SwiGLU decode-batch route (0: not taken)
-static int swiglu_slices(int m, int n, int k) {
-    if (m <= 16 || m > 256 || (k <= 2048 && m <= 128)) return 0;
+// split-K slices of the SwiGLU decode-batch route (0: not taken); force:
+// ignore the short-K rule (A/B)
+static int swiglu_slices(int m, int n, int k, bool force = false) {
+    if (m <= 16 || m > 256) return 0;
+    if (force) return pli::splitk_slices(m, n, k, 512);
+    // short K splits too here (unlike the plain GEMM): gate + up are twice
+    // the weights per output (32 / 64 / 128 x 5632 x 2048: 18.1 / 21.1 / 32.5
+    // vs 20.9 / 27.9 / 45.7 us unsplit, tools/tune.py swr)
     // the phased 256 x 128 SwiGLU tile has enough tiles here (M 256 x 14336:
     // 104.5 vs 126 us split)
     if (m >= 256 && (int64_t)pli::cdiv(m, 256) * pli::cdiv(n, 128) >= 96) return 0;
@@ -1959,7 +1964,7 @@ static int swiglu_slices(int m, int n, int k) {
 
 extern "C" size_t pli_gemm_swiglu_workspace_size(int m, int n, int k, int dtype) {
     if ((dtype != PLI_BF16 && dtype != PLI_F16) || m <= 0 || n <= 0 || k <= 0) return 0;
-    const int ks = swiglu_slices(m, n, k);
+    const int ks = swiglu_slices(m, n, k, true);  // the most any route or variant uses
     return ks > 0 ? (size_t)2 * ks * m * n * sizeof(float) : 0;
 }
 
@@ -1977,9 +1982,19 @@ extern "C" int pli_gemm_swiglu_ws(const void* x, const void* wg, const void* wu,
                            workspace_bytes);
 }
 
+// Not in pli.h: variant 1 = split K wherever the split-K route applies,
+// 2 = never split (A/B of the decode-batch routing)
+extern "C" int pli_gemm_swiglu_ws_variant(const void* x, const void* wg, const void* wu, void* h,
+                                          int m, int n, int k, int64_t ldx, int64_t ldwg,
+                                          int64_t ldwu, int64_t ldh, int dtype, void* workspace,
+                                          size_t workspace_bytes, void* stream, int variant) {
+    return swiglu_dispatch(x, wg, wu, h, m, n, k, ldx, ldwg, ldwu, ldh, dtype, stream, workspace,
+                           workspace_bytes, variant);
+}
+
 static int swiglu_dispatch(const void* x, const void* wg, const void* wu, void* h, int m, int n,
                            int k, int64_t ldx, int64_t ldwg, int64_t ldwu, int64_t ldh, int dtype,
-                           void* stream, void* ws, size_t ws_bytes) {
+                           void* stream, void* ws, size_t ws_bytes, int variant) {
     using namespace pli;
     clear_error();
     PLI_REQUIRE(x && wg && wu && h, "pli_gemm_swiglu: null pointer");
@@ -1997,7 +2012,7 @@ static int swiglu_dispatch(const void* x, const void* wg, const void* wu, void* 
     // decode batches (16 < m <= 256, K > 2048 or m > 128) with a workspace:
     // gate and up split-K planes in one LDS-staged launch, silu(g) * u in the
     // fixed-order reduce (profiles/r01/gemm/tune_swiglu_splitk.log)
-    const int ks = vec ? swiglu_slices(m, n, k) : 0;
+    const int ks = vec && variant != 2 ? swiglu_slices(m, n, k, variant == 1) : 0;
     if (ks > 0 && ws != nullptr && ws_bytes >= (size_t)2 * ks * m * n * sizeof(float)) {
         PLI_REQUIRE(((uintptr_t)ws & 15) == 0, "pli_gemm_swiglu_ws: workspace must be 16-byte aligned");
         if (dtype == PLI_BF16)

@@ -42,6 +42,8 @@ _SIGS = {
     "pli_gemm_swiglu_workspace_size": [_c_int, _c_int, _c_int, _c_int],
     "pli_gemm_swiglu_ws": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_i64, _c_i64, _c_i64,
                            _c_i64, _c_int, _vp, ctypes.c_size_t, _vp],
+    "pli_gemm_swiglu_ws_variant": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_i64, _c_i64,
+                                   _c_i64, _c_i64, _c_int, _vp, ctypes.c_size_t, _vp, _c_int],
     "pli_gemm_swiglu": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_i64, _c_i64, _c_i64,
                         _c_i64, _c_int, _vp],
     "pli_rmsnorm": [_vp, _vp, _vp, _vp, _vp, _c_i64, _c_int, _c_i64, _c_i64, _c_i64, _c_i64,
@@ -535,7 +537,8 @@ def rms_qkv_into_cache(a: torch.Tensor, norm_weight: torch.Tensor, eps: float,
 
 # ------------------------------------------------------------ fused SwiGLU
 def gemm_swiglu(x: torch.Tensor, w_gate: torch.Tensor, w_up: torch.Tensor,
-                out: torch.Tensor | None = None, split_k: bool = True) -> torch.Tensor:
+                out: torch.Tensor | None = None, split_k: bool = True,
+                variant: int | None = None) -> torch.Tensor:
     """h = silu(x W_gate^T) * (x W_up^T) in one launch; x [m, k], W_* [n, k]
     (unit column stride; any row stride, e.g. the two halves of a fused
     gate_up weight)."""
@@ -556,7 +559,10 @@ def gemm_swiglu(x: torch.Tensor, w_gate: torch.Tensor, w_up: torch.Tensor,
             w_up.stride(0), out.stride(0), _dtype_code(x))
     with _on_device(dev):
         wsb = lib().pli_gemm_swiglu_workspace_size(m, n, k, _dtype_code(x)) if split_k else 0
-        if wsb:
+        if wsb and variant is not None:
+            ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+            rc = lib().pli_gemm_swiglu_ws_variant(*head, _ptr(ws), wsb, _stream(dev), int(variant))
+        elif wsb:
             ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
             rc = lib().pli_gemm_swiglu_ws(*head, _ptr(ws), wsb, _stream(dev))
         else:

@@ -473,6 +473,26 @@ def tune_moe_grouped():
                           "rel_diff_v1_v2": diff}), flush=True)
 
 
+def tune_swiglu_routes():
+    """SwiGLU decode-batch routes on the same shapes: default, forced split-K
+    (variant 1), never split (2), torch (2 GEMMs + silu * mul)."""
+    import torch.nn.functional as F
+    shapes = [tuple(int(x) for x in sh.split("x")) for sh in os.environ.get(
+        "PLI_SWIGLU_SHAPES", "32x5632x2048,64x5632x2048,128x5632x2048,32x14336x4096,32x1792x4096,128x1792x4096").split(",")]
+    for (m, n, k) in shapes:
+        x = torch.randn(m, k, device="cuda", dtype=torch.bfloat16)
+        wg = torch.randn(n, k, device="cuda", dtype=torch.bfloat16) * k ** -0.5
+        wu = torch.randn(n, k, device="cuda", dtype=torch.bfloat16) * k ** -0.5
+        out = torch.empty(m, n, device="cuda", dtype=torch.bfloat16)
+        fns = {"default": lambda: pli_hip.gemm_swiglu(x, wg, wu, out=out),
+               "split": lambda: pli_hip.gemm_swiglu(x, wg, wu, out=out, variant=1),
+               "nosplit": lambda: pli_hip.gemm_swiglu(x, wg, wu, out=out, variant=2),
+               "torch": lambda: torch.mul(F.silu(x @ wg.t()), x @ wu.t(), out=out)}
+        t = interleave(fns, 10, 3)
+        print(json.dumps({"kernel": "swiglu_routes", "m": m, "n": n, "k": k,
+                          "us": {kk: round(v[0] * 1e3, 1) for kk, v in t.items()}}), flush=True)
+
+
 if __name__ == "__main__":
     what = sys.argv[1:] or ["hbm", "gemv", "flash", "gemm"]
     if "hbm" in what:
@@ -494,6 +514,8 @@ if __name__ == "__main__":
         tune_midm()
     if "moeg" in what:
         tune_moe_grouped()
+    if "swr" in what:
+        tune_swiglu_routes()
     if "gemmshapes" in what:
         tune_gemm_shapes()
     if "decode" in what:
