@@ -198,8 +198,12 @@ def bench_tp(stream, world: int, rank: int, iters: int) -> dict:
     for _ in range(2):
         gemm()
     ms_gemm = event_time_ms(gemm, iters, stream)
+    tl = lambda: torch.nn.functional.linear(x, w)  # noqa: E731  (hipBLASLt, same shapes)
+    tl()
+    ms_torch = event_time_ms(tl, iters, stream)
     out = {"workload": f"ch09 RowParallel 8192x8192 TP={world}, M={M}, bf16",
-           "gemm_us": ms_gemm * 1e3, "gemm_TFLOP/s": 2 * M * N * kl / (ms_gemm * 1e-3) / 1e12}
+           "gemm_us": ms_gemm * 1e3, "gemm_TFLOP/s": 2 * M * N * kl / (ms_gemm * 1e-3) / 1e12,
+           "torch_F.linear_TFLOP/s": 2 * M * N * kl / (ms_torch * 1e-3) / 1e12}
     # also M in {1, 128} (decode batches; W streamed from HBM)
     small = {}
     for m in (1, 128):
@@ -208,8 +212,11 @@ def bench_tp(stream, world: int, rank: int, iters: int) -> dict:
         fs = lambda: pli_hip.gemm(xs, w, trans_b=True, out=ys)  # noqa: E731
         fs()
         ms = event_time_ms(fs, 20, stream)
+        tls = lambda: torch.nn.functional.linear(xs, w)  # noqa: E731
+        tls()
+        ms_t = event_time_ms(tls, 20, stream)
         small[str(m)] = {"gemm_us": ms * 1e3, "weight_GB/s": N * kl * 2 / (ms * 1e-3) / 1e9,
-                         "TFLOP/s": 2 * m * N * kl / (ms * 1e-3) / 1e12}
+                         "TFLOP/s": 2 * m * N * kl / (ms * 1e-3) / 1e12, "torch_F.linear_us": ms_t * 1e3}
     out["small_m"] = small
     if world > 1:
         def ar():
