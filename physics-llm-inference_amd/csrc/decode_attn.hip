@@ -348,9 +348,17 @@ struct DecPlan {
     int chunk, splits;
 };
 constexpr int64_t kDefaultTargetWgs = 1024;
+// Short caches (<= kNoSplitKeys keys) with >= kNoSplitWgs (batch, kv head)
+// pairs take one chunk per pair: the combine launch (~4.7 us) costs more than
+// the serial key loop it saves (graph decode step, batch 32, 560-key cache:
+// 1.279 -> 1.246 ms/token); with few pairs the split stays (batch 1: 8
+// one-chunk workgroups ran 0.715 vs 0.681 ms/token).
+constexpr int kNoSplitKeys = 1024, kNoSplitWgs = 128;
 DecPlan plan_decode(int64_t bh, int n_kv, int64_t kTargetWgs = kDefaultTargetWgs) {
     const int64_t max_splits = cdiv(n_kv, DEC_QUANT);
-    int64_t splits = bh >= kTargetWgs ? 1 : cdiv(kTargetWgs, bh);
+    int64_t splits = bh >= kTargetWgs || (n_kv <= kNoSplitKeys && bh >= kNoSplitWgs)
+                         ? 1
+                         : cdiv(kTargetWgs, bh);
     splits = splits < 1 ? 1 : (splits > max_splits ? max_splits : splits);
     const int chunk = (int)(cdiv(cdiv(n_kv, splits), DEC_QUANT) * DEC_QUANT);
     return {chunk, (int)cdiv(n_kv, chunk)};
