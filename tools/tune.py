@@ -1,7 +1,14 @@
 #!/usr/bin/env python3
 """A/B kernel variants in ONE process (interleaved rounds), GPU box only.
 
-    python tools/tune.py [flash] [gemv] [hbm] [gemm]
+    python tools/tune.py [leg ...]   (default: hbm gemv flash gemm)
+
+Legs: hbm (copy ceiling), gemv / bgemv / gemvsweep (decode GEMV), flash /
+flash64 (prefill variants, PLI_FLASH_VARIANTS), gemm / gemmshapes (256-tile
+schedules, PLI_GEMM_VARIANTS / PLI_GEMM_SHAPES), midm (decode-batch and
+few-tile NT routes), swiglu / swr (fused SwiGLU, decode-batch routes), moe /
+moeg (MoE layer, grouped expert GEMM routes), decode (decode attention
+modes), graph (HIP-graph decode step at batch 1 / 8 / 32).
 
 Prints one JSON object per measurement; correctness of every variant is
 checked against variant 0 (and flash against the f64 oracle on one head).
