@@ -2167,11 +2167,17 @@ static int gemm_dispatch(const void* a, const void* b, void* c, const void* bias
         // 9-11: one-phase tile with grouped rasterization (group_m 4, 8, 16);
         // 12-15: phased SCHED 7 with group_m 8, 4, 2, 16
         // default (0): phased SCHED 7 with group_m 4 (= variant 13; NT 8192^3
-        // 1371-1414 vs 1145-1185 TF for the one-phase tile, NN 4096^3 1104 vs 935)
+        // 1371-1414 vs 1145-1185 TF for the ungrouped one-phase tile, NN 4096^3
+        // 1104 vs 935), except NT with K <= 4096 (below)
         int phased = variant == 3 ? 0 : (variant >= 5 && variant <= 8) ? 2 * (variant - 5) + 1 : -1;
         int group_m = 0;
         if (variant == 0) {
-            phased = 7;
+            // NT with K <= 4096: the one-phase tile, grouped (= variant 9;
+            // sustained, interleaved: 8192^2 x 1024 947 -> 1016 TF, x 2048
+            // 1109 -> 1166, 4096^3 1213 -> 1274, 4096 x 14336 x 4096 1109 ->
+            // 1179, profiles/r01/gemm/sustained.log); NN and deep K keep the
+            // phased schedule (NN 8192^3 1258 vs 1070)
+            phased = trans_b && k <= 4096 ? -1 : 7;
             group_m = 4;
         }
         if (variant >= 9 && variant <= 11) group_m = 4 << (variant - 9);
