@@ -236,12 +236,13 @@ int pli_kv_append(const void* k_new, const void* v_new, void* k_cache,
                   const int32_t* pos_dev, int dtype, void* stream);
 /* pli_gemm_multi_nt: the q, k and v projections of a decode step in one
  * launch, k / v written straight into the caches (fuses pli_kv_append).
- * Up to 3 groups share x [m, k] (m <= 16 rows = batch x tokens_per_batch);
+ * Up to 3 groups share x [m, k] (m <= 128 rows = batch x tokens_per_batch);
  * group g computes x W_g^T ([n_g, k] weights, ldw_g) and stores row
  * r = b * tokens_per_batch + s at
  *   c_g + b * stride_batch_g + (s + *row_offset_g) * stride_token_g (+ col),
  * row_offset_g a device int32 or NULL (= 0); rows >= capacity_g are dropped.
- * bf16/fp16, k % 8 == 0. */
+ * bf16/fp16, k % 8 == 0; m > 16 (small-M MFMA kernel) also needs k % 128 == 0,
+ * n_g % 16 == 0, strides % 4 == 0 and 8-byte aligned c_g. */
 int pli_gemm_multi_nt(const void* x, int64_t ldx, int m, int k,
                       int tokens_per_batch, const void* const* w,
                       void* const* c, const int* n, const int64_t* ldw,

@@ -77,10 +77,13 @@ class CachedGQA(nn.Module):
     def forward(self, x: torch.Tensor, cache: LayerKVCache | None = None, start_pos: int = 0
                 ) -> torch.Tensor:
         B, S, _ = x.shape
-        if (cache is not None and cache.pos is not None and x.is_cuda and B * S <= 16
+        if (cache is not None and cache.pos is not None and x.is_cuda
+                and (B * S <= 16 or (B * S <= 32 and x.shape[-1] % 128 == 0))
                 and _device_len_ok_shape(x, S, self.num_heads, self.num_kv_heads, self.head_dim)):
             # decode step, device-resident length: q/k/v projections in one
             # launch with k/v written straight into the cache rows at pos
+            # (skinny kernel up to 16 rows, small-M MFMA kernel up to 32: above
+            # that the mid-M kernel of the packed GEMM + the append win)
             q = torch.empty(B, S, self.num_heads * self.head_dim, device=x.device, dtype=x.dtype)
             pli_hip.qkv_into_cache(x, self.q_proj.weight, self.k_proj.weight, self.v_proj.weight,
                                    q, cache.k, cache.v, cache.pos)

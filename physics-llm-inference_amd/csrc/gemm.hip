@@ -981,7 +981,13 @@ int launch_skinny(const void* a, const void* b, void* c, const void* bias, int M
 // rows), X fragments come from L2.  Partial C^T tiles are summed through LDS.
 // SWIGLU: each wave streams the 16 rows of Wg (W) AND of Wu over its K range
 // into two accumulators per batch group; the epilogue writes silu(g) * u.
-template <typename T, int NBG, bool BIAS, bool SWIGLU = false>
+// MULTI (pli_gemm_multi_nt at 16 < m <= 128): the columns are the
+// concatenated groups of `margs` (each a multiple of 16 wide, so a workgroup's
+// 16 columns lie in one group) and row r = b * mtok + s of group g is stored
+// at c_g + b * stride_batch + (s + *row_offset) * stride_token, as
+// gemm_skinny_multi does: the packed q/k/v GEMM writes k / v straight into
+// the caches.
+template <typename T, int NBG, bool BIAS, bool SWIGLU = false, bool MULTI = false>
 __global__ __launch_bounds__(256) void gemm_smallm_nt(const uint16_t* __restrict__ X,
                                                       const uint16_t* __restrict__ W,
                                                       uint16_t* __restrict__ C,
@@ -989,12 +995,20 @@ __global__ __launch_bounds__(256) void gemm_smallm_nt(const uint16_t* __restrict
                                                       int N, int K, int64_t ldx, int64_t ldw,
                                                       int64_t ldc,
                                                       const uint16_t* __restrict__ Wu = nullptr,
-                                                      int64_t ldwu = 0) {
+                                                      int64_t ldwu = 0, MultiArgs margs = {},
+                                                      int mtok = 1) {
     constexpr int NW = SWIGLU ? 2 : 1;     // weight matrices streamed
     constexpr int U = SWIGLU ? 4 : 8;      // k-steps issued ahead per wave (8 KiB of W in flight)
     __shared__ __attribute__((aligned(16))) float part[4][NBG][NW][4][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int n0 = blockIdx.x * 16;
+    int n0 = blockIdx.x * 16;
+    int gsel = 0;
+    if constexpr (MULTI) {  // the host sizes the grid to the groups' total width
+        while (gsel < margs.ngroups - 1 && n0 >= margs.g[gsel].n) n0 -= margs.g[gsel++].n;
+        W = margs.g[gsel].w;
+        ldw = margs.g[gsel].ldw;
+        N = margs.g[gsel].n;
+    }
     const int r16 = lane & 15, kq = 8 * (lane >> 4);
     const int kw = K / 4;  // this wave's K range
     const uint16_t* wp[NW];
@@ -1058,7 +1072,13 @@ __global__ __launch_bounds__(256) void gemm_smallm_nt(const uint16_t* __restrict
                 v[r] = silu_mul(v[r], part[0][gi][NW - 1][r][lane] + part[1][gi][NW - 1][r][lane] +
                                           part[2][gi][NW - 1][r][lane] + part[3][gi][NW - 1][r][lane]);
         }
-        if (bt < M && nr < N) {
+        if constexpr (MULTI) {
+            const MultiGroup& G = margs.g[gsel];
+            const int b = bt / mtok, srow = bt % mtok + (G.row_offset ? *G.row_offset : 0);
+            if (bt < M && nr < N && srow < G.capacity)
+                *reinterpret_cast<i32x2*>(G.c + b * G.stride_batch + (int64_t)srow * G.stride_token + nr) =
+                    i32x2{(int)pack2<T>(v[0], v[1]), (int)pack2<T>(v[2], v[3])};
+        } else if (bt < M && nr < N) {
             if constexpr (BIAS) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) v[r] += elem<T>::to_f32(T{bias[nr + r]});
@@ -2366,20 +2386,46 @@ extern "C" int pli_gemm_multi_nt(const void* x, int64_t ldx, int m, int k, int t
     PLI_REQUIRE(x && w && c && n && ldw && stride_batch && stride_token && row_offset && capacity,
                 "pli_gemm_multi_nt: null pointer");
     PLI_REQUIRE(ngroups >= 1 && ngroups <= 3, "pli_gemm_multi_nt: 1..3 groups, got %d", ngroups);
-    PLI_REQUIRE(m >= 1 && m <= 16 && k > 0 && k % 8 == 0 && ldx >= k && ldx % 8 == 0 &&
+    PLI_REQUIRE(m >= 1 && m <= 128 && k > 0 && k % 8 == 0 && ldx >= k && ldx % 8 == 0 &&
                     tokens_per_batch >= 1 && m % tokens_per_batch == 0 && al16(x),
-                "pli_gemm_multi_nt: needs 1 <= m <= 16 rows (whole batches), k %% 8 == 0, aligned x");
+                "pli_gemm_multi_nt: needs 1 <= m <= 128 rows (whole batches), k %% 8 == 0, aligned x");
+    PLI_REQUIRE(m <= 16 || k % 128 == 0, "pli_gemm_multi_nt: m > 16 needs k %% 128 == 0");
     PLI_REQUIRE(dtype == PLI_BF16 || dtype == PLI_F16, "pli_gemm_multi_nt: bf16/fp16 only");
     MultiArgs args{};
     int ntot = 0;
     for (int g = 0; g < ngroups; ++g) {
         PLI_REQUIRE(w[g] && c[g] && n[g] > 0 && ldw[g] >= k && ldw[g] % 8 == 0 && al16(w[g]),
                     "pli_gemm_multi_nt: bad group %d", g);
+        PLI_REQUIRE(m <= 16 || (n[g] % 16 == 0 && stride_batch[g] % 4 == 0 &&
+                                stride_token[g] % 4 == 0 && ((uintptr_t)c[g] & 7) == 0),
+                    "pli_gemm_multi_nt: m > 16 needs group widths %% 16 == 0 and 8-byte "
+                    "aligned output rows (group %d)", g);
         args.g[g] = MultiGroup{(const uint16_t*)w[g], (uint16_t*)c[g], n[g], ldw[g],
                                stride_batch[g], stride_token[g], row_offset[g], capacity[g]};
         ntot += n[g];
     }
     args.ngroups = ngroups;
+    if (m > 16) {
+        // 16 < m <= 128: the small-M MFMA kernel with the per-group row
+        // addressing in its epilogue (one launch for q/k/v + the cache append)
+        hipStream_t st = (hipStream_t)stream;
+        const dim3 grid(ntot / 16), block(256);
+        const auto* X = (const uint16_t*)x;
+#define PLI_MSM(TT, G)                                                                        \
+    hipLaunchKernelGGL((gemm_smallm_nt<TT, G, false, false, true>), grid, block, 0, st, X,     \
+                       nullptr, nullptr, nullptr, m, 0, k, ldx, 0, 0, nullptr, 0, args,         \
+                       tokens_per_batch)
+#define PLI_MSM_G(TT)                          \
+    do {                                       \
+        if (m <= 32) PLI_MSM(TT, 2);           \
+        else if (m <= 64) PLI_MSM(TT, 4);      \
+        else PLI_MSM(TT, 8);                   \
+    } while (0)
+        if (dtype == PLI_BF16) PLI_MSM_G(bf16_t); else PLI_MSM_G(f16_t);
+#undef PLI_MSM_G
+#undef PLI_MSM
+        return launch_status("pli_gemm_multi_nt<smallm>");
+    }
     const dim3 grid(cdiv(ntot, 2)), block(128);
     hipStream_t s = (hipStream_t)stream;
     const auto* X = (const uint16_t*)x;

@@ -412,8 +412,9 @@ def qkv_into_cache(x: torch.Tensor, wq: torch.Tensor, wk: torch.Tensor, wv: torc
                    q_out: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
                    pos: torch.Tensor) -> torch.Tensor:
     """Decode-step projections in one launch (pli_gemm_multi_nt): x [B, S, hidden]
-    (B*S <= 16) -> q_out [B, S, Hq*D]; k / v rows written into [B, S_max, Hkv, D]
-    caches at rows pos[0] + s.  Returns q_out."""
+    (B*S <= 128; above 16 rows hidden % 128 == 0) -> q_out [B, S, Hq*D]; k / v
+    rows written into [B, S_max, Hkv, D] caches at rows pos[0] + s.  Returns
+    q_out."""
     dev = _require_gpu(x, wq, wk, wv, q_out, k_cache, v_cache)
     B, S, hidden = x.shape
     x2 = x.reshape(B * S, hidden)

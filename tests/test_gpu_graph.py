@@ -41,10 +41,12 @@ def test_attn_decode_dev_equals_host_length(n, add):
     assert (got.float() - ref.float()).abs().max().item() <= 2 ** -7
 
 
-@pytest.mark.parametrize("B,S", [(1, 1), (2, 1), (4, 4), (16, 1), (3, 5)])
+@pytest.mark.parametrize("B,S", [(1, 1), (2, 1), (4, 4), (16, 1), (3, 5),
+                                 (17, 1), (32, 1), (8, 4), (5, 5), (64, 1), (3, 40), (128, 1)])
 def test_qkv_into_cache_matches_separate_projections(B, S):
     """pli_gemm_multi_nt: q plus k/v rows written into the caches at pos ==
-    three pli_gemm calls + pli_kv_append; rows past the capacity dropped."""
+    three pli_gemm calls + pli_kv_append; rows past the capacity dropped.
+    Up to 16 rows the skinny kernel, 17-128 the small-M MFMA kernel."""
     import pli_hip
     torch.manual_seed(B * 10 + S)
     hidden, H, Hkv, D, S_max = 1024, 16, 4, 64, 40
@@ -80,12 +82,14 @@ def _model():
     return CachedTransformerModel(1000, 512, 2, 8, 2, 1024).cuda().bfloat16().eval()
 
 
-def test_decode_step_graph_replays_eager_steps():
+@pytest.mark.parametrize("B", [2, 24])
+def test_decode_step_graph_replays_eager_steps(B):
     """Greedy decode: graph replay == eager steps over the same device-length
-    kernels (bitwise), and tracks the host-length eager path."""
+    kernels (bitwise), and tracks the host-length eager path (batch 24: q/k/v
+    and the cache append in one small-M launch)."""
     from ch08 import DecodeStepGraph
     model = _model()
-    B, P, N = 2, 24, 12
+    P, N = 24, 12
     ids = torch.randint(0, 1000, (B, P), device="cuda")
     with torch.no_grad():
         # eager, device-length caches
