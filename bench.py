@@ -240,6 +240,38 @@ def bench_tp(stream, world: int, rank: int, iters: int) -> dict:
     return out
 
 
+def bench_decode_step(batches=(1, 32), prompt: int = 512, steps: int = 32) -> dict:
+    """ch02 decode step of a Llama-shaped 0.85B model (vocab 32000, hidden
+    2048, 16 layers, 32/8 heads, intermediate 5632, random bf16 weights) as
+    one HIP-graph launch per token (ch08.DecodeStepGraph): per-token latency
+    over `steps` replays after a `prompt`-token prefill, host loop included."""
+    from ch02 import CachedTransformerModel
+    from ch08 import DecodeStepGraph
+    torch.manual_seed(0)
+    model = CachedTransformerModel(32000, 2048, 16, 32, 8, 5632).cuda().bfloat16().eval()
+    out = {"workload": "ch02/ch08 decode step, 0.85B Llama shape, bf16, HIP graph per token",
+           "prompt": prompt, "timing": f"perf_counter over {steps} replays after 1 warm replay"}
+    with torch.no_grad():
+        for B in batches:
+            ids = torch.randint(0, 32000, (B, prompt), device="cuda")
+            tok = torch.randint(0, 32000, (B, 1), device="cuda")
+            g = DecodeStepGraph(model, B, prompt + steps + 8, torch.bfloat16)
+            g.prefill(ids)
+            g.step(tok)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                g.step(tok)
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) / steps * 1e3
+            out[f"batch{B}_ms_per_token"] = ms
+            out[f"batch{B}_tok/s"] = B / (ms * 1e-3)
+            del g
+    del model
+    torch.cuda.empty_cache()
+    return out
+
+
 def cpu_baseline(seconds: float = 15.0) -> dict:
     """The reference tile loop (oracle restatement, torch CPU) on a sample of
     the flash workload: B=1 (1/8 of the batch), all 32 heads, S=4096, D=128."""
@@ -384,6 +416,8 @@ def main():
         extra["decode_attn"] = bench_decode(stream, 20)
         extra["gemm"] = bench_gemm(stream, 20)
         extra["tp_gemm"] = bench_tp(stream, world, rank, 10)
+        if world == 1:
+            extra["decode_step"] = bench_decode_step()
     else:
         extra["gemv"] = bench_gemv(stream, 200)
         if args.with_decode:
