@@ -64,6 +64,20 @@ def event_time_ms(fn, iters: int, stream) -> float:
     return s.elapsed_time(e) / iters
 
 
+def paired_time_ms(fns: dict, iters: int, stream, rounds: int = 3, warm: int = 5) -> dict:
+    """Median over `rounds` of event_time_ms per callable, the callables
+    interleaved round by round after `warm` calls each, so that neither side
+    of a comparison pays the clock ramp of the first measurement."""
+    for fn in fns.values():
+        for _ in range(warm):
+            fn()
+    res = {k: [] for k in fns}
+    for _ in range(rounds):
+        for k, fn in fns.items():
+            res[k].append(event_time_ms(fn, iters, stream))
+    return {k: sorted(v)[len(v) // 2] for k, v in res.items()}
+
+
 def load_traffic(kernel: str):
     """Per-launch HBM bytes of ``kernel`` from the committed rocprofv3 PMC
     summary (profiles/traffic.json), or None."""
@@ -173,13 +187,12 @@ def bench_gemm(stream, iters: int) -> dict:
     a = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
     b = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
     c = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
-    for _ in range(3):
-        pli_hip.gemm(a, b, out=c)
-        torch.mm(a, b)
-    ms = event_time_ms(lambda: pli_hip.gemm(a, b, out=c), iters, stream)
+    t = paired_time_ms({"ours": lambda: pli_hip.gemm(a, b, out=c), "torch": lambda: torch.mm(a, b)},
+                       iters, stream)
+    ms, ms_t = t["ours"], t["torch"]
     tf = 2 * n ** 3 / (ms * 1e-3) / 1e12
-    ms_t = event_time_ms(lambda: torch.mm(a, b), iters, stream)
     return {"workload": "ch05/ch03 GEMM 4096^3 bf16 NN", "us_per_launch": ms * 1e3,
+            "timing": f"events, median of 3 interleaved rounds of {iters} launches (ours / torch)",
             "TFLOP/s": tf, "torch_mm_TFLOP/s": 2 * n ** 3 / (ms_t * 1e-3) / 1e12,
             "roofline": {"bound": "mfma", "achieved": tf, "peak": PEAK_BF16_TFLOPS,
                          "unit": "TFLOP/s", "frac": tf / PEAK_BF16_TFLOPS}}
@@ -195,13 +208,11 @@ def bench_tp(stream, world: int, rank: int, iters: int) -> dict:
     w = torch.randn(N, kl, device="cuda", dtype=torch.bfloat16) * kl ** -0.5
     y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
     gemm = lambda: pli_hip.gemm(x, w, trans_b=True, out=y)  # noqa: E731
-    for _ in range(2):
-        gemm()
-    ms_gemm = event_time_ms(gemm, iters, stream)
     tl = lambda: torch.nn.functional.linear(x, w)  # noqa: E731  (hipBLASLt, same shapes)
-    tl()
-    ms_torch = event_time_ms(tl, iters, stream)
+    t = paired_time_ms({"ours": gemm, "torch": tl}, iters, stream)
+    ms_gemm, ms_torch = t["ours"], t["torch"]
     out = {"workload": f"ch09 RowParallel 8192x8192 TP={world}, M={M}, bf16",
+           "timing": f"events, median of 3 interleaved rounds of {iters} launches (ours / torch)",
            "gemm_us": ms_gemm * 1e3, "gemm_TFLOP/s": 2 * M * N * kl / (ms_gemm * 1e-3) / 1e12,
            "torch_F.linear_TFLOP/s": 2 * M * N * kl / (ms_torch * 1e-3) / 1e12}
     # also M in {1, 128} (decode batches; W streamed from HBM)
@@ -210,11 +221,9 @@ def bench_tp(stream, world: int, rank: int, iters: int) -> dict:
         xs = torch.randn(m, kl, device="cuda", dtype=torch.bfloat16)
         ys = torch.empty(m, N, device="cuda", dtype=torch.bfloat16)
         fs = lambda: pli_hip.gemm(xs, w, trans_b=True, out=ys)  # noqa: E731
-        fs()
-        ms = event_time_ms(fs, 20, stream)
         tls = lambda: torch.nn.functional.linear(xs, w)  # noqa: E731
-        tls()
-        ms_t = event_time_ms(tls, 20, stream)
+        t = paired_time_ms({"ours": fs, "torch": tls}, 20, stream)
+        ms, ms_t = t["ours"], t["torch"]
         small[str(m)] = {"gemm_us": ms * 1e3, "weight_GB/s": N * kl * 2 / (ms * 1e-3) / 1e9,
                          "TFLOP/s": 2 * m * N * kl / (ms * 1e-3) / 1e12, "torch_F.linear_us": ms_t * 1e3}
     out["small_m"] = small
