@@ -70,12 +70,13 @@ def test_argument_validation_without_gpu(built_lib):
     st_dec = (ctypes.c_int64 * 12)(*([8] * 12))
     rc = L.pli_attn_decode(p, p, p, p, 1, 32, 8, 1, 32768, 128, st_dec, 0.1, 0, None, need - 1, 2, None)
     assert rc == EINVAL and b"workspace" in L.pli_last_error()
-    # fused decode projection: at most 16 rows, whole batches, 1..3 groups
+    # fused decode projection: at most 128 rows (k % 128 == 0 past 16), whole batches, 1..3 groups
     P3, I3, L3 = ctypes.c_void_p * 3, ctypes.c_int * 3, ctypes.c_int64 * 3
     w3, n3, ld3 = P3(16, 16, 16), I3(64, 64, 64), L3(64, 64, 64)
     multi = lambda m, tpb, ng: L.pli_gemm_multi_nt(p, 64, m, 64, tpb, w3, w3, n3, ld3, ld3, ld3,
                                                    P3(None, None, None), I3(9, 9, 9), ng, 2, None)
-    assert multi(17, 1, 3) == EINVAL and b"m <= 16" in L.pli_last_error()
+    assert multi(129, 1, 3) == EINVAL and b"m <= 128" in L.pli_last_error()
+    assert multi(17, 1, 3) == EINVAL and b"k % 128" in L.pli_last_error()  # k = 64
     assert multi(6, 4, 3) == EINVAL  # 6 rows are not whole batches of 4
     assert multi(4, 1, 4) == EINVAL and b"groups" in L.pli_last_error()
     # fused norm + projection: <= 4 rows, k <= 8192
