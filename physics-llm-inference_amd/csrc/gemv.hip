@@ -106,14 +106,16 @@ __global__ __launch_bounds__(256) void gemv_scalar(const T* __restrict__ w, cons
 // per k-step x non-temporal W loads.
 //   0: 2x8 nt  1: 4x8 nt  2: 1x8 nt  3: 2x8 plain  4: 4x4 nt  5: 8x4 nt
 //   6: 2x8 nt, 1-wave blocks   7: 2x8 nt, 8-wave blocks   8: 1x8 nt, 2-wave blocks
-// Default: 8 (1 row per wave, 2-wave blocks); for tall W (M >= 16384, e.g. the
-// 32000x2048 LM head) variant 0 (2 rows per wave, 4-wave blocks): median of 5
-// interleaved rounds, HBM-resident W, tools/gemv_vs_skinny.py (gv.log):
-// 32000x2048 5718 vs 5051 GB/s; at M <= 8192 variant 8 is equal or ahead
-// (8192^2 5857 vs 5594, 4096^2 4434 vs 4248).
+//   9: 1x4 nt, 2-wave blocks  10: 2x4 nt, 4-wave blocks  11: 1x4 nt, 4-wave blocks
+// Default: 8 (1 row per wave, 2-wave blocks).  Tall W with short rows
+// (M >= 16384, at most 256 16-byte chunks per row, e.g. the 32000 x 2048 LM
+// head): variant 9 (4 chunks per lane, so all 64 lanes carry a 4 KiB row):
+// 6.35 vs 5.03 TB/s (median of 5 interleaved rounds, HBM-resident W,
+// tools/gemv_vs_skinny.py, profiles/r01/gemm/gemv_variants_kshort.log).
 constexpr int kDefaultGemvVariant = 8;
-constexpr int kTallGemvVariant = 0;
+constexpr int kTallShortGemvVariant = 9;
 constexpr int kTallGemvRows = 16384;
+constexpr int kShortRowChunks = 256;
 
 template <typename T, int ROWS, int CPL, bool NTL, int WPB = 4>
 int launch_vec(const void* w, const void* x, void* y, int m, int nchunks, int64_t ldw_b,
@@ -137,7 +139,9 @@ int launch(const void* w, const void* x, void* y, int m, int k, int64_t ldw, hip
     }
     const int nchunks = k / EPC;
     const int64_t ldw_b = ldw * elem<T>::bytes;
-    if (variant < 0) variant = m >= kTallGemvRows ? kTallGemvVariant : kDefaultGemvVariant;
+    if (variant < 0)
+        variant = (m >= kTallGemvRows && nchunks <= kShortRowChunks) ? kTallShortGemvVariant
+                                                                    : kDefaultGemvVariant;
     switch (variant) {
         case 0: return launch_vec<T, 2, 8, true>(w, x, y, m, nchunks, ldw_b, s);
         case 1: return launch_vec<T, 4, 8, true>(w, x, y, m, nchunks, ldw_b, s);
@@ -148,6 +152,9 @@ int launch(const void* w, const void* x, void* y, int m, int k, int64_t ldw, hip
         case 6: return launch_vec<T, 2, 8, true, 1>(w, x, y, m, nchunks, ldw_b, s);
         case 7: return launch_vec<T, 2, 8, true, 8>(w, x, y, m, nchunks, ldw_b, s);
         case 8: return launch_vec<T, 1, 8, true, 2>(w, x, y, m, nchunks, ldw_b, s);
+        case 9: return launch_vec<T, 1, 4, true, 2>(w, x, y, m, nchunks, ldw_b, s);
+        case 10: return launch_vec<T, 2, 4, true, 4>(w, x, y, m, nchunks, ldw_b, s);
+        case 11: return launch_vec<T, 1, 4, true, 4>(w, x, y, m, nchunks, ldw_b, s);
         default: set_error("pli_gemv: unknown variant %d", variant); return PLI_EINVAL;
     }
 }
