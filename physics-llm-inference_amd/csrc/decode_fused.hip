@@ -56,7 +56,9 @@ __global__ __launch_bounds__(256) void rms_gemm_skinny(const uint16_t* __restric
     extern __shared__ __attribute__((aligned(16))) char dsm[];  // y [M][K]
     __shared__ float red[4];
     constexpr int NWT = SW ? 2 : 1;
-    constexpr int CPL = SW ? 4 : 8;
+    // RPT == 1 <=> K <= 2048 (<= 256 chunks): 4 chunks per lane cover the row with
+    // all 64 lanes (same per-lane chunk order as 8, so bitwise the same result)
+    constexpr int CPL = (SW || RPT == 1) ? 4 : 8;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nch = K / 8;
     uint16_t* xs = reinterpret_cast<uint16_t*>(dsm);

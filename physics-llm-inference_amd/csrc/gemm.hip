@@ -887,11 +887,10 @@ struct MultiArgs {
     int ngroups;
 };
 
-template <typename T, int NB>
+template <typename T, int NB, int CPL = 8>
 __global__ __launch_bounds__(128) void gemm_skinny_multi(const uint16_t* __restrict__ X, int M,
                                                          int S, int nchunks, int64_t ldx,
                                                          MultiArgs args) {
-    constexpr int CPL = 8;
     const int lane = threadIdx.x & 63;
     int n = blockIdx.x * 2 + (threadIdx.x >> 6);
     int gi = 0;
@@ -957,8 +956,11 @@ int launch_skinny(const void* a, const void* b, void* c, const void* bias, int M
     // lane rounded up to 4, at least 8), so a wave waits on HBM once.  With
     // CPL 8, a 5632-column row takes two round trips. That row is the decode
     // step's down projection, where CPL 12 cuts 9.1 us to 8.3 us per launch.
+    // K <= 2048 (<= 256 chunks): CPL 4, all 64 lanes carry the row (the same
+    // per-lane chunk order as CPL 8, whose upper half would be masked off).
 #define PLI_SKINNY_CPL(NB)                    \
-    if (nch <= 512) PLI_SKINNY(NB, 8);        \
+    if (nch <= 256) PLI_SKINNY(NB, 4);        \
+    else if (nch <= 512) PLI_SKINNY(NB, 8);   \
     else if (nch <= 768) PLI_SKINNY(NB, 12);  \
     else if (nch <= 1024) PLI_SKINNY(NB, 16); \
     else PLI_SKINNY(NB, 8);
@@ -2430,8 +2432,13 @@ extern "C" int pli_gemm_multi_nt(const void* x, int64_t ldx, int m, int k, int t
     hipStream_t s = (hipStream_t)stream;
     const auto* X = (const uint16_t*)x;
     const int nch = k / 8;
-#define PLI_MULTI(TT, NB) \
-    hipLaunchKernelGGL((gemm_skinny_multi<TT, NB>), grid, block, 0, s, X, m, tokens_per_batch, nch, ldx, args)
+#define PLI_MULTI(TT, NB)                                                                              \
+    do {                                                                                               \
+        if (nch <= 256) /* K <= 2048: 4 chunks per lane, same chunk order */                          \
+            hipLaunchKernelGGL((gemm_skinny_multi<TT, NB, 4>), grid, block, 0, s, X, m, tokens_per_batch, nch, ldx, args); \
+        else                                                                                           \
+            hipLaunchKernelGGL((gemm_skinny_multi<TT, NB>), grid, block, 0, s, X, m, tokens_per_batch, nch, ldx, args); \
+    } while (0)
 #define PLI_MULTI_NB(TT)                  \
     do {                                  \
         if (m <= 1) PLI_MULTI(TT, 1);     \
