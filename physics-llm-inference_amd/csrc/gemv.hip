@@ -107,6 +107,7 @@ __global__ __launch_bounds__(256) void gemv_scalar(const T* __restrict__ w, cons
 //   0: 2x8 nt  1: 4x8 nt  2: 1x8 nt  3: 2x8 plain  4: 4x4 nt  5: 8x4 nt
 //   6: 2x8 nt, 1-wave blocks   7: 2x8 nt, 8-wave blocks   8: 1x8 nt, 2-wave blocks
 //   9: 1x4 nt, 2-wave blocks  10: 2x4 nt, 4-wave blocks  11: 1x4 nt, 4-wave blocks
+//  12: 1x8 nt, 1-wave blocks  13: 1x8 nt, 4-wave blocks  14: 1x8 plain, 2-wave blocks
 // Default: 8 (1 row per wave, 2-wave blocks).  Tall W with short rows
 // (M >= 16384, at most 256 16-byte chunks per row, e.g. the 32000 x 2048 LM
 // head): variant 9 (4 chunks per lane, so all 64 lanes carry a 4 KiB row):
@@ -155,6 +156,9 @@ int launch(const void* w, const void* x, void* y, int m, int k, int64_t ldw, hip
         case 9: return launch_vec<T, 1, 4, true, 2>(w, x, y, m, nchunks, ldw_b, s);
         case 10: return launch_vec<T, 2, 4, true, 4>(w, x, y, m, nchunks, ldw_b, s);
         case 11: return launch_vec<T, 1, 4, true, 4>(w, x, y, m, nchunks, ldw_b, s);
+        case 12: return launch_vec<T, 1, 8, true, 1>(w, x, y, m, nchunks, ldw_b, s);
+        case 13: return launch_vec<T, 1, 8, true, 4>(w, x, y, m, nchunks, ldw_b, s);
+        case 14: return launch_vec<T, 1, 8, false, 2>(w, x, y, m, nchunks, ldw_b, s);
         default: set_error("pli_gemv: unknown variant %d", variant); return PLI_EINVAL;
     }
 }
