@@ -108,12 +108,18 @@ __global__ __launch_bounds__(256) void gemv_scalar(const T* __restrict__ w, cons
 //   6: 2x8 nt, 1-wave blocks   7: 2x8 nt, 8-wave blocks   8: 1x8 nt, 2-wave blocks
 //   9: 1x4 nt, 2-wave blocks  10: 2x4 nt, 4-wave blocks  11: 1x4 nt, 4-wave blocks
 //  12: 1x8 nt, 1-wave blocks  13: 1x8 nt, 4-wave blocks  14: 1x8 plain, 2-wave blocks
-// Default: 8 (1 row per wave, 2-wave blocks).  Tall W with short rows
-// (M >= 16384, at most 256 16-byte chunks per row, e.g. the 32000 x 2048 LM
-// head): variant 9 (4 chunks per lane, so all 64 lanes carry a 4 KiB row):
-// 6.35 vs 5.03 TB/s (median of 5 interleaved rounds, HBM-resident W,
-// tools/gemv_vs_skinny.py, profiles/r01/gemm/gemv_variants_kshort.log).
+//  15: 1x2 nt, 2-wave blocks  16: 2x2 nt, 4-wave blocks
+// Default: 8 (1 row per wave, 2-wave blocks, 8 chunks per lane).  Short rows
+// leave lanes idle at 8 chunks per lane, so (median of 5 interleaved rounds,
+// HBM-resident W, tools/gemv_vs_skinny.py, profiles/r01/gemm/gemv_*.log):
+//  * <= 128 16-byte chunks per row (K <= 1024 bf16): variant 16 (2 rows x 2
+//    chunks per lane): 32000x1024 4.58 -> 5.69 TB/s, 16384x1024 2.62 -> 4.71,
+//    8192x1024 2.12 -> 2.66, equal at 4096x1024;
+//  * <= 256 chunks and M >= 16384 (the 32000 x 2048 LM head): variant 9 (4
+//    chunks per lane): 32000x2048 5.03 -> 6.36 TB/s, 128256x2048 5.51 -> 7.09.
 constexpr int kDefaultGemvVariant = 8;
+constexpr int kVeryShortRowVariant = 16;
+constexpr int kVeryShortRowChunks = 128;
 constexpr int kTallShortGemvVariant = 9;
 constexpr int kTallGemvRows = 16384;
 constexpr int kShortRowChunks = 256;
@@ -141,8 +147,9 @@ int launch(const void* w, const void* x, void* y, int m, int k, int64_t ldw, hip
     const int nchunks = k / EPC;
     const int64_t ldw_b = ldw * elem<T>::bytes;
     if (variant < 0)
-        variant = (m >= kTallGemvRows && nchunks <= kShortRowChunks) ? kTallShortGemvVariant
-                                                                    : kDefaultGemvVariant;
+        variant = nchunks <= kVeryShortRowChunks                        ? kVeryShortRowVariant
+                  : (m >= kTallGemvRows && nchunks <= kShortRowChunks) ? kTallShortGemvVariant
+                                                                       : kDefaultGemvVariant;
     switch (variant) {
         case 0: return launch_vec<T, 2, 8, true>(w, x, y, m, nchunks, ldw_b, s);
         case 1: return launch_vec<T, 4, 8, true>(w, x, y, m, nchunks, ldw_b, s);
@@ -159,6 +166,8 @@ int launch(const void* w, const void* x, void* y, int m, int k, int64_t ldw, hip
         case 12: return launch_vec<T, 1, 8, true, 1>(w, x, y, m, nchunks, ldw_b, s);
         case 13: return launch_vec<T, 1, 8, true, 4>(w, x, y, m, nchunks, ldw_b, s);
         case 14: return launch_vec<T, 1, 8, false, 2>(w, x, y, m, nchunks, ldw_b, s);
+        case 15: return launch_vec<T, 1, 2, true, 2>(w, x, y, m, nchunks, ldw_b, s);
+        case 16: return launch_vec<T, 2, 2, true, 4>(w, x, y, m, nchunks, ldw_b, s);
         default: set_error("pli_gemv: unknown variant %d", variant); return PLI_EINVAL;
     }
 }

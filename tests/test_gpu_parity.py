@@ -198,7 +198,9 @@ def test_ch06_reference_gpu_cases():
                                     (333, 1000, "bf16"), (128, 4104, "bf16"), (64, 37, "bf16"),
                                     (7, 8192, "fp16"), (8192, 8192, "bf16"),
                                     # tall W (M >= 16384: 2-rows-per-wave variant): LM head, odd M
-                                    (32000, 2048, "bf16"), (16385, 520, "fp16")])
+                                    (32000, 2048, "bf16"), (16385, 520, "fp16"),
+                                    # short rows (<= 128 chunks: 2 rows x 2 chunks per lane)
+                                    (8192, 1024, "bf16"), (1001, 512, "fp32"), (3, 1024, "fp16")])
 def test_gemv_vs_oracle(m, k, dt):
     import pli_hip
     w = seeded_normal((m, k), m + k, dt)
