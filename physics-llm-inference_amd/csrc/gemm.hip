@@ -956,10 +956,12 @@ int launch_skinny(const void* a, const void* b, void* c, const void* bias, int M
     // lane rounded up to 4, at least 8), so a wave waits on HBM once.  With
     // CPL 8, a 5632-column row takes two round trips. That row is the decode
     // step's down projection, where CPL 12 cuts 9.1 us to 8.3 us per launch.
-    // K <= 2048 (<= 256 chunks): CPL 4, all 64 lanes carry the row (the same
-    // per-lane chunk order as CPL 8, whose upper half would be masked off).
+    // K <= 1024 / 2048 (<= 128 / 256 chunks): CPL 2 / 4, all 64 lanes carry the
+    // row (the same per-lane chunk order as CPL 8, whose upper part would be
+    // masked off, so bitwise the same result).
 #define PLI_SKINNY_CPL(NB)                    \
-    if (nch <= 256) PLI_SKINNY(NB, 4);        \
+    if (nch <= 128) PLI_SKINNY(NB, 2);        \
+    else if (nch <= 256) PLI_SKINNY(NB, 4);   \
     else if (nch <= 512) PLI_SKINNY(NB, 8);   \
     else if (nch <= 768) PLI_SKINNY(NB, 12);  \
     else if (nch <= 1024) PLI_SKINNY(NB, 16); \
@@ -2434,7 +2436,9 @@ extern "C" int pli_gemm_multi_nt(const void* x, int64_t ldx, int m, int k, int t
     const int nch = k / 8;
 #define PLI_MULTI(TT, NB)                                                                              \
     do {                                                                                               \
-        if (nch <= 256) /* K <= 2048: 4 chunks per lane, same chunk order */                          \
+        if (nch <= 128) /* K <= 1024: 2 chunks per lane, same chunk order */                          \
+            hipLaunchKernelGGL((gemm_skinny_multi<TT, NB, 2>), grid, block, 0, s, X, m, tokens_per_batch, nch, ldx, args); \
+        else if (nch <= 256) /* K <= 2048: 4 chunks per lane */                                        \
             hipLaunchKernelGGL((gemm_skinny_multi<TT, NB, 4>), grid, block, 0, s, X, m, tokens_per_batch, nch, ldx, args); \
         else                                                                                           \
             hipLaunchKernelGGL((gemm_skinny_multi<TT, NB>), grid, block, 0, s, X, m, tokens_per_batch, nch, ldx, args); \

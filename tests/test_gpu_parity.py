@@ -293,6 +293,18 @@ def test_gemm_decode_batch_paths(m, n, k, dt, bias, variant):
     assert_lin_close(out, olin.linear(a, w, bb), dt, f"decode-batch gemm {m}x{n}x{k} v{variant}")
 
 
+# M <= 4 skinny NT path (gemm_skinny_nt): chunks per lane 2 / 4 / 8 / 12 chosen
+# by K; each side of every boundary
+@pytest.mark.parametrize("m", [1, 3])
+@pytest.mark.parametrize("k", [512, 1024, 1032, 2048, 2056, 5632])
+def test_gemm_skinny_cpl_boundaries(m, k):
+    import pli_hip
+    a = seeded_normal((m, k), 11 + k, "bf16")
+    w = seeded_normal((300, k), 12 + k, "bf16")
+    out = pli_hip.gemm(dev(a, "bf16"), dev(w, "bf16"), trans_b=True)
+    assert_lin_close(out, olin.linear(a, w, None), "bf16", f"skinny gemm {m}x300x{k}")
+
+
 def test_gemm_ws_abi_direct():
     """pli_gemm_ws through the C ABI: undersized workspace falls back, a
     sized one takes the split-K path; both match the oracle."""
