@@ -2138,6 +2138,10 @@ static int gemm_dispatch(const void* a, const void* b, void* c, const void* bias
     // decode batches: W streamed once.  M == 1: GEMV-style VALU kernel;
     // M <= 128 (K a multiple of 128, N of 16): small-M MFMA kernel.
     if (vec && trans_b && m == 1) {
+        // no bias: y = W x is pli_gemv (same per-row chunk and FMA order as the
+        // skinny kernel, so bitwise the same; 8192^2 5.85 vs 5.18 TB/s, 4096^2
+        // 4.48 vs 3.98, tools/gemv_vs_skinny.py, profiles/r01/gemm/)
+        if (bias == nullptr) return pli_gemv(b, a, c, n, k, ldb, dtype, stream);
         if (dtype == PLI_BF16)
             return launch_skinny<bf16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, s);
         return launch_skinny<f16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, s);
