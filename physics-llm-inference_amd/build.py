@@ -27,6 +27,10 @@ ARCH = os.environ.get("PLI_OFFLOAD_ARCH", "gfx950")
 
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I" + INCLUDE, "-I" + CSRC,
           "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
+# per-source extra flags.  flash_v7: no NaN ever reaches the softmax (masks
+# use -inf), so fmaxf on MFMA results folds into v_max3_f32 without the
+# canonicalising v_max_f32 hipcc otherwise puts in front of each one.
+EXTRA = {"flash_v7.hip": ["-fno-honor-nans"]}
 
 
 def hipcc() -> str:
@@ -45,7 +49,7 @@ def _compile(src: str, force: bool) -> str:
     headers = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(INCLUDE, "*.h"))
     if not force and os.path.exists(obj) and os.path.getmtime(obj) >= _newest([src] + headers):
         return obj
-    cmd = [hipcc(), *CFLAGS, "-c", src, "-o", obj]
+    cmd = [hipcc(), *CFLAGS, *EXTRA.get(os.path.basename(src), []), "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

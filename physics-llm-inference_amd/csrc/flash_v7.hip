@@ -1,0 +1,400 @@
+// attn_fwd_v7: flash-attention forward with a lean softmax (gfx950, D 64/128).
+//
+// Same tile structure as attn_fwd_v2 (flash_attn.hip; reference
+// ch06/flash_attention.py:14-74): 8 waves x 32 query rows, 64-key K/V tiles
+// register-staged into padded LDS images, S^T = K Q^T and O^T += V^T P^T on
+// v_mfma_f32_32x32x16 with the query row on the lane.  What changes is the
+// VALU work per score, which is what held v2 at ~40 % of the MFMA roof (it is
+// issue-bound: ~5.8 VALU per MFMA):
+//
+//  * Q is prescaled once by c = scale * log2(e) (rounded to the 16-bit input
+//    type), and the first MFMA of every S chain takes its C operand from a
+//    register block holding -m (the running row max, log2 units).  The MFMA
+//    then leaves S' = S*c - m and p = exp2(S') needs no fma: 1 VALU per score
+//    instead of 2.
+//  * The exp is speculative: it does not wait for the row max.  The max (16
+//    v_max3 + one permlane) only decides whether the tile raised it by more
+//    than 8 (defer-max); in that rare case the wave recomputes the tile's S
+//    from LDS with the new -m block, redoes the exps and rescales O and l.
+//  * The row sum l is taken by the matrix core: one v_mfma_f32_16x16x32 per
+//    16-key step with a 0/1 selector as A and the packed bf16 P fragment as B
+//    sums exactly the rounded P the PV product uses (the v2 default used 16
+//    v_dot2c per tile for that), for 1/16 more matrix time and no VALU.
+//
+// Per 64-key tile and lane that leaves 32 v_exp + 16 v_cvt_pk + 16 v_max3
+// (was + 32 v_fma + 16 v_dot2c).
+#include <cmath>
+#include <type_traits>
+
+#include "flash_v7.h"
+#include "pli_common.h"
+
+namespace pli {
+namespace {
+
+constexpr int V7_KT = 64;       // keys per tile
+constexpr int V7_QW = 32;       // query rows per wave
+constexpr int V7_NW = 8;        // waves per workgroup
+constexpr float V7_THR = 8.f;   // defer-max threshold (log2 units): P <= 2^8
+
+template <int D> struct V7Layout {
+    static constexpr int KS = 2 * D + 16;  // K row stride (bytes): b128 reads conflict-free
+    static constexpr int VS = 2 * D + 64;  // V row stride (bytes): tr_b16 reads conflict-free
+    static constexpr int KSZ = V7_KT * KS, VSZ = V7_KT * VS, BUF = KSZ + VSZ;
+};
+
+template <typename T> struct V7Ones;
+template <> struct V7Ones<bf16_t> { static constexpr int pair = 0x3F803F80; };
+template <> struct V7Ones<f16_t> { static constexpr int pair = 0x3C003C00; };
+
+// both 16-bit halves of a word, scaled by c and re-rounded to T
+template <typename T> __device__ __forceinline__ int v7_scale_pair(int w, float c);
+template <> __device__ __forceinline__ int v7_scale_pair<bf16_t>(int w, float c) {
+    const float lo = __uint_as_float((uint32_t)w << 16), hi = __uint_as_float((uint32_t)w & 0xffff0000u);
+    return (int)pack2<bf16_t>(lo * c, hi * c);
+}
+template <> __device__ __forceinline__ int v7_scale_pair<f16_t>(int w, float c) {
+    const float lo = (float)__builtin_bit_cast(_Float16, (uint16_t)((uint32_t)w & 0xffffu));
+    const float hi = (float)__builtin_bit_cast(_Float16, (uint16_t)((uint32_t)w >> 16));
+    return (int)pack2<f16_t>(lo * c, hi * c);
+}
+
+__device__ __forceinline__ float v7_xor32_max(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float v7_xor32_sum(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// PRE = 1: Q prescaled by c (rounded to the 16-bit input type) and -m as the
+//          C operand of the first QK^T MFMA: p = exp2(acc), no fma per score;
+//          the Q rounding costs score precision (2^-9 relative in bf16).
+// PRE = 0: exact scaling, S accumulates from 0 and p = exp2(fma(s, c, -m)).
+template <typename T, int D, int PRE>
+__global__ __launch_bounds__(512, 2) void attn_fwd_v7(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
+    const uint16_t* __restrict__ v, uint16_t* __restrict__ o, int H, int group,
+    int Nq, int Nk, V7Strides st, float c, int causal, int qblocks, int nblocks) {
+    using L = V7Layout<D>;
+    constexpr int NT = V7_NW * 64;
+    constexpr int CPR = D / 8;     // 16-byte chunks per row
+    constexpr int RPI = NT / CPR;  // rows covered by one staging step
+    constexpr int CPT = V7_KT / RPI;
+    static_assert(NT % CPR == 0 && V7_KT % RPI == 0, "staging must tile evenly");
+    __shared__ __attribute__((aligned(16))) char smem[2 * L::BUF];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h32 = lane >> 5, l32 = lane & 31;
+    const int lb = xcd_remap(blockIdx.x, nblocks);
+    const int bh = lb / qblocks;
+    // causal: heaviest query blocks of a head first, so the grid drains on light ones
+    const int qblk = causal ? qblocks - 1 - lb % qblocks : lb % qblocks;
+    const int b = bh / H, hq = bh % H, hk = hq / group;
+    const int qbase = qblk * (V7_NW * V7_QW);
+    const int q0 = qbase + wave * V7_QW;
+    const int off_diag = Nk - Nq;  // causal (bottom-right): row i sees keys <= i + off_diag
+
+    const uint16_t* qp = q + b * st.qb + hq * st.qh;
+    const uint16_t* kp = k + b * st.kb + hk * st.kh;
+    const uint16_t* vp = v + b * st.vb + hk * st.vh;
+
+    // Q^T fragments (B operand): query row q0 + l32, d = 16kk + 8h32 .. +7
+    i32x4 qf[D / 16];
+    {
+        const int qr = q0 + l32;
+        const bool ok = qr < Nq;
+        const uint16_t* src = qp + (int64_t)(ok ? qr : 0) * st.qn + 8 * h32;
+#pragma unroll
+        for (int kk = 0; kk < D / 16; ++kk) {
+            const i32x4 x = *reinterpret_cast<const i32x4*>(src + 16 * kk);
+            qf[kk] = ok ? x : i32x4{0, 0, 0, 0};
+        }
+        if constexpr (PRE != 0) {
+#pragma unroll
+            for (int kk = 0; kk < D / 16; ++kk)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) qf[kk][j] = v7_scale_pair<T>(qf[kk][j], c);
+        }
+    }
+
+    int kv_end = Nk;
+    if (causal) kv_end = min(Nk, qbase + V7_NW * V7_QW + off_diag);
+    const int nt = kv_end > 0 ? cdiv(kv_end, V7_KT) : 0;
+    const int t_full = Nk / V7_KT;  // tiles [0, t_full) need no row clamp
+    int t_mask = t_full;            // first tile this wave must mask
+    if (causal) t_mask = min(t_mask, max(0, (q0 + off_diag + 1) / V7_KT));
+
+    // staging: thread owns chunk `sch` of rows srow + i*RPI
+    const int srow = tid / CPR, sch = tid % CPR;
+    const uint16_t* kg = kp + (int64_t)srow * st.kn + sch * 8;
+    const uint16_t* vg = vp + (int64_t)srow * st.vn + sch * 8;
+    const int kw = srow * L::KS + sch * 16, vw = L::KSZ + srow * L::VS + sch * 16;
+    i32x4 kst[CPT], vst[CPT];
+    auto load_tile = [&](int t) {
+        if (t < t_full) {
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) {
+                const int64_t r = (int64_t)t * V7_KT + i * RPI;
+                kst[i] = *reinterpret_cast<const i32x4*>(kg + r * st.kn);
+                vst[i] = *reinterpret_cast<const i32x4*>(vg + r * st.vn);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) {
+                const int key = t * V7_KT + i * RPI + srow;
+                const int64_t r = min(key, Nk - 1) - srow;
+                const i32x4 kx = *reinterpret_cast<const i32x4*>(kg + r * st.kn);
+                const i32x4 vx = *reinterpret_cast<const i32x4*>(vg + r * st.vn);
+                kst[i] = key < Nk ? kx : i32x4{0, 0, 0, 0};
+                vst[i] = key < Nk ? vx : i32x4{0, 0, 0, 0};
+            }
+        }
+    };
+    auto store_tile = [&](int buf) {
+        char* base = smem + buf * L::BUF;
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+            lds_write_b128(base, kw + i * RPI * L::KS, kst[i]);
+            lds_write_b128(base, vw + i * RPI * L::VS, vst[i]);
+        }
+    };
+
+    // per-lane fragment bases (byte offsets inside one buffer)
+    const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+    const int kr = l32 * L::KS + h32 * 16;
+    const int vr = L::KSZ + (4 * h32 + qq) * L::VS + (2 * (g & 1) + (pp >> 1)) * 16 + 8 * (pp & 1);
+
+    // Row-sum selector (A of v_mfma_f32_16x16x32): lane l supplies row l&15,
+    // k' = 8(l>>4)..+7.  Read as that MFMA's B, the P^T fragment of a 32x32x16
+    // k-step puts query n's keys in k' groups 0 and 2 and query n+16's in 1 and
+    // 3 (n = l&15), so row 0 = ones on groups {0,2}, row 4 = ones on {1,3}
+    // leaves query l's sum in register 0 of lane l (l < 32) and zeros in lanes
+    // 32..63.
+    const bool sel_on = (i16 == 0 && (g & 1) == 0) || (i16 == 4 && (g & 1) == 1);
+    const int one = sel_on ? V7Ones<T>::pair : 0;
+    const i32x4 sel = {one, one, one, one};
+
+    f32x16 oacc[D / 32];
+#pragma unroll
+    for (int d = 0; d < D / 32; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[d][r] = 0.f;
+    f32x16 negm;  // PRE: -m_run in every register, C of the first QK^T MFMA
+#pragma unroll
+    for (int r = 0; r < 16; ++r) negm[r] = 0.f;
+    // running max, log2 units (PRE: the offset already inside S')
+    float m_run = PRE != 0 ? 0.f : -1e30f;
+    f32x4 lsum = {0.f, 0.f, 0.f, 0.f};
+
+    if (nt > 0) {
+        load_tile(0);
+        store_tile(0);
+    }
+    __syncthreads();
+
+    auto body = [&](int t, auto first_tag) {
+        constexpr bool FIRST = decltype(first_tag)::value;
+        if (t + 1 < nt) load_tile(t + 1);
+        const char* kb = smem + (t & 1) * L::BUF + kr;
+        const char* vb = smem + (t & 1) * L::BUF + vr;
+
+        // s[tt][r] = S(key 32tt + 8(r>>2) + 4h32 + (r&3), query l32)  (PRE: S*c - m)
+        f32x16 s[2];
+        auto qk = [&]() {
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt) {
+                if constexpr (PRE != 0) {
+                    s[tt] = mfma32x32x16<T>(lds_read_b128(kb, tt * 32 * L::KS), qf[0], negm);
+                } else {
+                    f32x16 z;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) z[r] = 0.f;
+                    s[tt] = mfma32x32x16<T>(lds_read_b128(kb, tt * 32 * L::KS), qf[0], z);
+                }
+#pragma unroll
+                for (int kk = 1; kk < D / 16; ++kk)
+                    s[tt] = mfma32x32x16<T>(lds_read_b128(kb, tt * 32 * L::KS + kk * 32), qf[kk], s[tt]);
+            }
+            if (t >= t_mask) {
+                const int lim = causal ? q0 + l32 + off_diag : Nk;
+#pragma unroll
+                for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int key = t * V7_KT + tt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
+                        if (key >= Nk || key > lim) s[tt][r] = -INFINITY;
+                    }
+            }
+        };
+        auto expo = [&]() {
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    s[tt][r] = __builtin_amdgcn_exp2f(PRE != 0 ? s[tt][r] : fmaf(s[tt][r], c, -m_run));
+        };
+        qk();
+
+        // row max: two v_max3 chains (-fno-honor-nans: no canonicalising
+        // v_max_f32 in front of the MFMA results) + one cross-half swap
+        float mx = fmaxf(s[0][0], s[1][0]), my = fmaxf(s[0][1], s[1][1]);
+#pragma unroll
+        for (int r = 2; r < 16; r += 2) {
+            mx = fmaxf(fmaxf(mx, s[0][r]), s[1][r]);
+            my = fmaxf(fmaxf(my, s[0][r + 1]), s[1][r + 1]);
+        }
+        mx = v7_xor32_max(fmaxf(mx, my));
+
+        if constexpr (FIRST) {
+            // the first tile sets the running max (O and l are still zero)
+            if constexpr (PRE != 0) {
+                const float delta = mx == -INFINITY ? 0.f : mx;
+                m_run = delta;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) negm[r] = -m_run;
+#pragma unroll
+                for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) s[tt][r] -= delta;
+            } else {
+                m_run = mx == -INFINITY ? -1e30f : mx * c;
+            }
+            expo();
+        } else {
+            // speculative exps against the running max, kept ahead of the
+            // branch (hipcc would otherwise sink them into both arms, behind
+            // the max chain)
+            expo();
+            asm volatile("" : "+v"(s[0]), "+v"(s[1]));
+            const bool up = PRE != 0 ? mx > V7_THR : mx * c > m_run + V7_THR;
+            if (__ballot(up)) {
+                // rare: some row's max rose by more than the threshold.  K(t)
+                // is still in LDS: recompute S and redo the exps.
+                float alpha;
+                if constexpr (PRE != 0) {
+                    const float delta = up ? mx : 0.f;
+                    m_run += delta;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) negm[r] = -m_run;
+                    alpha = __builtin_amdgcn_exp2f(-delta);
+                } else {
+                    const float m_new = up ? mx * c : m_run;
+                    alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+                    m_run = m_new;
+                }
+                qk();
+                expo();
+#pragma unroll
+                for (int d = 0; d < D / 32; ++d)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
+                lsum[0] *= alpha;
+            }
+        }
+
+        // P^T fragments: registers 8s2..8s2+7 of s[tt] are k-step s2
+        i32x4 pb[2][2];
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const int r0 = 8 * s2;
+                pb[tt][s2] = i32x4{(int)pack2<T>(s[tt][r0 + 0], s[tt][r0 + 1]),
+                                   (int)pack2<T>(s[tt][r0 + 2], s[tt][r0 + 3]),
+                                   (int)pack2<T>(s[tt][r0 + 4], s[tt][r0 + 5]),
+                                   (int)pack2<T>(s[tt][r0 + 6], s[tt][r0 + 7])};
+            }
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) lsum = mfma16x16x32<T>(sel, pb[tt][s2], lsum);
+
+        // O^T += V^T P^T ; V^T fragment via two transposed reads
+#pragma unroll
+        for (int dblk = 0; dblk < D / 32; ++dblk)
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    const int ro = (tt * 32 + 16 * s2) * L::VS + dblk * 64;
+                    const i32x2 lo = lds_read_tr16(vb, ro);
+                    const i32x2 hi = lds_read_tr16(vb, ro + 8 * L::VS);
+                    oacc[dblk] = mfma32x32x16<T>(i32x4{lo.x, lo.y, hi.x, hi.y}, pb[tt][s2], oacc[dblk]);
+                }
+
+        if (t + 1 < nt) store_tile((t + 1) & 1);
+        __syncthreads();
+    };
+
+    if (nt > 0) body(0, std::true_type{});
+    for (int t = 1; t < nt; ++t) body(t, std::false_type{});
+
+    // ---- epilogue: O = O^T / l, query row l32
+    const float l = v7_xor32_sum(lsum[0]);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const int qr = q0 + l32;
+    if (qr < Nq) {
+        uint16_t* op = o + b * st.ob + hq * st.oh + (int64_t)qr * st.on;
+        // group k = 4*dblk + i holds columns 8k+4*h32 .. +3 of row qr; after
+        // swapping (k, k+1): lower lanes hold cols 8k..8k+7, upper 8k+8..8k+15
+#pragma unroll
+        for (int dblk = 0; dblk < D / 32; ++dblk)
+#pragma unroll
+            for (int i = 0; i < 4; i += 2) {
+                const f32x16& a = oacc[dblk];
+                const uint32_t ax = pack2<T>(a[4 * i] * inv, a[4 * i + 1] * inv);
+                const uint32_t ay = pack2<T>(a[4 * i + 2] * inv, a[4 * i + 3] * inv);
+                const uint32_t bx = pack2<T>(a[4 * i + 4] * inv, a[4 * i + 5] * inv);
+                const uint32_t by = pack2<T>(a[4 * i + 6] * inv, a[4 * i + 7] * inv);
+                const auto rx = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
+                const auto ry = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
+                const int d = dblk * 32 + 8 * i + 8 * h32;
+                *reinterpret_cast<i32x4*>(op + d) = i32x4{(int)rx[0], (int)ry[0], (int)rx[1], (int)ry[1]};
+            }
+    }
+}
+
+template <typename T, int D>
+int launch_v7_typed(const void* q, const void* k, const void* v, void* o, int B, int H, int group,
+                    int Nq, int Nk, const V7Strides& st, float c, int causal, hipStream_t stream,
+                    int sub) {
+    const int qblocks = cdiv(Nq, V7_NW * V7_QW);
+    const int64_t nb = (int64_t)B * H * qblocks;
+    PLI_REQUIRE(nb < (1ll << 31), "pli_flash_attn_fwd: grid too large");
+    const auto* qq = (const uint16_t*)q;
+    const auto* kk = (const uint16_t*)k;
+    const auto* vv = (const uint16_t*)v;
+    auto* oo = (uint16_t*)o;
+    const dim3 grid((unsigned)nb), block(V7_NW * 64);
+    switch (sub) {
+        case 0:
+            hipLaunchKernelGGL((attn_fwd_v7<T, D, 1>), grid, block, 0, stream, qq, kk, vv, oo, H, group,
+                               Nq, Nk, st, c, causal, qblocks, (int)nb);
+            break;
+        case 1:
+            hipLaunchKernelGGL((attn_fwd_v7<T, D, 0>), grid, block, 0, stream, qq, kk, vv, oo, H, group,
+                               Nq, Nk, st, c, causal, qblocks, (int)nb);
+            break;
+        default:
+            set_error("pli_flash_attn_fwd: unknown v7 body %d", sub);
+            return PLI_EINVAL;
+    }
+    return launch_status("attn_fwd_v7");
+}
+
+}  // namespace
+
+int launch_attn_v7(const void* q, const void* k, const void* v, void* o, int B, int H, int group,
+                   int Nq, int Nk, int D, const V7Strides& st, float scale, int causal, int is_bf16,
+                   hipStream_t stream, int sub) {
+    const float c = scale * 1.4426950408889634f;  // log2(e) folded into the Q prescale
+    if (is_bf16)
+        return D == 128 ? launch_v7_typed<bf16_t, 128>(q, k, v, o, B, H, group, Nq, Nk, st, c, causal, stream, sub)
+                        : launch_v7_typed<bf16_t, 64>(q, k, v, o, B, H, group, Nq, Nk, st, c, causal, stream, sub);
+    return D == 128 ? launch_v7_typed<f16_t, 128>(q, k, v, o, B, H, group, Nq, Nk, st, c, causal, stream, sub)
+                    : launch_v7_typed<f16_t, 64>(q, k, v, o, B, H, group, Nq, Nk, st, c, causal, stream, sub);
+}
+
+}  // namespace pli

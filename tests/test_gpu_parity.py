@@ -20,6 +20,7 @@ from conftest import GOLDEN, load_golden
 from oracle import attention as oatt
 from oracle import linear as olin
 from oracle.numerics import bf16_from_bits, seeded_normal
+from stress_cases import STRESS, prescaled_q, stress_inputs
 
 pytestmark = pytest.mark.gpu
 
@@ -105,8 +106,7 @@ def test_flash_vs_oracle(case):
 
 
 # every MFMA variant (alternates A/B-tested by tools/tune.py) on the MFMA-eligible cases
-MFMA_VARIANTS = (0, 1, 2, 3, 8, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 27, 28, 29, 30, 31, 40, 41, 42, 43, 44,
-                 45, 46)
+MFMA_VARIANTS = (21, 50, 51)
 
 
 
@@ -137,38 +137,71 @@ def test_flash_strided_views_and_out_param():
     assert_attn_close(o.transpose(1, 2), ref, "bf16", "strided")
 
 
-@pytest.mark.parametrize("variant", [2, 21, 22, 23, 27, 30, 31, 40, 41, 42, 43, 44, 45])
-def test_flash_forced_rescale_spike(variant):
-    """A key spike in a late tile forces the online max to jump past the
-    defer-max threshold (variants 18/19), exercising the rescale branch."""
+# variants whose Q is prescaled by scale*log2(e) and rounded to the 16-bit
+# input type before the MFMA (the rest scale the f32 scores exactly)
+PRESCALED = (50,)
+DEFAULT_VARIANT = 50
+
+
+def test_flash_default_is_variant_50():
     import pli_hip
-    B, H, N, D = 1, 2, 512, 128
-    q = seeded_normal((B, H, N, D), 7, "bf16")
-    k = seeded_normal((B, H, N, D), 8, "bf16")
-    v = seeded_normal((B, H, N, D), 9, "bf16")
-    k[:, :, 450] = np.float32(4.0) * np.sign(q[:, :, 3])  # row 3 jumps at tile 7
-    from oracle.numerics import round_to_bf16
-    k = round_to_bf16(k)
+    q, k, v = (dev(x, "bf16") for x in stress_inputs("late"))
+    assert torch.equal(pli_hip.flash_attn_fwd(q, k, v), pli_hip.flash_attn_fwd(q, k, v, variant=DEFAULT_VARIANT))
+
+
+@pytest.mark.parametrize("variant", MFMA_VARIANTS)
+@pytest.mark.parametrize("name", STRESS)
+def test_flash_stress(variant, name):
+    """Adversarial inputs (tests/stress_cases.py) that force the rescale
+    branch at chosen tiles, underflow against a zero max, or rescale in many
+    tiles.  Bound: 2^-8 * max|v| -- the bf16 rounding of the P weights fed to
+    the PV MFMA (2^-9 relative) plus the bf16 rounding of the output (2^-9),
+    each at most 2^-9 * max|v| when a few keys dominate a row (on random
+    inputs the suite's 1e-2 holds with a wide margin; here every variant,
+    the round-1 kernel included, lands near 1.0e-2).  Exact-scaling variants
+    are held to that against the f64 oracle.  Prescaled variants are held to
+    it against the f64 oracle given the same bf16-rounded Q*scale*log2(e) (the
+    kernel's arithmetic, every branch included), and, against the exact
+    answer, to no worse than the reference's own bf16 flash path on the same
+    input (tests/golden/stress_flash.npz, recorded from the reference)."""
+    import pli_hip
+    q, k, v = stress_inputs(name)
     out = pli_hip.flash_attn_fwd(dev(q, "bf16"), dev(k, "bf16"), dev(v, "bf16"), variant=variant)
-    assert_attn_close(out, oatt.naive_attention(q, k, v), "bf16", "spike")
+    o64 = out.float().cpu().numpy().astype(np.float64)
+    assert np.isfinite(o64).all(), f"stress {name}: non-finite output"
+    tol = 2.0 ** -8 * float(np.abs(v).max())
+    exact = oatt.naive_attention(q, k, v)
+    err = np.abs(o64 - exact).max()
+    if variant in PRESCALED:
+        own = np.abs(o64 - oatt.naive_attention(prescaled_q(q, q.shape[-1] ** -0.5), k, v)).max()
+        assert own <= tol, f"stress {name} (prescaled oracle): {own:.3e} > {tol:.3e}"
+        ref_err = float(load_golden("stress_flash.npz")[f"{name}_ref_err"])
+        assert err <= ref_err, f"stress {name}: {err:.3e} > reference bf16 flash {ref_err:.3e}"
+    else:
+        assert err <= tol, f"stress {name}: {err:.3e} > {tol:.3e}"
 
 
-def test_flash_full_config_properties():
+@pytest.mark.parametrize("variant", [None, 21])
+def test_flash_full_config_properties(variant):
     """B=8 S=4096 H=32 D=128 bf16 (the bench config): v = 1 gives exactly 1;
     two heads checked against the f64 oracle; key permutation invariance."""
     import pli_hip
     B, H, N, D = 8, 32, 4096, 128
     g = torch.Generator(device=DEV).manual_seed(0)
     q, k, v = (torch.randn(B, H, N, D, device=DEV, dtype=torch.bfloat16, generator=g) for _ in range(3))
-    out = pli_hip.flash_attn_fwd(q, k, v)
-    ones = pli_hip.flash_attn_fwd(q, k, torch.ones_like(v))
+    out = pli_hip.flash_attn_fwd(q, k, v, variant=variant)
+    ones = pli_hip.flash_attn_fwd(q, k, torch.ones_like(v), variant=variant)
     assert (ones.float() - 1).abs().max().item() <= 2 ** -8  # one bf16 ulp below 1
-    for (b, h) in ((0, 0), (7, 31)):
+    for (b, h) in ((0, 0), (3, 17), (7, 31)):
         ref = oatt.naive_attention(*(t[b:b + 1, h:h + 1].float().cpu().numpy() for t in (q, k, v)))
         assert_attn_close(out[b:b + 1, h:h + 1], ref, "bf16", f"full b{b} h{h}")
     perm = torch.randperm(N, device=DEV, generator=g)
-    out_p = pli_hip.flash_attn_fwd(q[:, :2], k[:, :2, perm], v[:, :2, perm])
+    out_p = pli_hip.flash_attn_fwd(q[:, :2], k[:, :2, perm], v[:, :2, perm], variant=variant)
     assert (out_p.float() - out[:, :2].float()).abs().max().item() <= 1e-2
+    # full-tensor agreement with the round-1 kernel (independent softmax code)
+    if variant is None:
+        base = pli_hip.flash_attn_fwd(q, k, v, variant=21)
+        assert (base.float() - out.float()).abs().max().item() <= 1.6e-2
 
 
 def test_mha_hip_matches_reference_golden():

@@ -141,3 +141,15 @@ def test_analytic_fixture_is_loadable():
     with open(os.path.join(GOLDEN, "analytic.json")) as f:
         a = json.load(f)
     assert {"gemm", "gemv", "roofline", "attn", "comm", "tp"} <= set(a)
+
+
+def test_stress_fixture_matches_inputs():
+    """stress_flash.npz (the reference's bf16 flash on tests/stress_cases.py
+    inputs): its recorded error equals the recomputed |out - f64 oracle|."""
+    from stress_cases import STRESS, stress_inputs
+    g = load_golden("stress_flash.npz")
+    for name in STRESS:
+        q, k, v = stress_inputs(name)
+        ref = oatt.naive_attention(q, k, v)
+        out = bf16_from_bits(g[f"{name}_ref_flash"]).astype(np.float64)
+        assert np.isclose(np.abs(out - ref).max(), float(g[f"{name}_ref_err"]), rtol=1e-9, atol=0)
