@@ -89,6 +89,38 @@ def load_traffic(kernel: str):
         return None
 
 
+def calibrate() -> dict:
+    """Measured ceilings beside the datasheet roofs: the HBM
+    stream kernel (pli_scale_copy, 2 x 1 GiB) and the MFMA probe
+    (pli_mfma_probe, both bf16 shapes, operands in registers)."""
+    from ch03.roofline import measure_hbm_bandwidth, measure_mfma_peak
+    return {"hbm_GB/s": measure_hbm_bandwidth(),
+            "mfma_32x32x16_TFLOP/s": measure_mfma_peak("32x32x16"),
+            "mfma_16x16x32_TFLOP/s": measure_mfma_peak("16x16x32"),
+            "how": "pli_scale_copy 2x1 GiB read+write, events; pli_mfma_probe 1024 WGs x 4 waves, "
+                   "4 independent MFMAs per wave from registers, pseudo-random bf16, best of 5"}
+
+
+def cpu_info() -> dict:
+    """Host CPU as the CPU baselines ran on it: model name, os.cpu_count(),
+    the cores this process may run on (cgroup/affinity) and torch threads."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    return {"cpu_model": model, "os_cpu_count": os.cpu_count(), "affinity_cores": affinity,
+            "torch_threads": torch.get_num_threads()}
+
+
 def bench_gemv(stream, iters: int) -> dict:
     """ch03 decode GEMV 4096x4096 bf16.  W is rotated over 24 copies (768 MiB,
     3x the 256 MiB Infinity Cache) so every launch streams W from HBM.  The
@@ -227,6 +259,23 @@ def bench_tp(stream, world: int, rank: int, iters: int) -> dict:
         small[str(m)] = {"gemm_us": ms * 1e3, "weight_GB/s": N * kl * 2 / (ms * 1e-3) / 1e9,
                          "TFLOP/s": 2 * m * N * kl / (ms * 1e-3) / 1e12, "torch_F.linear_us": ms_t * 1e3}
     out["small_m"] = small
+    if world == 1:
+        # per-rank compute of the TP = 2 / 4 / 8 row shards (K = 8192 / tp) on
+        # this one GPU, so every TP degree's GEMM is measured without a node
+        shards = {}
+        for tp in (2, 4, 8):
+            ks = K // tp
+            xs = torch.randn(M, ks, device="cuda", dtype=torch.bfloat16)
+            wsh = torch.randn(N, ks, device="cuda", dtype=torch.bfloat16) * ks ** -0.5
+            fs = lambda: pli_hip.gemm(xs, wsh, trans_b=True, out=y)  # noqa: E731
+            tls = lambda: torch.nn.functional.linear(xs, wsh)  # noqa: E731
+            t = paired_time_ms({"ours": fs, "torch": tls}, iters, stream)
+            fl = 2 * M * N * ks
+            shards[f"tp{tp}"] = {"K": ks, "gemm_us": t["ours"] * 1e3,
+                                 "TFLOP/s": fl / (t["ours"] * 1e-3) / 1e12,
+                                 "torch_F.linear_TFLOP/s": fl / (t["torch"] * 1e-3) / 1e12}
+            del xs, wsh
+        out["shard_gemm_per_rank"] = shards
     if world > 1:
         def ar():
             dist.all_reduce(y)
@@ -297,7 +346,7 @@ def cpu_baseline(seconds: float = 15.0) -> dict:
         times.append(time.perf_counter() - t0)
     sec = min(times)
     return {"value": flops / sec / 1e12, "unit": "TFLOP/s", "cores": torch.get_num_threads(),
-            "kind": "port",
+            "kind": "port", **cpu_info(),
             "sample": f"reference tile loop (ch06/flash_attention.py:14-74 restated, oracle/attention.py) "
                       f"on torch CPU bf16, B=1 H=32 S=4096 D=128 = 1/8 of the workload, "
                       f"best of {len(times)} runs ({sec:.2f} s each)"}
@@ -310,7 +359,8 @@ def cpu_other() -> dict:
     ([8192, 1024] x [8192, 1024]^T, 2 + 5)."""
     import torch.nn.functional as F
     g = torch.Generator().manual_seed(0)
-    out = {"cores": torch.get_num_threads(), "dtype": "bf16", "kind": "reference ops (torch CPU)"}
+    out = {"cores": torch.get_num_threads(), "dtype": "bf16", "kind": "reference ops (torch CPU)",
+           **cpu_info()}
 
     def tmin(fn, warm, iters):
         for _ in range(warm):
@@ -399,6 +449,12 @@ def main():
     achieved = flops_step / (kernel_ms * 1e-3) / 1e12
 
     extra = {}
+    measured_roof = {}
+    if not args.flash_only:
+        cal = calibrate()
+        extra["calibration"] = cal
+        measured_roof = {"measured_peak": cal["mfma_32x32x16_TFLOP/s"],
+                         "frac_of_measured": achieved / cal["mfma_32x32x16_TFLOP/s"]}
     if args.flash_only:
         args.quick, args.no_cpu_baseline = True, True
     # causal variant of the same workload (ch01 MHA semantics), reported only
@@ -432,6 +488,18 @@ def main():
         if args.with_decode:
             extra["decode_attn"] = bench_decode(stream, 20)
 
+    if "calibration" in extra:
+        hbm = extra["calibration"]["hbm_GB/s"]
+        for leg in ("gemv", "decode_attn"):
+            if leg in extra:
+                r = extra[leg]["roofline"]
+                r["measured_peak"] = hbm
+                r["frac_of_measured"] = r["achieved"] / hbm
+        if "gemm" in extra:
+            mp = extra["calibration"]["mfma_32x32x16_TFLOP/s"]
+            extra["gemm"]["roofline"].update({"measured_peak": mp,
+                                              "frac_of_measured": extra["gemm"]["TFLOP/s"] / mp})
+
     result = {
         "metric": METRIC,
         "value": value,
@@ -451,9 +519,11 @@ def main():
                    "parallelism": f"replicas x{world} (flash does not shard; TP GEMM row-parallel)"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved / PEAK_BF16_TFLOPS,
-                     "traffic": load_traffic("attn_fwd_v2"),
-                     "kernel": "attn_fwd_v2<bf16,128,8 waves,OPT 13>", "algorithmic_flops": flops_step,
-                     "kernel_ms": kernel_ms},
+                     "traffic": load_traffic("attn_fwd_v7"),
+                     "traffic_source": "profiles/traffic.json: rocprofv3 FETCH_SIZE x2 (gfx950) + WRITE_SIZE "
+                                       "per launch, separate --pmc passes (tools/pmc_summary.py), not this run",
+                     "kernel": "attn_fwd_v7<bf16,128,PRE 1> (variant 50)", "algorithmic_flops": flops_step,
+                     "kernel_ms": kernel_ms, **measured_roof},
         **extra,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.quick:

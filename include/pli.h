@@ -139,6 +139,16 @@ int pli_scale_copy(const float* in, float* out, int64_t n_out, int stride,
                    void* stream);
 
 /*
+ * Roofline calibration (ch03/roofline.py measure_mfma_peak): `blocks`
+ * workgroups of 256 threads, each wave issuing `iters` rounds of four
+ * independent bf16 MFMAs from registers on pseudo-random operands (shape 0:
+ * v_mfma_f32_32x32x16_bf16, 1: v_mfma_f32_16x16x32_bf16); one float per
+ * thread goes to out[blocks * 256] so the work is not dead.
+ * FLOPs = blocks * 4 * iters * 4 * 32768.
+ */
+int pli_mfma_probe(float* out, int blocks, int iters, int shape, void* stream);
+
+/*
  * Row softmax with the single-pass online (max, sum) recurrence of
  * ch06/online_softmax.py:13-25 (== standard_softmax, :5-10), over the last
  * dimension of a contiguous [rows, n] tensor; statistics in fp32.

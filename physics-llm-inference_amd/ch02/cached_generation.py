@@ -49,9 +49,24 @@ class LayerKVCache:
     seq_len: int = 0
     pos: torch.Tensor | None = None
 
+    def reserve(self, n: int) -> None:
+        """Raise when appending ``n`` rows would overrun ``max_seq_len`` -- the
+        reference raises there too (its slice assignment shapes stop matching,
+        ``:27-33``).  The device-length paths need the check on the host: the
+        append and attention kernels clamp to the capacity and would otherwise
+        return wrong logits silently."""
+        cap = self.k.shape[1]
+        if self.seq_len + n > cap:
+            raise RuntimeError(f"KV cache overflow: {self.seq_len} cached + {n} new rows > "
+                               f"max_seq_len {cap}")
+
     def update(self, k_new: torch.Tensor, v_new: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
-        """Append new K/V and return the valid prefixes (``:27-33``)."""
+        """Append new K/V and return the valid prefixes (``:27-33``).  With a
+        device ``pos`` the rows go to ``*pos``, which this method does NOT
+        advance: ``CachedTransformerModel.forward`` advances the one ``pos``
+        all layers share, once per forward (``seq_len`` is advanced here)."""
         n = k_new.shape[1]
+        self.reserve(n)
         if self.pos is not None:
             pli_hip.kv_append(k_new, v_new, self.k, self.v, self.pos)
         else:
@@ -84,6 +99,7 @@ class CachedGQA(nn.Module):
             # launch with k/v written straight into the cache rows at pos
             # (skinny kernel up to 16 rows, small-M MFMA kernel up to 32: above
             # that the mid-M kernel of the packed GEMM + the append win)
+            cache.reserve(S)
             q = torch.empty(B, S, self.num_heads * self.head_dim, device=x.device, dtype=x.dtype)
             pli_hip.qkv_into_cache(x, self.q_proj.weight, self.k_proj.weight, self.v_proj.weight,
                                    q, cache.k, cache.v, cache.pos)
@@ -204,6 +220,7 @@ class CachedTransformerBlock(nn.Module):
         pending FFN output)."""
         B, S, hd = x.shape
         at = self.attn
+        cache.reserve(S)
         q = torch.empty(B, S, at.num_heads * at.head_dim, device=x.device, dtype=x.dtype)
         if pending is None:
             pli_hip.rms_qkv_into_cache(x, self.input_norm.weight, self.input_norm.eps,

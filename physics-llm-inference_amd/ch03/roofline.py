@@ -106,6 +106,31 @@ def measure_hbm_bandwidth(nbytes: int = 1 << 30, iters: int = 20, device: str = 
     return 2 * n * 4 / sec / 1e9
 
 
+def measure_mfma_peak(shape: str = "32x32x16", iters: int = 4096, reps: int = 5,
+                      device: str = "cuda") -> float:
+    """Achievable bf16 MFMA TFLOP/s: ``pli_mfma_probe`` (four independent
+    MFMAs per wave from registers, pseudo-random operands, 4 waves per SIMD on
+    every CU), best of ``reps`` event-timed launches.  The clock the chip
+    holds under that load sets it (MI355X_MICROARCH.md 'DVFS give-back')."""
+    import torch
+
+    import pli_hip
+
+    blocks = MI355X_CUS * 4
+    out = torch.empty(blocks * 256, device=device, dtype=torch.float32)
+    sh = {"32x32x16": 0, "16x16x32": 1}[shape]
+    pli_hip.mfma_probe(out, blocks, iters, sh)
+    best = float("inf")
+    for _ in range(reps):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        pli_hip.mfma_probe(out, blocks, iters, sh)
+        e.record()
+        e.synchronize()
+        best = min(best, s.elapsed_time(e) / 1e3)
+    return blocks * 4 * iters * 4 * 32768 / best / 1e12
+
+
 def measured_spec(hbm_gbps: float, mfma_tflops: float | None = None) -> HardwareSpec:
     """An MI355X roof with measured ceilings (datasheet compute peak if None)."""
     return HardwareSpec(peak_tflops=mfma_tflops or MI355X.peak_tflops,

@@ -15,7 +15,7 @@ import torch
 
 __all__ = [
     "PliError", "lib", "library_path", "available", "DTYPE_CODE",
-    "flash_attn_fwd", "gemv", "gemm", "scale_copy", "softmax_rows",
+    "flash_attn_fwd", "gemv", "gemm", "scale_copy", "mfma_probe", "softmax_rows",
     "online_softmax_with_output",
 ]
 
@@ -60,6 +60,7 @@ _SIGS = {
                                  _c_i64, _c_i64, _c_i64, _c_int, _vp, _c_int],
     "pli_moe_combine": [_vp, _c_i64, _vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_int, _c_int, _vp],
     "pli_scale_copy": [_vp, _vp, _c_i64, _c_int, _vp],
+    "pli_mfma_probe": [_vp, _c_int, _c_int, _c_int, _vp],
     "pli_softmax_rows": [_vp, _vp, _c_i64, _c_int, _c_int, _vp],
     "pli_online_softmax_with_output": [_vp, _vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_int, _vp],
     "pli_attn_decode_workspace_size": [_c_int] * 6,
@@ -143,6 +144,19 @@ def _require_gpu(*ts: torch.Tensor) -> torch.device:
         if t.dtype != ts[0].dtype:
             raise PliError(f"mixed dtypes {t.dtype} vs {ts[0].dtype}")
     return dev
+
+
+def _check_out(out: torch.Tensor, ref: torch.Tensor, shape: tuple, what: str) -> None:
+    """A caller-supplied output: same device and dtype as ``ref``, exactly
+    ``shape``, unit inner stride, rows not overlapping (the kernels write
+    ``shape[0]`` rows of ``shape[-1]`` elements at the row stride)."""
+    _require_gpu(ref, out)
+    if tuple(out.shape) != tuple(shape):
+        raise PliError(f"{what}: out has shape {tuple(out.shape)}, expected {tuple(shape)}")
+    if out.dim() > 0 and out.stride(-1) != 1:
+        raise PliError(f"{what}: out needs a unit inner stride, got strides {out.stride()}")
+    if out.dim() == 2 and out.shape[0] > 1 and out.stride(0) < out.shape[1]:
+        raise PliError(f"{what}: out rows overlap (row stride {out.stride(0)} < {out.shape[1]})")
 
 
 def _stream(dev: torch.device) -> int:
@@ -395,6 +409,10 @@ def rmsnorm(x: torch.Tensor, weight: torch.Tensor, eps: float = 1e-6,
         if r2.stride(-1) != 1:
             r2 = r2.contiguous()
     weight = weight.contiguous()
+    if out is not None:
+        _check_out(out, x, tuple(x.shape), "rmsnorm")
+        if not out.is_contiguous():
+            raise PliError("rmsnorm: out must be contiguous")
     y = torch.empty_like(x2) if out is None else out.view(-1, n)
     h = torch.empty_like(x2) if residual is not None else None
     rows = x2.shape[0]
@@ -585,6 +603,8 @@ def gemv(w: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None,
     m, k = w.shape
     if out is None:
         out = torch.empty(m, dtype=w.dtype, device=dev)
+    else:
+        _check_out(out, w, (m,), "gemv")
     args = (_ptr(w), _ptr(x), _ptr(out), m, k, max(w.stride(0), k), _dtype_code(w), _stream(dev))
     with _on_device(dev):
         if variant is None:
@@ -618,6 +638,8 @@ def gemm(a: torch.Tensor, b: torch.Tensor, trans_b: bool = False,
             raise PliError(f"bias must be [{n}]")
     if out is None:
         out = torch.empty((m, n), dtype=a.dtype, device=dev)
+    else:
+        _check_out(out, a, (m, n), "gemm")
     lda = a.stride(0) if m > 1 else k
     ldb = b.stride(0) if b.shape[0] > 1 else b.shape[1]
     head = (_ptr(a), _ptr(b), _ptr(out), _ptr(bias), m, n, k, max(lda, 1), max(ldb, 1),
@@ -657,6 +679,19 @@ def scale_copy(inp: torch.Tensor, out: torch.Tensor, stride: int = 1) -> torch.T
 
 
 # ------------------------------------------------------------------ softmax
+def mfma_probe(out: torch.Tensor, blocks: int, iters: int, shape: int = 0) -> torch.Tensor:
+    """Launch the MFMA calibration kernel (pli_mfma_probe): ``blocks`` x 256
+    threads, ``iters`` rounds of four bf16 MFMAs per wave (shape 0:
+    32x32x16, 1: 16x16x32); FLOPs = blocks * 4 * iters * 4 * 32768."""
+    dev = _require_gpu(out)
+    if out.dtype != torch.float32 or not out.is_contiguous() or out.numel() < blocks * 256:
+        raise PliError("mfma_probe: out must be contiguous fp32 with >= blocks*256 elements")
+    with _Dev(dev):
+        rc = lib().pli_mfma_probe(_ptr(out), int(blocks), int(iters), int(shape), _stream(dev))
+    _check(rc, "pli_mfma_probe")
+    return out
+
+
 def softmax_rows(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     """Softmax over the last dim with the single-pass online (m, d) recurrence."""
     dev = _require_gpu(x)

@@ -215,3 +215,31 @@ def test_fused_decode_step_matches_unfused(B):
             assert ((a - b).norm() / b.norm()).item() < 1e-2
     if B == 1:
         assert torch.equal(kf, ku)
+
+
+@pytest.mark.parametrize("B", [1, 8])
+@pytest.mark.parametrize("fused", [True, False])
+def test_device_pos_cache_overflow_raises(B, fused):
+    """A device-length cache that would overrun max_seq_len raises (the
+    kernels clamp to the capacity and would otherwise return wrong logits
+    silently; the reference raises on its slice-assignment mismatch)."""
+    import ch02.cached_generation as cg
+    from ch02 import CachedTransformerModel
+    torch.manual_seed(0)
+    model = CachedTransformerModel(1000, 256, 2, 4, 2, 512).cuda().bfloat16().eval()
+    cg.FUSED_DECODE = fused
+    try:
+        with torch.no_grad():
+            caches = model.create_caches(B, 12, torch.device("cuda"), torch.bfloat16, device_pos=True)
+            ids = torch.randint(0, 1000, (B, 10), device="cuda")
+            model(ids, caches)
+            tok = torch.randint(0, 1000, (B, 1), device="cuda")
+            model(tok, caches, start_pos=10)
+            model(tok, caches, start_pos=11)           # fills the cache exactly
+            with pytest.raises(RuntimeError, match="overflow"):
+                model(tok, caches, start_pos=12)
+            with pytest.raises(RuntimeError, match="overflow"):
+                model(torch.randint(0, 1000, (B, 13), device="cuda"),
+                      model.create_caches(B, 12, torch.device("cuda"), torch.bfloat16, device_pos=True))
+    finally:
+        cg.FUSED_DECODE = True

@@ -331,11 +331,19 @@ def test_gemm_decode_batch_paths(m, n, k, dt, bias, variant):
 @pytest.mark.parametrize("m", [1, 3])
 @pytest.mark.parametrize("k", [512, 1024, 1032, 2048, 2056, 5632])
 def test_gemm_skinny_cpl_boundaries(m, k):
+    """Without a bias M = 1 routes to the gemv kernel; with one (zeros, so the
+    expected output is unchanged) to the skinny kernel: both vs the oracle,
+    and the two routes bitwise equal (same per-lane chunk order)."""
     import pli_hip
     a = seeded_normal((m, k), 11 + k, "bf16")
     w = seeded_normal((300, k), 12 + k, "bf16")
     out = pli_hip.gemm(dev(a, "bf16"), dev(w, "bf16"), trans_b=True)
     assert_lin_close(out, olin.linear(a, w, None), "bf16", f"skinny gemm {m}x300x{k}")
+    zb = torch.zeros(300, device=DEV, dtype=torch.bfloat16)
+    out_b = pli_hip.gemm(dev(a, "bf16"), dev(w, "bf16"), trans_b=True, bias=zb)
+    assert_lin_close(out_b, olin.linear(a, w, None), "bf16", f"skinny gemm {m}x300x{k} + bias")
+    if m == 1 and k in (512, 1024, 2048, 5632):
+        assert torch.equal(out, out_b), "gemv route differs from the skinny kernel"
 
 
 def test_gemm_ws_abi_direct():
@@ -384,6 +392,44 @@ def test_gemm_4096_cube_rows():
     c = pli_hip.gemm(dev(a, "bf16"), dev(b, "bf16")).float().cpu().numpy()
     rows = np.random.RandomState(0).choice(m, 64, replace=False)
     assert_lin_close(torch.from_numpy(c[rows]), olin.gemm(a[rows], b), "bf16", "4096^3")
+
+
+@pytest.mark.parametrize("tp", [8, 4, 2])
+def test_row_parallel_shard_full_config(tp):
+    """ch09 TP config (BASELINE configs[4]): the per-rank
+    row shard of the 8192x8192 weight at M = 8192, X [8192, 8192/tp] and
+    W [8192, 8192/tp] (NT, bf16) through RowParallelLinear (the HIP GEMM),
+    64 random output rows against the f64 oracle (ch09/tensor_parallel.py:43-68)."""
+    from ch09 import RowParallelLinear
+    M = N = K = 8192
+    ks = K // tp
+    r = tp - 1  # the last rank's slice
+    x = seeded_normal((M, ks), 40 + tp, "bf16")
+    w = seeded_normal((N, ks), 50 + tp, "bf16") * np.float32(ks ** -0.5)
+    from oracle.numerics import round_to_bf16
+    w = round_to_bf16(w)
+    layer = RowParallelLinear(K, N, world_size=tp, rank=r).to(DEV).to(torch.bfloat16)
+    assert tuple(layer.weight.shape) == (N, ks)
+    layer.weight.data.copy_(dev(w, "bf16"))
+    with torch.no_grad():
+        y = layer(dev(x, "bf16")).float().cpu().numpy()
+    rows = np.random.RandomState(tp).choice(M, 64, replace=False)
+    assert_lin_close(torch.from_numpy(y[rows]), olin.linear(x[rows], w), "bf16", f"TP{tp} shard")
+
+
+@pytest.mark.skipif(not torch.cuda.is_available() or torch.cuda.device_count() < 2,
+                    reason="needs >= 2 visible GPUs (RCCL all-reduce of the row-parallel partials)")
+def test_row_parallel_rccl_two_ranks():
+    """HIP shard GEMM + dist.all_reduce over RCCL ("nccl" backend), 2 ranks
+    on 2 GPUs: the all-reduced partials equal the full F.linear within the
+    bf16 partial-rounding bound (tests/tp_rccl_worker.py)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29517", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    worker = os.path.join(os.path.dirname(__file__), "tp_rccl_worker.py")
+    procs = [subprocess.Popen([sys.executable, worker, str(r), "2"], env=env) for r in range(2)]
+    rcs = [p.wait(timeout=110) for p in procs]
+    assert rcs == [0, 0], rcs
 
 
 # ------------------------------------------------------- softmax / stream ---
