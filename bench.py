@@ -91,13 +91,15 @@ def load_traffic(kernel: str):
 
 def calibrate() -> dict:
     """Measured ceilings beside the datasheet roofs: the HBM
-    stream kernel (pli_scale_copy, 2 x 1 GiB) and the MFMA probe
-    (pli_mfma_probe, both bf16 shapes, operands in registers)."""
-    from ch03.roofline import measure_hbm_bandwidth, measure_mfma_peak
-    return {"hbm_GB/s": measure_hbm_bandwidth(),
+    read stream (pli_hbm_read_probe) and copy (pli_scale_copy) kernels and the
+    MFMA probe (pli_mfma_probe, both bf16 shapes, operands in registers)."""
+    from ch03.roofline import measure_hbm_bandwidth, measure_hbm_read_bandwidth, measure_mfma_peak
+    return {"hbm_GB/s": measure_hbm_read_bandwidth(),
+            "hbm_copy_GB/s": measure_hbm_bandwidth(),
             "mfma_32x32x16_TFLOP/s": measure_mfma_peak("32x32x16"),
             "mfma_16x16x32_TFLOP/s": measure_mfma_peak("16x16x32"),
-            "how": "pli_scale_copy 2x1 GiB read+write, events; pli_mfma_probe 1024 WGs x 4 waves, "
+            "how": "hbm: pli_hbm_read_probe over 2 x 1 GiB (read-only, best of 10); hbm_copy: "
+                   "pli_scale_copy 2x1 GiB read+write; mfma: pli_mfma_probe 1024 WGs x 4 waves, "
                    "4 independent MFMAs per wave from registers, pseudo-random bf16, best of 5"}
 
 

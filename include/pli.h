@@ -144,9 +144,17 @@ int pli_scale_copy(const float* in, float* out, int64_t n_out, int stride,
  * independent bf16 MFMAs from registers on pseudo-random operands (shape 0:
  * v_mfma_f32_32x32x16_bf16, 1: v_mfma_f32_16x16x32_bf16); one float per
  * thread goes to out[blocks * 256] so the work is not dead.
- * FLOPs = blocks * 4 * iters * 4 * 32768.
+ * FLOPs = blocks * 4 * iters * 4 * (32768 for shape 0, 16384 for shape 1).
  */
 int pli_mfma_probe(float* out, int blocks, int iters, int shape, void* stream);
+
+/*
+ * Read-only HBM calibration (ch03/roofline.py measure_hbm_read_bandwidth):
+ * `blocks` x 256 threads stream `bytes` (16-byte aligned, multiple of 16)
+ * with 16-byte non-temporal loads; one XOR word per thread goes to
+ * out[blocks * 256].
+ */
+int pli_hbm_read_probe(const void* buf, int64_t bytes, uint32_t* out, int blocks, void* stream);
 
 /*
  * Row softmax with the single-pass online (max, sum) recurrence of

@@ -106,6 +106,32 @@ def measure_hbm_bandwidth(nbytes: int = 1 << 30, iters: int = 20, device: str = 
     return 2 * n * 4 / sec / 1e9
 
 
+def measure_hbm_read_bandwidth(nbytes: int = 1 << 30, iters: int = 10, device: str = "cuda") -> float:
+    """Achievable HBM READ GB/s: ``pli_hbm_read_probe`` (16-byte non-temporal
+    loads, four in flight per lane) over two alternating ``nbytes`` buffers
+    (2 GiB >> the 256 MiB Infinity Cache), 8 workgroups of 256 threads per CU,
+    best of ``iters`` event-timed launches -- the ceiling of the
+    read-dominated GEMV and decode-attention kernels."""
+    import torch
+
+    import pli_hip
+
+    bufs = [torch.empty(nbytes // 4, device=device, dtype=torch.int32).fill_(i + 1) for i in range(2)]
+    blocks = MI355X_CUS * 8
+    out = torch.empty(blocks * 256, device=device, dtype=torch.int32)
+    for b in bufs:
+        pli_hip.hbm_read_probe(b, out, blocks)
+    best = float("inf")
+    for i in range(iters):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        pli_hip.hbm_read_probe(bufs[i & 1], out, blocks)
+        e.record()
+        e.synchronize()
+        best = min(best, s.elapsed_time(e) / 1e3)
+    return nbytes / best / 1e9
+
+
 def measure_mfma_peak(shape: str = "32x32x16", iters: int = 4096, reps: int = 5,
                       device: str = "cuda") -> float:
     """Achievable bf16 MFMA TFLOP/s: ``pli_mfma_probe`` (four independent
@@ -128,7 +154,7 @@ def measure_mfma_peak(shape: str = "32x32x16", iters: int = 4096, reps: int = 5,
         e.record()
         e.synchronize()
         best = min(best, s.elapsed_time(e) / 1e3)
-    return blocks * 4 * iters * 4 * 32768 / best / 1e12
+    return blocks * 4 * iters * 4 * (32768 if sh == 0 else 16384) / best / 1e12
 
 
 def measured_spec(hbm_gbps: float, mfma_tflops: float | None = None) -> HardwareSpec:

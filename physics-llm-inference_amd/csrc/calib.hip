@@ -61,8 +61,39 @@ __global__ __launch_bounds__(256) void mfma_probe(float* __restrict__ out, int i
     out[blockIdx.x * 256 + threadIdx.x] = s;
 }
 
+__global__ __launch_bounds__(256) void hbm_read_probe(const i32x4* __restrict__ src, int64_t n16,
+                                                      uint32_t* __restrict__ out) {
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    uint32_t acc = 0;
+    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        const i32x4 a = __builtin_nontemporal_load(src + i);
+        const i32x4 b = __builtin_nontemporal_load(src + i + stride);
+        const i32x4 c = __builtin_nontemporal_load(src + i + 2 * stride);
+        const i32x4 d = __builtin_nontemporal_load(src + i + 3 * stride);
+        acc ^= (uint32_t)(a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w);
+        acc ^= (uint32_t)(c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^ d.z ^ d.w);
+    }
+    for (; i < n16; i += stride) {
+        const i32x4 a = __builtin_nontemporal_load(src + i);
+        acc ^= (uint32_t)(a.x ^ a.y ^ a.z ^ a.w);
+    }
+    out[(int64_t)blockIdx.x * 256 + threadIdx.x] = acc;
+}
+
 }  // namespace
 }  // namespace pli
+
+extern "C" int pli_hbm_read_probe(const void* buf, int64_t bytes, uint32_t* out, int blocks, void* stream) {
+    using namespace pli;
+    clear_error();
+    PLI_REQUIRE(buf != nullptr && out != nullptr, "pli_hbm_read_probe: null pointer");
+    PLI_REQUIRE(aligned16(buf) && bytes > 0 && bytes % 16 == 0 && blocks > 0,
+                "pli_hbm_read_probe: need a 16-byte aligned buffer of 16k bytes and blocks > 0");
+    hipLaunchKernelGGL(hbm_read_probe, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                       (const i32x4*)buf, bytes / 16, out);
+    return launch_status("hbm_read_probe");
+}
 
 extern "C" int pli_mfma_probe(float* out, int blocks, int iters, int shape, void* stream) {
     using namespace pli;

@@ -15,7 +15,7 @@ import torch
 
 __all__ = [
     "PliError", "lib", "library_path", "available", "DTYPE_CODE",
-    "flash_attn_fwd", "gemv", "gemm", "scale_copy", "mfma_probe", "softmax_rows",
+    "flash_attn_fwd", "gemv", "gemm", "scale_copy", "mfma_probe", "hbm_read_probe", "softmax_rows",
     "online_softmax_with_output",
 ]
 
@@ -61,6 +61,7 @@ _SIGS = {
     "pli_moe_combine": [_vp, _c_i64, _vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_int, _c_int, _vp],
     "pli_scale_copy": [_vp, _vp, _c_i64, _c_int, _vp],
     "pli_mfma_probe": [_vp, _c_int, _c_int, _c_int, _vp],
+    "pli_hbm_read_probe": [_vp, _c_i64, _vp, _c_int, _vp],
     "pli_softmax_rows": [_vp, _vp, _c_i64, _c_int, _c_int, _vp],
     "pli_online_softmax_with_output": [_vp, _vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_int, _vp],
     "pli_attn_decode_workspace_size": [_c_int] * 6,
@@ -682,13 +683,26 @@ def scale_copy(inp: torch.Tensor, out: torch.Tensor, stride: int = 1) -> torch.T
 def mfma_probe(out: torch.Tensor, blocks: int, iters: int, shape: int = 0) -> torch.Tensor:
     """Launch the MFMA calibration kernel (pli_mfma_probe): ``blocks`` x 256
     threads, ``iters`` rounds of four bf16 MFMAs per wave (shape 0:
-    32x32x16, 1: 16x16x32); FLOPs = blocks * 4 * iters * 4 * 32768."""
+    32x32x16, 1: 16x16x32); FLOPs = blocks * 4 * iters * 4 * (32768 or 16384)."""
     dev = _require_gpu(out)
     if out.dtype != torch.float32 or not out.is_contiguous() or out.numel() < blocks * 256:
         raise PliError("mfma_probe: out must be contiguous fp32 with >= blocks*256 elements")
-    with _Dev(dev):
+    with _on_device(dev):
         rc = lib().pli_mfma_probe(_ptr(out), int(blocks), int(iters), int(shape), _stream(dev))
     _check(rc, "pli_mfma_probe")
+    return out
+
+
+def hbm_read_probe(buf: torch.Tensor, out: torch.Tensor, blocks: int) -> torch.Tensor:
+    """Stream ``buf`` (contiguous, 16-byte multiple) with non-temporal 16-byte
+    loads, ``blocks`` x 256 threads (pli_hbm_read_probe); out: int32 >= blocks*256."""
+    dev = _require_gpu(buf)
+    nbytes = buf.numel() * buf.element_size()
+    if not buf.is_contiguous() or nbytes % 16 or out.numel() < blocks * 256 or out.element_size() != 4:
+        raise PliError("hbm_read_probe: contiguous buffer of 16k bytes, 4-byte out >= blocks*256")
+    with _on_device(dev):
+        rc = lib().pli_hbm_read_probe(_ptr(buf), nbytes, _ptr(out), int(blocks), _stream(dev))
+    _check(rc, "pli_hbm_read_probe")
     return out
 
 
