@@ -495,23 +495,28 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
 }
 
 // Kernel variants behind the same ABI (pli_flash_attn_fwd_variant, tuning /
-// A-B runs; every one is parity-tested at full size):
+// A-B runs; every one is parity-tested, the default at the full bench size):
 //  21: attn_fwd_v2, 8 waves, permlane row max + defer-max (THR 8, log2) +
-//      rounded-P row sum by v_dot2c (round-1 default; 1019 TF at the bench
-//      config, driver run r01)
-//  50: attn_fwd_v7 (flash_v7.hip): prescaled Q, -m as the first QK^T MFMA's C
-//      operand, speculative exp2, row sum on the matrix core (selector MFMA)
-//  51: attn_fwd_v7 with exact scaling (no Q prescale: p = exp2(fma(s, c, -m)))
+//      rounded-P row sum by v_dot2c (the round-1 default, kept as baseline)
+//  50: attn_fwd_v7 (flash_v7.hip): Q prescaled by scale*log2(e) (bf16-rounded)
+//      with -m as the first QK^T MFMA's C operand, speculative exp2, row sum
+//      on the matrix core; register-staged K/V, one tile ahead
+//  51: attn_fwd_v7 with exact scaling (p = exp2(fma(s, c, -m)))
+//  54: attn_fwd_v10: v7's body, K/V by LDS-DMA two tiles ahead into a 3-deep
+//      ring of XOR-swizzled images (D = 128; other head dims take v7), prescaled
+//  55: attn_fwd_v10 with exact scaling -- the DEFAULT (D = 128; D = 64 -> 51)
 // The round-1 experiments (XOR-swizzled v1, staggered v3, pipelined v4/v5,
-// 16x16x32 v6, ping-pong, segmented, one-wave-per-SIMD w4/w4p) were removed
-// from the library in round 2; their measurements are kept in DESIGN.md 3.1.
-constexpr int kDefaultVariant = 50;
+// 16x16x32 v6, ping-pong, segmented, one-wave-per-SIMD w4/w4p) and the
+// round-2 ones that lost (in-wave pipelined v8, one-wave-per-SIMD v9, a
+// two-barrier stagger with s_setprio, a half-tile lag on a 4-deep ring) are
+// not in the library; their measurements are in DESIGN.md 3.1.
+constexpr int kDefaultVariant = 55;
 
 template <typename T, int D>
 int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int H,
                 int group, int Nq, int Nk, const AttnStrides& st, float scale,
                 int causal, hipStream_t stream, int variant) {
-    if (variant == 50 || variant == 51) {
+    if (variant == 50 || variant == 51 || variant == 54 || variant == 55) {
         // v7 prescales Q by scale*log2(e); above 1 that could overflow fp16 Q
         if (scale * 1.4426950408889634f <= 1.f) {
             const V7Strides s7{st.qb, st.qh, st.qn, st.kb, st.kh, st.kn,

@@ -72,7 +72,13 @@ __device__ __forceinline__ float v7_xor32_sum(float x) {
 //          C operand of the first QK^T MFMA: p = exp2(acc), no fma per score;
 //          the Q rounding costs score precision (2^-9 relative in bf16).
 // PRE = 0: exact scaling, S accumulates from 0 and p = exp2(fma(s, c, -m)).
-template <typename T, int D, int PRE>
+#ifdef PLI_FLASH_STAMPS
+// diagnostic build only (tools/build_diag.sh -> tools/libpli_diag.so, never
+// the product library): per-segment s_memtime sums over all waves
+__device__ unsigned long long g_v7_stamps[16];
+#endif
+
+template <typename T, int D, int PRE, bool STAMP = false>
 __global__ __launch_bounds__(512, 2) void attn_fwd_v7(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
     const uint16_t* __restrict__ v, uint16_t* __restrict__ o, int H, int group,
@@ -87,6 +93,19 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v7(
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int h32 = lane >> 5, l32 = lane & 31;
+    // STAMP: segment cycle sums (see the .s: each stamp is fenced by
+    // sched_barriers, so the diagnostic build's schedule differs -- read shares)
+    unsigned long long st_sum[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0;
+    auto stamp = [&](int seg) __attribute__((always_inline)) {
+        if constexpr (STAMP) {
+            unsigned long long now;
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(now)::"memory");
+            __builtin_amdgcn_sched_barrier(0);
+            if (seg >= 0) st_sum[seg] += now - st_last;
+            st_last = now;
+        }
+    };
     const int lb = xcd_remap(blockIdx.x, nblocks);
     const int bh = lb / qblocks;
     // causal: heaviest query blocks of a head first, so the grid drains on light ones
@@ -132,7 +151,7 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v7(
     const uint16_t* vg = vp + (int64_t)srow * st.vn + sch * 8;
     const int kw = srow * L::KS + sch * 16, vw = L::KSZ + srow * L::VS + sch * 16;
     i32x4 kst[CPT], vst[CPT];
-    auto load_tile = [&](int t) {
+    auto load_tile = [&](int t) __attribute__((always_inline)) {
         if (t < t_full) {
 #pragma unroll
             for (int i = 0; i < CPT; ++i) {
@@ -152,7 +171,7 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v7(
             }
         }
     };
-    auto store_tile = [&](int buf) {
+    auto store_tile = [&](int buf) __attribute__((always_inline)) {
         char* base = smem + buf * L::BUF;
 #pragma unroll
         for (int i = 0; i < CPT; ++i) {
@@ -188,21 +207,15 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v7(
     float m_run = PRE != 0 ? 0.f : -1e30f;
     f32x4 lsum = {0.f, 0.f, 0.f, 0.f};
 
-    if (nt > 0) {
-        load_tile(0);
-        store_tile(0);
-    }
-    __syncthreads();
-
-    auto body = [&](int t, auto first_tag) {
+    // X(t): S = K(t) Q^T, mask, row max, (speculative) exps, pack -> pb
+    i32x4 pb[2][2];
+    auto X = [&](int t, auto first_tag) __attribute__((always_inline)) {
         constexpr bool FIRST = decltype(first_tag)::value;
-        if (t + 1 < nt) load_tile(t + 1);
         const char* kb = smem + (t & 1) * L::BUF + kr;
-        const char* vb = smem + (t & 1) * L::BUF + vr;
 
         // s[tt][r] = S(key 32tt + 8(r>>2) + 4h32 + (r&3), query l32)  (PRE: S*c - m)
         f32x16 s[2];
-        auto qk = [&]() {
+        auto qk = [&]() __attribute__((always_inline)) {
 #pragma unroll
             for (int tt = 0; tt < 2; ++tt) {
                 if constexpr (PRE != 0) {
@@ -228,13 +241,14 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v7(
                     }
             }
         };
-        auto expo = [&]() {
+        auto expo = [&]() __attribute__((always_inline)) {
 #pragma unroll
             for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
                 for (int r = 0; r < 16; ++r)
                     s[tt][r] = __builtin_amdgcn_exp2f(PRE != 0 ? s[tt][r] : fmaf(s[tt][r], c, -m_run));
         };
+        stamp(0);
         qk();
 
         // row max: two v_max3 chains (-fno-honor-nans: no canonicalising
@@ -246,6 +260,8 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v7(
             my = fmaxf(fmaxf(my, s[0][r + 1]), s[1][r + 1]);
         }
         mx = v7_xor32_max(fmaxf(mx, my));
+        if constexpr (STAMP) asm volatile("" ::"v"(mx));
+        stamp(1);
 
         if constexpr (FIRST) {
             // the first tile sets the running max (O and l are still zero)
@@ -268,10 +284,12 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v7(
             // the max chain)
             expo();
             asm volatile("" : "+v"(s[0]), "+v"(s[1]));
+            stamp(2);
             const bool up = PRE != 0 ? mx > V7_THR : mx * c > m_run + V7_THR;
             if (__ballot(up)) {
                 // rare: some row's max rose by more than the threshold.  K(t)
-                // is still in LDS: recompute S and redo the exps.
+                // is still in LDS: recompute S and redo the exps.  (O holds
+                // every earlier tile's PV: its rescale is exact here.)
                 float alpha;
                 if constexpr (PRE != 0) {
                     const float delta = up ? mx : 0.f;
@@ -295,7 +313,6 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v7(
         }
 
         // P^T fragments: registers 8s2..8s2+7 of s[tt] are k-step s2
-        i32x4 pb[2][2];
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
@@ -306,12 +323,16 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v7(
                                    (int)pack2<T>(s[tt][r0 + 4], s[tt][r0 + 5]),
                                    (int)pack2<T>(s[tt][r0 + 6], s[tt][r0 + 7])};
             }
+        if constexpr (STAMP) asm volatile("" ::"v"(pb[0][0]), "v"(pb[0][1]), "v"(pb[1][0]), "v"(pb[1][1]));
+        stamp(3);
+    };
+    // Y(t): l += rowsum(P) (selector MFMA), O^T += V(t)^T P^T
+    auto Y = [&](int t) __attribute__((always_inline)) {
+        const char* vb = smem + (t & 1) * L::BUF + vr;
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) lsum = mfma16x16x32<T>(sel, pb[tt][s2], lsum);
-
-        // O^T += V^T P^T ; V^T fragment via two transposed reads
 #pragma unroll
         for (int dblk = 0; dblk < D / 32; ++dblk)
 #pragma unroll
@@ -323,14 +344,38 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v7(
                     const i32x2 hi = lds_read_tr16(vb, ro + 8 * L::VS);
                     oacc[dblk] = mfma32x32x16<T>(i32x4{lo.x, lo.y, hi.x, hi.y}, pb[tt][s2], oacc[dblk]);
                 }
-
-        if (t + 1 < nt) store_tile((t + 1) & 1);
-        __syncthreads();
+        stamp(4);
     };
 
-    if (nt > 0) body(0, std::true_type{});
-    for (int t = 1; t < nt; ++t) body(t, std::false_type{});
+    // one barrier per tile; tile t+1 register-staged under tile t
+    if (nt > 0) {
+        load_tile(0);
+        store_tile(0);
+    }
+    __syncthreads();
+    auto tile = [&](int t, auto first_tag) __attribute__((always_inline)) {
+        stamp(-1);
+        if (t + 1 < nt) load_tile(t + 1);
+        X(t, first_tag);
+        Y(t);
+        if (t + 1 < nt) store_tile((t + 1) & 1);
+        stamp(5);
+        __syncthreads();
+        stamp(6);
+    };
+    if (nt > 0) tile(0, std::true_type{});
+    for (int t = 1; t < nt; ++t) tile(t, std::false_type{});
 
+#ifdef PLI_FLASH_STAMPS
+    if constexpr (STAMP) {
+        if (lane == 0) {
+#pragma unroll
+            for (int i = 0; i < 7; ++i) atomicAdd(&g_v7_stamps[i], st_sum[i]);
+            atomicAdd(&g_v7_stamps[8], (unsigned long long)nt);
+            atomicAdd(&g_v7_stamps[9], 1ull);
+        }
+    }
+#endif
     // ---- epilogue: O = O^T / l, query row l32
     const float l = v7_xor32_sum(lsum[0]);
     const float inv = l > 0.f ? 1.f / l : 0.f;
@@ -339,6 +384,298 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v7(
         uint16_t* op = o + b * st.ob + hq * st.oh + (int64_t)qr * st.on;
         // group k = 4*dblk + i holds columns 8k+4*h32 .. +3 of row qr; after
         // swapping (k, k+1): lower lanes hold cols 8k..8k+7, upper 8k+8..8k+15
+#pragma unroll
+        for (int dblk = 0; dblk < D / 32; ++dblk)
+#pragma unroll
+            for (int i = 0; i < 4; i += 2) {
+                const f32x16& a = oacc[dblk];
+                const uint32_t ax = pack2<T>(a[4 * i] * inv, a[4 * i + 1] * inv);
+                const uint32_t ay = pack2<T>(a[4 * i + 2] * inv, a[4 * i + 3] * inv);
+                const uint32_t bx = pack2<T>(a[4 * i + 4] * inv, a[4 * i + 5] * inv);
+                const uint32_t by = pack2<T>(a[4 * i + 6] * inv, a[4 * i + 7] * inv);
+                const auto rx = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
+                const auto ry = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
+                const int d = dblk * 32 + 8 * i + 8 * h32;
+                *reinterpret_cast<i32x4*>(op + d) = i32x4{(int)rx[0], (int)ry[0], (int)rx[1], (int)ry[1]};
+            }
+    }
+}
+
+// --------------------------------------------------------------------------
+// attn_fwd_v10 (D = 128): v7's body with the K/V staging moved off the
+// registers and two tiles ahead.  Stamps of v7 (tools/flash_stamps.py) put
+// ~19 % of a tile in the vmcnt wait before the LDS writes (the next tile's
+// global loads, issued one tile earlier, had not landed) and ~15 % at the
+// barrier.  Here every wave LDS-DMAs (global_load_lds_dwordx4, 1 KiB
+// lane-linear pieces: 2 of K + 2 of V per wave per tile) tile t+2 into a
+// 3-deep ring at the top of tile t, and only a counted vmcnt (tile t+1's
+// pieces landed, t+2's still in flight) precedes the barrier.  The images are
+// unpadded 256-byte rows with the 16-byte chunks XOR-swizzled by
+// f(row) = (row&3)<<2 | (row>>2)&3 on the DMA source address (conflict-free
+// for the b128 K-fragment read and the tr_b16 V^T read, cdna guide T10
+// layout (b)); the fragment address of k-step kk is A0 ^ (kk<<5), of V block
+// dblk B0 ^ (dblk<<6).  Rows past Nk re-read row Nk-1 (masked / weight 0).
+template <typename T, int PRE>
+__global__ __launch_bounds__(512, 2) void attn_fwd_v10(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
+    const uint16_t* __restrict__ v, uint16_t* __restrict__ o, int H, int group,
+    int Nq, int Nk, V7Strides st, float c, int causal, int qblocks, int nblocks) {
+    constexpr int D = 128;
+    constexpr int IMG = V7_KT * 256;  // one [64][128] 16-bit image
+    constexpr int BUFB = 2 * IMG;     // K image + V image
+    constexpr int NBUF = 3;
+    __shared__ __attribute__((aligned(1024))) char smem[NBUF * BUFB];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int h32 = lane >> 5, l32 = lane & 31;
+    const int lb = xcd_remap(blockIdx.x, nblocks);
+    const int bh = lb / qblocks;
+    const int qblk = causal ? qblocks - 1 - lb % qblocks : lb % qblocks;
+    const int b = bh / H, hq = bh % H, hk = hq / group;
+    const int qbase = qblk * (V7_NW * V7_QW);
+    const int q0 = qbase + wave * V7_QW;
+    const int off_diag = Nk - Nq;
+
+    const uint16_t* qp = q + b * st.qb + hq * st.qh;
+    const uint16_t* kp = k + b * st.kb + hk * st.kh;
+    const uint16_t* vp = v + b * st.vb + hk * st.vh;
+
+    int kv_end = Nk;
+    if (causal) kv_end = min(Nk, qbase + V7_NW * V7_QW + off_diag);
+    const int nt = kv_end > 0 ? cdiv(kv_end, V7_KT) : 0;
+    const int t_full = Nk / V7_KT;
+    int t_mask = t_full;
+    if (causal) t_mask = min(t_mask, max(0, (q0 + off_diag + 1) / V7_KT));
+
+    // ---- LDS-DMA plan: wave w fills pieces 2w, 2w+1 of the K and V images;
+    // lane -> row 4*piece + (lane>>4), stored chunk position lane&15 holds
+    // logical chunk (lane&15) ^ f(row)
+    auto fsw = [](int row) __attribute__((always_inline)) { return ((row & 3) << 2) | ((row >> 2) & 3); };
+    int drow[2];
+    uint32_t koff[2], voff[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        drow[i] = 4 * (2 * wave + i) + (lane >> 4);
+        const int ch = (lane & 15) ^ fsw(drow[i]);
+        koff[i] = (uint32_t)(drow[i] * (int)st.kn + 8 * ch) * 2u;
+        voff[i] = (uint32_t)(drow[i] * (int)st.vn + 8 * ch) * 2u;
+    }
+    auto dma = [&](const uint16_t* tbase, uint32_t off, uint32_t lds) __attribute__((always_inline)) {
+        uint32_t keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %3\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(keep) : "s"(lds), "v"(off), "s"(tbase) : "memory");
+    };
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
+    auto dma_tile = [&](int t, int buf) __attribute__((always_inline)) {
+        const uint16_t* kt = kp + (int64_t)t * V7_KT * st.kn;
+        const uint16_t* vt = vp + (int64_t)t * V7_KT * st.vn;
+        uint32_t ko[2] = {koff[0], koff[1]}, vo[2] = {voff[0], voff[1]};
+        if (t >= t_full) {  // ragged last tile: rows past Nk re-read row Nk-1
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int over = max(0, t * V7_KT + drow[i] - (Nk - 1));
+                ko[i] -= (uint32_t)(over * (int)st.kn * 2);
+                vo[i] -= (uint32_t)(over * (int)st.vn * 2);
+            }
+        }
+        const uint32_t base = lds0 + buf * BUFB + (2 * wave) * 1024;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            dma(kt, ko[i], base + i * 1024);
+            dma(vt, vo[i], base + IMG + i * 1024);
+        }
+    };
+
+    // ---- Q^T fragments (B operand)
+    i32x4 qf[D / 16];
+    {
+        const int qr = q0 + l32;
+        const bool ok = qr < Nq;
+        const uint16_t* src = qp + (int64_t)(ok ? qr : 0) * st.qn + 8 * h32;
+#pragma unroll
+        for (int kk = 0; kk < D / 16; ++kk) {
+            const i32x4 x = *reinterpret_cast<const i32x4*>(src + 16 * kk);
+            qf[kk] = ok ? x : i32x4{0, 0, 0, 0};
+        }
+        if constexpr (PRE != 0) {
+#pragma unroll
+            for (int kk = 0; kk < D / 16; ++kk)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) qf[kk][j] = v7_scale_pair<T>(qf[kk][j], c);
+        }
+    }
+
+    // ---- fragment addresses (byte offsets inside a buffer)
+    const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+    const int A0 = l32 * 256 + ((h32 ^ fsw(l32)) << 4);
+    const int c0 = 2 * (g & 1) + (pp >> 1);
+    const int B0 = IMG + (4 * h32 + qq) * 256 + ((c0 ^ ((qq << 2) | h32)) << 4) + 8 * (pp & 1);
+
+    const bool sel_on = (i16 == 0 && (g & 1) == 0) || (i16 == 4 && (g & 1) == 1);
+    const int one = sel_on ? V7Ones<T>::pair : 0;
+    const i32x4 sel = {one, one, one, one};
+
+    f32x16 oacc[D / 32];
+#pragma unroll
+    for (int d = 0; d < D / 32; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[d][r] = 0.f;
+    f32x16 negm;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) negm[r] = 0.f;
+    float m_run = PRE != 0 ? 0.f : -1e30f;
+    f32x4 lsum = {0.f, 0.f, 0.f, 0.f};
+
+    i32x4 pb[2][2];
+    auto X = [&](int t, int buf, auto first_tag) __attribute__((always_inline)) {
+        constexpr bool FIRST = decltype(first_tag)::value;
+        const char* kb = smem + buf * BUFB;
+        f32x16 s[2];
+        auto qk = [&]() __attribute__((always_inline)) {
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt) {
+                const i32x4 k0 = lds_read_b128(kb, A0 + tt * 8192);
+                if constexpr (PRE != 0) {
+                    s[tt] = mfma32x32x16<T>(k0, qf[0], negm);
+                } else {
+                    f32x16 z;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) z[r] = 0.f;
+                    s[tt] = mfma32x32x16<T>(k0, qf[0], z);
+                }
+#pragma unroll
+                for (int kk = 1; kk < D / 16; ++kk)
+                    s[tt] = mfma32x32x16<T>(lds_read_b128(kb, (A0 ^ (kk << 5)) + tt * 8192), qf[kk], s[tt]);
+            }
+            if (t >= t_mask) {
+                const int lim = causal ? q0 + l32 + off_diag : Nk;
+#pragma unroll
+                for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int key = t * V7_KT + tt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
+                        if (key >= Nk || key > lim) s[tt][r] = -INFINITY;
+                    }
+            }
+        };
+        auto expo = [&]() __attribute__((always_inline)) {
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    s[tt][r] = __builtin_amdgcn_exp2f(PRE != 0 ? s[tt][r] : fmaf(s[tt][r], c, -m_run));
+        };
+        qk();
+        float mx = fmaxf(s[0][0], s[1][0]), my = fmaxf(s[0][1], s[1][1]);
+#pragma unroll
+        for (int r = 2; r < 16; r += 2) {
+            mx = fmaxf(fmaxf(mx, s[0][r]), s[1][r]);
+            my = fmaxf(fmaxf(my, s[0][r + 1]), s[1][r + 1]);
+        }
+        mx = v7_xor32_max(fmaxf(mx, my));
+        if constexpr (FIRST) {
+            if constexpr (PRE != 0) {
+                const float delta = mx == -INFINITY ? 0.f : mx;
+                m_run = delta;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) negm[r] = -m_run;
+#pragma unroll
+                for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) s[tt][r] -= delta;
+            } else {
+                m_run = mx == -INFINITY ? -1e30f : mx * c;
+            }
+            expo();
+        } else {
+            expo();
+            asm volatile("" : "+v"(s[0]), "+v"(s[1]));
+            const bool up = PRE != 0 ? mx > V7_THR : mx * c > m_run + V7_THR;
+            if (__ballot(up)) {
+                float alpha;
+                if constexpr (PRE != 0) {
+                    const float delta = up ? mx : 0.f;
+                    m_run += delta;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) negm[r] = -m_run;
+                    alpha = __builtin_amdgcn_exp2f(-delta);
+                } else {
+                    const float m_new = up ? mx * c : m_run;
+                    alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+                    m_run = m_new;
+                }
+                qk();
+                expo();
+#pragma unroll
+                for (int d = 0; d < D / 32; ++d)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
+                lsum[0] *= alpha;
+            }
+        }
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const int r0 = 8 * s2;
+                pb[tt][s2] = i32x4{(int)pack2<T>(s[tt][r0 + 0], s[tt][r0 + 1]),
+                                   (int)pack2<T>(s[tt][r0 + 2], s[tt][r0 + 3]),
+                                   (int)pack2<T>(s[tt][r0 + 4], s[tt][r0 + 5]),
+                                   (int)pack2<T>(s[tt][r0 + 6], s[tt][r0 + 7])};
+            }
+    };
+    auto Y = [&](int buf) __attribute__((always_inline)) {
+        const char* vb = smem + buf * BUFB;
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) lsum = mfma16x16x32<T>(sel, pb[tt][s2], lsum);
+#pragma unroll
+        for (int dblk = 0; dblk < D / 32; ++dblk) {
+            const int alo = B0 ^ (dblk << 6), ahi = (alo ^ 32) + 2048;
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    const int ro = (tt * 32 + 16 * s2) * 256;
+                    const i32x2 lo = lds_read_tr16(vb, alo + ro);
+                    const i32x2 hi = lds_read_tr16(vb, ahi + ro);
+                    oacc[dblk] = mfma32x32x16<T>(i32x4{lo.x, lo.y, hi.x, hi.y}, pb[tt][s2], oacc[dblk]);
+                }
+        }
+    };
+    // counted wait: tile t+1's pieces landed while t+2's (4 per wave) fly
+    auto wait_next = [&](bool two_in_flight) __attribute__((always_inline)) {
+        if (two_in_flight) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    };
+
+    if (nt > 0) {
+        dma_tile(0, 0);
+        if (nt > 1) dma_tile(1, 1);
+        // (Q's own loads were waited for by the compiler above)
+        wait_next(nt > 1);
+        int cur = 0;
+        auto tile = [&](int t, auto first_tag) __attribute__((always_inline)) {
+            const int n2 = cur == 0 ? 2 : cur - 1;  // (cur + 2) % 3
+            if (t + 2 < nt) dma_tile(t + 2, n2);
+            X(t, cur, first_tag);
+            Y(cur);
+            wait_next(t + 2 < nt);
+            cur = cur == 2 ? 0 : cur + 1;
+        };
+        tile(0, std::true_type{});
+        for (int t = 1; t < nt; ++t) tile(t, std::false_type{});
+    }
+
+    const float l = v7_xor32_sum(lsum[0]);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const int qr = q0 + l32;
+    if (qr < Nq) {
+        uint16_t* op = o + b * st.ob + hq * st.oh + (int64_t)qr * st.on;
 #pragma unroll
         for (int dblk = 0; dblk < D / 32; ++dblk)
 #pragma unroll
@@ -377,6 +714,24 @@ int launch_v7_typed(const void* q, const void* k, const void* v, void* o, int B,
             hipLaunchKernelGGL((attn_fwd_v7<T, D, 0>), grid, block, 0, stream, qq, kk, vv, oo, H, group,
                                Nq, Nk, st, c, causal, qblocks, (int)nb);
             break;
+        case 4:
+        case 5:
+            // v10 is D = 128 only; other head dims take the matching v7 body
+            if constexpr (D == 128) {
+                if (sub == 4)
+                    hipLaunchKernelGGL((attn_fwd_v10<T, 1>), grid, block, 0, stream, qq, kk, vv, oo, H, group,
+                                       Nq, Nk, st, c, causal, qblocks, (int)nb);
+                else
+                    hipLaunchKernelGGL((attn_fwd_v10<T, 0>), grid, block, 0, stream, qq, kk, vv, oo, H, group,
+                                       Nq, Nk, st, c, causal, qblocks, (int)nb);
+            } else if (sub == 4) {
+                hipLaunchKernelGGL((attn_fwd_v7<T, D, 1>), grid, block, 0, stream, qq, kk, vv, oo, H, group,
+                                   Nq, Nk, st, c, causal, qblocks, (int)nb);
+            } else {
+                hipLaunchKernelGGL((attn_fwd_v7<T, D, 0>), grid, block, 0, stream, qq, kk, vv, oo, H, group,
+                                   Nq, Nk, st, c, causal, qblocks, (int)nb);
+            }
+            break;
         default:
             set_error("pli_flash_attn_fwd: unknown v7 body %d", sub);
             return PLI_EINVAL;
@@ -398,3 +753,37 @@ int launch_attn_v7(const void* q, const void* k, const void* v, void* o, int B, 
 }
 
 }  // namespace pli
+
+#ifdef PLI_FLASH_STAMPS
+// Diagnostic entry (tools/libpli_diag.so only): one launch of the v7 body
+// `sub` (0..3 as launch_attn_v7) with stamps, contiguous [B,H,N,D] bf16,
+// then the 16 stamp words (segment sums, tiles, waves) copied to `out`.
+extern "C" int pli_diag_flash_stamps(const void* q, const void* k, const void* v, void* o, int B, int H,
+                                     int N, int sub, unsigned long long* out) {
+    using namespace pli;
+    constexpr int D = 128;
+    const int64_t sn = D, sh = (int64_t)N * D, sb = (int64_t)H * N * D;
+    const V7Strides st{sb, sh, sn, sb, sh, sn, sb, sh, sn, sb, sh, sn};
+    const int qblocks = cdiv(N, V7_NW * V7_QW);
+    const int nb = B * H * qblocks;
+    const float c = (1.f / sqrtf((float)D)) * 1.4426950408889634f;
+    unsigned long long zero[16] = {0};
+    hipMemcpyToSymbol(HIP_SYMBOL(g_v7_stamps), zero, sizeof(zero));
+    const auto* qq = (const uint16_t*)q;
+    const auto* kk = (const uint16_t*)k;
+    const auto* vv = (const uint16_t*)v;
+    auto* oo = (uint16_t*)o;
+#define PLI_DIAG(PRE_) \
+    hipLaunchKernelGGL((attn_fwd_v7<bf16_t, D, PRE_, true>), dim3(nb), dim3(512), 0, 0, qq, kk, vv, oo, H, 1, \
+                       N, N, st, c, 0, qblocks, nb)
+    switch (sub) {
+        case 0: PLI_DIAG(1); break;
+        case 1: PLI_DIAG(0); break;
+        default: return PLI_EINVAL;
+    }
+#undef PLI_DIAG
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    hipMemcpyFromSymbol(out, HIP_SYMBOL(g_v7_stamps), 16 * sizeof(unsigned long long));
+    return 0;
+}
+#endif

@@ -106,7 +106,7 @@ def test_flash_vs_oracle(case):
 
 
 # every MFMA variant (alternates A/B-tested by tools/tune.py) on the MFMA-eligible cases
-MFMA_VARIANTS = (21, 50, 51)
+MFMA_VARIANTS = (21, 50, 51, 54, 55)
 
 
 
@@ -139,11 +139,11 @@ def test_flash_strided_views_and_out_param():
 
 # variants whose Q is prescaled by scale*log2(e) and rounded to the 16-bit
 # input type before the MFMA (the rest scale the f32 scores exactly)
-PRESCALED = (50,)
-DEFAULT_VARIANT = 50
+PRESCALED = (50, 54)
+DEFAULT_VARIANT = 55
 
 
-def test_flash_default_is_variant_50():
+def test_flash_default_is_variant_55():
     import pli_hip
     q, k, v = (dev(x, "bf16") for x in stress_inputs("late"))
     assert torch.equal(pli_hip.flash_attn_fwd(q, k, v), pli_hip.flash_attn_fwd(q, k, v, variant=DEFAULT_VARIANT))
@@ -181,7 +181,7 @@ def test_flash_stress(variant, name):
         assert err <= tol, f"stress {name}: {err:.3e} > {tol:.3e}"
 
 
-@pytest.mark.parametrize("variant", [None, 21])
+@pytest.mark.parametrize("variant", [None, 21, 50, 51, 54])
 def test_flash_full_config_properties(variant):
     """B=8 S=4096 H=32 D=128 bf16 (the bench config): v = 1 gives exactly 1;
     two heads checked against the f64 oracle; key permutation invariance."""
