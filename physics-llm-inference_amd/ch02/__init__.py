@@ -2,8 +2,7 @@
 
 Decode attention over the cache runs on ``pli_attn_decode`` (split-K
 flash-decoding).  ``naive_generate`` (``ch02/generation.py``) re-runs the
-whole ``ch01.transformer`` model per token; that model is outside the hot
-path and is not mirrored.
+whole ``ch01.TransformerModel`` per token (every layer on the HIP kernels).
 """
 
 from .cached_generation import (
@@ -15,6 +14,7 @@ from .cached_generation import (
     SwiGLUFFN,
     cached_generate,
 )
+from .generation import naive_generate
 from .kv_cache import GQAWithCache, KVCache, attend_cached, calculate_kv_cache_size
 
 __all__ = [
@@ -28,5 +28,6 @@ __all__ = [
     "CachedTransformerModel",
     "RMSNorm",
     "SwiGLUFFN",
+    "naive_generate",
     "cached_generate",
 ]

@@ -415,7 +415,7 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v7(
 // for the b128 K-fragment read and the tr_b16 V^T read, cdna guide T10
 // layout (b)); the fragment address of k-step kk is A0 ^ (kk<<5), of V block
 // dblk B0 ^ (dblk<<6).  Rows past Nk re-read row Nk-1 (masked / weight 0).
-template <typename T, int PRE>
+template <typename T, int PRE, bool STAMP = false>
 __global__ __launch_bounds__(512, 2) void attn_fwd_v10(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
     const uint16_t* __restrict__ v, uint16_t* __restrict__ o, int H, int group,
@@ -429,6 +429,17 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v10(
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int h32 = lane >> 5, l32 = lane & 31;
+    unsigned long long st_sum[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0;
+    auto stamp = [&](int seg) __attribute__((always_inline)) {
+        if constexpr (STAMP) {
+            unsigned long long now;
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(now)::"memory");
+            __builtin_amdgcn_sched_barrier(0);
+            if (seg >= 0) st_sum[seg] += now - st_last;
+            st_last = now;
+        }
+    };
     const int lb = xcd_remap(blockIdx.x, nblocks);
     const int bh = lb / qblocks;
     const int qblk = causal ? qblocks - 1 - lb % qblocks : lb % qblocks;
@@ -567,6 +578,7 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v10(
                 for (int r = 0; r < 16; ++r)
                     s[tt][r] = __builtin_amdgcn_exp2f(PRE != 0 ? s[tt][r] : fmaf(s[tt][r], c, -m_run));
         };
+        stamp(0);
         qk();
         float mx = fmaxf(s[0][0], s[1][0]), my = fmaxf(s[0][1], s[1][1]);
 #pragma unroll
@@ -575,6 +587,8 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v10(
             my = fmaxf(fmaxf(my, s[0][r + 1]), s[1][r + 1]);
         }
         mx = v7_xor32_max(fmaxf(mx, my));
+        if constexpr (STAMP) asm volatile("" ::"v"(mx));
+        stamp(1);
         if constexpr (FIRST) {
             if constexpr (PRE != 0) {
                 const float delta = mx == -INFINITY ? 0.f : mx;
@@ -592,6 +606,7 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v10(
         } else {
             expo();
             asm volatile("" : "+v"(s[0]), "+v"(s[1]));
+            stamp(2);
             const bool up = PRE != 0 ? mx > V7_THR : mx * c > m_run + V7_THR;
             if (__ballot(up)) {
                 float alpha;
@@ -625,6 +640,8 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v10(
                                    (int)pack2<T>(s[tt][r0 + 4], s[tt][r0 + 5]),
                                    (int)pack2<T>(s[tt][r0 + 6], s[tt][r0 + 7])};
             }
+        if constexpr (STAMP) asm volatile("" ::"v"(pb[0][0]), "v"(pb[0][1]), "v"(pb[1][0]), "v"(pb[1][1]));
+        stamp(3);
     };
     auto Y = [&](int buf) __attribute__((always_inline)) {
         const char* vb = smem + buf * BUFB;
@@ -645,12 +662,15 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v10(
                     oacc[dblk] = mfma32x32x16<T>(i32x4{lo.x, lo.y, hi.x, hi.y}, pb[tt][s2], oacc[dblk]);
                 }
         }
+        stamp(4);
     };
     // counted wait: tile t+1's pieces landed while t+2's (4 per wave) fly
     auto wait_next = [&](bool two_in_flight) __attribute__((always_inline)) {
         if (two_in_flight) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        stamp(5);
         __syncthreads();
+        stamp(6);
     };
 
     if (nt > 0) {
@@ -660,6 +680,7 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v10(
         wait_next(nt > 1);
         int cur = 0;
         auto tile = [&](int t, auto first_tag) __attribute__((always_inline)) {
+            stamp(-1);
             const int n2 = cur == 0 ? 2 : cur - 1;  // (cur + 2) % 3
             if (t + 2 < nt) dma_tile(t + 2, n2);
             X(t, cur, first_tag);
@@ -671,6 +692,16 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v10(
         for (int t = 1; t < nt; ++t) tile(t, std::false_type{});
     }
 
+#ifdef PLI_FLASH_STAMPS
+    if constexpr (STAMP) {
+        if (lane == 0) {
+#pragma unroll
+            for (int i = 0; i < 7; ++i) atomicAdd(&g_v7_stamps[i], st_sum[i]);
+            atomicAdd(&g_v7_stamps[8], (unsigned long long)nt);
+            atomicAdd(&g_v7_stamps[9], 1ull);
+        }
+    }
+#endif
     const float l = v7_xor32_sum(lsum[0]);
     const float inv = l > 0.f ? 1.f / l : 0.f;
     const int qr = q0 + l32;
@@ -779,6 +810,14 @@ extern "C" int pli_diag_flash_stamps(const void* q, const void* k, const void* v
     switch (sub) {
         case 0: PLI_DIAG(1); break;
         case 1: PLI_DIAG(0); break;
+        case 4:
+            hipLaunchKernelGGL((attn_fwd_v10<bf16_t, 1, true>), dim3(nb), dim3(512), 0, 0, qq, kk, vv, oo, H, 1, N, N,
+                               st, c, 0, qblocks, nb);
+            break;
+        case 5:
+            hipLaunchKernelGGL((attn_fwd_v10<bf16_t, 0, true>), dim3(nb), dim3(512), 0, 0, qq, kk, vv, oo, H, 1, N, N,
+                               st, c, 0, qblocks, nb);
+            break;
         default: return PLI_EINVAL;
     }
 #undef PLI_DIAG

@@ -7,11 +7,12 @@ resolve to the MI355X implementation.  Test classes / methods are collected
 here and run one pytest case each; the reference's ``skipif`` markers are
 honoured (its CUDA-gated classes run on a ROCm box, skip elsewhere).
 
-Only chapters whose test modules import nothing outside the hot-path scope
-are run (ch03, ch06); ch01/ch05/ch09's test modules import out-of-scope
-symbols (FFN/GQA/transformer, shared_memory, MoE) at module level -- their
-in-scope assertions are restated in test_host_cpu.py / test_gpu_parity.py.
-Skipped entirely when /root/reference is absent (e.g. on the GPU box).
+Chapters run: ch01, ch02, ch03, ch05, ch06 -- every module their test files
+import exists in this build.  Not run: ch09 (its test module imports
+``moe_inference``, expert offloading, out of scope), ch04 / ch07 / ch08 / ch10
+(pedagogy / control plane, out of scope).  Skipped entirely when
+/root/reference is absent (e.g. on the GPU box, where tests/test_gpu_*.py
+restate the CUDA-gated assertions with committed fixtures).
 """
 from __future__ import annotations
 
@@ -22,7 +23,7 @@ import os
 import pytest
 
 REF = os.environ.get("PLI_REFERENCE", "/root/reference")
-CHAPTERS = ("ch03", "ch06")
+CHAPTERS = ("ch01", "ch02", "ch03", "ch05", "ch06")
 
 
 def _load(chapter: str):

@@ -16,7 +16,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libpli_diag.so"))
 lib.pli_diag_flash_stamps.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int] * 4 + [ctypes.POINTER(ctypes.c_ulonglong)]
-SEGS = ["loads_issue", "qk_mfma+max", "exp", "rescale_chk+pack", "pv_issue", "lds_store", "barrier"]
+SEGS = ["loads/dma_issue", "qk_mfma+max", "exp", "rescale_chk+pack", "pv_issue", "lds_store", "barrier"]
 
 B, H, N, D = 8, 32, 4096, 128
 g = torch.Generator(device="cuda").manual_seed(0)
