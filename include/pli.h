@@ -149,6 +149,15 @@ int pli_scale_copy(const float* in, float* out, int64_t n_out, int stride,
 int pli_mfma_probe(float* out, int blocks, int iters, int shape, void* stream);
 
 /*
+ * ch05/tiled_matmul.cu:9-20 naive_matmul (the contrast kernel of the ch05
+ * demo): C[m][n] = sum_k A[m][k] B[k][n], fp32 row-major, one thread per
+ * output element straight from global memory.  Not a production path --
+ * pli_gemm with PLI_F32 runs the MFMA tile kernel.
+ */
+int pli_gemm_naive(const float* a, const float* b, float* c, int m, int n, int k, int64_t lda,
+                   int64_t ldb, int64_t ldc, void* stream);
+
+/*
  * Read-only HBM calibration (ch03/roofline.py measure_hbm_read_bandwidth):
  * `blocks` x 256 threads stream `bytes` (16-byte aligned, multiple of 16)
  * with 16-byte non-temporal loads; one XOR word per thread goes to

@@ -10,7 +10,7 @@ from .memory_coalescing import (
 )
 from .shared_memory import demonstrate_bank_conflicts, tiled_reduce
 from .tensor_cores import benchmark_tensor_cores, tensor_core_info
-from .tiled_matmul import benchmark_tiled_matmul, tiled_matmul
+from .tiled_matmul import benchmark_matmul_demo, benchmark_tiled_matmul, naive_matmul, tiled_matmul
 from .triton_matmul import benchmark_triton_matmul, triton_matmul
 
 __all__ = [
@@ -21,6 +21,8 @@ __all__ = [
     "tiled_reduce",
     "demonstrate_bank_conflicts",
     "tiled_matmul",
+    "naive_matmul",
+    "benchmark_matmul_demo",
     "triton_matmul",
     "benchmark_triton_matmul",
     "benchmark_tiled_matmul",

@@ -8,7 +8,14 @@ signature, one C ABI entry point, two kernels behind it --
 * bf16/fp16: 128x128x64 LDS-staged tile on ``v_mfma_f32_32x32x16`` (fp32
   accumulate, output in the input dtype; the Triton kernel stored fp16,
   ``:61``);
-* fp32 (and ragged shapes): 64x64 LDS-tiled VALU kernel, fp32 accumulate.
+* fp32: 128x128x32 LDS-staged tile on ``v_mfma_f32_32x32x2_f32`` (exact
+  fp32 fma chain); unaligned / K % 4 != 0 shapes take a 64x64 LDS-tiled VALU
+  kernel.
+
+``naive_matmul`` is the demo's contrast kernel (``:9-20``, one thread per
+output, ``pli_gemm_naive``) and ``benchmark_matmul_demo`` re-runs the demo's
+``main`` (``:96-136``: 2048^3 fp32, uniform [0, 0.99] inputs, naive vs
+tiled, ms and TFLOP/s).
 
 ``block_m/block_n/block_k`` are accepted for signature compatibility; the
 HIP tile is fixed by the MFMA / LDS mapping.
@@ -34,8 +41,41 @@ def tiled_matmul(a: torch.Tensor, b: torch.Tensor, block_m: int = 64, block_n: i
     return pli_hip.gemm(a, b, trans_b=False)
 
 
-# the reference's public name for the same operation (ch05/triton_matmul.py:67)
-triton_matmul = tiled_matmul
+def naive_matmul(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """fp32 C = A @ B, one thread per output element (ch05/tiled_matmul.cu:9-20)."""
+    assert a.shape[1] == b.shape[0], f"Dimension mismatch: {a.shape[1]} vs {b.shape[0]}"
+    if not a.is_cuda:
+        return torch.matmul(a, b)
+    return pli_hip.gemm_naive(a, b)
+
+
+def benchmark_matmul_demo(size: int = 2048, warmup: int = 3, iterations: int = 10,
+                          device: str = "cuda") -> dict | None:
+    """The ch05/tiled_matmul.cu ``main`` (:96-136): naive vs tiled fp32 GEMM
+    at ``size``^3, inputs ``(rand() % 100) / 100`` (here a seeded torch
+    draw of the same 100 levels); returns {name: {"ms", "tflops"}} plus the
+    max |tiled - naive| difference."""
+    if not torch.cuda.is_available():
+        return None
+    g = torch.Generator(device="cpu").manual_seed(0)
+    a = (torch.randint(0, 100, (size, size), generator=g).float() / 100).to(device)
+    b = (torch.randint(0, 100, (size, size), generator=g).float() / 100).to(device)
+    flops = 2.0 * size ** 3
+    res = {}
+    outs = {}
+    for name, fn in (("naive", naive_matmul), ("tiled", tiled_matmul)):
+        for _ in range(warmup):
+            outs[name] = fn(a, b)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iterations):
+            fn(a, b)
+        e.record()
+        e.synchronize()
+        ms = s.elapsed_time(e) / iterations
+        res[name] = {"ms": ms, "tflops": flops / ms / 1e9}
+    res["max_abs_diff"] = float((outs["tiled"] - outs["naive"]).abs().max())
+    return res
 
 
 @dataclass
@@ -75,6 +115,9 @@ def benchmark_tiled_matmul(m: int = 1024, n: int = 1024, k: int = 1024, warmup: 
 
 if __name__ == "__main__":
     if torch.cuda.is_available():
+        d = benchmark_matmul_demo()
+        for name in ("naive", "tiled"):
+            print(f"{name}: {d[name]['ms']:.3f} ms, {d[name]['tflops']:.2f} TFLOPS (2048^3 fp32)")
         for size in [512, 1024, 2048, 4096]:
             r = benchmark_tiled_matmul(size, size, size)
             print(f"{size}^3 bf16: HIP {r.hip_us:.1f} us ({2 * size**3 / r.hip_us / 1e6:.1f} TFLOP/s), "

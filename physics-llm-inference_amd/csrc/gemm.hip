@@ -23,6 +23,7 @@
 // kernel, 4x4 outputs per thread, fp32 accumulate.
 #include <type_traits>
 
+#include "gemm_f32.h"
 #include "pli_common.h"
 
 namespace pli {
@@ -2237,6 +2238,10 @@ static int gemm_dispatch(const void* a, const void* b, void* c, const void* bias
             return launch_mfma<bf16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, s);
         return launch_mfma<f16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, s);
     }
+    // fp32 (the ch01 MHA / ch05 demo dtype): v_mfma_f32_32x32x2_f32 tiles
+    // (gemm_f32.hip); the VALU kernel below keeps unaligned / K % 4 != 0 shapes
+    if (dtype == PLI_F32 && gemm_f32_mfma_ok(a, b, c, k, n, lda, ldb, trans_b))
+        return launch_gemm_f32_mfma(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, s);
     switch (dtype) {
         case PLI_F32: return launch_generic<float>(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, s);
         case PLI_F16: return launch_generic<f16_t>(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, s);

@@ -60,6 +60,7 @@ _SIGS = {
                                  _c_i64, _c_i64, _c_i64, _c_int, _vp, _c_int],
     "pli_moe_combine": [_vp, _c_i64, _vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_int, _c_int, _vp],
     "pli_scale_copy": [_vp, _vp, _c_i64, _c_int, _vp],
+    "pli_gemm_naive": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_i64, _c_i64, _c_i64, _vp],
     "pli_mfma_probe": [_vp, _c_int, _c_int, _c_int, _vp],
     "pli_hbm_read_probe": [_vp, _c_i64, _vp, _c_int, _vp],
     "pli_softmax_rows": [_vp, _vp, _c_i64, _c_int, _c_int, _vp],
@@ -661,6 +662,29 @@ def gemm(a: torch.Tensor, b: torch.Tensor, trans_b: bool = False,
         else:
             rc = lib().pli_gemm_variant(*head, _stream(dev), int(variant))
     _check(rc, "pli_gemm")
+    return out
+
+
+def gemm_naive(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """C = A B for fp32 [M,K] x [K,N] with the ch05 naive kernel
+    (pli_gemm_naive, one thread per output) -- the demo's contrast, not a
+    production path."""
+    dev = _require_gpu(a, b)
+    if a.dtype != torch.float32 or b.dtype != torch.float32 or a.dim() != 2 or b.dim() != 2:
+        raise PliError("gemm_naive expects 2-D fp32 operands")
+    if a.shape[1] != b.shape[0]:
+        raise PliError(f"gemm_naive inner dims differ: {tuple(a.shape)} vs {tuple(b.shape)}")
+    a, b = a.contiguous(), b.contiguous()
+    m, k = a.shape
+    n = b.shape[1]
+    if out is None:
+        out = torch.empty((m, n), dtype=torch.float32, device=dev)
+    else:
+        _check_out(out, a, (m, n), "gemm_naive")
+    with _on_device(dev):
+        rc = lib().pli_gemm_naive(_ptr(a), _ptr(b), _ptr(out), m, n, k, max(k, 1), max(n, 1),
+                                  max(out.stride(0), n), _stream(dev))
+    _check(rc, "pli_gemm_naive")
     return out
 
 

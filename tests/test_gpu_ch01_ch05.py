@@ -110,3 +110,53 @@ def test_ch05_benchmarks_run_on_gpu():
     a = torch.randn(128, 256, device=DEV, dtype=torch.float16)
     b = torch.randn(256, 64, device=DEV, dtype=torch.float16)
     torch.testing.assert_close(triton_matmul(a, b), torch.matmul(a, b), rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("m,n,k,trans_b,bias", [(128, 128, 32, False, False), (200, 136, 68, False, True),
+                                                (1, 300, 1024, True, True), (257, 129, 4, True, False),
+                                                (512, 384, 1000, True, True), (96, 4, 12, False, False)])
+def test_fp32_gemm_mfma_vs_f64(m, n, k, trans_b, bias):
+    """pli_gemm at fp32 (v_mfma_f32_32x32x2_f32 tile, ragged M/N edges, both
+    layouts, bias) against the f64 product of the same fp32 inputs."""
+    import pli_hip
+    a = seeded_normal((m, k), 81)
+    b = seeded_normal((n, k) if trans_b else (k, n), 82)
+    bi = seeded_normal((n,), 83) if bias else None
+    ref = a.astype(np.float64) @ (b.T if trans_b else b).astype(np.float64)
+    if bias:
+        ref = ref + bi
+    out = pli_hip.gemm(torch.from_numpy(a).to(DEV), torch.from_numpy(b).to(DEV), trans_b=trans_b,
+                       bias=None if bi is None else torch.from_numpy(bi).to(DEV)).cpu().numpy()
+    # fp32 accumulation of k products of N(0,1): error ~ k * 2^-24 * sqrt(k)
+    assert np.abs(out - ref).max() <= 4e-6 * k + 1e-5
+
+
+def test_fp32_gemm_unaligned_takes_valu_path():
+    """K % 4 != 0 / odd leading dimension: the VALU fallback, same contract."""
+    import pli_hip
+    a = seeded_normal((70, 33), 84)
+    b = seeded_normal((33, 45), 85)
+    out = pli_hip.gemm(torch.from_numpy(a).to(DEV), torch.from_numpy(b).to(DEV)).cpu().numpy()
+    np.testing.assert_allclose(out, a.astype(np.float64) @ b, rtol=0, atol=1e-4)
+
+
+def test_naive_matmul_and_demo_2048():
+    """ch05/tiled_matmul.cu main at its own size (2048^3 fp32): the naive
+    contrast kernel and the MFMA tile kernel agree, both match f64 on sampled
+    rows, and the tile kernel is many times faster."""
+    from ch05 import benchmark_matmul_demo, naive_matmul, tiled_matmul
+    a = torch.from_numpy(seeded_normal((100, 36), 86)).to(DEV)
+    b = torch.from_numpy(seeded_normal((36, 70), 87)).to(DEV)
+    ref = a.double().cpu() @ b.double().cpu()
+    torch.testing.assert_close(naive_matmul(a, b).cpu().double(), ref, rtol=0, atol=1e-4)
+    d = benchmark_matmul_demo(2048, warmup=2, iterations=5)
+    # inputs in [0, 0.99]: sums ~500, fp32 ulp there 2^-15; different orders
+    assert d["max_abs_diff"] < 0.05, d
+    assert d["tiled"]["ms"] * 4 < d["naive"]["ms"], d
+    g = torch.Generator(device="cpu").manual_seed(0)
+    a2 = torch.randint(0, 100, (2048, 2048), generator=g).float() / 100
+    b2 = torch.randint(0, 100, (2048, 2048), generator=g).float() / 100
+    c = tiled_matmul(a2.to(DEV), b2.to(DEV)).cpu()
+    rows = torch.tensor([0, 1, 777, 2047])
+    ref2 = a2[rows].double() @ b2.double()
+    assert (c[rows].double() - ref2).abs().max().item() < 0.02
