@@ -1,9 +1,10 @@
 #!/bin/bash
 # Diagnostic library (never the product): flash_v7.hip with PLI_FLASH_STAMPS ->
-# tools/libpli_diag.so exporting pli_diag_flash_stamps (tools/flash_stamps.py).
+# tools/libpli_diag.so exporting pli_diag_flash_stamps (tools/flash_stamps.py) and
+# pli_diag_gemv (tools/diag/gemv_diag.hip, tools/gemv_stamps.py).
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 C=$R/physics-llm-inference_amd/csrc
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -fno-honor-nans -DPLI_FLASH_STAMPS \
-    -I$R/include -I$C -shared $C/flash_v7.hip $C/capi.cpp -o $R/tools/libpli_diag.so
+    -I$R/include -I$C -shared $C/flash_v7.hip $R/tools/diag/gemv_diag.hip $C/capi.cpp -o $R/tools/libpli_diag.so
 echo "built $R/tools/libpli_diag.so"
