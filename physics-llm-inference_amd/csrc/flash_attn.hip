@@ -508,7 +508,9 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
 // The round-1 experiments (XOR-swizzled v1, staggered v3, pipelined v4/v5,
 // 16x16x32 v6, ping-pong, segmented, one-wave-per-SIMD w4/w4p) and the
 // round-2 ones that lost (in-wave pipelined v8, one-wave-per-SIMD v9, a
-// two-barrier stagger with s_setprio, a half-tile lag on a 4-deep ring) are
+// two-barrier stagger with s_setprio, a half-tile lag on a 4-deep ring, the
+// 4-wave one-wave-per-SIMD software-pipelined v11: 719-760 TF, static
+// s_setprio 1 on waves 4-7: 1088 vs 1088 TF) are
 // not in the library; their measurements are in DESIGN.md 3.1.
 constexpr int kDefaultVariant = 55;
 
