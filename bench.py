@@ -98,7 +98,7 @@ def calibrate() -> dict:
             "hbm_copy_GB/s": measure_hbm_bandwidth(),
             "mfma_32x32x16_TFLOP/s": measure_mfma_peak("32x32x16"),
             "mfma_16x16x32_TFLOP/s": measure_mfma_peak("16x16x32"),
-            "how": "hbm: pli_hbm_read_probe over 2 x 1 GiB (read-only, best of 10); hbm_copy: "
+            "how": "hbm: pli_hbm_read_probe over 2 x 1 GiB (read-only, best of 10 per layout: grid-stride, contiguous slice per workgroup at 2/4/8 per CU); hbm_copy: "
                    "pli_scale_copy 2x1 GiB read+write; mfma: pli_mfma_probe 1024 WGs x 4 waves, "
                    "4 independent MFMAs per wave from registers, pseudo-random bf16, best of 5"}
 

@@ -161,9 +161,11 @@ int pli_gemm_naive(const float* a, const float* b, float* c, int m, int n, int k
  * Read-only HBM calibration (ch03/roofline.py measure_hbm_read_bandwidth):
  * `blocks` x 256 threads stream `bytes` (16-byte aligned, multiple of 16)
  * with 16-byte non-temporal loads; one XOR word per thread goes to
- * out[blocks * 256].
+ * out[blocks * 256].  mode 0: grid-stride (4 loads per lane in flight);
+ * mode 1: one contiguous slice per block, 8 loads per lane in flight.
  */
-int pli_hbm_read_probe(const void* buf, int64_t bytes, uint32_t* out, int blocks, void* stream);
+int pli_hbm_read_probe(const void* buf, int64_t bytes, uint32_t* out, int blocks, int mode,
+                       void* stream);
 
 /*
  * Row softmax with the single-pass online (max, sum) recurrence of

@@ -108,27 +108,29 @@ def measure_hbm_bandwidth(nbytes: int = 1 << 30, iters: int = 20, device: str = 
 
 def measure_hbm_read_bandwidth(nbytes: int = 1 << 30, iters: int = 10, device: str = "cuda") -> float:
     """Achievable HBM READ GB/s: ``pli_hbm_read_probe`` (16-byte non-temporal
-    loads, four in flight per lane) over two alternating ``nbytes`` buffers
-    (2 GiB >> the 256 MiB Infinity Cache), 8 workgroups of 256 threads per CU,
-    best of ``iters`` event-timed launches -- the ceiling of the
-    read-dominated GEMV and decode-attention kernels."""
+    loads) over two alternating ``nbytes`` buffers (2 GiB >> the 256 MiB
+    Infinity Cache), best of ``iters`` event-timed launches of each probe
+    layout (grid-stride at 8 workgroups per CU; one contiguous slice per
+    workgroup at 2, 4 and 8 per CU) -- the ceiling of the read-dominated GEMV
+    and decode-attention kernels."""
     import torch
 
     import pli_hip
 
     bufs = [torch.empty(nbytes // 4, device=device, dtype=torch.int32).fill_(i + 1) for i in range(2)]
-    blocks = MI355X_CUS * 8
-    out = torch.empty(blocks * 256, device=device, dtype=torch.int32)
-    for b in bufs:
-        pli_hip.hbm_read_probe(b, out, blocks)
     best = float("inf")
-    for i in range(iters):
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        pli_hip.hbm_read_probe(bufs[i & 1], out, blocks)
-        e.record()
-        e.synchronize()
-        best = min(best, s.elapsed_time(e) / 1e3)
+    for mode, per_cu in ((0, 8), (1, 2), (1, 4), (1, 8)):
+        blocks = MI355X_CUS * per_cu
+        out = torch.empty(blocks * 256, device=device, dtype=torch.int32)
+        for b in bufs:
+            pli_hip.hbm_read_probe(b, out, blocks, mode)
+        for i in range(iters):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            pli_hip.hbm_read_probe(bufs[i & 1], out, blocks, mode)
+            e.record()
+            e.synchronize()
+            best = min(best, s.elapsed_time(e) / 1e3)
     return nbytes / best / 1e9
 
 

@@ -81,17 +81,48 @@ __global__ __launch_bounds__(256) void hbm_read_probe(const i32x4* __restrict__ 
     out[(int64_t)blockIdx.x * 256 + threadIdx.x] = acc;
 }
 
+// mode 1: block b streams its own contiguous slice of the buffer; each wave
+// reads 8 KiB per step (8 x 16-B non-temporal loads per lane in flight,
+// consecutive lanes on consecutive 16 B), so every DRAM page is opened by one
+// wave at a time.
+__global__ __launch_bounds__(256) void hbm_read_probe_chunked(const i32x4* __restrict__ src, int64_t n16,
+                                                              uint32_t* __restrict__ out) {
+    const int64_t per_block = (n16 + gridDim.x - 1) / gridDim.x;
+    const int64_t lo = (int64_t)blockIdx.x * per_block, hi = min(n16, lo + per_block);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint32_t acc = 0;
+    int64_t i = lo + wave * 512 + lane;
+    for (; i + 7 * 64 < hi; i += 4 * 512) {
+        i32x4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(src + i + 64 * u);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc ^= (uint32_t)(v[u].x ^ v[u].y ^ v[u].z ^ v[u].w);
+    }
+    for (; i < hi; i += 64) {
+        const i32x4 a = __builtin_nontemporal_load(src + i);
+        acc ^= (uint32_t)(a.x ^ a.y ^ a.z ^ a.w);
+    }
+    out[(int64_t)blockIdx.x * 256 + threadIdx.x] = acc;
+}
+
 }  // namespace
 }  // namespace pli
 
-extern "C" int pli_hbm_read_probe(const void* buf, int64_t bytes, uint32_t* out, int blocks, void* stream) {
+extern "C" int pli_hbm_read_probe(const void* buf, int64_t bytes, uint32_t* out, int blocks, int mode,
+                                  void* stream) {
     using namespace pli;
     clear_error();
     PLI_REQUIRE(buf != nullptr && out != nullptr, "pli_hbm_read_probe: null pointer");
     PLI_REQUIRE(aligned16(buf) && bytes > 0 && bytes % 16 == 0 && blocks > 0,
                 "pli_hbm_read_probe: need a 16-byte aligned buffer of 16k bytes and blocks > 0");
-    hipLaunchKernelGGL(hbm_read_probe, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
-                       (const i32x4*)buf, bytes / 16, out);
+    PLI_REQUIRE(mode == 0 || mode == 1, "pli_hbm_read_probe: mode %d", mode);
+    if (mode == 0)
+        hipLaunchKernelGGL(hbm_read_probe, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const i32x4*)buf,
+                           bytes / 16, out);
+    else
+        hipLaunchKernelGGL(hbm_read_probe_chunked, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                           (const i32x4*)buf, bytes / 16, out);
     return launch_status("hbm_read_probe");
 }
 

@@ -62,7 +62,7 @@ _SIGS = {
     "pli_scale_copy": [_vp, _vp, _c_i64, _c_int, _vp],
     "pli_gemm_naive": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_i64, _c_i64, _c_i64, _vp],
     "pli_mfma_probe": [_vp, _c_int, _c_int, _c_int, _vp],
-    "pli_hbm_read_probe": [_vp, _c_i64, _vp, _c_int, _vp],
+    "pli_hbm_read_probe": [_vp, _c_i64, _vp, _c_int, _c_int, _vp],
     "pli_softmax_rows": [_vp, _vp, _c_i64, _c_int, _c_int, _vp],
     "pli_online_softmax_with_output": [_vp, _vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_int, _vp],
     "pli_attn_decode_workspace_size": [_c_int] * 6,
@@ -717,15 +717,16 @@ def mfma_probe(out: torch.Tensor, blocks: int, iters: int, shape: int = 0) -> to
     return out
 
 
-def hbm_read_probe(buf: torch.Tensor, out: torch.Tensor, blocks: int) -> torch.Tensor:
+def hbm_read_probe(buf: torch.Tensor, out: torch.Tensor, blocks: int, mode: int = 0) -> torch.Tensor:
     """Stream ``buf`` (contiguous, 16-byte multiple) with non-temporal 16-byte
-    loads, ``blocks`` x 256 threads (pli_hbm_read_probe); out: int32 >= blocks*256."""
+    loads, ``blocks`` x 256 threads (pli_hbm_read_probe; mode 0 grid-stride,
+    1 one contiguous slice per block); out: int32 >= blocks*256."""
     dev = _require_gpu(buf)
     nbytes = buf.numel() * buf.element_size()
     if not buf.is_contiguous() or nbytes % 16 or out.numel() < blocks * 256 or out.element_size() != 4:
         raise PliError("hbm_read_probe: contiguous buffer of 16k bytes, 4-byte out >= blocks*256")
     with _on_device(dev):
-        rc = lib().pli_hbm_read_probe(_ptr(buf), nbytes, _ptr(out), int(blocks), _stream(dev))
+        rc = lib().pli_hbm_read_probe(_ptr(buf), nbytes, _ptr(out), int(blocks), int(mode), _stream(dev))
     _check(rc, "pli_hbm_read_probe")
     return out
 

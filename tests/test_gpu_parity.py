@@ -508,12 +508,13 @@ def test_calibration_probes():
     import pli_hip
     g = torch.Generator(device=DEV).manual_seed(3)
     buf = torch.randint(-2 ** 31, 2 ** 31 - 1, ((1 << 20) + 4 * 37,), device=DEV, dtype=torch.int32, generator=g)
-    for blocks in (1, 8, 300):
-        out = torch.zeros(blocks * 256, device=DEV, dtype=torch.int32)
-        pli_hip.hbm_read_probe(buf, out, blocks)
-        want = np.bitwise_xor.reduce(buf.cpu().numpy().view(np.uint32))
-        got = np.bitwise_xor.reduce(out.cpu().numpy().view(np.uint32))
-        assert got == want, blocks
+    want = np.bitwise_xor.reduce(buf.cpu().numpy().view(np.uint32))
+    for mode in (0, 1):
+        for blocks in (1, 8, 300, 1023):
+            out = torch.zeros(blocks * 256, device=DEV, dtype=torch.int32)
+            pli_hip.hbm_read_probe(buf, out, blocks, mode)
+            got = np.bitwise_xor.reduce(out.cpu().numpy().view(np.uint32))
+            assert got == want, (mode, blocks)
     for shape in (0, 1):
         o = torch.zeros(16 * 256, device=DEV, dtype=torch.float32)
         pli_hip.mfma_probe(o, 16, 64, shape)

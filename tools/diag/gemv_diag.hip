@@ -125,11 +125,69 @@ __global__ __launch_bounds__(WPB * 64) void gemv_persist(const char* __restrict_
     }
 }
 
+// contiguous: wave gw handles rows gw*R .. gw*R + R - 1 (R = ceil(M / waves)),
+// the next row's loads issued before the current row is reduced
+template <bool STAMP, int WPB>
+__global__ __launch_bounds__(WPB * 64) void gemv_contig(const char* __restrict__ w, const char* __restrict__ x,
+                                                        bf16_t* __restrict__ y, int M, int64_t ldw,
+                                                        uint64_t* __restrict__ st) {
+    uint64_t t0 = 0, t1 = 0;
+    if constexpr (STAMP) t0 = rt_now();
+    const int lane = threadIdx.x & 63, gw = blockIdx.x * WPB + (threadIdx.x >> 6);
+    const int nw = gridDim.x * WPB;
+    const int R = (M + nw - 1) / nw;
+    const int r0 = gw * R, r1 = min(M, r0 + R);
+    i32x4 xv[8], wa[8], wb[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) xv[u] = *reinterpret_cast<const i32x4*>(x + (int64_t)(lane + 64 * u) * 16);
+    auto ld = [&](i32x4* dst, int r) __attribute__((always_inline)) {
+        const char* wr = w + (int64_t)min(r, M - 1) * ldw;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            dst[u] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(wr + (int64_t)(lane + 64 * u) * 16));
+    };
+    auto fin = [&](const i32x4* src, int r) __attribute__((always_inline)) {
+        float acc = 0.f;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) dot8(src[u], xv[u], acc);
+        acc = wave_sum(acc);
+        if (lane == 0 && r < M) y[r] = elem<bf16_t>::from_f32(acc);
+    };
+    int row = r0;
+    if (row < r1) ld(wa, row);
+    bool first = true;
+    while (row < r1) {
+        if (row + 1 < r1) ld(wb, row + 1);
+        if constexpr (STAMP) {
+            if (first) {
+                asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                t1 = rt_now();
+                first = false;
+            }
+        }
+        fin(wa, row);
+        if (++row >= r1) break;
+        if (row + 1 < r1) ld(wa, row + 1);
+        fin(wb, row);
+        ++row;
+    }
+    if constexpr (STAMP) {
+        const uint64_t t2 = rt_now();
+        if (lane == 0) {
+            st[4 * gw + 0] = t0;
+            st[4 * gw + 1] = t1;
+            st[4 * gw + 2] = t2;
+            st[4 * gw + 3] = (uint64_t)xcc_id();
+        }
+    }
+}
+
 }  // namespace
 }  // namespace pli
 
 // kind 0: row-per-wave (product shape), 1: persistent 4-wave blocks, 2:
-// persistent 8-wave blocks, 3: persistent 2-wave blocks.  stamps: null or
+// persistent 8-wave blocks, 3: persistent 2-wave blocks, 4 / 5: contiguous
+// row ranges per wave, 4- / 2-wave blocks.  stamps: null or
 // 4 x u64 per wave (row-per-wave: M waves; persistent: grid * WPB waves).
 // K must be 4096 (512 chunks), operands 16-byte aligned.
 extern "C" int pli_diag_gemv(int kind, const void* w, const void* x, void* y, int m, int k, int64_t ldw,
@@ -158,6 +216,14 @@ extern "C" int pli_diag_gemv(int kind, const void* w, const void* x, void* y, in
         case 3:
             if (st) hipLaunchKernelGGL((gemv_persist<true, 2>), dim3(grid), dim3(128), 0, s, wc, xc, yb, m, ldb, stamps);
             else hipLaunchKernelGGL((gemv_persist<false, 2>), dim3(grid), dim3(128), 0, s, wc, xc, yb, m, ldb, stamps);
+            break;
+        case 4:
+            if (st) hipLaunchKernelGGL((gemv_contig<true, 4>), dim3(grid), dim3(256), 0, s, wc, xc, yb, m, ldb, stamps);
+            else hipLaunchKernelGGL((gemv_contig<false, 4>), dim3(grid), dim3(256), 0, s, wc, xc, yb, m, ldb, stamps);
+            break;
+        case 5:
+            if (st) hipLaunchKernelGGL((gemv_contig<true, 2>), dim3(grid), dim3(128), 0, s, wc, xc, yb, m, ldb, stamps);
+            else hipLaunchKernelGGL((gemv_contig<false, 2>), dim3(grid), dim3(128), 0, s, wc, xc, yb, m, ldb, stamps);
             break;
         default: return PLI_EINVAL;
     }

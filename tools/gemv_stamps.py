@@ -30,7 +30,7 @@ ws = [torch.randn(M, K, device="cuda", dtype=torch.bfloat16) for _ in range(COPI
 x = torch.randn(K, device="cuda", dtype=torch.bfloat16)
 y = torch.empty(M, device="cuda", dtype=torch.bfloat16)
 st = torch.cuda.current_stream()
-WPB = {0: 2, 1: 4, 2: 8, 3: 2}
+WPB = {0: 2, 1: 4, 2: 8, 3: 2, 4: 4, 5: 2}
 
 
 def launch(kind, grid, w, stamps=None):
@@ -62,7 +62,11 @@ def graph_us(fn):
 
 
 configs = [(0, 0)] + [(1, g) for g in (256, 512, 1024)] + [(2, g) for g in (128, 256, 512)] + \
-          [(3, g) for g in (512, 1024, 2048)]
+          [(3, g) for g in (512, 1024, 2048)] + [(4, g) for g in (128, 256, 512, 1024)] + \
+          [(5, g) for g in (256, 512, 1024, 2048)]
+if os.environ.get("GEMV_KINDS"):
+    ks = {int(k) for k in os.environ["GEMV_KINDS"].split(",")}
+    configs = [c for c in configs if c[0] in ks]
 ref = pli_hip.gemv(ws[0], x)
 out = {"product_pli_gemv_us": graph_us(lambda w: pli_hip.gemv(w, x, out=y))}
 for kind, grid in configs:
