@@ -414,9 +414,17 @@ def tune_gemm_shapes():
             fns[f"nn_v{v}"] = (lambda v=v: pli_hip.gemm(a, bn, out=c, variant=v))
         fns["nt_torch"] = lambda: torch.mm(a, bt.t())
         fns["nn_torch"] = lambda: torch.mm(a, bn)
+        # every variant against torch's product (relative to |ref| + 1)
+        errs = {}
+        for lay, bb, tb in (("nt", bt, True), ("nn", bn, False)):
+            ref = torch.mm(a, bb.t() if tb else bb).float()
+            for v in vs:
+                o = pli_hip.gemm(a, bb, trans_b=tb, variant=v).float()
+                errs[f"{lay}_v{v}"] = round(((o - ref).abs() / (ref.abs() + 1)).max().item(), 4)
         t = interleave(fns, 5, int(os.environ.get("PLI_TUNE_ROUNDS", "3")))
         row = {kname: round(2 * m * n * k / med / 1e9, 1) for kname, (med, mn) in t.items()}
-        print(json.dumps({"kernel": "gemm_shapes", "m": m, "n": n, "k": k, "TFLOP/s": row}), flush=True)
+        print(json.dumps({"kernel": "gemm_shapes", "m": m, "n": n, "k": k, "TFLOP/s": row, "max_rel_err": errs}),
+              flush=True)
 
 
 def tune_midm():
