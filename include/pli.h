@@ -300,6 +300,58 @@ int pli_attn_decode_dev(const void* q, const void* k, const void* v, void* o,
                         int n_kv_add, void* workspace, size_t workspace_bytes,
                         int dtype, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Tuning section: the same operations with an explicit kernel choice, for
+ * A/B runs (tools/tune.py) and the per-variant parity tests.  Not part of
+ * the drop-in surface above -- a caller that binds the reference's
+ * interface never needs them.  variant / mode < 0 (or 0 where noted) is the
+ * default route; every listed value is parity-tested at the bench sizes
+ * (tests/test_gpu_fullsize.py) and on the small edge cases
+ * (tests/test_gpu_parity.py, test_gpu_decode.py, test_gpu_moe.py,
+ * test_gpu_swiglu.py).
+ *
+ * pli_flash_attn_fwd_variant: 21 attn_fwd_v2 (round-1 kernel), 50 / 51
+ *   attn_fwd_v7 prescaled / exact, 54 / 55 attn_fwd_v10 prescaled / exact
+ *   (55 = default).  Prescaled variants round Q * scale * log2(e) to the
+ *   16-bit input type (2^-9 relative score error in bf16).
+ * pli_gemm_variant / pli_gemm_ws_variant: 0 default; 1 128^2 tile; 2 256^2
+ *   one-phase; 3 phased SCHED 0; 4 one-phase + setprio; 5-8 phased SCHED
+ *   1/3/5/7; 9-11 grouped one-phase (group_m 4/8/16); 12-15 grouped phased
+ *   (8/4/2/16); 20 mid-M; 21 small-M; 22/24 direct-load split-K; 25-29 LDS
+ *   split-K (256/512/128 targets, 3-deep ring).
+ * pli_gemv_variant: 0-16 (rows per wave x 16-B chunks per lane x waves per
+ *   block, gemv.hip), -1 default.
+ * pli_attn_decode_variant: mode -1 default, 2/9/11/13 load-layout modes
+ *   (decode_attn.hip); target_wgs 0 = automatic split.
+ * pli_gemm_swiglu_ws_variant, pli_gemm_grouped_variant: 0 default, 1/2
+ *   alternate routes (gemm.hip swiglu_dispatch / grouped_dispatch).
+ */
+int pli_flash_attn_fwd_variant(const void* q, const void* k, const void* v, void* o, int batch,
+                               int heads, int kv_heads, int n_q, int n_kv, int head_dim,
+                               const int64_t* strides, float scale, int causal, int dtype,
+                               void* stream, int variant);
+int pli_gemm_variant(const void* a, const void* b, void* c, const void* bias, int m, int n, int k,
+                     int64_t lda, int64_t ldb, int64_t ldc, int trans_b, int dtype, void* stream,
+                     int variant);
+int pli_gemm_ws_variant(const void* a, const void* b, void* c, const void* bias, int m, int n,
+                        int k, int64_t lda, int64_t ldb, int64_t ldc, int trans_b, int dtype,
+                        void* workspace, size_t workspace_bytes, void* stream, int variant);
+int pli_gemv_variant(const void* w, const void* x, void* y, int m, int k, int64_t ldw, int dtype,
+                     void* stream, int variant);
+int pli_attn_decode_variant(const void* q, const void* k, const void* v, void* o, int batch,
+                            int heads, int kv_heads, int n_q, int n_kv, int head_dim,
+                            const int64_t* strides, float scale, int causal, void* workspace,
+                            size_t workspace_bytes, int dtype, void* stream, int mode,
+                            int target_wgs);
+int pli_gemm_swiglu_ws_variant(const void* x, const void* wg, const void* wu, void* h, int m, int n,
+                               int k, int64_t ldx, int64_t ldwg, int64_t ldwu, int64_t ldh,
+                               int dtype, void* workspace, size_t workspace_bytes, void* stream,
+                               int variant);
+int pli_gemm_grouped_variant(const void* x, const int32_t* gather, const void* const* w_ptrs,
+                             const void* const* wu_ptrs, void* c, const int32_t* offsets,
+                             int experts, int rows_bound, int n, int k, int64_t ldx, int64_t ldw,
+                             int64_t ldc, int dtype, void* stream, int variant);
+
 #ifdef __cplusplus
 }
 #endif

@@ -73,7 +73,7 @@ _SIGS = {
                             ctypes.c_size_t, _c_int, _vp],
     "pli_attn_decode": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
                         ctypes.POINTER(_c_i64), _c_f32, _c_int, _vp, ctypes.c_size_t, _c_int, _vp],
-    # tuning entry points (not part of include/pli.h): explicit kernel variant
+    # tuning entry points (include/pli.h tuning section): explicit kernel variant
     "pli_flash_attn_fwd_variant": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int,
                                    _c_int, ctypes.POINTER(_c_i64), _c_f32, _c_int, _c_int, _vp,
                                    _c_int],
