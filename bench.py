@@ -171,6 +171,19 @@ def bench_gemv(stream, iters: int) -> dict:
                          "traffic": load_traffic("gemv_vec")}}
 
 
+def bench_matmul_demo() -> dict:
+    """ch05/tiled_matmul.cu main at its own size (2048^3 fp32, inputs
+    (rand() % 100) / 100): the naive contrast kernel vs the fp32 MFMA tile
+    (ch05.benchmark_matmul_demo), with the f32 MFMA roofline of the tile."""
+    from ch05 import benchmark_matmul_demo
+    d = benchmark_matmul_demo(2048, warmup=3, iterations=10)
+    peak = PEAK_BF16_TFLOPS / 16  # v_mfma_f32_32x32x2_f32: 1/16 of the bf16 rate
+    d["workload"] = "ch05/tiled_matmul.cu 2048^3 fp32, naive vs MFMA tile"
+    d["roofline"] = {"bound": "mfma", "achieved": d["tiled"]["tflops"], "peak": peak, "unit": "TFLOP/s",
+                     "frac": d["tiled"]["tflops"] / peak, "kernel": "gemm_f32_mfma (v_mfma_f32_32x32x2_f32)"}
+    return d
+
+
 def bench_decode(stream, iters: int) -> dict:
     """ch02 decode step attention: one new token per sequence over the cache
     (GQA 32/8), bf16.  Two caches (2 GiB) alternate so no launch re-reads the
@@ -485,6 +498,7 @@ def main():
         extra["tp_gemm"] = bench_tp(stream, world, rank, 10)
         if world == 1:
             extra["decode_step"] = bench_decode_step()
+            extra["ch05_matmul_demo"] = bench_matmul_demo()
     else:
         extra["gemv"] = bench_gemv(stream, 200)
         if args.with_decode:
