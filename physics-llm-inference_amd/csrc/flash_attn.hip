@@ -518,7 +518,7 @@ template <typename T, int D>
 int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int H,
                 int group, int Nq, int Nk, const AttnStrides& st, float scale,
                 int causal, hipStream_t stream, int variant) {
-    if (variant == 50 || variant == 51 || variant == 54 || variant == 55) {
+    if (variant == 50 || variant == 51 || variant == 54 || variant == 55 || variant == 57) {
         // v7 prescales Q by scale*log2(e); above 1 that could overflow fp16 Q
         if (scale * 1.4426950408889634f <= 1.f) {
             const V7Strides s7{st.qb, st.qh, st.qn, st.kb, st.kh, st.kn,
