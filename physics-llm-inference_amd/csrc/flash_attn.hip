@@ -510,7 +510,8 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
 // round-2 ones that lost (in-wave pipelined v8, one-wave-per-SIMD v9, a
 // two-barrier stagger with s_setprio, a half-tile lag on a 4-deep ring, the
 // 4-wave one-wave-per-SIMD software-pipelined v11: 719-760 TF, static
-// s_setprio 1 on waves 4-7: 1088 vs 1088 TF) are
+// s_setprio 1 on waves 4-7: 1088 vs 1088 TF, the DMA pieces issued between
+// the PV MFMAs: 1035 vs 1061 TF) are
 // not in the library; their measurements are in DESIGN.md 3.1.
 constexpr int kDefaultVariant = 55;
 
@@ -518,7 +519,7 @@ template <typename T, int D>
 int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int H,
                 int group, int Nq, int Nk, const AttnStrides& st, float scale,
                 int causal, hipStream_t stream, int variant) {
-    if (variant == 50 || variant == 51 || variant == 54 || variant == 55 || variant == 57) {
+    if (variant == 50 || variant == 51 || variant == 54 || variant == 55) {
         // v7 prescales Q by scale*log2(e); above 1 that could overflow fp16 Q
         if (scale * 1.4426950408889634f <= 1.f) {
             const V7Strides s7{st.qb, st.qh, st.qn, st.kb, st.kh, st.kn,

@@ -415,7 +415,7 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v7(
 // for the b128 K-fragment read and the tr_b16 V^T read, cdna guide T10
 // layout (b)); the fragment address of k-step kk is A0 ^ (kk<<5), of V block
 // dblk B0 ^ (dblk<<6).  Rows past Nk re-read row Nk-1 (masked / weight 0).
-template <typename T, int PRE, bool STAMP = false, bool DMA_PV = false>
+template <typename T, int PRE, bool STAMP = false>
 __global__ __launch_bounds__(512, 2) void attn_fwd_v10(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
     const uint16_t* __restrict__ v, uint16_t* __restrict__ o, int H, int group,
@@ -497,19 +497,6 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v10(
             dma(kt, ko[i], base + i * 1024);
             dma(vt, vo[i], base + IMG + i * 1024);
         }
-    };
-    // DMA_PV: piece p (0, 1: K; 2, 3: V) of tile t, issued between the PV
-    // MFMAs instead of in one burst at the top of the tile
-    auto dma_piece = [&](int t, int buf, int p) __attribute__((always_inline)) {
-        const bool isv = p >= 2;
-        const int i = p & 1;
-        uint32_t off = isv ? voff[i] : koff[i];
-        if (t >= t_full) {
-            const int over = max(0, t * V7_KT + drow[i] - (Nk - 1));
-            off -= (uint32_t)(over * (int)(isv ? st.vn : st.kn) * 2);
-        }
-        const uint16_t* tb = isv ? vp + (int64_t)t * V7_KT * st.vn : kp + (int64_t)t * V7_KT * st.kn;
-        dma(tb, off, lds0 + buf * BUFB + (isv ? IMG : 0) + (2 * wave + i) * 1024);
     };
 
     // ---- Q^T fragments (B operand)
@@ -656,53 +643,24 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v10(
         if constexpr (STAMP) asm volatile("" ::"v"(pb[0][0]), "v"(pb[0][1]), "v"(pb[1][0]), "v"(pb[1][1]));
         stamp(3);
     };
-    auto Y = [&](int buf, int dma_t, int dma_buf) __attribute__((always_inline)) {
+    auto Y = [&](int buf) __attribute__((always_inline)) {
         const char* vb = smem + buf * BUFB;
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) lsum = mfma16x16x32<T>(sel, pb[tt][s2], lsum);
-        if constexpr (DMA_PV) {
-            // every V fragment of the tile is read before the first DMA (an
-            // asm DMA orders the LDS reads around it), then one DMA piece per
-            // d-block of PV MFMAs
-            i32x4 vf[D / 32][2][2];
 #pragma unroll
-            for (int dblk = 0; dblk < D / 32; ++dblk) {
-                const int alo = B0 ^ (dblk << 6), ahi = (alo ^ 32) + 2048;
+        for (int dblk = 0; dblk < D / 32; ++dblk) {
+            const int alo = B0 ^ (dblk << 6), ahi = (alo ^ 32) + 2048;
 #pragma unroll
-                for (int tt = 0; tt < 2; ++tt)
+            for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
-                    for (int s2 = 0; s2 < 2; ++s2) {
-                        const int ro = (tt * 32 + 16 * s2) * 256;
-                        const i32x2 lo = lds_read_tr16(vb, alo + ro);
-                        const i32x2 hi = lds_read_tr16(vb, ahi + ro);
-                        vf[dblk][tt][s2] = i32x4{lo.x, lo.y, hi.x, hi.y};
-                    }
-            }
-#pragma unroll
-            for (int dblk = 0; dblk < D / 32; ++dblk) {
-                if (dma_t >= 0) dma_piece(dma_t, dma_buf, dblk);
-#pragma unroll
-                for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-                    for (int s2 = 0; s2 < 2; ++s2)
-                        oacc[dblk] = mfma32x32x16<T>(vf[dblk][tt][s2], pb[tt][s2], oacc[dblk]);
-            }
-        } else {
-#pragma unroll
-            for (int dblk = 0; dblk < D / 32; ++dblk) {
-                const int alo = B0 ^ (dblk << 6), ahi = (alo ^ 32) + 2048;
-#pragma unroll
-                for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-                    for (int s2 = 0; s2 < 2; ++s2) {
-                        const int ro = (tt * 32 + 16 * s2) * 256;
-                        const i32x2 lo = lds_read_tr16(vb, alo + ro);
-                        const i32x2 hi = lds_read_tr16(vb, ahi + ro);
-                        oacc[dblk] = mfma32x32x16<T>(i32x4{lo.x, lo.y, hi.x, hi.y}, pb[tt][s2], oacc[dblk]);
-                    }
-            }
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    const int ro = (tt * 32 + 16 * s2) * 256;
+                    const i32x2 lo = lds_read_tr16(vb, alo + ro);
+                    const i32x2 hi = lds_read_tr16(vb, ahi + ro);
+                    oacc[dblk] = mfma32x32x16<T>(i32x4{lo.x, lo.y, hi.x, hi.y}, pb[tt][s2], oacc[dblk]);
+                }
         }
         stamp(4);
     };
@@ -724,9 +682,9 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v10(
         auto tile = [&](int t, auto first_tag) __attribute__((always_inline)) {
             stamp(-1);
             const int n2 = cur == 0 ? 2 : cur - 1;  // (cur + 2) % 3
-            if (!DMA_PV && t + 2 < nt) dma_tile(t + 2, n2);
+            if (t + 2 < nt) dma_tile(t + 2, n2);
             X(t, cur, first_tag);
-            Y(cur, DMA_PV && t + 2 < nt ? t + 2 : -1, n2);
+            Y(cur);
             wait_next(t + 2 < nt);
             cur = cur == 2 ? 0 : cur + 1;
         };
@@ -787,13 +745,6 @@ int launch_v7_typed(const void* q, const void* k, const void* v, void* o, int B,
             hipLaunchKernelGGL((attn_fwd_v7<T, D, 0>), grid, block, 0, stream, qq, kk, vv, oo, H, group,
                                Nq, Nk, st, c, causal, qblocks, (int)nb);
             break;
-        case 7:
-            if constexpr (D == 128) {
-                hipLaunchKernelGGL((attn_fwd_v10<T, 0, false, true>), grid, block, 0, stream, qq, kk, vv, oo, H,
-                                   group, Nq, Nk, st, c, causal, qblocks, (int)nb);
-                break;
-            }
-            [[fallthrough]];
         case 4:
         case 5:
             // v10 is D = 128 only; other head dims take the matching v7 body
