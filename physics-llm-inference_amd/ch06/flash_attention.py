@@ -11,11 +11,16 @@ reference signature and return contract (a NEW tensor shaped like ``q`` in
 * CPU tensors -> the same online-softmax tile recurrence in torch CPU ops
   (fp32 statistics), so CPU callers keep working.
 
-``FlashAttentionConfig`` keeps its four fields (``:6-11``).  The HIP kernel's
-tiles are fixed by the hardware mapping (64-key LDS tiles, 32 query rows per
-wave, 4 waves per workgroup); ``block_q``/``block_k`` only shape the CPU
-recurrence, which -- like the reference -- is mathematically independent of
-the blocking.  Softmax statistics are fp32 on both paths (the reference keeps
+``FlashAttentionConfig`` keeps its four fields (``:6-11``).  They are Triton
+launch knobs in the reference's design notes; on MI355X each one maps to a
+fixed property of the HIP kernel (``hip_tiling`` returns the mapping):
+``block_q`` -> 256 query rows per workgroup (8 waves x 32 rows, one row per
+lane of the swapped QK^T), ``block_k`` -> 64-key K/V tiles, ``num_warps`` ->
+8 wave64s per workgroup, ``num_stages`` -> a 3-deep LDS ring with K/V DMA'd
+two tiles ahead.  The GPU path ignores the requested values (results do not
+depend on the blocking; the kernel's tiles are set by the MFMA / LDS
+mapping); the CPU recurrence uses ``block_q``/``block_k`` as the reference
+does.  Non-positive or non-integer fields are rejected on both paths.  Softmax statistics are fp32 on both paths (the reference keeps
 them in ``q.dtype``, ``:32-33``; that only adds rounding).
 """
 from __future__ import annotations
@@ -33,6 +38,25 @@ class FlashAttentionConfig:
     block_k: int = 64
     num_warps: int = 4
     num_stages: int = 2
+
+
+# what each FlashAttentionConfig knob means on the HIP path (attn_fwd_v10)
+HIP_TILING = {"block_q": 256, "block_k": 64, "num_warps": 8, "num_stages": 3}
+
+
+def hip_tiling(config: "FlashAttentionConfig | None" = None) -> dict:
+    """The HIP kernel's fixed tiling next to the requested config:
+    {field: {"requested": value, "hip": value}} (the GPU path runs "hip")."""
+    config = config or FlashAttentionConfig()
+    _check_config(config)
+    return {f: {"requested": getattr(config, f), "hip": v} for f, v in HIP_TILING.items()}
+
+
+def _check_config(config) -> None:
+    for f in ("block_q", "block_k", "num_warps", "num_stages"):
+        v = getattr(config, f)
+        if isinstance(v, bool) or not isinstance(v, int) or v <= 0:
+            raise ValueError(f"FlashAttentionConfig.{f} must be a positive int, got {v!r}")
 
 
 def _flash_cpu(q, k, v, scale, block_q, block_k, causal=False):
@@ -73,6 +97,7 @@ def flash_attention_forward(
 ) -> torch.Tensor:
     if config is None:
         config = FlashAttentionConfig()
+    _check_config(config)
     B, H, N, D = q.shape
     if scale is None:
         scale = D ** -0.5

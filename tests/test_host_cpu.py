@@ -184,3 +184,21 @@ def test_triton_name_is_the_hip_gemm_on_cpu():
     for fn in (tiled_matmul, triton_matmul):
         with pytest.raises(AssertionError):
             fn(a, torch.randn(15, 4))
+
+
+def test_flash_config_mapping_and_validation():
+    """FlashAttentionConfig knobs: the HIP mapping is reported, bad values are
+    rejected on the CPU path as on the GPU path."""
+    from ch06 import FlashAttentionConfig, flash_attention_forward
+    from ch06.flash_attention import HIP_TILING, hip_tiling
+    m = hip_tiling(FlashAttentionConfig(block_q=128))
+    assert m["block_q"] == {"requested": 128, "hip": 256} and m["num_stages"]["hip"] == HIP_TILING["num_stages"]
+    q = torch.randn(1, 2, 32, 16)
+    for bad in (FlashAttentionConfig(block_q=0), FlashAttentionConfig(block_k=-64),
+                FlashAttentionConfig(num_warps=2.5), FlashAttentionConfig(num_stages=True)):
+        with pytest.raises(ValueError):
+            flash_attention_forward(q, q, q, config=bad)
+    # any valid blocking gives the same result on the CPU recurrence
+    a = flash_attention_forward(q, q, q, config=FlashAttentionConfig(block_q=8, block_k=16))
+    b = flash_attention_forward(q, q, q)
+    torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
