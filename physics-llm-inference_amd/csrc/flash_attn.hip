@@ -505,6 +505,8 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
 //  54: attn_fwd_v10: v7's body, K/V by LDS-DMA two tiles ahead into a 3-deep
 //      ring of XOR-swizzled images (D = 128; other head dims take v7), prescaled
 //  55: attn_fwd_v10 with exact scaling -- the DEFAULT (D = 128; D = 64 -> 51)
+//  60: attn_fwd_v10 exact with 4-wave workgroups (128 rows), two per CU, a
+//      2-slot ring one tile ahead -- the CAUSAL default (D = 128; D = 64 -> 51)
 // The round-1 experiments (XOR-swizzled v1, staggered v3, pipelined v4/v5,
 // 16x16x32 v6, ping-pong, segmented, one-wave-per-SIMD w4/w4p) and the
 // round-2 ones that lost (in-wave pipelined v8, one-wave-per-SIMD v9, a
@@ -514,12 +516,16 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
 // the PV MFMAs: 1035 vs 1061 TF) are
 // not in the library; their measurements are in DESIGN.md 3.1.
 constexpr int kDefaultVariant = 55;
+// causal: the 4-wave workgroups of 60 -- 128-row blocks balance the
+// triangular work better and the two workgroups per CU drift apart
+// (B8 S4096 H32 D128 bf16: 924 vs 834 TF/s; non-causal 1085 vs 1100)
+constexpr int kDefaultCausalVariant = 60;
 
 template <typename T, int D>
 int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int H,
                 int group, int Nq, int Nk, const AttnStrides& st, float scale,
                 int causal, hipStream_t stream, int variant) {
-    if (variant == 50 || variant == 51 || variant == 54 || variant == 55) {
+    if (variant == 50 || variant == 51 || variant == 54 || variant == 55 || variant == 60) {
         // v7 prescales Q by scale*log2(e); above 1 that could overflow fp16 Q
         if (scale * 1.4426950408889634f <= 1.f) {
             const V7Strides s7{st.qb, st.qh, st.qn, st.kb, st.kh, st.kn,
@@ -601,7 +607,7 @@ extern "C" int pli_flash_attn_fwd_variant(const void* q, const void* k, const vo
         vec = vec && (strides[i] % 8 == 0) && (!inner || strides[i] >= head_dim);
     }
     if (vec) {
-        if (variant < 0) variant = kDefaultVariant;
+        if (variant < 0) variant = causal ? kDefaultCausalVariant : kDefaultVariant;
         if (dtype == PLI_BF16)
             return head_dim == 128 ? launch_mfma<bf16_t, 128>(q, k, v, o, batch, heads, group, n_q, n_kv, st, scale, causal, s, variant)
                                    : launch_mfma<bf16_t, 64>(q, k, v, o, batch, heads, group, n_q, n_kv, st, scale, causal, s, variant);

@@ -415,15 +415,21 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v7(
 // for the b128 K-fragment read and the tr_b16 V^T read, cdna guide T10
 // layout (b)); the fragment address of k-step kk is A0 ^ (kk<<5), of V block
 // dblk B0 ^ (dblk<<6).  Rows past Nk re-read row Nk-1 (masked / weight 0).
-template <typename T, int PRE, bool STAMP = false>
-__global__ __launch_bounds__(512, 2) void attn_fwd_v10(
+// NW4: 4-wave workgroups (128 query rows), two per CU: the two waves of a
+// SIMD then belong to different workgroups with their own barriers, so they
+// drift apart instead of reaching the softmax together; 2-slot ring, K/V one
+// tile ahead.
+template <typename T, int PRE, bool STAMP = false, bool NW4 = false>
+__global__ __launch_bounds__(NW4 ? 256 : 512, 2) void attn_fwd_v10(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
     const uint16_t* __restrict__ v, uint16_t* __restrict__ o, int H, int group,
     int Nq, int Nk, V7Strides st, float c, int causal, int qblocks, int nblocks) {
     constexpr int D = 128;
     constexpr int IMG = V7_KT * 256;  // one [64][128] 16-bit image
     constexpr int BUFB = 2 * IMG;     // K image + V image
-    constexpr int NBUF = 3;
+    constexpr int NBUF = NW4 ? 2 : 3;
+    constexpr int NW = NW4 ? 4 : V7_NW;   // waves per workgroup
+    constexpr int PPW = 16 / NW;          // K (and V) 1-KiB pieces per wave per tile
     __shared__ __attribute__((aligned(1024))) char smem[NBUF * BUFB];
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -444,7 +450,7 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v10(
     const int bh = lb / qblocks;
     const int qblk = causal ? qblocks - 1 - lb % qblocks : lb % qblocks;
     const int b = bh / H, hq = bh % H, hk = hq / group;
-    const int qbase = qblk * (V7_NW * V7_QW);
+    const int qbase = qblk * (NW * V7_QW);
     const int q0 = qbase + wave * V7_QW;
     const int off_diag = Nk - Nq;
 
@@ -453,7 +459,7 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v10(
     const uint16_t* vp = v + b * st.vb + hk * st.vh;
 
     int kv_end = Nk;
-    if (causal) kv_end = min(Nk, qbase + V7_NW * V7_QW + off_diag);
+    if (causal) kv_end = min(Nk, qbase + NW * V7_QW + off_diag);
     const int nt = kv_end > 0 ? cdiv(kv_end, V7_KT) : 0;
     const int t_full = Nk / V7_KT;
     int t_mask = t_full;
@@ -463,11 +469,11 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v10(
     // lane -> row 4*piece + (lane>>4), stored chunk position lane&15 holds
     // logical chunk (lane&15) ^ f(row)
     auto fsw = [](int row) __attribute__((always_inline)) { return ((row & 3) << 2) | ((row >> 2) & 3); };
-    int drow[2];
-    uint32_t koff[2], voff[2];
+    int drow[PPW];
+    uint32_t koff[PPW], voff[PPW];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        drow[i] = 4 * (2 * wave + i) + (lane >> 4);
+    for (int i = 0; i < PPW; ++i) {
+        drow[i] = 4 * (PPW * wave + i) + (lane >> 4);
         const int ch = (lane & 15) ^ fsw(drow[i]);
         koff[i] = (uint32_t)(drow[i] * (int)st.kn + 8 * ch) * 2u;
         voff[i] = (uint32_t)(drow[i] * (int)st.vn + 8 * ch) * 2u;
@@ -482,18 +488,23 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v10(
     auto dma_tile = [&](int t, int buf) __attribute__((always_inline)) {
         const uint16_t* kt = kp + (int64_t)t * V7_KT * st.kn;
         const uint16_t* vt = vp + (int64_t)t * V7_KT * st.vn;
-        uint32_t ko[2] = {koff[0], koff[1]}, vo[2] = {voff[0], voff[1]};
+        uint32_t ko[PPW], vo[PPW];
+#pragma unroll
+        for (int i = 0; i < PPW; ++i) {
+            ko[i] = koff[i];
+            vo[i] = voff[i];
+        }
         if (t >= t_full) {  // ragged last tile: rows past Nk re-read row Nk-1
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
+            for (int i = 0; i < PPW; ++i) {
                 const int over = max(0, t * V7_KT + drow[i] - (Nk - 1));
                 ko[i] -= (uint32_t)(over * (int)st.kn * 2);
                 vo[i] -= (uint32_t)(over * (int)st.vn * 2);
             }
         }
-        const uint32_t base = lds0 + buf * BUFB + (2 * wave) * 1024;
+        const uint32_t base = lds0 + buf * BUFB + (PPW * wave) * 1024;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < PPW; ++i) {
             dma(kt, ko[i], base + i * 1024);
             dma(vt, vo[i], base + IMG + i * 1024);
         }
@@ -673,7 +684,25 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v10(
         stamp(6);
     };
 
-    if (nt > 0) {
+    if constexpr (NW4) {
+        if (nt > 0) {
+            dma_tile(0, 0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            auto tile4 = [&](int t, auto first_tag) __attribute__((always_inline)) {
+                stamp(-1);
+                if (t + 1 < nt) dma_tile(t + 1, (t + 1) & 1);
+                X(t, t & 1, first_tag);
+                Y(t & 1);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                stamp(5);
+                __syncthreads();
+                stamp(6);
+            };
+            tile4(0, std::true_type{});
+            for (int t = 1; t < nt; ++t) tile4(t, std::false_type{});
+        }
+    } else if (nt > 0) {
         dma_tile(0, 0);
         if (nt > 1) dma_tile(1, 1);
         // (Q's own loads were waited for by the compiler above)
@@ -745,6 +774,15 @@ int launch_v7_typed(const void* q, const void* k, const void* v, void* o, int B,
             hipLaunchKernelGGL((attn_fwd_v7<T, D, 0>), grid, block, 0, stream, qq, kk, vv, oo, H, group,
                                Nq, Nk, st, c, causal, qblocks, (int)nb);
             break;
+        case 10:
+            if constexpr (D == 128) {
+                const int qb4 = cdiv(Nq, 4 * V7_QW);
+                const int64_t nb4 = (int64_t)B * H * qb4;
+                hipLaunchKernelGGL((attn_fwd_v10<T, 0, false, true>), dim3((unsigned)nb4), dim3(256), 0, stream, qq,
+                                   kk, vv, oo, H, group, Nq, Nk, st, c, causal, qb4, (int)nb4);
+                break;
+            }
+            [[fallthrough]];
         case 4:
         case 5:
             // v10 is D = 128 only; other head dims take the matching v7 body

@@ -106,7 +106,7 @@ def test_flash_vs_oracle(case):
 
 
 # every MFMA variant (alternates A/B-tested by tools/tune.py) on the MFMA-eligible cases
-MFMA_VARIANTS = (21, 50, 51, 54, 55)
+MFMA_VARIANTS = (21, 50, 51, 54, 55, 60)
 
 
 
@@ -143,10 +143,15 @@ PRESCALED = (50, 54)
 DEFAULT_VARIANT = 55
 
 
+DEFAULT_CAUSAL_VARIANT = 60
+
+
 def test_flash_default_is_variant_55():
     import pli_hip
     q, k, v = (dev(x, "bf16") for x in stress_inputs("late"))
     assert torch.equal(pli_hip.flash_attn_fwd(q, k, v), pli_hip.flash_attn_fwd(q, k, v, variant=DEFAULT_VARIANT))
+    assert torch.equal(pli_hip.flash_attn_fwd(q, k, v, causal=True),
+                       pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=DEFAULT_CAUSAL_VARIANT))
 
 
 @pytest.mark.parametrize("variant", MFMA_VARIANTS)
@@ -181,7 +186,7 @@ def test_flash_stress(variant, name):
         assert err <= tol, f"stress {name}: {err:.3e} > {tol:.3e}"
 
 
-@pytest.mark.parametrize("variant", [None, 21, 50, 51, 54])
+@pytest.mark.parametrize("variant", [None, 21, 50, 51, 54, 60])
 def test_flash_full_config_properties(variant):
     """B=8 S=4096 H=32 D=128 bf16 (the bench config): v = 1 gives exactly 1;
     two heads checked against the f64 oracle; key permutation invariance."""
@@ -202,6 +207,29 @@ def test_flash_full_config_properties(variant):
     if variant is None:
         base = pli_hip.flash_attn_fwd(q, k, v, variant=21)
         assert (base.float() - out.float()).abs().max().item() <= 1.6e-2
+
+
+@pytest.mark.parametrize("variant", [None, 55, 21])
+def test_flash_full_config_causal(variant):
+    """Causal at the bench config (the ch01 MHA / GQA semantics): rows 0,
+    1000 and 4095 of three heads against the f64 oracle (row i sees keys
+    0..i), v = 1 gives 1, and the default agrees with the 8-wave kernel."""
+    import pli_hip
+    B, H, N, D = 8, 32, 4096, 128
+    g = torch.Generator(device=DEV).manual_seed(5)
+    q, k, v = (torch.randn(B, H, N, D, device=DEV, dtype=torch.bfloat16, generator=g) for _ in range(3))
+    out = pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=variant).float().cpu().numpy()
+    ones = pli_hip.flash_attn_fwd(q, k, torch.ones_like(v), causal=True, variant=variant)
+    assert (ones.float() - 1).abs().max().item() <= 2 ** -8
+    for (b, h) in ((0, 0), (3, 17), (7, 31)):
+        qq, kk, vv = (t[b:b + 1, h:h + 1].float().cpu().numpy() for t in (q, k, v))
+        for i in (0, 1000, 4095):
+            ref = oatt.naive_attention(qq[:, :, i:i + 1], kk[:, :, :i + 1], vv[:, :, :i + 1])
+            err = np.abs(out[b, h, i] - ref[0, 0, 0]).max()
+            assert err <= 1e-2, f"causal b{b} h{h} row {i}: {err:.3e}"
+    if variant is None:
+        base = pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=55).float().cpu().numpy()
+        assert np.abs(base - out).max() <= 1.6e-2
 
 
 def test_mha_hip_matches_reference_golden():
