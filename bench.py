@@ -488,7 +488,8 @@ def main():
                                        "timing": "sync + perf_counter per call, 5 calls"}
         ms_c = event_time_ms(lambda: pli_hip.flash_attn_fwd(q, k, v, causal=True, out=o), 5, stream)
         extra["flash_causal"] = {"ms": ms_c,
-                                 "TFLOP/s": 4 * B * H * D * (S * (S + 1) // 2) / (ms_c * 1e-3) / 1e12}
+                                 "TFLOP/s": 4 * B * H * D * (S * (S + 1) // 2) / (ms_c * 1e-3) / 1e12,
+                                 "kernel": "attn_fwd_v10<bf16,exact>, 4-wave workgroups (variant 60)"}
     if args.flash_only:
         pass
     elif not args.quick:
