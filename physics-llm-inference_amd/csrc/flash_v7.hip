@@ -856,6 +856,12 @@ extern "C" int pli_diag_flash_stamps(const void* q, const void* k, const void* v
             hipLaunchKernelGGL((attn_fwd_v10<bf16_t, 0, true>), dim3(nb), dim3(512), 0, 0, qq, kk, vv, oo, H, 1, N, N,
                                st, c, 0, qblocks, nb);
             break;
+        case 10: {
+            const int qb4 = cdiv(N, 4 * V7_QW), nb4 = B * H * qb4;
+            hipLaunchKernelGGL((attn_fwd_v10<bf16_t, 0, true, true>), dim3(nb4), dim3(256), 0, 0, qq, kk, vv, oo, H, 1,
+                               N, N, st, c, 0, qb4, nb4);
+            break;
+        }
         default: return PLI_EINVAL;
     }
 #undef PLI_DIAG
