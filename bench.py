@@ -21,6 +21,7 @@ The same JSON line carries, as sub-objects, the other hot-path rows:
   cpu_other     torch.mv / torch.mm / one TP8 shard F.linear on the host cores
   tp_gemm.small_m  the TP shard GEMM at M = 1 and 128
   flash_wallclock_ms  the reference's timing style (sync per call) beside the events
+  flash_torch_sdpa    torch SDPA's fused backends on the same tensors (comparison)
 
 All device times are HIP events recorded on the stream the kernels run on.
 """
@@ -121,6 +122,38 @@ def cpu_info() -> dict:
         affinity = None
     return {"cpu_model": model, "os_cpu_count": os.cpu_count(), "affinity_cores": affinity,
             "torch_threads": torch.get_num_threads()}
+
+
+def bench_torch_sdpa(q, k, v, o, stream) -> dict:
+    """The vendor path on the same workload, for comparison only: PyTorch's
+    scaled_dot_product_attention restricted to its fused backends (flash, then
+    memory-efficient; on ROCm these are AOTriton / CK kernels), non-causal and
+    causal, with the max |diff| to this build's output."""
+    import pli_hip
+    import torch.nn.functional as F
+    from torch.nn.attention import SDPBackend, sdpa_kernel
+    B_, H_, S_, D_ = q.shape
+    out = {}
+    for name, be in (("flash", SDPBackend.FLASH_ATTENTION), ("efficient", SDPBackend.EFFICIENT_ATTENTION)):
+        try:
+            with sdpa_kernel([be]):
+                r = {}
+                for causal in (False, True):
+                    fn = lambda: F.scaled_dot_product_attention(q, k, v, is_causal=causal)  # noqa: E731
+                    ref = fn()
+                    torch.cuda.synchronize()
+                    pli_out = pli_hip.flash_attn_fwd(q, k, v, causal=causal, out=o)
+                    diff = (ref.float() - pli_out.float()).abs().max().item()
+                    ms = event_time_ms(fn, 5, torch.cuda.current_stream())
+                    pairs = S_ * (S_ + 1) // 2 if causal else S_ * S_
+                    r["causal" if causal else "non_causal"] = {
+                        "ms": ms, "TFLOP/s": 4 * B_ * H_ * D_ * pairs / (ms * 1e-3) / 1e12,
+                        "max_abs_diff_vs_pli": diff}
+                out[name] = r
+        except Exception as e:  # backend not built for this arch / dtype
+            out[name] = {"unavailable": f"{type(e).__name__}: {str(e)[:160]}"}
+    out["note"] = "comparison only (vendor kernels via torch), not part of value"
+    return out
 
 
 def bench_gemv(stream, iters: int) -> dict:
@@ -490,6 +523,7 @@ def main():
         extra["flash_causal"] = {"ms": ms_c,
                                  "TFLOP/s": 4 * B * H * D * (S * (S + 1) // 2) / (ms_c * 1e-3) / 1e12,
                                  "kernel": "attn_fwd_v10<bf16,exact>, 4-wave workgroups (variant 60)"}
+        extra["flash_torch_sdpa"] = bench_torch_sdpa(q, k, v, o, stream)
     if args.flash_only:
         pass
     elif not args.quick:

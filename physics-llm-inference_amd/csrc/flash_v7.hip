@@ -32,6 +32,8 @@
 namespace pli {
 namespace {
 
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+
 constexpr int V7_KT = 64;       // keys per tile
 constexpr int V7_QW = 32;       // query rows per wave
 constexpr int V7_NW = 8;        // waves per workgroup
@@ -123,13 +125,12 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v7(
     i32x4 qf[D / 16];
     {
         const int qr = q0 + l32;
-        const bool ok = qr < Nq;
-        const uint16_t* src = qp + (int64_t)(ok ? qr : 0) * st.qn + 8 * h32;
+        // rows past Nq read row 0 (finite scores, never stored): no select,
+        // which hipcc otherwise re-materialises inside the K loop (32 v_cndmask
+        // per tile)
+        const uint16_t* src = qp + (int64_t)(qr < Nq ? qr : 0) * st.qn + 8 * h32;
 #pragma unroll
-        for (int kk = 0; kk < D / 16; ++kk) {
-            const i32x4 x = *reinterpret_cast<const i32x4*>(src + 16 * kk);
-            qf[kk] = ok ? x : i32x4{0, 0, 0, 0};
-        }
+        for (int kk = 0; kk < D / 16; ++kk) qf[kk] = *reinterpret_cast<const i32x4*>(src + 16 * kk);
         if constexpr (PRE != 0) {
 #pragma unroll
             for (int kk = 0; kk < D / 16; ++kk)
@@ -514,13 +515,12 @@ __global__ __launch_bounds__(NW4 ? 256 : 512, 2) void attn_fwd_v10(
     i32x4 qf[D / 16];
     {
         const int qr = q0 + l32;
-        const bool ok = qr < Nq;
-        const uint16_t* src = qp + (int64_t)(ok ? qr : 0) * st.qn + 8 * h32;
+        // rows past Nq read row 0 (finite scores, never stored): no select,
+        // which hipcc otherwise re-materialises inside the K loop (32 v_cndmask
+        // per tile)
+        const uint16_t* src = qp + (int64_t)(qr < Nq ? qr : 0) * st.qn + 8 * h32;
 #pragma unroll
-        for (int kk = 0; kk < D / 16; ++kk) {
-            const i32x4 x = *reinterpret_cast<const i32x4*>(src + 16 * kk);
-            qf[kk] = ok ? x : i32x4{0, 0, 0, 0};
-        }
+        for (int kk = 0; kk < D / 16; ++kk) qf[kk] = *reinterpret_cast<const i32x4*>(src + 16 * kk);
         if constexpr (PRE != 0) {
 #pragma unroll
             for (int kk = 0; kk < D / 16; ++kk)
@@ -583,11 +583,23 @@ __global__ __launch_bounds__(NW4 ? 256 : 512, 2) void attn_fwd_v10(
             }
         };
         auto expo = [&]() __attribute__((always_inline)) {
+            if constexpr (PRE != 0) {
 #pragma unroll
-            for (int tt = 0; tt < 2; ++tt)
+                for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    s[tt][r] = __builtin_amdgcn_exp2f(PRE != 0 ? s[tt][r] : fmaf(s[tt][r], c, -m_run));
+                    for (int r = 0; r < 16; ++r) s[tt][r] = __builtin_amdgcn_exp2f(s[tt][r]);
+            } else {
+                // s*c - m two scores at a time (v_pk_fma_f32)
+                const f32x2 c2 = {c, c}, nm2 = {-m_run, -m_run};
+#pragma unroll
+                for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                    for (int r = 0; r < 16; r += 2) {
+                        const f32x2 y = __builtin_elementwise_fma(f32x2{s[tt][r], s[tt][r + 1]}, c2, nm2);
+                        s[tt][r] = __builtin_amdgcn_exp2f(y.x);
+                        s[tt][r + 1] = __builtin_amdgcn_exp2f(y.y);
+                    }
+            }
         };
         stamp(0);
         qk();
