@@ -186,6 +186,18 @@ def bench_gemv(stream, iters: int) -> dict:
         pli_hip.gemv(ws[state["i"] % copies], x, out=y)
         state["i"] += 1
     ms_eager = event_time_ms(eager, 4 * copies, stream)
+    # the vendor path under the same rotation and graph (comparison only)
+    yt = torch.empty(m, device="cuda", dtype=torch.bfloat16)
+    for w in ws:
+        torch.mv(w, x, out=yt)
+    torch.cuda.synchronize()
+    tgraph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(tgraph):
+        for w in ws:
+            torch.mv(w, x, out=yt)
+    for _ in range(3):
+        tgraph.replay()
+    ms_torch = event_time_ms(tgraph.replay, reps, stream) / copies
     nbytes = gemv_bytes(m, k, torch.bfloat16)
     gbps = nbytes / (ms * 1e-3) / 1e9
     # streaming asymptote of the same kernel: one 16384x16384 launch (512 MiB)
@@ -198,6 +210,7 @@ def bench_gemv(stream, iters: int) -> dict:
     return {"workload": "ch03 GEMV 4096x4096 bf16, batch 1, W rotated over 768 MiB (HBM-resident)",
             "us_per_launch": ms * 1e3, "GB/s": gbps, "timing": "HIP graph of 24 launches, events",
             "eager_us_per_call": ms_eager * 1e3,
+            "torch_mv_us_per_launch": ms_torch * 1e3,
             "streaming_16384sq_GB/s": gemv_bytes(16384, 16384, torch.bfloat16) / (ms_big * 1e-3) / 1e9,
             "roofline": {"bound": "hbm", "achieved": gbps, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                          "frac": gbps / PEAK_HBM_GBPS, "algorithmic_bytes": nbytes,

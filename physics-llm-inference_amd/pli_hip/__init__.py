@@ -20,7 +20,8 @@ __all__ = [
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "libpli_hip.so")
+# PLI_HIP_LIB: an alternate in-tree build (A/B tooling); default the package .so
+_LIB_PATH = os.environ.get("PLI_HIP_LIB") or os.path.join(_HERE, "libpli_hip.so")
 _lib = None
 
 DTYPE_CODE = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}
