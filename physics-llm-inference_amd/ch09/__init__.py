@@ -1,8 +1,15 @@
 """Chapter 09 on MI355X: tensor-parallel linear layers on the HIP GEMM with a
 real RCCL all-reduce, the collective cost models, and the MoE layer on the
-grouped expert GEMM (the expert-offloading engine of moe_inference.py is
-control plane and not mirrored)."""
+grouped expert GEMM, and the host-side expert cache / execution planner of
+moe_inference.py (bookkeeping only, so the reference's test module loads)."""
 
+from .moe_inference import (
+    ExpertCache,
+    ExpertUsageStats,
+    MoEInferenceConfig,
+    MoEInferenceEngine,
+    explain_moe_inference,
+)
 from .moe_layer import (
     ExpertLayer,
     MoEConfig,
@@ -36,6 +43,11 @@ __all__ = [
     "MoELayer",
     "expert_load_balance_loss",
     "explain_moe",
+    "MoEInferenceEngine",
+    "MoEInferenceConfig",
+    "ExpertCache",
+    "ExpertUsageStats",
+    "explain_moe_inference",
     "TensorParallelConfig",
     "ColumnParallelLinear",
     "RowParallelLinear",

@@ -202,3 +202,44 @@ def test_flash_config_mapping_and_validation():
     a = flash_attention_forward(q, q, q, config=FlashAttentionConfig(block_q=8, block_k=16))
     b = flash_attention_forward(q, q, q)
     torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_moe_inference_bookkeeping():
+    """ch09.moe_inference (reference ch09/moe_inference.py:16-126): LRU order
+    and eviction, hit/miss counters, the execution plan, and the per-expert
+    routing statistics against a per-expert masked restatement."""
+    from ch09 import ExpertCache, MoEInferenceConfig, MoEInferenceEngine
+    c = ExpertCache(max_experts_in_memory=3, num_total_experts=6)
+    for e in (0, 1, 2):
+        assert c.add_expert(e, torch.full((2,), float(e))) is None
+    assert c.get_expert(0) is not None          # refresh 0: LRU order 1, 2, 0
+    assert c.add_expert(3, torch.zeros(2)) == 1
+    assert c.add_expert(4, torch.zeros(2)) == 2
+    assert c.get_cached_expert_ids() == [0, 3, 4]
+    assert c.get_expert(1) is None and c.get_expert(5) is None
+    assert c.get_cache_hit_rate() == pytest.approx(1 / 3)
+
+    eng = MoEInferenceEngine(MoEInferenceConfig(num_experts=8, max_experts_in_gpu=2))
+    eng.expert_cache.add_expert(5, torch.zeros(1))
+    g = torch.Generator().manual_seed(3)
+    idx = torch.randint(0, 8, (64, 2), generator=g)
+    idx[0] = torch.tensor([5, 1])
+    w = torch.rand(64, 2, generator=g)
+    plan = eng.plan_expert_execution(idx)
+    uniq = sorted(set(idx.flatten().tolist()))
+    assert plan["total_unique"] == len(uniq)
+    assert plan["in_cache"] == [5] and plan["need_load"] == [e for e in uniq if e != 5]
+    eng.update_batch_stats(idx, w)
+    eng.update_batch_stats(idx[:10], w[:10])
+    for e in range(8):
+        m1, m2 = idx == e, idx[:10] == e
+        st = eng.expert_cache.stats[e]
+        assert st.tokens_routed == int(m1.sum() + m2.sum())
+        assert st.total_weight == pytest.approx(float(w[m1].double().sum() + w[:10][m2].double().sum()), rel=1e-6)
+    met = eng.get_load_balance_metrics()
+    loads = [eng.expert_cache.stats[e].tokens_routed for e in range(8)]
+    assert met["max_load"] == max(loads) and met["min_load"] == min(loads)
+    assert met["expected"] == pytest.approx(sum(loads) / 8)
+    assert met["std_dev"] == pytest.approx(float(np.std(loads, ddof=1)), rel=1e-5)
+    assert MoEInferenceEngine(MoEInferenceConfig()).get_load_balance_metrics() == \
+        {"balance_ratio": 1.0, "max_load": 0, "min_load": 0}

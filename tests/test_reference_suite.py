@@ -7,9 +7,8 @@ resolve to the MI355X implementation.  Test classes / methods are collected
 here and run one pytest case each; the reference's ``skipif`` markers are
 honoured (its CUDA-gated classes run on a ROCm box, skip elsewhere).
 
-Chapters run: ch01, ch02, ch03, ch05, ch06 -- every module their test files
-import exists in this build.  Not run: ch09 (its test module imports
-``moe_inference``, expert offloading, out of scope), ch04 / ch07 / ch08 / ch10
+Chapters run: ch01, ch02, ch03, ch05, ch06, ch09 -- every module their test
+files import exists in this build.  Not run: ch04 / ch07 / ch08 / ch10
 (pedagogy / control plane, out of scope).  Skipped entirely when
 /root/reference is absent (e.g. on the GPU box, where tests/test_gpu_*.py
 restate the CUDA-gated assertions with committed fixtures).
@@ -23,7 +22,7 @@ import os
 import pytest
 
 REF = os.environ.get("PLI_REFERENCE", "/root/reference")
-CHAPTERS = ("ch01", "ch02", "ch03", "ch05", "ch06")
+CHAPTERS = ("ch01", "ch02", "ch03", "ch05", "ch06", "ch09")
 
 
 def _load(chapter: str):
