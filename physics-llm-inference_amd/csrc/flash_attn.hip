@@ -513,7 +513,8 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
 // two-barrier stagger with s_setprio, a half-tile lag on a 4-deep ring, the
 // 4-wave one-wave-per-SIMD software-pipelined v11: 719-760 TF, static
 // s_setprio 1 on waves 4-7: 1088 vs 1088 TF, the DMA pieces issued between
-// the PV MFMAs: 1035 vs 1061 TF) are
+// the PV MFMAs: 1035 vs 1061 TF, two 64-key tiles per barrier on a 4-slot
+// ring: 1054 vs 1054 TF, causal 850 vs 844) are
 // not in the library; their measurements are in DESIGN.md 3.1.
 constexpr int kDefaultVariant = 55;
 // causal: the 4-wave workgroups of 60 -- 128-row blocks balance the

@@ -465,9 +465,11 @@ __global__ __launch_bounds__(NW4 ? 256 : 512, 2) void attn_fwd_v10(
     const int t_full = Nk / V7_KT;
     int t_mask = t_full;
     if (causal) t_mask = min(t_mask, max(0, (q0 + off_diag + 1) / V7_KT));
-    // (skipping the compute of tiles wholly above a wave's diagonal loses: the
-    // branch makes hipcc wait for every DMA in flight (vmcnt(0)) before the
-    // loop's LDS reads -- 941-960 vs 998-1049 TF/s non-causal, causal -4 %)
+    // causal: tiles past this wave's last visible key are all -inf for its
+    // rows; the wave skips their compute but still issues its DMA pieces and
+    // meets the barriers (workgroup-uniform pipeline)
+    int t_last = nt;
+    if (causal) t_last = (q0 + V7_QW - 1 + off_diag) < 0 ? -1 : (q0 + V7_QW - 1 + off_diag) / V7_KT;
 
     // ---- LDS-DMA plan: wave w fills pieces 2w, 2w+1 of the K and V images;
     // lane -> row 4*piece + (lane>>4), stored chunk position lane&15 holds
@@ -524,6 +526,13 @@ __global__ __launch_bounds__(NW4 ? 256 : 512, 2) void attn_fwd_v10(
         const uint16_t* src = qp + (int64_t)(qr < Nq ? qr : 0) * st.qn + 8 * h32;
 #pragma unroll
         for (int kk = 0; kk < D / 16; ++kk) qf[kk] = *reinterpret_cast<const i32x4*>(src + 16 * kk);
+        // retire the Q loads here, before the first LDS-DMA: a volatile asm
+        // that "reads" qf makes hipcc wait for the loads at this point (and
+        // volatile asms keep their order, so the DMAs come after).  Otherwise
+        // its vmcnt(N) waits for Q, placed at Q's first use, also wait for
+        // every DMA issued since (its waitcnt pass does not count inline asm)
+#pragma unroll
+        for (int kk = 0; kk < D / 16; ++kk) asm volatile("" : "+v"(qf[kk]));
         if constexpr (PRE != 0) {
 #pragma unroll
             for (int kk = 0; kk < D / 16; ++kk)
@@ -707,8 +716,10 @@ __global__ __launch_bounds__(NW4 ? 256 : 512, 2) void attn_fwd_v10(
             auto tile4 = [&](int t, auto first_tag) __attribute__((always_inline)) {
                 stamp(-1);
                 if (t + 1 < nt) dma_tile(t + 1, (t + 1) & 1);
-                X(t, t & 1, first_tag);
-                Y(t & 1);
+                if (t <= t_last) {
+                    X(t, t & 1, first_tag);
+                    Y(t & 1);
+                }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 stamp(5);
                 __syncthreads();
@@ -727,8 +738,10 @@ __global__ __launch_bounds__(NW4 ? 256 : 512, 2) void attn_fwd_v10(
             stamp(-1);
             const int n2 = cur == 0 ? 2 : cur - 1;  // (cur + 2) % 3
             if (t + 2 < nt) dma_tile(t + 2, n2);
-            X(t, cur, first_tag);
-            Y(cur);
+            if (t <= t_last) {
+                X(t, cur, first_tag);
+                Y(cur);
+            }
             wait_next(t + 2 < nt);
             cur = cur == 2 ? 0 : cur + 1;
         };
