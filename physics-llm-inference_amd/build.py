@@ -30,7 +30,7 @@ CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I" + INCLUDE
 # per-source extra flags.  flash_v7: no NaN ever reaches the softmax (masks
 # use -inf), so fmaxf on MFMA results folds into v_max3_f32 without the
 # canonicalising v_max_f32 hipcc otherwise puts in front of each one.
-EXTRA = {"flash_v7.hip": ["-fno-honor-nans"]}
+EXTRA = {"flash_v7.hip": ["-fno-honor-nans"], "flash_v12.hip": ["-fno-honor-nans"]}
 
 
 def hipcc() -> str:

@@ -1,0 +1,405 @@
+// attn_fwd_v12: flash-attention forward, one wave per SIMD, 64 query rows per
+// wave (reference ch06/flash_attention.py:14-74; gfx950, bf16, D = 128,
+// non-causal, Nk a multiple of 64 -- other cases take attn_fwd_v10).
+//
+// The structure of cdna_hip_programming.md's 4-wave persistent example,
+// without persistence: a workgroup is 4 waves x 64 rows (two 32-row blocks A
+// and B per wave), one workgroup per CU, and each wave owns the whole
+// 512-entry register file.  O^T (128 registers), Q^T (64) and the K
+// fragments of one tile (64) live in the accumulator file, named literally
+// by the inline-asm MFMAs of flash_v12_asm.h; hipcc keeps S, P and the
+// softmax in the architectural VGPRs.  One K fragment feeds the QK^T MFMAs of
+// both blocks and one V^T fragment both blocks' PV MFMAs, so LDS bytes per
+// MFMA are half of attn_fwd_v10's.
+//
+// Per tile t (steady state), two MFMA phases with the VALU work beside them:
+//   phase Q:  S(t) = K(t) Q^T, block A's chain then block B's (32 MFMAs);
+//             beside B's chain, block A's softmax slices (running max,
+//             speculative exps with the current m, packed P into P(t&1))
+//   barrier (tile t+1 landed; every wave past PV(t-2)), DMA of tile t+2
+//   phase P:  O += V(t-1)^T P(t-1) (32 MFMAs) + the row-sum MFMAs of P(t-1)
+//             || block B's softmax slices || K(t+1) fragments -> AGPR
+// then the defer-max ballot of tile t (rare path: drain, rescale O and l,
+// recompute S(t) from the LDS copy of K(t), redo its exps and P).  One S
+// state, two P states (t even / odd).  K/V tiles arrive by LDS-DMA into a
+// 4-slot ring of XOR-swizzled images (attn_fwd_v10's layout), one tile ahead.
+//
+// Arithmetic is attn_fwd_v10's (exact scaling, same MFMA chains and orders,
+// same defer-max rule per row), so outputs are bitwise those of variant 55.
+//
+// hipcc does not see the asm statements as MFMAs or loads, so this file
+// carries its own hazard padding (s_nop after MFMA results before VALU or
+// accumulator reads, before MFMAs reading freshly written P) and its own LDS
+// counts (every LDS access of the loop is asm, in a fixed order).
+#include <type_traits>
+#include <utility>
+
+#include "flash_v7.h"
+#include "pli_common.h"
+#include "flash_v12_asm.h"
+
+namespace pli {
+namespace {
+
+template <int... I, class Fn>
+__device__ __forceinline__ void v12_for(std::integer_sequence<int, I...>, Fn&& fn) {
+    (fn(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class Fn> __device__ __forceinline__ void sfor(Fn&& fn) {
+    v12_for(std::make_integer_sequence<int, N>{}, fn);
+}
+
+template <int N> __device__ __forceinline__ void lgkm() { asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory"); }
+
+struct V12Frag { i32x2 lo, hi; };
+
+// V^T fragment (two tr-reads); `ro` an immediate byte offset
+template <int RO> __device__ __forceinline__ void v12_vread(V12Frag& f, uint32_t alo, uint32_t ahi) {
+    asm volatile("ds_read_b64_tr_b16 %0, %2 offset:%4\n\tds_read_b64_tr_b16 %1, %3 offset:%4"
+                 : "=&v"(f.lo), "=&v"(f.hi) : "v"(alo), "v"(ahi), "n"(RO) : "memory");
+}
+// wait until at most N LDS accesses are outstanding; the fragment's registers
+// are "written" here as far as hipcc knows, so nothing reads them earlier
+template <int N> __device__ __forceinline__ void v12_vwait(V12Frag& f) {
+    asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(f.lo), "+v"(f.hi) : "n"(N) : "memory");
+}
+
+// row sums: the four selector MFMAs of one block in ONE statement, strictly
+// back to back (an MFMA takes the previous result as C without wait states
+// only as the very next instruction; an s_nop between them lost a step's sum);
+// the leading s_nop covers a hipcc v_mov of l right before the statement, the
+// trailing ones a v_mov of the result right after it (4-pass XDL -> VALU)
+__device__ __forceinline__ void v12_sel4(f32x4& l, i32x4 sel, i32x4 p0, i32x4 p1, i32x4 p2, i32x4 p3) {
+    asm volatile("s_nop 2\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0\n\t"
+                 "v_mfma_f32_16x16x32_bf16 %0, %1, %3, %0\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %4, %0\n\t"
+                 "v_mfma_f32_16x16x32_bf16 %0, %1, %5, %0\n\ts_nop 7\n\ts_nop 2"
+                 : "+v"(l) : "v"(sel), "v"(p0), "v"(p1), "v"(p2), "v"(p3));
+}
+
+// MFMA results -> VALU reads: 8-pass XDL needs 12 wait states
+__device__ __forceinline__ void v12_sfence(f32x16 (&s)[2][2]) {
+    asm volatile("s_nop 7\n\ts_nop 4" : "+v"(s[0][0]), "+v"(s[0][1]), "+v"(s[1][0]), "+v"(s[1][1]));
+}
+
+__device__ __forceinline__ float v12_xor32_max(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float v12_xor32_sum(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+typedef __attribute__((ext_vector_type(2))) float v12f2;
+constexpr float V12_THR = 8.f;
+
+__global__ __launch_bounds__(256, 1) void attn_fwd_v12(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
+    uint16_t* __restrict__ o, int H, int group, int Nq, int Nk, V7Strides st, float c, int qblocks,
+    int nblocks) {
+    constexpr int KT = 64, IMG = KT * 256, BUFB = 2 * IMG, NBUF = 4, PPW = 4;
+    __shared__ __attribute__((aligned(1024))) char smem[NBUF * BUFB];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int h32 = lane >> 5, l32 = lane & 31;
+    const int lb = xcd_remap(blockIdx.x, nblocks);
+    const int bh = lb / qblocks, qblk = lb % qblocks;
+    const int b = bh / H, hq = bh % H, hk = hq / group;
+    const int q0 = qblk * 256 + wave * 64;
+    const uint16_t* qp = q + b * st.qb + hq * st.qh;
+    const uint16_t* kp = k + b * st.kb + hk * st.kh;
+    const uint16_t* vp = v + b * st.vb + hk * st.vh;
+    const int nt = Nk / KT;
+
+    // ---- LDS-DMA plan (attn_fwd_v10's, 4 waves: 4 K + 4 V pieces per wave)
+    auto fsw = [](int row) __attribute__((always_inline)) { return ((row & 3) << 2) | ((row >> 2) & 3); };
+    uint32_t koff[PPW], voff[PPW];
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+        const int drow = 4 * (PPW * wave + i) + (lane >> 4);
+        const int ch = (lane & 15) ^ fsw(drow);
+        koff[i] = (uint32_t)(drow * (int)st.kn + 8 * ch) * 2u;
+        voff[i] = (uint32_t)(drow * (int)st.vn + 8 * ch) * 2u;
+    }
+    auto dma = [&](const uint16_t* tbase, uint32_t off, uint32_t lds) __attribute__((always_inline)) {
+        uint32_t keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %3\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(keep) : "s"(lds), "v"(off), "s"(tbase) : "memory");
+    };
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
+    auto dma_tile = [&](int t, int slot) __attribute__((always_inline)) {
+        const uint16_t* kt = kp + (int64_t)t * KT * st.kn;
+        const uint16_t* vt = vp + (int64_t)t * KT * st.vn;
+        const uint32_t base = lds0 + slot * BUFB + (PPW * wave) * 1024;
+#pragma unroll
+        for (int i = 0; i < PPW; ++i) {
+            dma(kt, koff[i], base + i * 1024);
+            dma(vt, voff[i], base + IMG + i * 1024);
+        }
+    };
+
+    // ---- Q^T fragments -> AGPR; O = 0
+    {
+        const int ra = q0 + l32, rb = q0 + 32 + l32;
+        const uint16_t* sa = qp + (int64_t)(ra < Nq ? ra : 0) * st.qn + 8 * h32;
+        const uint16_t* sb = qp + (int64_t)(rb < Nq ? rb : 0) * st.qn + 8 * h32;
+        i32x4 qa[8], qb[8];
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) {
+            qa[kk] = *reinterpret_cast<const i32x4*>(sa + 16 * kk);
+            qb[kk] = *reinterpret_cast<const i32x4*>(sb + 16 * kk);
+        }
+        sfor<8>([&](auto KK) {
+            v12::q_to_agpr<0, KK>(qa[KK]);
+            v12::q_to_agpr<1, KK>(qb[KK]);
+        });
+    }
+    v12::o_zero();
+
+    // ---- fragment addresses (LDS byte addresses; + slot * BUFB per tile)
+    const int A0 = l32 * 256 + ((h32 ^ fsw(l32)) << 4);
+    uint32_t kaddr[8];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) kaddr[kk] = lds0 + (uint32_t)(A0 ^ (kk << 5));
+    const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+    const int c0 = 2 * (g & 1) + (pp >> 1);
+    const int B0 = IMG + (4 * h32 + qq) * 256 + ((c0 ^ ((qq << 2) | h32)) << 4) + 8 * (pp & 1);
+    uint32_t valo[4], vahi[4];
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+        const int alo = B0 ^ (db << 6);
+        valo[db] = lds0 + (uint32_t)alo;
+        vahi[db] = lds0 + (uint32_t)((alo ^ 32) + 2048);
+    }
+    const bool sel_on = (i16 == 0 && (g & 1) == 0) || (i16 == 4 && (g & 1) == 1);
+    const int one = sel_on ? 0x3F803F80 : 0;
+    const i32x4 sel = {one, one, one, one};
+
+    float mA = -1e30f, mB = -1e30f;
+    f32x4 lA = {0.f, 0.f, 0.f, 0.f}, lB = {0.f, 0.f, 0.f, 0.f};
+    // hipcc does not know the row-sum asm MFMAs read l as C: materialise the
+    // zeros here, wait states after (VALU write -> MFMA source)
+    asm volatile("s_nop 2" : "+v"(lA), "+v"(lB));
+    f32x16 S[2][2];               // [block][key half]: one tile's scores / exps
+    i32x4 P0[2][2][2], P1[2][2][2];  // [block][key half][16-key step]; tile t in P(t&1)
+    float mxA = -INFINITY, mxB = -INFINITY;
+
+    // one softmax slice of block X: elements 2i, 2i+1 -- running max, the
+    // speculative exps with the current m, the packed bf16 pair into P
+    auto slice = [&](auto x_tag, auto i_tag, i32x4 (&Pc)[2][2][2]) __attribute__((always_inline)) {
+        constexpr int X = decltype(x_tag)::value, i = decltype(i_tag)::value;
+        constexpr int tt = i / 8, r = 2 * (i % 8), s2 = (i % 8) / 4, j = i % 4;
+        float& mx = X == 0 ? mxA : mxB;
+        const float m = X == 0 ? mA : mB;
+        mx = max3(mx, S[X][tt][r], S[X][tt][r + 1]);
+        const v12f2 y = __builtin_elementwise_fma(v12f2{S[X][tt][r], S[X][tt][r + 1]}, v12f2{c, c}, v12f2{-m, -m});
+        const float e0 = __builtin_amdgcn_exp2f(y.x), e1 = __builtin_amdgcn_exp2f(y.y);
+        Pc[X][tt][s2][j] = (int)pack2<bf16_t>(e0, e1);
+        // pin the exps here: without a use at this point hipcc sinks them to
+        // the next tile's PV, where P is read
+        asm volatile("" : "+v"(Pc[X][tt][s2]));
+    };
+    // VALU-written P -> MFMA operands: pin P here and pad
+    auto pfence = [&](i32x4 (&Pc)[2][2][2]) __attribute__((always_inline)) {
+        asm volatile("s_nop 1" : "+v"(Pc[0][0][0]), "+v"(Pc[0][0][1]), "+v"(Pc[0][1][0]), "+v"(Pc[0][1][1]),
+                     "+v"(Pc[1][0][0]), "+v"(Pc[1][0][1]), "+v"(Pc[1][1][0]), "+v"(Pc[1][1][1]));
+    };
+    // exps (current m) and P of every element of S (first tile, rare path)
+    auto expo_cvt_all = [&](i32x4 (&Pc)[2][2][2]) __attribute__((always_inline)) {
+        sfor<16>([&](auto I) {
+            constexpr int i = I;
+            constexpr int tt = i / 8, r = 2 * (i % 8), s2 = (i % 8) / 4, j = i % 4;
+#pragma unroll
+            for (int X = 0; X < 2; ++X) {
+                const float m = X == 0 ? mA : mB;
+                const v12f2 y = __builtin_elementwise_fma(v12f2{S[X][tt][r], S[X][tt][r + 1]}, v12f2{c, c},
+                                                          v12f2{-m, -m});
+                Pc[X][tt][s2][j] = (int)pack2<bf16_t>(__builtin_amdgcn_exp2f(y.x), __builtin_amdgcn_exp2f(y.y));
+            }
+        });
+    };
+
+    // phase Q: S(t) = K(t) Q^T from the AGPR fragments, block A's chain first;
+    // beside block B's chain, block A's softmax slices (SM)
+    auto phaseQ = [&](i32x4 (&Pc)[2][2][2], auto sm_tag) __attribute__((always_inline)) {
+        constexpr bool SM = decltype(sm_tag)::value;
+        sfor<16>([&](auto FF) { v12::qk1<FF, 0>(S[0][FF / 8]); });
+        asm volatile("s_nop 7\n\ts_nop 4" : "+v"(S[0][0]), "+v"(S[0][1]));
+        mxA = -INFINITY;
+        sfor<16>([&](auto FF) {
+            v12::qk1<FF, 1>(S[1][FF / 8]);
+            if constexpr (SM) slice(std::integral_constant<int, 0>{}, FF, Pc);
+            __builtin_amdgcn_sched_barrier(0);
+        });
+        asm volatile("s_nop 7\n\ts_nop 4" : "+v"(S[1][0]), "+v"(S[1][1]));
+    };
+
+    // phase P: PV of the tile in slot sv with Pv (PV); beside it block B's
+    // softmax slices into Pc (SM) and the K fragments of the tile in slot sk
+    // into AGPR (KR)
+    auto phaseP = [&](int sv, i32x4 (&Pv)[2][2][2], i32x4 (&Pc)[2][2][2], int sk, auto pv_tag, auto sm_tag,
+                      auto kr_tag) __attribute__((always_inline)) {
+        constexpr bool PV = decltype(pv_tag)::value, SM = decltype(sm_tag)::value, KR = decltype(kr_tag)::value;
+        const uint32_t vs = (uint32_t)sv * BUFB, ks = (uint32_t)sk * BUFB;
+        mxB = -INFINITY;
+        V12Frag vf[2];
+        if constexpr (PV) v12_vread<0>(vf[0], valo[0] + vs, vahi[0] + vs);
+        sfor<16>([&](auto II) {
+            constexpr int i = II;
+            constexpr int db = i / 4, tt = (i / 2) & 1, s2 = i & 1;
+            if constexpr (PV && i + 1 < 16) {
+                constexpr int i1 = i + 1, db1 = i1 / 4, tt1 = (i1 / 2) & 1, s21 = i1 & 1;
+                v12_vread<(tt1 * 32 + 16 * s21) * 256>(vf[i1 & 1], valo[db1] + vs, vahi[db1] + vs);
+            }
+            if constexpr (KR) v12::kread<i>(kaddr[i % 8] + ks);
+            if constexpr (PV) {
+                constexpr int N = (i < 15 ? 2 : 0) + (KR ? ((i >= 1 ? 1 : 0) + 1) : 0);
+                v12_vwait<N>(vf[i & 1]);
+                const V12Frag& f = vf[i & 1];
+                v12::pv2<db>(i32x4{f.lo.x, f.lo.y, f.hi.x, f.hi.y}, Pv[0][tt][s2], Pv[1][tt][s2]);
+            }
+            if constexpr (SM) slice(std::integral_constant<int, 1>{}, II, Pc);
+            __builtin_amdgcn_sched_barrier(0);
+        });
+        if constexpr (PV) {
+            v12_sel4(lA, sel, Pv[0][0][0], Pv[0][0][1], Pv[0][1][0], Pv[0][1][1]);
+            v12_sel4(lB, sel, Pv[1][0][0], Pv[1][0][1], Pv[1][1][0], Pv[1][1][1]);
+        }
+        if constexpr (SM) {
+            mxA = v12_xor32_max(mxA);
+            mxB = v12_xor32_max(mxB);
+        }
+    };
+
+    // defer-max decision for the tile in S (rare path: drain, rescale O and
+    // l, recompute S from the LDS copy of K in slot sk, redo exps and P)
+    auto settle = [&](i32x4 (&Pc)[2][2][2], int sk) __attribute__((always_inline)) {
+        const bool upA = mxA * c > mA + V12_THR, upB = mxB * c > mB + V12_THR;
+        if (__ballot(upA || upB)) {
+            asm volatile("s_nop 7\n\ts_nop 7" : "+v"(lA), "+v"(lB));
+            const float nA = upA ? mxA * c : mA, nB = upB ? mxB * c : mB;
+            const float alA = __builtin_amdgcn_exp2f(mA - nA), alB = __builtin_amdgcn_exp2f(mB - nB);
+            mA = nA;
+            mB = nB;
+            v12::o_scale(alA, alB);
+            lA[0] *= alA;
+            lB[0] *= alB;
+            const char* kb = smem + sk * BUFB;
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt)
+                sfor<8>([&](auto KK) {
+                    const i32x4 kf = lds_read_b128(kb, (A0 ^ (KK << 5)) + tt * 8192);
+                    v12::qk_v<0, KK>(S[0][tt], kf);
+                    v12::qk_v<1, KK>(S[1][tt], kf);
+                });
+            v12_sfence(S);
+            expo_cvt_all(Pc);
+            pfence(Pc);
+        }
+    };
+
+    if (nt <= 0) return;  // host guarantees Nk >= 64
+    // ---- prologue: tiles 0 and 1 in flight, K(0) fragments, S(0), softmax(0)
+    dma_tile(0, 0);
+    if (nt > 1) dma_tile(1, 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    sfor<16>([&](auto FF) { v12::kread<FF>(kaddr[FF % 8]); });
+    lgkm<0>();
+    phaseQ(P0, std::false_type{});
+    if (nt > 2) dma_tile(2, 2);
+    if (nt > 1) phaseP(0, P1, P1, 1, std::false_type{}, std::false_type{}, std::true_type{});
+    {   // first tile: the max decides m before any exp
+        mxA = -INFINITY;
+        mxB = -INFINITY;
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) {
+                mxA = max3(mxA, S[0][tt][r], S[0][tt][r + 1]);
+                mxB = max3(mxB, S[1][tt][r], S[1][tt][r + 1]);
+            }
+        mxA = v12_xor32_max(mxA);
+        mxB = v12_xor32_max(mxB);
+        mA = mxA == -INFINITY ? -1e30f : mxA * c;
+        mB = mxB == -INFINITY ? -1e30f : mxB * c;
+        expo_cvt_all(P0);
+        pfence(P0);
+    }
+
+    // tile t: S(t) and P(t) in Pc = P(t&1); PV of tile t-1 from Pv
+    auto step = [&](int t, i32x4 (&Pc)[2][2][2], i32x4 (&Pv)[2][2][2]) __attribute__((always_inline)) {
+        lgkm<0>();  // K(t) fragments in AGPR
+        phaseQ(Pc, std::true_type{});
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t+1 (issued one step ago)
+        __syncthreads();
+        if (t + 2 < nt) dma_tile(t + 2, (t + 2) & 3);
+        asm volatile("s_nop 1" ::: "memory");  // P just written -> MFMA operands
+        if (t + 1 < nt)
+            phaseP((t - 1) & 3, Pv, Pc, (t + 1) & 3, std::true_type{}, std::true_type{}, std::true_type{});
+        else
+            phaseP((t - 1) & 3, Pv, Pc, 0, std::true_type{}, std::true_type{}, std::false_type{});
+        settle(Pc, t & 3);
+    };
+    int t = 1;
+    for (; t + 1 < nt; t += 2) {
+        step(t, P1, P0);
+        step(t + 1, P0, P1);
+    }
+    if (t < nt) step(t, P1, P0);
+
+    // ---- epilogue: PV of the last tile, l, O read-out and store
+    if ((nt - 1) & 1) pfence(P1);
+    else pfence(P0);
+    if ((nt - 1) & 1) phaseP((nt - 1) & 3, P1, P1, 0, std::true_type{}, std::false_type{}, std::false_type{});
+    else phaseP((nt - 1) & 3, P0, P0, 0, std::true_type{}, std::false_type{}, std::false_type{});
+    asm volatile("s_nop 15\n\ts_nop 7" : "+v"(lA), "+v"(lB));
+    const float invA = [&] { const float l = v12_xor32_sum(lA[0]); return l > 0.f ? 1.f / l : 0.f; }();
+    const float invB = [&] { const float l = v12_xor32_sum(lB[0]); return l > 0.f ? 1.f / l : 0.f; }();
+    auto store = [&](auto x_tag, float inv) __attribute__((always_inline)) {
+        constexpr int X = decltype(x_tag)::value;
+        const int qr = q0 + 32 * X + l32;
+        sfor<4>([&](auto DB) {
+            f32x16 a;
+            v12::o_read<X, DB>(a);
+            if (qr < Nq) {
+                uint16_t* op = o + b * st.ob + hq * st.oh + (int64_t)qr * st.on;
+#pragma unroll
+                for (int i = 0; i < 4; i += 2) {
+                    const uint32_t ax = pack2<bf16_t>(a[4 * i] * inv, a[4 * i + 1] * inv);
+                    const uint32_t ay = pack2<bf16_t>(a[4 * i + 2] * inv, a[4 * i + 3] * inv);
+                    const uint32_t bx = pack2<bf16_t>(a[4 * i + 4] * inv, a[4 * i + 5] * inv);
+                    const uint32_t by = pack2<bf16_t>(a[4 * i + 6] * inv, a[4 * i + 7] * inv);
+                    const auto rx = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
+                    const auto ry = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
+                    const int d = DB * 32 + 8 * i + 8 * h32;
+                    *reinterpret_cast<i32x4*>(op + d) = i32x4{(int)rx[0], (int)ry[0], (int)rx[1], (int)ry[1]};
+                }
+            }
+        });
+    };
+    store(std::integral_constant<int, 0>{}, invA);
+    store(std::integral_constant<int, 1>{}, invB);
+}
+
+}  // namespace
+
+bool attn_v12_ok(int D, int is_bf16, int causal, int Nk) {
+    return D == 128 && is_bf16 && !causal && Nk >= 64 && Nk % 64 == 0;
+}
+
+int launch_attn_v12(const void* q, const void* k, const void* v, void* o, int B, int H, int group, int Nq,
+                    int Nk, const V7Strides& st, float scale, hipStream_t stream) {
+    const int qblocks = cdiv(Nq, 256);
+    const int64_t nb = (int64_t)B * H * qblocks;
+    PLI_REQUIRE(nb < (1ll << 31), "pli_flash_attn_fwd: grid too large");
+    const float c = scale * 1.4426950408889634f;
+    hipLaunchKernelGGL(attn_fwd_v12, dim3((unsigned)nb), dim3(256), 0, stream, (const uint16_t*)q,
+                       (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, H, group, Nq, Nk, st, c, qblocks,
+                       (int)nb);
+    return hipGetLastError() == hipSuccess ? PLI_OK : PLI_EINVAL;
+}
+
+}  // namespace pli

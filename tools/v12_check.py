@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""GPU box: attn_fwd_v12 (flash variant 70) against variant 55 (bitwise) and
+a torch fp32 reference on small shapes, then an interleaved timing at the
+bench config.
+
+    python tools/v12_check.py
+"""
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "physics-llm-inference_amd"), ROOT]
+import pli_hip  # noqa: E402
+
+
+def ref(q, k, v):
+    g = q.shape[1] // k.shape[1]
+    kk = k.float().repeat_interleave(g, 1)
+    vv = v.float().repeat_interleave(g, 1)
+    s = q.float() @ kk.transpose(-1, -2) / q.shape[-1] ** 0.5
+    return torch.softmax(s, -1) @ vv
+
+
+gen = torch.Generator(device="cuda").manual_seed(5)
+cases = [(1, 1, 1, 256, 64), (1, 2, 2, 256, 256), (2, 4, 4, 512, 512), (1, 8, 2, 1024, 1024),
+         (1, 2, 2, 300, 512), (1, 2, 2, 256, 1024), (2, 4, 1, 2048, 192), (1, 4, 4, 4096, 4096)]
+ok = True
+for (B, H, Hkv, Nq, Nk) in cases:
+    q = torch.randn(B, H, Nq, 128, device="cuda", dtype=torch.bfloat16, generator=gen)
+    k = torch.randn(B, Hkv, Nk, 128, device="cuda", dtype=torch.bfloat16, generator=gen)
+    v = torch.randn(B, Hkv, Nk, 128, device="cuda", dtype=torch.bfloat16, generator=gen)
+    if Nq == 2048:  # large scores: exercises the defer-max rescale path
+        q = q * 4
+    a = pli_hip.flash_attn_fwd(q, k, v, variant=55)
+    b = pli_hip.flash_attn_fwd(q, k, v, variant=70)
+    torch.cuda.synchronize()
+    same = bool(torch.equal(a, b))
+    err = (b.float() - ref(q, k, v)).abs().max().item()
+    nan = bool(torch.isnan(b).any())
+    ok &= same and not nan
+    if not same:
+        d = (a.float() - b.float()).abs()  # [B, H, Nq, 128]
+        rows = d.amax(dim=(0, 1, 3))[: min(Nq, 256)]
+        rmod = [round(rows[i::64].max().item(), 3) for i in range(64)]
+        cols = [round(d.amax(dim=(0, 1, 2))[j * 8:(j + 1) * 8].max().item(), 3) for j in range(16)]
+        print(json.dumps({"row_mod64_maxdiff": rmod, "col8_maxdiff": cols}), flush=True)
+    print(json.dumps({"case": [B, H, Hkv, Nq, Nk], "bitwise_eq_v55": same, "max_err_vs_fp32": err,
+                      "max_diff_v55": (a.float() - b.float()).abs().max().item(), "nan": nan}), flush=True)
+
+if ok or os.environ.get("V12_TIME"):
+    B, H, S, D = 8, 32, 4096, 128
+    q, k, v = (torch.randn(B, H, S, D, device="cuda", dtype=torch.bfloat16, generator=gen) for _ in range(3))
+    o = torch.empty_like(q)
+    flops = 4 * B * H * S * S * D
+    res = {55: [], 70: []}
+    for var in (55, 70):
+        for _ in range(3):
+            pli_hip.flash_attn_fwd(q, k, v, out=o, variant=var)
+    for _ in range(5):
+        for var in (55, 70):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(10):
+                pli_hip.flash_attn_fwd(q, k, v, out=o, variant=var)
+            e.record()
+            e.synchronize()
+            res[var].append(s.elapsed_time(e) / 10)
+    for var, ts in res.items():
+        ms = sorted(ts)[len(ts) // 2]
+        print(json.dumps({"variant": var, "ms_med": ms, "TFLOP/s": flops / ms / 1e9}), flush=True)
+print("ALL_OK" if ok else "MISMATCH", flush=True)
