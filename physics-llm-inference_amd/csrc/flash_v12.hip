@@ -69,6 +69,26 @@ template <int N> __device__ __forceinline__ void v12_vwait(V12Frag& f) {
 // only as the very next instruction; an s_nop between them lost a step's sum);
 // the leading s_nop covers a hipcc v_mov of l right before the statement, the
 // trailing ones a v_mov of the result right after it (4-pass XDL -> VALU)
+// LDS accesses issued after V^T fragment I's two reads by the time step I
+// waits for it: pre-loop reads V0..V(D-1); step s reads V(s+D) (if < 16) and
+// the K fragment s (if KR)
+template <int I, bool KR, int D> constexpr int v12_vwait_n() {
+    int n = 0;
+    bool after = false;
+    for (int v = 0; v < D; ++v) {
+        if (after) n += 2;
+        if (v == I) after = true;
+    }
+    for (int s = 0; s <= I; ++s) {
+        if (s + D < 16) {
+            if (after) n += 2;
+            if (s + D == I) after = true;
+        }
+        if (KR && after) n += 1;
+    }
+    return n;
+}
+
 __device__ __forceinline__ void v12_sel4(f32x4& l, i32x4 sel, i32x4 p0, i32x4 p1, i32x4 p2, i32x4 p3) {
     asm volatile("s_nop 2\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0\n\t"
                  "v_mfma_f32_16x16x32_bf16 %0, %1, %3, %0\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %4, %0\n\t"
@@ -93,6 +113,12 @@ __device__ __forceinline__ float v12_xor32_sum(float x) {
 typedef __attribute__((ext_vector_type(2))) float v12f2;
 constexpr float V12_THR = 8.f;
 
+#ifdef PLI_FLASH_STAMPS
+// diagnostic build only (tools/build_diag.sh): per-segment s_memtime sums
+__device__ unsigned long long g_v12_stamps[16];
+#endif
+
+template <bool STAMP = false>
 __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
     uint16_t* __restrict__ o, int H, int group, int Nq, int Nk, V7Strides st, float c, int qblocks,
@@ -111,6 +137,18 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     const uint16_t* kp = k + b * st.kb + hk * st.kh;
     const uint16_t* vp = v + b * st.vb + hk * st.vh;
     const int nt = Nk / KT;
+    unsigned long long st_sum[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0;
+    auto stamp = [&](int seg) __attribute__((always_inline)) {
+        if constexpr (STAMP) {
+            unsigned long long now;
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(now)::"memory");
+            __builtin_amdgcn_sched_barrier(0);
+            if (seg >= 0) st_sum[seg] += now - st_last;
+            st_last = now;
+        }
+    };
+    stamp(-1);
 
     // ---- LDS-DMA plan (attn_fwd_v10's, 4 waves: 4 K + 4 V pieces per wave)
     auto fsw = [](int row) __attribute__((always_inline)) { return ((row & 3) << 2) | ((row >> 2) & 3); };
@@ -140,7 +178,9 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         }
     };
 
-    // ---- Q^T fragments -> AGPR; O = 0
+    // ---- tiles 0 and 1 in flight first, then Q^T fragments -> AGPR; O = 0
+    if (nt > 0) dma_tile(0, 0);
+    if (nt > 1) dma_tile(1, 1);
     {
         const int ra = q0 + l32, rb = q0 + 32 + l32;
         const uint16_t* sa = qp + (int64_t)(ra < Nq ? ra : 0) * st.qn + 8 * h32;
@@ -201,6 +241,36 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         // the next tile's PV, where P is read
         asm volatile("" : "+v"(Pc[X][tt][s2]));
     };
+    // the same slice split into three stages run in consecutive MFMA gaps (one
+    // wave per SIMD: a dependent fma -> exp -> cvt chain inside one gap stalls
+    // on each result); ring of 6 slices
+    v12f2 sy[6], se[6];
+    auto st_fma = [&](auto x_tag, auto i_tag) __attribute__((always_inline)) {
+        constexpr int X = decltype(x_tag)::value, i = decltype(i_tag)::value;
+        if constexpr (i < 16) {
+            constexpr int tt = i / 8, r = 2 * (i % 8);
+            float& mx = X == 0 ? mxA : mxB;
+            const float m = X == 0 ? mA : mB;
+            mx = max3(mx, S[X][tt][r], S[X][tt][r + 1]);
+            sy[i % 6] = __builtin_elementwise_fma(v12f2{S[X][tt][r], S[X][tt][r + 1]}, v12f2{c, c}, v12f2{-m, -m});
+            asm volatile("" : "+v"(sy[i % 6]));
+        }
+    };
+    auto st_exp = [&](auto i_tag) __attribute__((always_inline)) {
+        constexpr int i = decltype(i_tag)::value;
+        if constexpr (i >= 0 && i < 16) {
+            se[i % 6] = v12f2{__builtin_amdgcn_exp2f(sy[i % 6].x), __builtin_amdgcn_exp2f(sy[i % 6].y)};
+            asm volatile("" : "+v"(se[i % 6]));
+        }
+    };
+    auto st_cvt = [&](auto x_tag, auto i_tag, i32x4 (&Pc)[2][2][2]) __attribute__((always_inline)) {
+        constexpr int X = decltype(x_tag)::value, i = decltype(i_tag)::value;
+        if constexpr (i >= 0 && i < 16) {
+            constexpr int tt = i / 8, s2 = (i % 8) / 4, j = i % 4;
+            Pc[X][tt][s2][j] = (int)pack2<bf16_t>(se[i % 6].x, se[i % 6].y);
+            asm volatile("" : "+v"(Pc[X][tt][s2]));
+        }
+    };
     // VALU-written P -> MFMA operands: pin P here and pad
     auto pfence = [&](i32x4 (&Pc)[2][2][2]) __attribute__((always_inline)) {
         asm volatile("s_nop 1" : "+v"(Pc[0][0][0]), "+v"(Pc[0][0][1]), "+v"(Pc[0][1][0]), "+v"(Pc[0][1][1]),
@@ -221,48 +291,95 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         });
     };
 
-    // phase Q: S(t) = K(t) Q^T from the AGPR fragments, block A's chain first;
-    // beside block B's chain, block A's softmax slices (SM)
+    // phase Q: S(t) = K(t) Q^T from the AGPR fragments.  Every accumulator
+    // chain runs back to back in MFMA order (the next MFMA takes the previous
+    // result as C without a stall; VALU between them is fine, another MFMA is
+    // not).  Block A's two chains first, no VALU; beside block B's two chains,
+    // block A's softmax slices, one per MFMA, in three stages (fma, exp, cvt)
+    // one MFMA apart (one wave per SIMD: nothing else hides a dependent chain)
     auto phaseQ = [&](i32x4 (&Pc)[2][2][2], auto sm_tag) __attribute__((always_inline)) {
         constexpr bool SM = decltype(sm_tag)::value;
-        sfor<16>([&](auto FF) { v12::qk1<FF, 0>(S[0][FF / 8]); });
+        v12::qk_chain<0, 0>(S[0][0]);
+        v12::qk_chain<0, 1>(S[0][1]);
         asm volatile("s_nop 7\n\ts_nop 4" : "+v"(S[0][0]), "+v"(S[0][1]));
+#ifdef V12_EXP_ACHAIN
+        stamp(0);
+#endif
         mxA = -INFINITY;
+        using X0 = std::integral_constant<int, 0>;
+        if constexpr (SM) st_fma(X0{}, std::integral_constant<int, 0>{});
         sfor<16>([&](auto FF) {
-            v12::qk1<FF, 1>(S[1][FF / 8]);
-            if constexpr (SM) slice(std::integral_constant<int, 0>{}, FF, Pc);
+            constexpr int F = FF;
+            v12::qk1<F, 1>(S[1][F / 8]);
+            if constexpr (SM) {
+                st_fma(X0{}, std::integral_constant<int, F + 1>{});
+                st_exp(std::integral_constant<int, F>{});
+                st_cvt(X0{}, std::integral_constant<int, F - 1>{}, Pc);
+            }
             __builtin_amdgcn_sched_barrier(0);
         });
+        if constexpr (SM) st_cvt(X0{}, std::integral_constant<int, 15>{}, Pc);
         asm volatile("s_nop 7\n\ts_nop 4" : "+v"(S[1][0]), "+v"(S[1][1]));
     };
 
-    // phase P: PV of the tile in slot sv with Pv (PV); beside it block B's
-    // softmax slices into Pc (SM) and the K fragments of the tile in slot sk
-    // into AGPR (KR)
-    auto phaseP = [&](int sv, i32x4 (&Pv)[2][2][2], i32x4 (&Pc)[2][2][2], int sk, auto pv_tag, auto sm_tag,
-                      auto kr_tag) __attribute__((always_inline)) {
+    // phase P: PV of the tile in slot sv with Pv (PV) as 8 accumulator chains
+    // of 4 (d-block major: O_A[db] then O_B[db], sharing db's 4 V^T fragments,
+    // the next d-block's fragments read under the current chains); beside them
+    // block B's softmax slices into Pc (SM, one stage per MFMA) and the K
+    // fragments of the tile in slot sk into AGPR (KR, 4 per d-block)
+    auto phaseP = [&](int sv, i32x4 (&Pv)[2][2][2], i32x4 (&Pc)[2][2][2], int sk, int dt, int ds, auto pv_tag,
+                      auto sm_tag, auto kr_tag, auto dma_tag) __attribute__((always_inline)) {
         constexpr bool PV = decltype(pv_tag)::value, SM = decltype(sm_tag)::value, KR = decltype(kr_tag)::value;
+        (void)dt;
+        (void)ds;
+        (void)dma_tag;
         const uint32_t vs = (uint32_t)sv * BUFB, ks = (uint32_t)sk * BUFB;
         mxB = -INFINITY;
-        V12Frag vf[2];
-        if constexpr (PV) v12_vread<0>(vf[0], valo[0] + vs, vahi[0] + vs);
-        sfor<16>([&](auto II) {
-            constexpr int i = II;
-            constexpr int db = i / 4, tt = (i / 2) & 1, s2 = i & 1;
-            if constexpr (PV && i + 1 < 16) {
-                constexpr int i1 = i + 1, db1 = i1 / 4, tt1 = (i1 / 2) & 1, s21 = i1 & 1;
-                v12_vread<(tt1 * 32 + 16 * s21) * 256>(vf[i1 & 1], valo[db1] + vs, vahi[db1] + vs);
-            }
-            if constexpr (KR) v12::kread<i>(kaddr[i % 8] + ks);
+        V12Frag vf[2][4];
+        using X1 = std::integral_constant<int, 1>;
+        auto vreads = [&](auto db_tag) __attribute__((always_inline)) {
+            constexpr int db = decltype(db_tag)::value;
+            sfor<4>([&](auto KS) {
+                constexpr int k = KS;
+                v12_vread<((k / 2) * 32 + 16 * (k & 1)) * 256>(vf[db & 1][k], valo[db] + vs, vahi[db] + vs);
+            });
+        };
+        if constexpr (PV) vreads(std::integral_constant<int, 0>{});
+        sfor<4>([&](auto DBB) {
+            constexpr int db = DBB;
             if constexpr (PV) {
-                constexpr int N = (i < 15 ? 2 : 0) + (KR ? ((i >= 1 ? 1 : 0) + 1) : 0);
-                v12_vwait<N>(vf[i & 1]);
-                const V12Frag& f = vf[i & 1];
-                v12::pv2<db>(i32x4{f.lo.x, f.lo.y, f.hi.x, f.hi.y}, Pv[0][tt][s2], Pv[1][tt][s2]);
+                if constexpr (db + 1 < 4) vreads(std::integral_constant<int, db + 1>{});
+                constexpr int N = (db + 1 < 4 ? 8 : 0) + (KR && db > 0 ? 4 : 0);
+                V12Frag* f = vf[db & 1];
+                asm volatile("s_waitcnt lgkmcnt(%8)"
+                             : "+v"(f[0].lo), "+v"(f[0].hi), "+v"(f[1].lo), "+v"(f[1].hi), "+v"(f[2].lo),
+                               "+v"(f[2].hi), "+v"(f[3].lo), "+v"(f[3].hi)
+                             : "n"(N) : "memory");
             }
-            if constexpr (SM) slice(std::integral_constant<int, 1>{}, II, Pc);
-            __builtin_amdgcn_sched_barrier(0);
+            sfor<8>([&](auto JJ) {
+                constexpr int j = JJ, X = j / 4, k = j % 4, slot = 8 * db + j;
+                if constexpr (KR && X == 0) v12::kread<4 * db + k>(kaddr[(4 * db + k) % 8] + ks);
+                if constexpr (PV) {
+                    const V12Frag& ff = vf[db & 1][k];
+                    v12::pv1<X, db>(i32x4{ff.lo.x, ff.lo.y, ff.hi.x, ff.hi.y}, Pv[X][k / 2][k & 1]);
+                }
+#ifndef V12_EXP_NOSM
+                if constexpr (SM) {
+                    // slice s: fma at slot 2s, exp at 2s+1, cvt at 2s+2
+                    if constexpr ((slot & 1) == 0) {
+                        st_fma(X1{}, std::integral_constant<int, slot / 2>{});
+                        st_cvt(X1{}, std::integral_constant<int, slot / 2 - 1>{}, Pc);
+                    } else {
+                        st_exp(std::integral_constant<int, slot / 2>{});
+                    }
+                }
+#endif
+                __builtin_amdgcn_sched_barrier(0);
+            });
         });
+#ifndef V12_EXP_NOSM
+        if constexpr (SM) st_cvt(X1{}, std::integral_constant<int, 15>{}, Pc);
+#endif
         if constexpr (PV) {
             v12_sel4(lA, sel, Pv[0][0][0], Pv[0][0][1], Pv[0][1][0], Pv[0][1][1]);
             v12_sel4(lB, sel, Pv[1][0][0], Pv[1][0][1], Pv[1][1][0], Pv[1][1][1]);
@@ -301,16 +418,14 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     };
 
     if (nt <= 0) return;  // host guarantees Nk >= 64
-    // ---- prologue: tiles 0 and 1 in flight, K(0) fragments, S(0), softmax(0)
-    dma_tile(0, 0);
-    if (nt > 1) dma_tile(1, 1);
+    // ---- prologue: tiles 0 and 1 landed, K(0) fragments, S(0), softmax(0)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     sfor<16>([&](auto FF) { v12::kread<FF>(kaddr[FF % 8]); });
     lgkm<0>();
     phaseQ(P0, std::false_type{});
     if (nt > 2) dma_tile(2, 2);
-    if (nt > 1) phaseP(0, P1, P1, 1, std::false_type{}, std::false_type{}, std::true_type{});
+    if (nt > 1) phaseP(0, P1, P1, 1, 0, 0, std::false_type{}, std::false_type{}, std::true_type{}, std::false_type{});
     {   // first tile: the max decides m before any exp
         mxA = -INFINITY;
         mxB = -INFINITY;
@@ -331,18 +446,28 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
 
     // tile t: S(t) and P(t) in Pc = P(t&1); PV of tile t-1 from Pv
     auto step = [&](int t, i32x4 (&Pc)[2][2][2], i32x4 (&Pv)[2][2][2]) __attribute__((always_inline)) {
+        stamp(6);
         lgkm<0>();  // K(t) fragments in AGPR
+#ifndef V12_EXP_ACHAIN
+        stamp(0);
+#endif
         phaseQ(Pc, std::true_type{});
+        stamp(1);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t+1 (issued one step ago)
+        stamp(2);
         __syncthreads();
+        stamp(3);
         if (t + 2 < nt) dma_tile(t + 2, (t + 2) & 3);
         asm volatile("s_nop 1" ::: "memory");  // P just written -> MFMA operands
         if (t + 1 < nt)
-            phaseP((t - 1) & 3, Pv, Pc, (t + 1) & 3, std::true_type{}, std::true_type{}, std::true_type{});
+            phaseP((t - 1) & 3, Pv, Pc, (t + 1) & 3, 0, 0, std::true_type{}, std::true_type{}, std::true_type{}, std::false_type{});
         else
-            phaseP((t - 1) & 3, Pv, Pc, 0, std::true_type{}, std::true_type{}, std::false_type{});
+            phaseP((t - 1) & 3, Pv, Pc, 0, 0, 0, std::true_type{}, std::true_type{}, std::false_type{}, std::false_type{});
+        stamp(4);
         settle(Pc, t & 3);
+        stamp(5);
     };
+    stamp(6);
     int t = 1;
     for (; t + 1 < nt; t += 2) {
         step(t, P1, P0);
@@ -353,8 +478,8 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     // ---- epilogue: PV of the last tile, l, O read-out and store
     if ((nt - 1) & 1) pfence(P1);
     else pfence(P0);
-    if ((nt - 1) & 1) phaseP((nt - 1) & 3, P1, P1, 0, std::true_type{}, std::false_type{}, std::false_type{});
-    else phaseP((nt - 1) & 3, P0, P0, 0, std::true_type{}, std::false_type{}, std::false_type{});
+    if ((nt - 1) & 1) phaseP((nt - 1) & 3, P1, P1, 0, 0, 0, std::true_type{}, std::false_type{}, std::false_type{}, std::false_type{});
+    else phaseP((nt - 1) & 3, P0, P0, 0, 0, 0, std::true_type{}, std::false_type{}, std::false_type{}, std::false_type{});
     asm volatile("s_nop 15\n\ts_nop 7" : "+v"(lA), "+v"(lB));
     const float invA = [&] { const float l = v12_xor32_sum(lA[0]); return l > 0.f ? 1.f / l : 0.f; }();
     const float invB = [&] { const float l = v12_xor32_sum(lB[0]); return l > 0.f ? 1.f / l : 0.f; }();
@@ -382,6 +507,17 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     };
     store(std::integral_constant<int, 0>{}, invA);
     store(std::integral_constant<int, 1>{}, invB);
+#ifdef PLI_FLASH_STAMPS
+    if constexpr (STAMP) {
+        stamp(7);
+        if (lane == 0) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) atomicAdd(&g_v12_stamps[i], st_sum[i]);
+            atomicAdd(&g_v12_stamps[8], (unsigned long long)nt);
+            atomicAdd(&g_v12_stamps[9], 1ull);
+        }
+    }
+#endif
 }
 
 }  // namespace
@@ -396,10 +532,32 @@ int launch_attn_v12(const void* q, const void* k, const void* v, void* o, int B,
     const int64_t nb = (int64_t)B * H * qblocks;
     PLI_REQUIRE(nb < (1ll << 31), "pli_flash_attn_fwd: grid too large");
     const float c = scale * 1.4426950408889634f;
-    hipLaunchKernelGGL(attn_fwd_v12, dim3((unsigned)nb), dim3(256), 0, stream, (const uint16_t*)q,
+    hipLaunchKernelGGL(attn_fwd_v12<false>, dim3((unsigned)nb), dim3(256), 0, stream, (const uint16_t*)q,
                        (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, H, group, Nq, Nk, st, c, qblocks,
                        (int)nb);
     return hipGetLastError() == hipSuccess ? PLI_OK : PLI_EINVAL;
 }
 
 }  // namespace pli
+
+#ifdef PLI_FLASH_STAMPS
+// Diagnostic entry (tools/libpli_diag.so only): one stamped launch of
+// attn_fwd_v12 on contiguous [B,H,N,128] bf16, the 16 stamp words to `out`
+// (0 K-fragment wait, 1 phase Q, 2 DMA wait, 3 barrier, 4 phase P, 5 defer-max
+// check, 6 prologue + loop overhead, 7 epilogue; 8 tiles, 9 waves).
+extern "C" int pli_diag_v12_stamps(const void* q, const void* k, const void* v, void* o, int B, int H, int N,
+                                   unsigned long long* out) {
+    using namespace pli;
+    const int64_t sn = 128, sh = (int64_t)N * 128, sb = (int64_t)H * N * 128;
+    const V7Strides st{sb, sh, sn, sb, sh, sn, sb, sh, sn, sb, sh, sn};
+    const int qblocks = cdiv(N, 256), nb = B * H * qblocks;
+    const float c = (1.f / sqrtf(128.f)) * 1.4426950408889634f;
+    unsigned long long zero[16] = {0};
+    hipMemcpyToSymbol(HIP_SYMBOL(g_v12_stamps), zero, sizeof(zero));
+    hipLaunchKernelGGL(attn_fwd_v12<true>, dim3(nb), dim3(256), 0, 0, (const uint16_t*)q, (const uint16_t*)k,
+                       (const uint16_t*)v, (uint16_t*)o, H, 1, N, N, st, c, qblocks, nb);
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    hipMemcpyFromSymbol(out, HIP_SYMBOL(g_v12_stamps), 16 * sizeof(unsigned long long));
+    return 0;
+}
+#endif

@@ -6,5 +6,6 @@ set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 C=$R/physics-llm-inference_amd/csrc
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -fno-honor-nans -DPLI_FLASH_STAMPS \
-    -I$R/include -I$C -shared $C/flash_v7.hip $R/tools/diag/gemv_diag.hip $C/capi.cpp -o $R/tools/libpli_diag.so
+    ${DIAG_FLAGS:-} -I$R/include -I$C -shared $C/flash_v7.hip $C/flash_v12.hip $R/tools/diag/gemv_diag.hip $C/capi.cpp \
+    -o ${DIAG_OUT:-$R/tools/libpli_diag.so}
 echo "built $R/tools/libpli_diag.so"
