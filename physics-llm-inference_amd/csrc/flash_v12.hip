@@ -112,6 +112,15 @@ __device__ __forceinline__ float v12_xor32_sum(float x) {
 
 typedef __attribute__((ext_vector_type(2))) float v12f2;
 constexpr float V12_THR = 8.f;
+#ifndef V12_VPRE
+#define V12_VPRE 1
+#endif
+#ifndef V12_CVEVEN
+#define V12_CVEVEN 0
+#endif
+#ifndef V12_KEARLY
+#define V12_KEARLY 0
+#endif
 
 #ifdef PLI_FLASH_STAMPS
 // diagnostic build only (tools/build_diag.sh): per-segment s_memtime sums
@@ -123,7 +132,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
     uint16_t* __restrict__ o, int H, int group, int Nq, int Nk, V7Strides st, float c, int qblocks,
     int nblocks) {
-    constexpr int KT = 64, IMG = KT * 256, BUFB = 2 * IMG, NBUF = 4, PPW = 4;
+    constexpr int KT = 64, IMG = KT * 256, BUFB = 2 * IMG, NBUF = 5, PPW = 4;
     __shared__ __attribute__((aligned(1024))) char smem[NBUF * BUFB];
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -222,53 +231,65 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     // hipcc does not know the row-sum asm MFMAs read l as C: materialise the
     // zeros here, wait states after (VALU write -> MFMA source)
     asm volatile("s_nop 2" : "+v"(lA), "+v"(lB));
-    f32x16 S[2][2];               // [block][key half]: one tile's scores / exps
+    f32x16 S[2][2];               // [block][key half]: one tile's scores
     i32x4 P0[2][2][2], P1[2][2][2];  // [block][key half][16-key step]; tile t in P(t&1)
     float mxA = -INFINITY, mxB = -INFINITY;
 
-    // one softmax slice of block X: elements 2i, 2i+1 -- running max, the
-    // speculative exps with the current m, the packed bf16 pair into P
-    auto slice = [&](auto x_tag, auto i_tag, i32x4 (&Pc)[2][2][2]) __attribute__((always_inline)) {
-        constexpr int X = decltype(x_tag)::value, i = decltype(i_tag)::value;
-        constexpr int tt = i / 8, r = 2 * (i % 8), s2 = (i % 8) / 4, j = i % 4;
+    // ---- softmax slice i (elements 2i, 2i+1 of a lane's row) of block X as
+    // five single-issue stages placed one by one into MFMA gaps: MX (running
+    // max), FM (two v_fma_f32: s*c - m; v_pk_fma_f32 costs ~22 cycles more
+    // beside an MFMA), E0 / E1 (one v_exp_f32 each: at most one 8-cycle
+    // instruction per gap), CV (packed bf16 pair into P).  Each result is
+    // pinned where it is made (an empty volatile asm), or hipcc sinks the
+    // exps to their use in the next tile's PV.
+    v12f2 sy[2][4], se[2][4];
+    auto opMX = [&](auto x_tag, auto i_tag) __attribute__((always_inline)) {
+        constexpr int X = decltype(x_tag)::value, i = decltype(i_tag)::value, tt = i / 8, r = 2 * (i % 8);
         float& mx = X == 0 ? mxA : mxB;
-        const float m = X == 0 ? mA : mB;
         mx = max3(mx, S[X][tt][r], S[X][tt][r + 1]);
-        const v12f2 y = __builtin_elementwise_fma(v12f2{S[X][tt][r], S[X][tt][r + 1]}, v12f2{c, c}, v12f2{-m, -m});
-        const float e0 = __builtin_amdgcn_exp2f(y.x), e1 = __builtin_amdgcn_exp2f(y.y);
-        Pc[X][tt][s2][j] = (int)pack2<bf16_t>(e0, e1);
-        // pin the exps here: without a use at this point hipcc sinks them to
-        // the next tile's PV, where P is read
+        asm volatile("" : "+v"(mx));
+    };
+    auto opFM = [&](auto x_tag, auto i_tag) __attribute__((always_inline)) {
+        constexpr int X = decltype(x_tag)::value, i = decltype(i_tag)::value, tt = i / 8, r = 2 * (i % 8);
+        const float m = X == 0 ? mA : mB;
+        const float s0 = S[X][tt][r], s1 = S[X][tt][r + 1], cc = c;
+        float y0, y1;
+        asm volatile("v_fma_f32 %0, %2, %4, -%5\n\tv_fma_f32 %1, %3, %4, -%5"
+                     : "=&v"(y0), "=&v"(y1) : "v"(s0), "v"(s1), "v"(cc), "v"(m));
+        sy[X][i % 4] = v12f2{y0, y1};
+    };
+    auto opE = [&](auto x_tag, auto i_tag, auto h_tag) __attribute__((always_inline)) {
+        constexpr int X = decltype(x_tag)::value, i = decltype(i_tag)::value, h = decltype(h_tag)::value;
+        if constexpr (h == 0) {
+            se[X][i % 4].x = __builtin_amdgcn_exp2f(sy[X][i % 4].x);
+            asm volatile("" : "+v"(se[X][i % 4].x));
+        } else {
+            se[X][i % 4].y = __builtin_amdgcn_exp2f(sy[X][i % 4].y);
+            asm volatile("" : "+v"(se[X][i % 4].y));
+        }
+    };
+    auto opCV = [&](auto x_tag, auto i_tag, i32x4 (&Pc)[2][2][2]) __attribute__((always_inline)) {
+        constexpr int X = decltype(x_tag)::value, i = decltype(i_tag)::value;
+        constexpr int tt = i / 8, s2 = (i % 8) / 4, j = i % 4;
+        Pc[X][tt][s2][j] = (int)pack2<bf16_t>(se[X][i % 4].x, se[X][i % 4].y);
         asm volatile("" : "+v"(Pc[X][tt][s2]));
     };
-    // the same slice split into three stages run in consecutive MFMA gaps (one
-    // wave per SIMD: a dependent fma -> exp -> cvt chain inside one gap stalls
-    // on each result); ring of 6 slices
-    v12f2 sy[6], se[6];
-    auto st_fma = [&](auto x_tag, auto i_tag) __attribute__((always_inline)) {
-        constexpr int X = decltype(x_tag)::value, i = decltype(i_tag)::value;
-        if constexpr (i < 16) {
-            constexpr int tt = i / 8, r = 2 * (i % 8);
-            float& mx = X == 0 ? mxA : mxB;
-            const float m = X == 0 ? mA : mB;
-            mx = max3(mx, S[X][tt][r], S[X][tt][r + 1]);
-            sy[i % 6] = __builtin_elementwise_fma(v12f2{S[X][tt][r], S[X][tt][r + 1]}, v12f2{c, c}, v12f2{-m, -m});
-            asm volatile("" : "+v"(sy[i % 6]));
-        }
-    };
-    auto st_exp = [&](auto i_tag) __attribute__((always_inline)) {
-        constexpr int i = decltype(i_tag)::value;
-        if constexpr (i >= 0 && i < 16) {
-            se[i % 6] = v12f2{__builtin_amdgcn_exp2f(sy[i % 6].x), __builtin_amdgcn_exp2f(sy[i % 6].y)};
-            asm volatile("" : "+v"(se[i % 6]));
-        }
-    };
-    auto st_cvt = [&](auto x_tag, auto i_tag, i32x4 (&Pc)[2][2][2]) __attribute__((always_inline)) {
-        constexpr int X = decltype(x_tag)::value, i = decltype(i_tag)::value;
-        if constexpr (i >= 0 && i < 16) {
-            constexpr int tt = i / 8, s2 = (i % 8) / 4, j = i % 4;
-            Pc[X][tt][s2][j] = (int)pack2<bf16_t>(se[i % 6].x, se[i % 6].y);
-            asm volatile("" : "+v"(Pc[X][tt][s2]));
+    using X0 = std::integral_constant<int, 0>;
+    using X1 = std::integral_constant<int, 1>;
+    using H0 = std::integral_constant<int, 0>;
+    using H1 = std::integral_constant<int, 1>;
+    // slice stream: slice I0 + a over gaps 2a (FM, E0) and 2a + 1 (E1, CV of
+    // the slice before); gap g of the stream.  The CV of the stream's last
+    // slice is left to the caller.
+    auto stream = [&](auto x_tag, auto i0_tag, auto g_tag, i32x4 (&Pc)[2][2][2]) __attribute__((always_inline)) {
+        constexpr int g = decltype(g_tag)::value, I0 = decltype(i0_tag)::value, i = I0 + g / 2;
+        if constexpr (g % 2 == 0) {
+            opFM(x_tag, std::integral_constant<int, i>{});
+            if constexpr (V12_CVEVEN && g > 0) opCV(x_tag, std::integral_constant<int, i - 1>{}, Pc);
+            opE(x_tag, std::integral_constant<int, i>{}, H0{});
+        } else {
+            opE(x_tag, std::integral_constant<int, i>{}, H1{});
+            if constexpr (!V12_CVEVEN && g > 1) opCV(x_tag, std::integral_constant<int, i - 1>{}, Pc);
         }
     };
     // VALU-written P -> MFMA operands: pin P here and pad
@@ -290,66 +311,90 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
             }
         });
     };
+    // block B's slices 8..15 (key half 1) of a tile, no MFMAs (epilogue)
+    auto tailB = [&](i32x4 (&Pc)[2][2][2]) __attribute__((always_inline)) {
+        sfor<8>([&](auto A) {
+            constexpr int i = 8 + A;
+            opFM(X1{}, std::integral_constant<int, i>{});
+            opE(X1{}, std::integral_constant<int, i>{}, H0{});
+            opE(X1{}, std::integral_constant<int, i>{}, H1{});
+            opCV(X1{}, std::integral_constant<int, i>{}, Pc);
+        });
+    };
 
-    // phase Q: S(t) = K(t) Q^T from the AGPR fragments.  Every accumulator
-    // chain runs back to back in MFMA order (the next MFMA takes the previous
-    // result as C without a stall; VALU between them is fine, another MFMA is
-    // not).  Block A's two chains first, no VALU; beside block B's two chains,
-    // block A's softmax slices, one per MFMA, in three stages (fma, exp, cvt)
-    // one MFMA apart (one wave per SIMD: nothing else hides a dependent chain)
-    auto phaseQ = [&](i32x4 (&Pc)[2][2][2], auto sm_tag) __attribute__((always_inline)) {
+    // DMA piece j of a tile (even: K piece j/2, odd: V piece j/2)
+    auto dma_piece = [&](auto j_tag, const uint16_t* kt, const uint16_t* vt, uint32_t base) __attribute__((always_inline)) {
+        constexpr int j = decltype(j_tag)::value;
+        if constexpr (j % 2 == 0) dma(kt, koff[j / 2], base + (j / 2) * 1024);
+        else dma(vt, voff[j / 2], base + IMG + (j / 2) * 1024);
+    };
+
+    // phase QA: block A's QK^T chains (16 MFMAs); beside them block B's slices
+    // 8..15 of the previous tile (m already settled) into Pp, and the 8 DMA
+    // pieces of a tile two ahead (one per odd gap)
+    auto phaseQA = [&](i32x4 (&Pp)[2][2][2], auto sm_tag, const uint16_t* kt, const uint16_t* vt, uint32_t dbase)
+        __attribute__((always_inline)) {
         constexpr bool SM = decltype(sm_tag)::value;
-        v12::qk_chain<0, 0>(S[0][0]);
-        v12::qk_chain<0, 1>(S[0][1]);
-        asm volatile("s_nop 7\n\ts_nop 4" : "+v"(S[0][0]), "+v"(S[0][1]));
-#ifdef V12_EXP_ACHAIN
-        stamp(0);
-#endif
+        sfor<16>([&](auto FF) {
+            constexpr int F = FF;
+            v12::qk1<F, 0>(S[0][F / 8]);
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (SM) stream(X1{}, std::integral_constant<int, 8>{}, FF, Pp);
+            if constexpr (F % 2 == 1) dma_piece(std::integral_constant<int, F / 2>{}, kt, vt, dbase);
+            __builtin_amdgcn_sched_barrier(0);
+        });
+    };
+    // V^T fragments of d-block db of the tile at LDS byte offset vs: fragment
+    // k is two tr-reads
+    V12Frag vf[2][4];
+    auto vread1 = [&](auto db_tag, auto k_tag, uint32_t vs) __attribute__((always_inline)) {
+        constexpr int db = decltype(db_tag)::value, k = decltype(k_tag)::value;
+        v12_vread<((k / 2) * 32 + 16 * (k & 1)) * 256>(vf[db & 1][k], valo[db] + vs, vahi[db] + vs);
+    };
+    // phase QB: block B's QK^T chains (16 MFMAs); beside them the last P pair
+    // of phase QA, block A's slices 0..7 (key half 0, written 8 MFMAs ago),
+    // the running max over key half 1 (odd gaps) and (VR) the V^T d-block 0
+    // fragments of the tile in slot sv for the next phase P (gaps 1, 3, 5, 7)
+    auto phaseQB = [&](i32x4 (&Pp)[2][2][2], i32x4 (&Pc)[2][2][2], auto sm_tag, int sv) __attribute__((always_inline)) {
+        constexpr bool SM = decltype(sm_tag)::value;
+        const uint32_t vs = (uint32_t)sv * BUFB;
         mxA = -INFINITY;
-        using X0 = std::integral_constant<int, 0>;
-        if constexpr (SM) st_fma(X0{}, std::integral_constant<int, 0>{});
         sfor<16>([&](auto FF) {
             constexpr int F = FF;
             v12::qk1<F, 1>(S[1][F / 8]);
+            __builtin_amdgcn_sched_barrier(0);
             if constexpr (SM) {
-                st_fma(X0{}, std::integral_constant<int, F + 1>{});
-                st_exp(std::integral_constant<int, F>{});
-                st_cvt(X0{}, std::integral_constant<int, F - 1>{}, Pc);
+                if constexpr (F == 0) opCV(X1{}, std::integral_constant<int, 15>{}, Pp);
+                if constexpr (F % 2 == 0) opMX(X0{}, std::integral_constant<int, F / 2>{});
+                else opMX(X0{}, std::integral_constant<int, 8 + F / 2>{});
+                stream(X0{}, std::integral_constant<int, 0>{}, FF, Pc);
+                if constexpr (F % 2 == 1 && F < 8 && V12_VPRE)
+                    vread1(std::integral_constant<int, 0>{}, std::integral_constant<int, F / 2>{}, vs);
             }
             __builtin_amdgcn_sched_barrier(0);
         });
-        if constexpr (SM) st_cvt(X0{}, std::integral_constant<int, 15>{}, Pc);
-        asm volatile("s_nop 7\n\ts_nop 4" : "+v"(S[1][0]), "+v"(S[1][1]));
     };
 
     // phase P: PV of the tile in slot sv with Pv (PV) as 8 accumulator chains
     // of 4 (d-block major: O_A[db] then O_B[db], sharing db's 4 V^T fragments,
     // the next d-block's fragments read under the current chains); beside them
-    // block B's softmax slices into Pc (SM, one stage per MFMA) and the K
-    // fragments of the tile in slot sk into AGPR (KR, 4 per d-block)
-    auto phaseP = [&](int sv, i32x4 (&Pv)[2][2][2], i32x4 (&Pc)[2][2][2], int sk, int dt, int ds, auto pv_tag,
-                      auto sm_tag, auto kr_tag, auto dma_tag) __attribute__((always_inline)) {
+    // (SM) block A's slices 8..15, block B's running max and slices 0..7 into
+    // Pc, one stage per gap, and the K fragments of the tile in slot sk into
+    // AGPR (KR, 4 per d-block)
+    auto phaseP = [&](int sv, i32x4 (&Pv)[2][2][2], i32x4 (&Pc)[2][2][2], int sk, auto pv_tag,
+                      auto sm_tag, auto kr_tag, auto vpre_tag) __attribute__((always_inline)) {
         constexpr bool PV = decltype(pv_tag)::value, SM = decltype(sm_tag)::value, KR = decltype(kr_tag)::value;
-        (void)dt;
-        (void)ds;
-        (void)dma_tag;
+        constexpr bool VPRE = decltype(vpre_tag)::value;  // d-block 0 fragments already issued (phase QB)
         const uint32_t vs = (uint32_t)sv * BUFB, ks = (uint32_t)sk * BUFB;
         mxB = -INFINITY;
-        V12Frag vf[2][4];
-        using X1 = std::integral_constant<int, 1>;
-        auto vreads = [&](auto db_tag) __attribute__((always_inline)) {
-            constexpr int db = decltype(db_tag)::value;
-            sfor<4>([&](auto KS) {
-                constexpr int k = KS;
-                v12_vread<((k / 2) * 32 + 16 * (k & 1)) * 256>(vf[db & 1][k], valo[db] + vs, vahi[db] + vs);
-            });
-        };
-        if constexpr (PV) vreads(std::integral_constant<int, 0>{});
+        if constexpr (PV && !VPRE)
+            sfor<4>([&](auto KS) { vread1(std::integral_constant<int, 0>{}, KS, vs); });
         sfor<4>([&](auto DBB) {
             constexpr int db = DBB;
             if constexpr (PV) {
-                if constexpr (db + 1 < 4) vreads(std::integral_constant<int, db + 1>{});
-                constexpr int N = (db + 1 < 4 ? 8 : 0) + (KR && db > 0 ? 4 : 0);
+                // d-block db's 8 reads were issued before the K reads of the
+                // previous d-block's gaps 4..7
+                constexpr int N = (KR && db > 0 && !V12_KEARLY) ? 4 : 0;
                 V12Frag* f = vf[db & 1];
                 asm volatile("s_waitcnt lgkmcnt(%8)"
                              : "+v"(f[0].lo), "+v"(f[0].hi), "+v"(f[1].lo), "+v"(f[1].hi), "+v"(f[2].lo),
@@ -358,28 +403,30 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
             }
             sfor<8>([&](auto JJ) {
                 constexpr int j = JJ, X = j / 4, k = j % 4, slot = 8 * db + j;
-                if constexpr (KR && X == 0) v12::kread<4 * db + k>(kaddr[(4 * db + k) % 8] + ks);
                 if constexpr (PV) {
                     const V12Frag& ff = vf[db & 1][k];
                     v12::pv1<X, db>(i32x4{ff.lo.x, ff.lo.y, ff.hi.x, ff.hi.y}, Pv[X][k / 2][k & 1]);
                 }
-#ifndef V12_EXP_NOSM
+                __builtin_amdgcn_sched_barrier(0);
+                // gaps 0..3: the next d-block's fragment j; gaps 4..7: K fragment
+                if constexpr (PV && j < 4 && db + 1 < 4)
+                    vread1(std::integral_constant<int, db + 1>{}, std::integral_constant<int, j>{}, vs);
+                if constexpr (KR && (V12_KEARLY ? j < 4 : j >= 4))
+                    v12::kread<4 * db + (j & 3)>(kaddr[(4 * db + (j & 3)) % 8] + ks);
                 if constexpr (SM) {
-                    // slice s: fma at slot 2s, exp at 2s+1, cvt at 2s+2
-                    if constexpr ((slot & 1) == 0) {
-                        st_fma(X1{}, std::integral_constant<int, slot / 2>{});
-                        st_cvt(X1{}, std::integral_constant<int, slot / 2 - 1>{}, Pc);
+                    if constexpr (slot == 0) opCV(X0{}, std::integral_constant<int, 7>{}, Pc);
+                    if constexpr (slot % 2 == 1) opMX(X1{}, std::integral_constant<int, slot / 2>{});
+                    if constexpr (slot < 16) {
+                        stream(X0{}, std::integral_constant<int, 8>{}, std::integral_constant<int, slot>{}, Pc);
                     } else {
-                        st_exp(std::integral_constant<int, slot / 2>{});
+                        if constexpr (slot == 16) opCV(X0{}, std::integral_constant<int, 15>{}, Pc);
+                        stream(X1{}, std::integral_constant<int, 0>{}, std::integral_constant<int, slot - 16>{}, Pc);
                     }
                 }
-#endif
                 __builtin_amdgcn_sched_barrier(0);
             });
         });
-#ifndef V12_EXP_NOSM
-        if constexpr (SM) st_cvt(X1{}, std::integral_constant<int, 15>{}, Pc);
-#endif
+        if constexpr (SM) opCV(X1{}, std::integral_constant<int, 7>{}, Pc);
         if constexpr (PV) {
             v12_sel4(lA, sel, Pv[0][0][0], Pv[0][0][1], Pv[0][1][0], Pv[0][1][1]);
             v12_sel4(lB, sel, Pv[1][0][0], Pv[1][0][1], Pv[1][1][0], Pv[1][1][1]);
@@ -391,7 +438,8 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     };
 
     // defer-max decision for the tile in S (rare path: drain, rescale O and
-    // l, recompute S from the LDS copy of K in slot sk, redo exps and P)
+    // l, recompute S from the LDS copy of K in slot sk, redo exps and P; block
+    // B's slices 8..15, still to come, then use the new m)
     auto settle = [&](i32x4 (&Pc)[2][2][2], int sk) __attribute__((always_inline)) {
         const bool upA = mxA * c > mA + V12_THR, upB = mxB * c > mB + V12_THR;
         if (__ballot(upA || upB)) {
@@ -418,14 +466,20 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     };
 
     if (nt <= 0) return;  // host guarantees Nk >= 64
-    // ---- prologue: tiles 0 and 1 landed, K(0) fragments, S(0), softmax(0)
+    // ---- prologue: tiles 0 and 1 landed, K(0) fragments, S(0), tile 2's
+    // DMA beside block A's chains, softmax(0), K(1) fragments
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     sfor<16>([&](auto FF) { v12::kread<FF>(kaddr[FF % 8]); });
     lgkm<0>();
-    phaseQ(P0, std::false_type{});
-    if (nt > 2) dma_tile(2, 2);
-    if (nt > 1) phaseP(0, P1, P1, 1, 0, 0, std::false_type{}, std::false_type{}, std::true_type{}, std::false_type{});
+    {
+        const int td = nt > 2 ? 2 : nt - 1;
+        phaseQA(P1, std::false_type{}, kp + (int64_t)td * KT * st.kn, vp + (int64_t)td * KT * st.vn,
+                lds0 + 2 * BUFB + (PPW * wave) * 1024);
+    }
+    phaseQB(P1, P0, std::false_type{}, 0);
+    asm volatile("s_nop 7\n\ts_nop 4" : "+v"(S[0][0]), "+v"(S[0][1]), "+v"(S[1][0]), "+v"(S[1][1]));
+    if (nt > 1) phaseP(0, P1, P1, 1, std::false_type{}, std::false_type{}, std::true_type{}, std::false_type{});
     {   // first tile: the max decides m before any exp
         mxA = -INFINITY;
         mxB = -INFINITY;
@@ -444,27 +498,36 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         pfence(P0);
     }
 
-    // tile t: S(t) and P(t) in Pc = P(t&1); PV of tile t-1 from Pv
+    // tile t: S(t) and P(t) in Pc = P(t&1); PV of tile t-1 from Pv.  LDS ring
+    // of 5 slots, tile u in slot u % 5: tile t+2's DMA goes out during phase
+    // QA(t) into the slot of tile t-3, whose last reader (PV(t-3) in phase
+    // P(t-2)) every wave has passed at barrier(t-1); the counted vmcnt(8)
+    // before barrier(t) retires tile t+1 and leaves tile t+2 in flight.  Past
+    // the last tile the DMA reloads tile nt-1 (the count stays constant).
     auto step = [&](int t, i32x4 (&Pc)[2][2][2], i32x4 (&Pv)[2][2][2]) __attribute__((always_inline)) {
         stamp(6);
         lgkm<0>();  // K(t) fragments in AGPR
-#ifndef V12_EXP_ACHAIN
         stamp(0);
-#endif
-        phaseQ(Pc, std::true_type{});
+        {
+            const int td = t + 2 < nt ? t + 2 : nt - 1;
+            phaseQA(Pv, std::true_type{}, kp + (int64_t)td * KT * st.kn, vp + (int64_t)td * KT * st.vn,
+                    lds0 + (uint32_t)((t + 2) % NBUF) * BUFB + (PPW * wave) * 1024);
+        }
+        phaseQB(Pv, Pc, std::true_type{}, (t - 1) % NBUF);
         stamp(1);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t+1 (issued one step ago)
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile t+1 (issued one step ago)
         stamp(2);
         __syncthreads();
         stamp(3);
-        if (t + 2 < nt) dma_tile(t + 2, (t + 2) & 3);
         asm volatile("s_nop 1" ::: "memory");  // P just written -> MFMA operands
-        if (t + 1 < nt)
-            phaseP((t - 1) & 3, Pv, Pc, (t + 1) & 3, 0, 0, std::true_type{}, std::true_type{}, std::true_type{}, std::false_type{});
-        else
-            phaseP((t - 1) & 3, Pv, Pc, 0, 0, 0, std::true_type{}, std::true_type{}, std::false_type{}, std::false_type{});
+        // K(t+1) fragments; past the last tile they read a stale slot (never
+        // used) -- one instantiation, so no branch between phase QB's V^T reads
+        // and their use here (at a branch hipcc may copy the not-yet-landed
+        // fragment registers)
+        phaseP((t - 1) % NBUF, Pv, Pc, (t + 1) % NBUF, std::true_type{}, std::true_type{}, std::true_type{},
+               std::integral_constant<bool, V12_VPRE>{});
         stamp(4);
-        settle(Pc, t & 3);
+        settle(Pc, t % NBUF);
         stamp(5);
     };
     stamp(6);
@@ -475,11 +538,17 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     }
     if (t < nt) step(t, P1, P0);
 
-    // ---- epilogue: PV of the last tile, l, O read-out and store
-    if ((nt - 1) & 1) pfence(P1);
-    else pfence(P0);
-    if ((nt - 1) & 1) phaseP((nt - 1) & 3, P1, P1, 0, 0, 0, std::true_type{}, std::false_type{}, std::false_type{}, std::false_type{});
-    else phaseP((nt - 1) & 3, P0, P0, 0, 0, 0, std::true_type{}, std::false_type{}, std::false_type{}, std::false_type{});
+    // ---- epilogue: block B's slices 8..15 and PV of the last tile, l, O
+    // read-out and store.  The V^T addresses are made opaque here, or hipcc
+    // precomputes the epilogue's slot addresses before the loop and parks
+    // them in accumulator registers it thinks are free (the Q fragments).
+#pragma unroll
+    for (int db = 0; db < 4; ++db) asm volatile("" : "+v"(valo[db]), "+v"(vahi[db]));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if ((nt - 1) & 1) { tailB(P1); pfence(P1); }
+    else { tailB(P0); pfence(P0); }
+    if ((nt - 1) & 1) phaseP((nt - 1) % NBUF, P1, P1, 0, std::true_type{}, std::false_type{}, std::false_type{}, std::false_type{});
+    else phaseP((nt - 1) % NBUF, P0, P0, 0, std::true_type{}, std::false_type{}, std::false_type{}, std::false_type{});
     asm volatile("s_nop 15\n\ts_nop 7" : "+v"(lA), "+v"(lB));
     const float invA = [&] { const float l = v12_xor32_sum(lA[0]); return l > 0.f ? 1.f / l : 0.f; }();
     const float invB = [&] { const float l = v12_xor32_sum(lB[0]); return l > 0.f ? 1.f / l : 0.f; }();
