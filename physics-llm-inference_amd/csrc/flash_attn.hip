@@ -526,12 +526,12 @@ template <typename T, int D>
 int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int H,
                 int group, int Nq, int Nk, const AttnStrides& st, float scale,
                 int causal, hipStream_t stream, int variant) {
-    if (variant == 70) {
+    if (variant == 70 || variant == 71) {
         const bool bf = std::is_same<T, bf16_t>::value;
         if (attn_v12_ok(D, bf ? 1 : 0, causal, Nk) && scale * 1.4426950408889634f <= 1.f) {
             const V7Strides s7{st.qb, st.qh, st.qn, st.kb, st.kh, st.kn,
                                st.vb, st.vh, st.vn, st.ob, st.oh, st.on};
-            return launch_attn_v12(q, k, v, o, B, H, group, Nq, Nk, s7, scale, stream);
+            return launch_attn_v12(q, k, v, o, B, H, group, Nq, Nk, s7, scale, stream, variant == 71);
         }
         variant = 55;
     }

@@ -138,13 +138,24 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int h32 = lane >> 5, l32 = lane & 31;
-    const int lb = xcd_remap(blockIdx.x, nblocks);
-    const int bh = lb / qblocks, qblk = lb % qblocks;
-    const int b = bh / H, hq = bh % H, hk = hq / group;
-    const int q0 = qblk * 256 + wave * 64;
-    const uint16_t* qp = q + b * st.qb + hq * st.qh;
-    const uint16_t* kp = k + b * st.kb + hk * st.kh;
-    const uint16_t* vp = v + b * st.vb + hk * st.vh;
+    // persistent form: workgroup w walks the blocks w, w + G, w + 2G, ...
+    // (G = gridDim.x, a multiple of 8, so every block of one walk stays on
+    // the workgroup's XCD and xcd_remap keeps a head's blocks together)
+    int L = blockIdx.x, b = 0, hq = 0, q0 = 0;
+    const uint16_t *qp = q, *kp = k, *vp = v;
+    auto block_ptrs = [&](int l, int& bb, int& hh, int& r0, const uint16_t*& qq, const uint16_t*& kk,
+                          const uint16_t*& vv) __attribute__((always_inline)) {
+        const int lb = xcd_remap(l, nblocks);
+        const int bh = lb / qblocks, qblk = lb % qblocks;
+        bb = bh / H;
+        hh = bh % H;
+        const int hk = hh / group;
+        r0 = qblk * 256 + wave * 64;
+        qq = q + bb * st.qb + hh * st.qh;
+        kk = k + bb * st.kb + hk * st.kh;
+        vv = v + bb * st.vb + hk * st.vh;
+    };
+    block_ptrs(L, b, hq, q0, qp, kp, vp);
     const int nt = Nk / KT;
     unsigned long long st_sum[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0;
     auto stamp = [&](int seg) __attribute__((always_inline)) {
@@ -187,25 +198,22 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         }
     };
 
-    // ---- tiles 0 and 1 in flight first, then Q^T fragments -> AGPR; O = 0
+    // ---- tiles 0 and 1 in flight first, then the Q^T fragments (VGPRs;
+    // into the accumulators at the block's prologue)
     if (nt > 0) dma_tile(0, 0);
     if (nt > 1) dma_tile(1, 1);
-    {
-        const int ra = q0 + l32, rb = q0 + 32 + l32;
-        const uint16_t* sa = qp + (int64_t)(ra < Nq ? ra : 0) * st.qn + 8 * h32;
-        const uint16_t* sb = qp + (int64_t)(rb < Nq ? rb : 0) * st.qn + 8 * h32;
-        i32x4 qa[8], qb[8];
+    i32x4 qa[8], qb[8];
+    auto load_q = [&](const uint16_t* qbase, int r0) __attribute__((always_inline)) {
+        const int ra = r0 + l32, rb = r0 + 32 + l32;
+        const uint16_t* sa = qbase + (int64_t)(ra < Nq ? ra : 0) * st.qn + 8 * h32;
+        const uint16_t* sb = qbase + (int64_t)(rb < Nq ? rb : 0) * st.qn + 8 * h32;
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk) {
             qa[kk] = *reinterpret_cast<const i32x4*>(sa + 16 * kk);
             qb[kk] = *reinterpret_cast<const i32x4*>(sb + 16 * kk);
         }
-        sfor<8>([&](auto KK) {
-            v12::q_to_agpr<0, KK>(qa[KK]);
-            v12::q_to_agpr<1, KK>(qb[KK]);
-        });
-    }
-    v12::o_zero();
+    };
+    load_q(qp, q0);
 
     // ---- fragment addresses (LDS byte addresses; + slot * BUFB per tile)
     const int A0 = l32 * 256 + ((h32 ^ fsw(l32)) << 4);
@@ -228,9 +236,9 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
 
     float mA = -1e30f, mB = -1e30f;
     f32x4 lA = {0.f, 0.f, 0.f, 0.f}, lB = {0.f, 0.f, 0.f, 0.f};
-    // hipcc does not know the row-sum asm MFMAs read l as C: materialise the
-    // zeros here, wait states after (VALU write -> MFMA source)
-    asm volatile("s_nop 2" : "+v"(lA), "+v"(lB));
+    // stream position: the block's tile t sits in LDS slot (s0 + t) % NBUF
+    int s0 = 0;
+    bool has_next = false;
     f32x16 S[2][2];               // [block][key half]: one tile's scores
     i32x4 P0[2][2][2], P1[2][2][2];  // [block][key half][16-key step]; tile t in P(t&1)
     float mxA = -INFINITY, mxB = -INFINITY;
@@ -442,7 +450,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     // B's slices 8..15, still to come, then use the new m)
     auto settle = [&](i32x4 (&Pc)[2][2][2], int sk) __attribute__((always_inline)) {
         const bool upA = mxA * c > mA + V12_THR, upB = mxB * c > mB + V12_THR;
-        if (__ballot(upA || upB)) {
+        if (__builtin_expect(__ballot(upA || upB) != 0, 0)) {
             asm volatile("s_nop 7\n\ts_nop 7" : "+v"(lA), "+v"(lB));
             const float nA = upA ? mxA * c : mA, nB = upB ? mxB * c : mB;
             const float alA = __builtin_amdgcn_exp2f(mA - nA), alB = __builtin_amdgcn_exp2f(mB - nB);
@@ -466,54 +474,43 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     };
 
     if (nt <= 0) return;  // host guarantees Nk >= 64
-    // ---- prologue: tiles 0 and 1 landed, K(0) fragments, S(0), tile 2's
-    // DMA beside block A's chains, softmax(0), K(1) fragments
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    sfor<16>([&](auto FF) { v12::kread<FF>(kaddr[FF % 8]); });
-    lgkm<0>();
-    {
-        const int td = nt > 2 ? 2 : nt - 1;
-        phaseQA(P1, std::false_type{}, kp + (int64_t)td * KT * st.kn, vp + (int64_t)td * KT * st.vn,
-                lds0 + 2 * BUFB + (PPW * wave) * 1024);
-    }
-    phaseQB(P1, P0, std::false_type{}, 0);
-    asm volatile("s_nop 7\n\ts_nop 4" : "+v"(S[0][0]), "+v"(S[0][1]), "+v"(S[1][0]), "+v"(S[1][1]));
-    if (nt > 1) phaseP(0, P1, P1, 1, std::false_type{}, std::false_type{}, std::true_type{}, std::false_type{});
-    {   // first tile: the max decides m before any exp
-        mxA = -INFINITY;
-        mxB = -INFINITY;
-#pragma unroll
-        for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-            for (int r = 0; r < 16; r += 2) {
-                mxA = max3(mxA, S[0][tt][r], S[0][tt][r + 1]);
-                mxB = max3(mxB, S[1][tt][r], S[1][tt][r + 1]);
-            }
-        mxA = v12_xor32_max(mxA);
-        mxB = v12_xor32_max(mxB);
-        mA = mxA == -INFINITY ? -1e30f : mxA * c;
-        mB = mxB == -INFINITY ? -1e30f : mxB * c;
-        expo_cvt_all(P0);
-        pfence(P0);
-    }
+    // K/V source of the stream tile t+2 positions ahead of this block's tile
+    // t: this block, the next block's tile 0 or 1 (persistent), or past the
+    // last block a reload of tile nt-1 (keeps the vmcnt count constant)
+    auto dma_src = [&](int t2, const uint16_t*& kt, const uint16_t*& vt) __attribute__((always_inline)) {
+        if (t2 < nt) {
+            kt = kp + (int64_t)t2 * KT * st.kn;
+            vt = vp + (int64_t)t2 * KT * st.vn;
+        } else if (has_next) {  // recomputed here: fewer scalars live through the block
+            int b2, h2, r2;
+            const uint16_t *q2, *k2, *v2;
+            block_ptrs(L + (int)gridDim.x, b2, h2, r2, q2, k2, v2);
+            kt = k2 + (int64_t)(t2 - nt) * KT * st.kn;
+            vt = v2 + (int64_t)(t2 - nt) * KT * st.vn;
+        } else {
+            kt = kp + (int64_t)(nt - 1) * KT * st.kn;
+            vt = vp + (int64_t)(nt - 1) * KT * st.vn;
+        }
+    };
+    auto slot = [&](int t) __attribute__((always_inline)) { return (s0 + t) % NBUF; };
 
     // tile t: S(t) and P(t) in Pc = P(t&1); PV of tile t-1 from Pv.  LDS ring
-    // of 5 slots, tile u in slot u % 5: tile t+2's DMA goes out during phase
-    // QA(t) into the slot of tile t-3, whose last reader (PV(t-3) in phase
-    // P(t-2)) every wave has passed at barrier(t-1); the counted vmcnt(8)
-    // before barrier(t) retires tile t+1 and leaves tile t+2 in flight.  Past
-    // the last tile the DMA reloads tile nt-1 (the count stays constant).
+    // of 5 slots, stream tile u in slot u % 5: the DMA of the stream tile two
+    // ahead goes out during phase QA(t) into the slot of stream tile u-3,
+    // whose last reader (PV(u-3) in phase P(u-2)) every wave has passed at
+    // barrier(u-1); the counted vmcnt(8) before barrier(u) retires tile u+1
+    // and leaves u+2 in flight.  Across a block seam the stream continues
+    // (the next block's tiles 0 and 1 are DMA'd by this block's last steps).
     auto step = [&](int t, i32x4 (&Pc)[2][2][2], i32x4 (&Pv)[2][2][2]) __attribute__((always_inline)) {
         stamp(6);
         lgkm<0>();  // K(t) fragments in AGPR
         stamp(0);
         {
-            const int td = t + 2 < nt ? t + 2 : nt - 1;
-            phaseQA(Pv, std::true_type{}, kp + (int64_t)td * KT * st.kn, vp + (int64_t)td * KT * st.vn,
-                    lds0 + (uint32_t)((t + 2) % NBUF) * BUFB + (PPW * wave) * 1024);
+            const uint16_t *kt, *vt;
+            dma_src(t + 2, kt, vt);
+            phaseQA(Pv, std::true_type{}, kt, vt, lds0 + (uint32_t)slot(t + 2) * BUFB + (PPW * wave) * 1024);
         }
-        phaseQB(Pv, Pc, std::true_type{}, (t - 1) % NBUF);
+        phaseQB(Pv, Pc, std::true_type{}, slot(t - 1));
         stamp(1);
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile t+1 (issued one step ago)
         stamp(2);
@@ -524,58 +521,130 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         // used) -- one instantiation, so no branch between phase QB's V^T reads
         // and their use here (at a branch hipcc may copy the not-yet-landed
         // fragment registers)
-        phaseP((t - 1) % NBUF, Pv, Pc, (t + 1) % NBUF, std::true_type{}, std::true_type{}, std::true_type{},
+        phaseP(slot(t - 1), Pv, Pc, slot(t + 1), std::true_type{}, std::true_type{}, std::true_type{},
                std::integral_constant<bool, V12_VPRE>{});
         stamp(4);
-        settle(Pc, t % NBUF);
+        settle(Pc, slot(t));
         stamp(5);
     };
-    stamp(6);
-    int t = 1;
-    for (; t + 1 < nt; t += 2) {
-        step(t, P1, P0);
-        step(t + 1, P0, P1);
-    }
-    if (t < nt) step(t, P1, P0);
 
-    // ---- epilogue: block B's slices 8..15 and PV of the last tile, l, O
-    // read-out and store.  The V^T addresses are made opaque here, or hipcc
-    // precomputes the epilogue's slot addresses before the loop and parks
-    // them in accumulator registers it thinks are free (the Q fragments).
-#pragma unroll
-    for (int db = 0; db < 4; ++db) asm volatile("" : "+v"(valo[db]), "+v"(vahi[db]));
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if ((nt - 1) & 1) { tailB(P1); pfence(P1); }
-    else { tailB(P0); pfence(P0); }
-    if ((nt - 1) & 1) phaseP((nt - 1) % NBUF, P1, P1, 0, std::true_type{}, std::false_type{}, std::false_type{}, std::false_type{});
-    else phaseP((nt - 1) % NBUF, P0, P0, 0, std::true_type{}, std::false_type{}, std::false_type{}, std::false_type{});
-    asm volatile("s_nop 15\n\ts_nop 7" : "+v"(lA), "+v"(lB));
-    const float invA = [&] { const float l = v12_xor32_sum(lA[0]); return l > 0.f ? 1.f / l : 0.f; }();
-    const float invB = [&] { const float l = v12_xor32_sum(lB[0]); return l > 0.f ? 1.f / l : 0.f; }();
-    auto store = [&](auto x_tag, float inv) __attribute__((always_inline)) {
-        constexpr int X = decltype(x_tag)::value;
-        const int qr = q0 + 32 * X + l32;
-        sfor<4>([&](auto DB) {
-            f32x16 a;
-            v12::o_read<X, DB>(a);
-            if (qr < Nq) {
-                uint16_t* op = o + b * st.ob + hq * st.oh + (int64_t)qr * st.on;
-#pragma unroll
-                for (int i = 0; i < 4; i += 2) {
-                    const uint32_t ax = pack2<bf16_t>(a[4 * i] * inv, a[4 * i + 1] * inv);
-                    const uint32_t ay = pack2<bf16_t>(a[4 * i + 2] * inv, a[4 * i + 3] * inv);
-                    const uint32_t bx = pack2<bf16_t>(a[4 * i + 4] * inv, a[4 * i + 5] * inv);
-                    const uint32_t by = pack2<bf16_t>(a[4 * i + 6] * inv, a[4 * i + 7] * inv);
-                    const auto rx = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
-                    const auto ry = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
-                    const int d = DB * 32 + 8 * i + 8 * h32;
-                    *reinterpret_cast<i32x4*>(op + d) = i32x4{(int)rx[0], (int)ry[0], (int)rx[1], (int)ry[1]};
-                }
-            }
+    for (;;) {
+        has_next = L + (int)gridDim.x < nblocks;
+
+        // ---- prologue: tiles 0 and 1 (and Q) landed, Q -> AGPR, O = 0, K(0)
+        // fragments, S(0), the stream tile two ahead's DMA beside block A's
+        // chains, softmax(0), K(1) fragments
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        sfor<8>([&](auto KK) {
+            v12::q_to_agpr<0, KK>(qa[KK]);
+            v12::q_to_agpr<1, KK>(qb[KK]);
         });
-    };
-    store(std::integral_constant<int, 0>{}, invA);
-    store(std::integral_constant<int, 1>{}, invB);
+        v12::o_zero();
+        mA = -1e30f;
+        mB = -1e30f;
+        lA = f32x4{0.f, 0.f, 0.f, 0.f};
+        lB = f32x4{0.f, 0.f, 0.f, 0.f};
+        // hipcc does not know the row-sum asm MFMAs read l as C: materialise
+        // the zeros here, wait states after (VALU write -> MFMA source)
+        asm volatile("s_nop 2" : "+v"(lA), "+v"(lB));
+        {
+            const uint32_t ks0 = (uint32_t)slot(0) * BUFB;
+            sfor<16>([&](auto FF) { v12::kread<FF>(kaddr[FF % 8] + ks0); });
+        }
+        lgkm<0>();
+        {
+            const uint16_t *kt, *vt;
+            dma_src(2, kt, vt);
+            phaseQA(P1, std::false_type{}, kt, vt, lds0 + (uint32_t)slot(2) * BUFB + (PPW * wave) * 1024);
+        }
+        phaseQB(P1, P0, std::false_type{}, 0);
+        asm volatile("s_nop 7\n\ts_nop 4" : "+v"(S[0][0]), "+v"(S[0][1]), "+v"(S[1][0]), "+v"(S[1][1]));
+        if (nt > 1)
+            phaseP(0, P1, P1, slot(1), std::false_type{}, std::false_type{}, std::true_type{}, std::false_type{});
+        {   // first tile: the max decides m before any exp
+            mxA = -INFINITY;
+            mxB = -INFINITY;
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                for (int r = 0; r < 16; r += 2) {
+                    mxA = max3(mxA, S[0][tt][r], S[0][tt][r + 1]);
+                    mxB = max3(mxB, S[1][tt][r], S[1][tt][r + 1]);
+                }
+            mxA = v12_xor32_max(mxA);
+            mxB = v12_xor32_max(mxB);
+            mA = mxA == -INFINITY ? -1e30f : mxA * c;
+            mB = mxB == -INFINITY ? -1e30f : mxB * c;
+            expo_cvt_all(P0);
+            pfence(P0);
+        }
+
+        stamp(6);
+        int t = 1;
+        for (; t + 1 < nt; t += 2) {
+            step(t, P1, P0);
+            step(t + 1, P0, P1);
+        }
+        if (t < nt) step(t, P1, P0);
+
+        // the next block's Q rows, in flight under this block's epilogue
+        // (past the last block a reload of this block's: unconditional, so
+        // the old fragments are not kept live through the block)
+        {
+            int b2, h2, r2;
+            const uint16_t *q2, *k2, *v2;
+            block_ptrs(has_next ? L + (int)gridDim.x : L, b2, h2, r2, q2, k2, v2);
+            load_q(q2, r2);
+        }
+
+        // ---- epilogue: block B's slices 8..15 and PV of the last tile, l, O
+        // read-out and store.  The V^T addresses are made opaque here, or
+        // hipcc precomputes the epilogue's slot addresses before the loop and
+        // parks them in accumulator registers it thinks are free (the Q
+        // fragments).
+#pragma unroll
+        for (int db = 0; db < 4; ++db) asm volatile("" : "+v"(valo[db]), "+v"(vahi[db]));
+        if ((nt - 1) & 1) { tailB(P1); pfence(P1); }
+        else { tailB(P0); pfence(P0); }
+        if ((nt - 1) & 1)
+            phaseP(slot(nt - 1), P1, P1, 0, std::true_type{}, std::false_type{}, std::false_type{}, std::false_type{});
+        else
+            phaseP(slot(nt - 1), P0, P0, 0, std::true_type{}, std::false_type{}, std::false_type{}, std::false_type{});
+        asm volatile("s_nop 15\n\ts_nop 7" : "+v"(lA), "+v"(lB));
+        const float invA = [&] { const float l = v12_xor32_sum(lA[0]); return l > 0.f ? 1.f / l : 0.f; }();
+        const float invB = [&] { const float l = v12_xor32_sum(lB[0]); return l > 0.f ? 1.f / l : 0.f; }();
+        auto store = [&](auto x_tag, float inv) __attribute__((always_inline)) {
+            constexpr int X = decltype(x_tag)::value;
+            const int qr = q0 + 32 * X + l32;
+            sfor<4>([&](auto DB) {
+                f32x16 a;
+                v12::o_read<X, DB>(a);
+                if (qr < Nq) {
+                    uint16_t* op = o + b * st.ob + hq * st.oh + (int64_t)qr * st.on;
+#pragma unroll
+                    for (int i = 0; i < 4; i += 2) {
+                        const uint32_t ax = pack2<bf16_t>(a[4 * i] * inv, a[4 * i + 1] * inv);
+                        const uint32_t ay = pack2<bf16_t>(a[4 * i + 2] * inv, a[4 * i + 3] * inv);
+                        const uint32_t bx = pack2<bf16_t>(a[4 * i + 4] * inv, a[4 * i + 5] * inv);
+                        const uint32_t by = pack2<bf16_t>(a[4 * i + 6] * inv, a[4 * i + 7] * inv);
+                        const auto rx = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
+                        const auto ry = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
+                        const int d = DB * 32 + 8 * i + 8 * h32;
+                        *reinterpret_cast<i32x4*>(op + d) = i32x4{(int)rx[0], (int)ry[0], (int)rx[1], (int)ry[1]};
+                    }
+                }
+            });
+        };
+        store(std::integral_constant<int, 0>{}, invA);
+        store(std::integral_constant<int, 1>{}, invB);
+        if (!has_next) break;
+        s0 = (s0 + nt) % NBUF;
+        L += (int)gridDim.x;
+        block_ptrs(L, b, hq, q0, qp, kp, vp);
+    }
+    // the last DMA (a reload of tile nt-1) lands before the LDS is released
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #ifdef PLI_FLASH_STAMPS
     if constexpr (STAMP) {
         stamp(7);
@@ -596,12 +665,27 @@ bool attn_v12_ok(int D, int is_bf16, int causal, int Nk) {
 }
 
 int launch_attn_v12(const void* q, const void* k, const void* v, void* o, int B, int H, int group, int Nq,
-                    int Nk, const V7Strides& st, float scale, hipStream_t stream) {
+                    int Nk, const V7Strides& st, float scale, hipStream_t stream, bool persistent) {
     const int qblocks = cdiv(Nq, 256);
     const int64_t nb = (int64_t)B * H * qblocks;
     PLI_REQUIRE(nb < (1ll << 31), "pli_flash_attn_fwd: grid too large");
     const float c = scale * 1.4426950408889634f;
-    hipLaunchKernelGGL(attn_fwd_v12<false>, dim3((unsigned)nb), dim3(256), 0, stream, (const uint16_t*)q,
+    // persistent: one workgroup per CU (the kernel holds 160 KiB of LDS and
+    // the whole register file), a multiple of 8 so each walks one XCD; the
+    // stream across block seams needs two tiles per block
+    int grid = (int)nb;
+    if (persistent && Nk >= 128) {
+        static int ncu = [] {
+            int dev = 0, n = 0;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+                n = 256;
+            return n;
+        }();
+        const int g = ncu / 8 * 8;
+        if (g >= 8 && nb > g) grid = g;
+    }
+    hipLaunchKernelGGL(attn_fwd_v12<false>, dim3((unsigned)grid), dim3(256), 0, stream, (const uint16_t*)q,
                        (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, H, group, Nq, Nk, st, c, qblocks,
                        (int)nb);
     return hipGetLastError() == hipSuccess ? PLI_OK : PLI_EINVAL;

@@ -1,0 +1,46 @@
+"""Build-time invariants of attn_fwd_v12 (csrc/flash_v12.hip), CPU only.
+
+The kernel names its accumulator registers literally in inline asm (O, Q, K
+fragments in a[0:255]); hipcc does not know the Q fragments stay live between
+the asm statements, so if it ever runs short of VGPRs it parks values in
+those AGPRs (v_accvgpr_write/read of its own) and the Q fragments are
+silently corrupted -- every output row of one 32-row block wrong.  This
+compiles the file the way build.py does and checks that no instruction
+outside the asm statements touches an AGPR and that nothing spills.
+"""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "physics-llm-inference_amd", "csrc")
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_v12_no_compiler_agpr_use_or_spill(tmp_path):
+    out = tmp_path / "v12.s"
+    cmd = [HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "-fno-honor-nans",
+           "-I" + os.path.join(ROOT, "include"), "-I" + CSRC, "-S", "--cuda-device-only",
+           os.path.join(CSRC, "flash_v12.hip"), "-o", str(out)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    text = out.read_text()
+    in_asm = False
+    own = []
+    for line in text.splitlines():
+        if ";;#ASMSTART" in line:
+            in_asm = True
+            continue
+        if ";;#ASMEND" in line:
+            in_asm = False
+            continue
+        if not in_asm and re.search(r"\bv_accvgpr_(read|write)|\bscratch_(load|store)|buffer_(load|store).*off, s\[0:3\]",
+                                    line):
+            own.append(line.strip())
+    assert not own, f"hipcc-generated AGPR/scratch accesses in attn_fwd_v12: {own[:8]}"
+    m = re.search(r"\.private_segment_fixed_size:\s+(\d+)", text)
+    assert m and int(m.group(1)) == 0, "attn_fwd_v12 uses scratch"
