@@ -583,10 +583,10 @@ def main():
                    "parallelism": f"replicas x{world} (flash does not shard; TP GEMM row-parallel)"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved / PEAK_BF16_TFLOPS,
-                     "traffic": load_traffic("attn_fwd_v10"),
+                     "traffic": load_traffic("attn_fwd_v12"),
                      "traffic_source": "profiles/traffic.json: rocprofv3 FETCH_SIZE x2 (gfx950) + WRITE_SIZE "
                                        "per launch, separate --pmc passes (tools/pmc_summary.py), not this run",
-                     "kernel": "attn_fwd_v10<bf16,exact> (variant 55)", "algorithmic_flops": flops_step,
+                     "kernel": "attn_fwd_v12 persistent (variant 71; bitwise = attn_fwd_v10 exact)", "algorithmic_flops": flops_step,
                      "kernel_ms": kernel_ms, **measured_roof},
         **extra,
     }

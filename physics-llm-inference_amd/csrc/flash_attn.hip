@@ -516,7 +516,14 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
 // the PV MFMAs: 1035 vs 1061 TF, two 64-key tiles per barrier on a 4-slot
 // ring: 1054 vs 1054 TF, causal 850 vs 844) are
 // not in the library; their measurements are in DESIGN.md 3.1.
-constexpr int kDefaultVariant = 55;
+//  70: attn_fwd_v12 (flash_v12.hip): 4 waves x 64 rows, one wave per SIMD,
+//      O / Q / K fragments in literally named accumulator registers, a
+//      hand-placed stream (one exp per MFMA gap), 5-slot LDS ring; bitwise
+//      equal to 55 (bf16, D = 128, non-causal, Nk % 64 == 0; else 55)
+//  71: attn_fwd_v12 persistent (one workgroup per CU walking its XCD's
+//      blocks, the K/V stream and the next block's Q across block seams) --
+//      the DEFAULT where 70 applies (1181 vs 1082 TF/s for 55)
+constexpr int kDefaultVariant = 71;
 // causal: the 4-wave workgroups of 60 -- 128-row blocks balance the
 // triangular work better and the two workgroups per CU drift apart
 // (B8 S4096 H32 D128 bf16: 924 vs 834 TF/s; non-causal 1085 vs 1100)

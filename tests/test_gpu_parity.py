@@ -106,7 +106,7 @@ def test_flash_vs_oracle(case):
 
 
 # every MFMA variant (alternates A/B-tested by tools/tune.py) on the MFMA-eligible cases
-MFMA_VARIANTS = (21, 50, 51, 54, 55, 60)
+MFMA_VARIANTS = (21, 50, 51, 54, 55, 60, 70, 71)
 
 
 
@@ -140,13 +140,13 @@ def test_flash_strided_views_and_out_param():
 # variants whose Q is prescaled by scale*log2(e) and rounded to the 16-bit
 # input type before the MFMA (the rest scale the f32 scores exactly)
 PRESCALED = (50, 54)
-DEFAULT_VARIANT = 55
+DEFAULT_VARIANT = 71
 
 
 DEFAULT_CAUSAL_VARIANT = 60
 
 
-def test_flash_default_is_variant_55():
+def test_flash_default_variants():
     import pli_hip
     q, k, v = (dev(x, "bf16") for x in stress_inputs("late"))
     assert torch.equal(pli_hip.flash_attn_fwd(q, k, v), pli_hip.flash_attn_fwd(q, k, v, variant=DEFAULT_VARIANT))
@@ -186,7 +186,7 @@ def test_flash_stress(variant, name):
         assert err <= tol, f"stress {name}: {err:.3e} > {tol:.3e}"
 
 
-@pytest.mark.parametrize("variant", [None, 21, 50, 51, 54, 60])
+@pytest.mark.parametrize("variant", [None, 21, 50, 51, 54, 55, 60, 70])
 def test_flash_full_config_properties(variant):
     """B=8 S=4096 H=32 D=128 bf16 (the bench config): v = 1 gives exactly 1;
     two heads checked against the f64 oracle; key permutation invariance."""
@@ -207,6 +207,29 @@ def test_flash_full_config_properties(variant):
     if variant is None:
         base = pli_hip.flash_attn_fwd(q, k, v, variant=21)
         assert (base.float() - out.float()).abs().max().item() <= 1.6e-2
+    # attn_fwd_v12 (70, 71 = default) runs attn_fwd_v10's arithmetic in the
+    # same order: bitwise equal to 55 over the whole tensor
+    if variant in (None, 70):
+        assert torch.equal(out, pli_hip.flash_attn_fwd(q, k, v, variant=55))
+
+
+@pytest.mark.parametrize("shape", [(4, 16, 4, 2048, 1024), (4, 32, 8, 1024, 128), (4, 32, 8, 1024, 192),
+                                   (3, 40, 8, 1000, 320), (2, 4, 1, 2048, 192)])
+def test_flash_v12_persistent_seams(shape):
+    """Variant 71 walks more than one block per workgroup once the grid
+    exceeds one workgroup per CU; the K/V stream then crosses block seams
+    (blocks of 2 and 3 tiles, ragged Nq, GQA).  Bitwise equal to 55 and to
+    the non-persistent form 70; the rescale path forced by scaled-up Q."""
+    import pli_hip
+    B, H, Hkv, Nq, Nk = shape
+    g = torch.Generator(device=DEV).manual_seed(sum(shape))
+    q = torch.randn(B, H, Nq, 128, device=DEV, dtype=torch.bfloat16, generator=g)
+    k = torch.randn(B, Hkv, Nk, 128, device=DEV, dtype=torch.bfloat16, generator=g)
+    v = torch.randn(B, Hkv, Nk, 128, device=DEV, dtype=torch.bfloat16, generator=g)
+    for qq in (q, q * 4):
+        a = pli_hip.flash_attn_fwd(qq, k, v, variant=55)
+        assert torch.equal(a, pli_hip.flash_attn_fwd(qq, k, v, variant=71)), f"{shape}: 71 != 55"
+        assert torch.equal(a, pli_hip.flash_attn_fwd(qq, k, v, variant=70)), f"{shape}: 70 != 55"
 
 
 @pytest.mark.parametrize("variant", [None, 55, 21])

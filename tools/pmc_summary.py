@@ -19,7 +19,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = ("attn_fwd_v10", "attn_fwd_v7", "gemm_f32_mfma", "gemm_naive_f32", "hbm_read_probe", "attn_fwd_v2", "attn_decode_chunk", "attn_decode_combine", "gemv_vec", "gemm_mfma",
+KERNELS = ("attn_fwd_v12", "attn_fwd_v10", "attn_fwd_v7", "gemm_f32_mfma", "gemm_naive_f32", "hbm_read_probe", "attn_fwd_v2", "attn_decode_chunk", "attn_decode_combine", "gemv_vec", "gemm_mfma",
            "gemm_smallm_nt", "scale_copy_vec")
 
 

@@ -16,7 +16,8 @@ import sys
 trace, bench = sys.argv[1], sys.argv[2]
 warmup = int(sys.argv[3]) if len(sys.argv) > 3 else 2
 steps = int(sys.argv[4]) if len(sys.argv) > 4 else 10
-rows = sorted((r for r in csv.DictReader(open(trace)) if "attn_fwd_v10" in r["Kernel_Name"]),
+kname = sys.argv[5] if len(sys.argv) > 5 else "attn_fwd_v12"
+rows = sorted((r for r in csv.DictReader(open(trace)) if kname in r["Kernel_Name"]),
               key=lambda r: int(r["Start_Timestamp"]))
 dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
 timed = dur[warmup:warmup + steps]
