@@ -112,15 +112,6 @@ __device__ __forceinline__ float v12_xor32_sum(float x) {
 
 typedef __attribute__((ext_vector_type(2))) float v12f2;
 constexpr float V12_THR = 8.f;
-#ifndef V12_VPRE
-#define V12_VPRE 1
-#endif
-#ifndef V12_CVEVEN
-#define V12_CVEVEN 0
-#endif
-#ifndef V12_KEARLY
-#define V12_KEARLY 0
-#endif
 
 #ifdef PLI_FLASH_STAMPS
 // diagnostic build only (tools/build_diag.sh): per-segment s_memtime sums
@@ -157,7 +148,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     };
     block_ptrs(L, b, hq, q0, qp, kp, vp);
     const int nt = Nk / KT;
-    unsigned long long st_sum[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0;
+    unsigned long long st_sum[14] = {}, st_last = 0;
     auto stamp = [&](int seg) __attribute__((always_inline)) {
         if constexpr (STAMP) {
             unsigned long long now;
@@ -293,11 +284,10 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         constexpr int g = decltype(g_tag)::value, I0 = decltype(i0_tag)::value, i = I0 + g / 2;
         if constexpr (g % 2 == 0) {
             opFM(x_tag, std::integral_constant<int, i>{});
-            if constexpr (V12_CVEVEN && g > 0) opCV(x_tag, std::integral_constant<int, i - 1>{}, Pc);
             opE(x_tag, std::integral_constant<int, i>{}, H0{});
         } else {
             opE(x_tag, std::integral_constant<int, i>{}, H1{});
-            if constexpr (!V12_CVEVEN && g > 1) opCV(x_tag, std::integral_constant<int, i - 1>{}, Pc);
+            if constexpr (g > 1) opCV(x_tag, std::integral_constant<int, i - 1>{}, Pc);
         }
     };
     // VALU-written P -> MFMA operands: pin P here and pad
@@ -376,7 +366,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
                 if constexpr (F % 2 == 0) opMX(X0{}, std::integral_constant<int, F / 2>{});
                 else opMX(X0{}, std::integral_constant<int, 8 + F / 2>{});
                 stream(X0{}, std::integral_constant<int, 0>{}, FF, Pc);
-                if constexpr (F % 2 == 1 && F < 8 && V12_VPRE)
+                if constexpr (F % 2 == 1 && F < 8)
                     vread1(std::integral_constant<int, 0>{}, std::integral_constant<int, F / 2>{}, vs);
             }
             __builtin_amdgcn_sched_barrier(0);
@@ -402,7 +392,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
             if constexpr (PV) {
                 // d-block db's 8 reads were issued before the K reads of the
                 // previous d-block's gaps 4..7
-                constexpr int N = (KR && db > 0 && !V12_KEARLY) ? 4 : 0;
+                constexpr int N = (KR && db > 0) ? 4 : 0;
                 V12Frag* f = vf[db & 1];
                 asm volatile("s_waitcnt lgkmcnt(%8)"
                              : "+v"(f[0].lo), "+v"(f[0].hi), "+v"(f[1].lo), "+v"(f[1].hi), "+v"(f[2].lo),
@@ -419,8 +409,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
                 // gaps 0..3: the next d-block's fragment j; gaps 4..7: K fragment
                 if constexpr (PV && j < 4 && db + 1 < 4)
                     vread1(std::integral_constant<int, db + 1>{}, std::integral_constant<int, j>{}, vs);
-                if constexpr (KR && (V12_KEARLY ? j < 4 : j >= 4))
-                    v12::kread<4 * db + (j & 3)>(kaddr[(4 * db + (j & 3)) % 8] + ks);
+                if constexpr (KR && j >= 4) v12::kread<4 * db + j - 4>(kaddr[(4 * db + j - 4) % 8] + ks);
                 if constexpr (SM) {
                     if constexpr (slot == 0) opCV(X0{}, std::integral_constant<int, 7>{}, Pc);
                     if constexpr (slot % 2 == 1) opMX(X1{}, std::integral_constant<int, slot / 2>{});
@@ -450,7 +439,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     // B's slices 8..15, still to come, then use the new m)
     auto settle = [&](i32x4 (&Pc)[2][2][2], int sk) __attribute__((always_inline)) {
         const bool upA = mxA * c > mA + V12_THR, upB = mxB * c > mB + V12_THR;
-        if (__builtin_expect(__ballot(upA || upB) != 0, 0)) {
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(upA || upB) != 0, 0)) {
             asm volatile("s_nop 7\n\ts_nop 7" : "+v"(lA), "+v"(lB));
             const float nA = upA ? mxA * c : mA, nB = upB ? mxB * c : mB;
             const float alA = __builtin_amdgcn_exp2f(mA - nA), alB = __builtin_amdgcn_exp2f(mB - nB);
@@ -508,9 +497,10 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         {
             const uint16_t *kt, *vt;
             dma_src(t + 2, kt, vt);
-            phaseQA(Pv, std::true_type{}, kt, vt, lds0 + (uint32_t)slot(t + 2) * BUFB + (PPW * wave) * 1024);
+            const uint32_t dbase = lds0 + (uint32_t)slot(t + 2) * BUFB + (PPW * wave) * 1024;
+            phaseQA(Pv, std::true_type{}, kt, vt, dbase);
+            phaseQB(Pv, Pc, std::true_type{}, slot(t - 1));
         }
-        phaseQB(Pv, Pc, std::true_type{}, slot(t - 1));
         stamp(1);
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile t+1 (issued one step ago)
         stamp(2);
@@ -522,25 +512,41 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         // and their use here (at a branch hipcc may copy the not-yet-landed
         // fragment registers)
         phaseP(slot(t - 1), Pv, Pc, slot(t + 1), std::true_type{}, std::true_type{}, std::true_type{},
-               std::integral_constant<bool, V12_VPRE>{});
+               std::true_type{});
         stamp(4);
         settle(Pc, slot(t));
         stamp(5);
     };
 
+    int nblk = 0;  // blocks walked
     for (;;) {
+        ++nblk;
         has_next = L + (int)gridDim.x < nblocks;
 
         // ---- prologue: tiles 0 and 1 (and Q) landed, Q -> AGPR, O = 0, K(0)
         // fragments, S(0), the stream tile two ahead's DMA beside block A's
         // chains, softmax(0), K(1) fragments
+        // Past the first block, tile 0 landed at the previous block's last
+        // barrier: O = 0 and the K(0) reads go ahead of the wait for the Q
+        // rows (issued under the previous epilogue) and the O stores.
+        const uint32_t ks0 = (uint32_t)slot(0) * BUFB;
+        if (nblk > 1) {
+            v12::o_zero();
+            sfor<16>([&](auto FF) { v12::kread<FF>(kaddr[FF % 8] + ks0); });
+        }
+        stamp(8);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        stamp(9);
         __syncthreads();
+        if (nblk == 1) {
+            v12::o_zero();
+            sfor<16>([&](auto FF) { v12::kread<FF>(kaddr[FF % 8] + ks0); });
+        }
         sfor<8>([&](auto KK) {
             v12::q_to_agpr<0, KK>(qa[KK]);
             v12::q_to_agpr<1, KK>(qb[KK]);
         });
-        v12::o_zero();
+        asm volatile("s_nop 2" ::: "memory");  // accvgpr writes -> MFMA operands
         mA = -1e30f;
         mB = -1e30f;
         lA = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -548,18 +554,17 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         // hipcc does not know the row-sum asm MFMAs read l as C: materialise
         // the zeros here, wait states after (VALU write -> MFMA source)
         asm volatile("s_nop 2" : "+v"(lA), "+v"(lB));
-        {
-            const uint32_t ks0 = (uint32_t)slot(0) * BUFB;
-            sfor<16>([&](auto FF) { v12::kread<FF>(kaddr[FF % 8] + ks0); });
-        }
         lgkm<0>();
+        stamp(10);
         {
             const uint16_t *kt, *vt;
             dma_src(2, kt, vt);
-            phaseQA(P1, std::false_type{}, kt, vt, lds0 + (uint32_t)slot(2) * BUFB + (PPW * wave) * 1024);
+            const uint32_t dbase = lds0 + (uint32_t)slot(2) * BUFB + (PPW * wave) * 1024;
+            phaseQA(P1, std::false_type{}, kt, vt, dbase);
+            phaseQB(P1, P0, std::false_type{}, 0);
         }
-        phaseQB(P1, P0, std::false_type{}, 0);
         asm volatile("s_nop 7\n\ts_nop 4" : "+v"(S[0][0]), "+v"(S[0][1]), "+v"(S[1][0]), "+v"(S[1][1]));
+        stamp(11);
         if (nt > 1)
             phaseP(0, P1, P1, slot(1), std::false_type{}, std::false_type{}, std::true_type{}, std::false_type{});
         {   // first tile: the max decides m before any exp
@@ -588,6 +593,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         }
         if (t < nt) step(t, P1, P0);
 
+        stamp(12);
         // the next block's Q rows, in flight under this block's epilogue
         // (past the last block a reload of this block's: unconditional, so
         // the old fragments are not kept live through the block)
@@ -638,6 +644,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         };
         store(std::integral_constant<int, 0>{}, invA);
         store(std::integral_constant<int, 1>{}, invB);
+        stamp(13);
         if (!has_next) break;
         s0 = (s0 + nt) % NBUF;
         L += (int)gridDim.x;
@@ -650,9 +657,9 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         stamp(7);
         if (lane == 0) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) atomicAdd(&g_v12_stamps[i], st_sum[i]);
-            atomicAdd(&g_v12_stamps[8], (unsigned long long)nt);
-            atomicAdd(&g_v12_stamps[9], 1ull);
+            for (int i = 0; i < 14; ++i) atomicAdd(&g_v12_stamps[i], st_sum[i]);
+            atomicAdd(&g_v12_stamps[14], (unsigned long long)nt * (unsigned long long)nblk);
+            atomicAdd(&g_v12_stamps[15], 1ull);
         }
     }
 #endif
@@ -696,10 +703,10 @@ int launch_attn_v12(const void* q, const void* k, const void* v, void* o, int B,
 #ifdef PLI_FLASH_STAMPS
 // Diagnostic entry (tools/libpli_diag.so only): one stamped launch of
 // attn_fwd_v12 on contiguous [B,H,N,128] bf16, the 16 stamp words to `out`
-// (0 K-fragment wait, 1 phase Q, 2 DMA wait, 3 barrier, 4 phase P, 5 defer-max
+// (segments: tools/v12_stamps.py SEGS; 14 tiles, 15 waves;
 // check, 6 prologue + loop overhead, 7 epilogue; 8 tiles, 9 waves).
 extern "C" int pli_diag_v12_stamps(const void* q, const void* k, const void* v, void* o, int B, int H, int N,
-                                   unsigned long long* out) {
+                                   unsigned long long* out, int grid) {
     using namespace pli;
     const int64_t sn = 128, sh = (int64_t)N * 128, sb = (int64_t)H * N * 128;
     const V7Strides st{sb, sh, sn, sb, sh, sn, sb, sh, sn, sb, sh, sn};
@@ -707,7 +714,8 @@ extern "C" int pli_diag_v12_stamps(const void* q, const void* k, const void* v, 
     const float c = (1.f / sqrtf(128.f)) * 1.4426950408889634f;
     unsigned long long zero[16] = {0};
     hipMemcpyToSymbol(HIP_SYMBOL(g_v12_stamps), zero, sizeof(zero));
-    hipLaunchKernelGGL(attn_fwd_v12<true>, dim3(nb), dim3(256), 0, 0, (const uint16_t*)q, (const uint16_t*)k,
+    hipLaunchKernelGGL(attn_fwd_v12<true>, dim3(grid > 0 && grid < nb ? grid : nb), dim3(256), 0, 0,
+                       (const uint16_t*)q, (const uint16_t*)k,
                        (const uint16_t*)v, (uint16_t*)o, H, 1, N, N, st, c, qblocks, nb);
     if (hipDeviceSynchronize() != hipSuccess) return -1;
     hipMemcpyFromSymbol(out, HIP_SYMBOL(g_v12_stamps), 16 * sizeof(unsigned long long));
