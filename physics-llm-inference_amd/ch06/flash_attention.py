@@ -40,8 +40,11 @@ class FlashAttentionConfig:
     num_stages: int = 2
 
 
-# what each FlashAttentionConfig knob means on the HIP path (attn_fwd_v10)
-HIP_TILING = {"block_q": 256, "block_k": 64, "num_warps": 8, "num_stages": 3}
+# what each FlashAttentionConfig knob means on the HIP path (non-causal bf16
+# D=128: attn_fwd_v12 -- 256-row blocks of 4 waves x 64 rows, 64-key tiles,
+# a 5-slot LDS ring; causal / fp16 / other D run attn_fwd_v10 with 8 waves and
+# a 3-slot ring, or 4 waves and 2 slots for causal)
+HIP_TILING = {"block_q": 256, "block_k": 64, "num_warps": 4, "num_stages": 5}
 
 
 def hip_tiling(config: "FlashAttentionConfig | None" = None) -> dict:
