@@ -451,7 +451,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    # untimed launches first: the first ~10 flash launches in a process run
+    # 2-15 % slower (clock / TLB warm-up; rocprof trace in profiles/r02/final)
+    ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--quick", action="store_true", help="skip gemm/tp/cpu legs")
     ap.add_argument("--with-decode", action="store_true", help="with --quick: keep the decode leg")
