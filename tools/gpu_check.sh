@@ -22,12 +22,12 @@ fi
 if [ "$MODE" = all ] || [ -n "$RUNALL" ] || [ "$MODE" = prof ]; then
   cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
       -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run -- \
-      python "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --steps 10 --warmup 2 \
+      python "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --steps 10 --warmup 30 \
       > "$GRAFT_REPO_ROOT/gpurun_out/prof_bench.json" 2> "$GRAFT_REPO_ROOT/gpurun_out/prof.err"
   rc=$?; echo "rocprof rc=$rc"; cd "$GRAFT_REPO_ROOT"
   find gpurun_out/prof -name "*kernel_stats.csv" -exec cat {} \; | cut -c1-250 | head -20
   [ $rc -eq 0 ] || exit $rc
-  python tools/trace_check.py gpurun_out/prof/run_kernel_trace.csv gpurun_out/prof_bench.json 2 10
+  python tools/trace_check.py gpurun_out/prof/run_kernel_trace.csv gpurun_out/prof_bench.json 30 10
   # headline kernel alone: its stats average is the bench's kernel_ms
   cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
       -d "$GRAFT_REPO_ROOT/gpurun_out/prof_flash" -o run -- \
