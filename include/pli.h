@@ -140,13 +140,17 @@ int pli_scale_copy(const float* in, float* out, int64_t n_out, int stride,
 
 /*
  * Roofline calibration (ch03/roofline.py measure_mfma_peak): `blocks`
- * workgroups of 256 threads, each wave issuing `iters` rounds of four
- * independent bf16 MFMAs from registers on pseudo-random operands (shape 0:
- * v_mfma_f32_32x32x16_bf16, 1: v_mfma_f32_16x16x32_bf16); one float per
- * thread goes to out[blocks * 256] so the work is not dead.
- * FLOPs = blocks * 4 * iters * 4 * (32768 for shape 0, 16384 for shape 1).
+ * workgroups of 256 threads, one per CU (96 KiB of LDS each) so ONE wave per
+ * SIMD, each wave issuing `iters` rounds of back-to-back bf16 MFMAs from
+ * registers into independent accumulators, pseudo-random operands; both
+ * shapes the same 64x64 output tile per wave and 262,144 FLOP per round
+ * (shape 0: 8 x v_mfma_f32_32x32x16_bf16, 1: 16 x v_mfma_f32_16x16x32_bf16).
+ * One float per thread goes to out[blocks * 256] so the work is not dead;
+ * when `clocks` is non-null, wave w writes clocks[2w] = s_memtime ticks
+ * (shader clock) and clocks[2w+1] = s_memrealtime ticks (100 MHz) around its
+ * loop.  FLOPs = blocks * 4 * iters * 262144.
  */
-int pli_mfma_probe(float* out, int blocks, int iters, int shape, void* stream);
+int pli_mfma_probe(float* out, uint64_t* clocks, int blocks, int iters, int shape, void* stream);
 
 /*
  * ch05/tiled_matmul.cu:9-20 naive_matmul (the contrast kernel of the ch05

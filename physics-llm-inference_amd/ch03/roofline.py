@@ -134,29 +134,102 @@ def measure_hbm_read_bandwidth(nbytes: int = 1 << 30, iters: int = 10, device: s
     return nbytes / best / 1e9
 
 
-def measure_mfma_peak(shape: str = "32x32x16", iters: int = 4096, reps: int = 5,
-                      device: str = "cuda") -> float:
-    """Achievable bf16 MFMA TFLOP/s: ``pli_mfma_probe`` (four independent
-    MFMAs per wave from registers, pseudo-random operands, 4 waves per SIMD on
-    every CU), best of ``reps`` event-timed launches.  The clock the chip
-    holds under that load sets it (MI355X_MICROARCH.md 'DVFS give-back')."""
+def measure_hbm_read_bandwidth_sized(nbytes: int = 33570816, copies: int = 24, reps: int = 8,
+                                     device: str = "cuda") -> dict:
+    """The size-matched HBM read roof of the ch03 GEMV: ``pli_hbm_read_probe``
+    reading ``nbytes`` per launch (default ``gemv_bytes(4096, 4096)``, the
+    GEMV's whole footprint) from ``copies`` distinct buffers in turn (24 x 32
+    MiB = 768 MiB, three times the 256 MiB Infinity Cache, so every launch
+    streams from HBM), the ``copies`` launches captured in ONE HIP graph and
+    replayed -- exactly how bench.py times the GEMV, so the per-launch time
+    includes the same kernel boundary.  Best per-launch time over the probe
+    layouts (grid-stride at 8 workgroups per CU; one contiguous slice per
+    workgroup at 2, 4, 8 and 16 per CU).  Returns GB/s, us per launch and
+    the layout."""
     import torch
 
     import pli_hip
 
-    blocks = MI355X_CUS * 4
+    n = (nbytes + 15) // 16 * 4
+    bufs = [torch.empty(n, device=device, dtype=torch.int32).fill_(i + 1) for i in range(copies)]
+    stream = torch.cuda.current_stream()
+    best = None
+    for mode, per_cu in ((0, 8), (1, 2), (1, 4), (1, 8), (1, 16)):
+        blocks = MI355X_CUS * per_cu
+        out = torch.empty(blocks * 256, device=device, dtype=torch.int32)
+        for b in bufs:
+            pli_hip.hbm_read_probe(b, out, blocks, mode)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for b in bufs:
+                pli_hip.hbm_read_probe(b, out, blocks, mode)
+        for _ in range(3):
+            g.replay()
+        times = []
+        for _ in range(reps):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record(stream)
+            g.replay()
+            e.record(stream)
+            e.synchronize()
+            times.append(s.elapsed_time(e) / 1e3 / copies)
+        t = sorted(times)[len(times) // 2]
+        if best is None or t < best[0]:
+            best = (t, mode, per_cu)
+        del g
+    t, mode, per_cu = best
+    return {"GB/s": nbytes / t / 1e9, "us_per_launch": t * 1e6, "bytes_per_launch": nbytes,
+            "layout": f"mode {mode} ({'grid-stride' if mode == 0 else 'slice per workgroup'}), {per_cu} WG/CU",
+            "how": f"{copies} buffers in turn, one HIP graph of {copies} launches, median of {reps} replays"}
+
+
+def measure_mfma_peak_detail(shape: str = "32x32x16", iters: int = 2048, reps: int = 5,
+                             ramp_s: float = 2.0, device: str = "cuda") -> dict:
+    """Achievable bf16 MFMA rate of one shape: ``pli_mfma_probe`` (one wave
+    per SIMD on every CU, back-to-back MFMAs from registers into independent
+    accumulators, pseudo-random operands, the same 64x64 output tile per wave
+    for both shapes).  ``ramp_s`` seconds of back-to-back launches first, then
+    the best of ``reps`` event-timed launches; the in-kernel clock is the
+    median over waves of s_memtime / s_memrealtime ticks x 100 MHz, stamped
+    in the last launch (MI355X_MICROARCH.md 'DVFS give-back' item 6)."""
+    import time
+
+    import torch
+
+    import pli_hip
+
+    blocks = MI355X_CUS
     out = torch.empty(blocks * 256, device=device, dtype=torch.float32)
+    clocks = torch.zeros(blocks * 8, device=device, dtype=torch.int64)
     sh = {"32x32x16": 0, "16x16x32": 1}[shape]
     pli_hip.mfma_probe(out, blocks, iters, sh)
+    torch.cuda.synchronize()
+    t_end = time.perf_counter() + ramp_s
+    while time.perf_counter() < t_end:
+        for _ in range(20):
+            pli_hip.mfma_probe(out, blocks, iters, sh)
+        torch.cuda.synchronize()
     best = float("inf")
     for _ in range(reps):
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
-        pli_hip.mfma_probe(out, blocks, iters, sh)
+        pli_hip.mfma_probe(out, blocks, iters, sh, clocks=clocks)
         e.record()
         e.synchronize()
         best = min(best, s.elapsed_time(e) / 1e3)
-    return blocks * 4 * iters * 4 * (32768 if sh == 0 else 16384) / best / 1e12
+    ck = clocks.view(-1, 2).double().cpu()
+    ghz = (ck[:, 0] / ck[:, 1] * 0.1).median().item()
+    flops = blocks * 4 * iters * 262144
+    return {"TFLOP/s": flops / best / 1e12, "clock_GHz": ghz,
+            "TFLOP/s_at_2.4GHz_equiv": flops / best / 1e12 * 2.4 / ghz if ghz > 0 else None}
+
+
+def measure_mfma_peak(shape: str = "32x32x16", iters: int = 2048, reps: int = 5,
+                      device: str = "cuda") -> float:
+    """Achievable bf16 MFMA TFLOP/s of one shape (``measure_mfma_peak_detail``
+    without the clock ramp)."""
+    return measure_mfma_peak_detail(shape, iters, reps, ramp_s=0.0, device=device)["TFLOP/s"]
 
 
 def measured_spec(hbm_gbps: float, mfma_tflops: float | None = None) -> HardwareSpec:

@@ -13,11 +13,12 @@ reference signature and return contract (a NEW tensor shaped like ``q`` in
 
 ``FlashAttentionConfig`` keeps its four fields (``:6-11``).  They are Triton
 launch knobs in the reference's design notes; on MI355X each one maps to a
-fixed property of the HIP kernel (``hip_tiling`` returns the mapping):
-``block_q`` -> 256 query rows per workgroup (8 waves x 32 rows, one row per
-lane of the swapped QK^T), ``block_k`` -> 64-key K/V tiles, ``num_warps`` ->
-8 wave64s per workgroup, ``num_stages`` -> a 3-deep LDS ring with K/V DMA'd
-two tiles ahead.  The GPU path ignores the requested values (results do not
+fixed property of the default HIP kernel, attn_fwd_v12 (``hip_tiling``
+returns the mapping): ``block_q`` -> 256 query rows per workgroup (4 waves x
+64 rows, one wave per SIMD, one row per lane of the swapped QK^T),
+``block_k`` -> 64-key K/V tiles, ``num_warps`` -> 4 wave64s per workgroup,
+``num_stages`` -> a 5-slot LDS ring with K/V DMA'd two tiles ahead (causal,
+fp16 and D = 64 take attn_fwd_v10 / v7: 4 or 8 waves x 32 rows).  The GPU path ignores the requested values (results do not
 depend on the blocking; the kernel's tiles are set by the MFMA / LDS
 mapping); the CPU recurrence uses ``block_q``/``block_k`` as the reference
 does.  Non-positive or non-integer fields are rejected on both paths.  Softmax statistics are fp32 on both paths (the reference keeps

@@ -1,12 +1,16 @@
 // Roofline calibration kernels (ch03/roofline.py measured ceilings).
 //
-// mfma_probe: every wave issues `iters` rounds of four independent bf16
-// MFMAs from registers (no memory traffic in the loop), operands a pseudo-
-// random bf16 pattern (zeros would let the chip hold a higher clock than any
-// real kernel gets: MI355X_MICROARCH.md 'DVFS give-back').  FLOP count =
-// waves x iters x 4 x (2*M*N*K of the shape).  Gives the matrix-core rate the
-// chip sustains at the clock it holds under that load -- the measured roof
-// beside the 2.5166 PF/s datasheet number.
+// mfma_probe: ONE wave per SIMD (256-thread workgroups holding 96 KiB of LDS,
+// so one per CU), each wave issuing `iters` rounds of back-to-back bf16 MFMAs
+// from registers into independent accumulators, on pseudo-random operands
+// (zeros would let the chip hold a higher clock than any real kernel gets:
+// MI355X_MICROARCH.md 'DVFS give-back').  Both shapes compute the same output
+// tile per wave (a 64x64 f32 block: four 32x32 or sixteen 16x16 accumulators)
+// and the same FLOPs per round (262,144: 8 x 32x32x16 or 16 x 16x16x32), so
+// the two rates compare at equal work -- the guide measures the 16x16x32
+// loop at about 1.15x the FLOP/s of the 32x32x16 one on random data (item 7),
+// a clock effect.  Every wave stamps s_memtime / s_memrealtime around its
+// loop (item 6): the in-kernel clock is dtime / drealtime x 100 MHz.
 #include "pli_common.h"
 
 namespace pli {
@@ -28,7 +32,8 @@ __device__ __forceinline__ int probe_pair(uint32_t h) {
 }
 
 template <int SHAPE>
-__global__ __launch_bounds__(256) void mfma_probe(float* __restrict__ out, int iters) {
+__global__ __launch_bounds__(256, 1) void mfma_probe(float* __restrict__ out,
+                                                     unsigned long long* __restrict__ clocks, int iters) {
     const uint32_t seed = probe_hash(blockIdx.x * 256u + threadIdx.x);
     i32x4 a, b;
 #pragma unroll
@@ -37,28 +42,53 @@ __global__ __launch_bounds__(256) void mfma_probe(float* __restrict__ out, int i
         b[j] = probe_pair(probe_hash(seed + 2 * j + 1));
     }
     float s = 0.f;
+    unsigned long long t0, r0, t1, r1;
+    asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0), "=s"(r0)::"memory");
+    // the MFMAs are asm statements with the accumulators pinned in VGPRs:
+    // compiled from the builtins, hipcc rotates the 16x16x32 accumulators
+    // through AGPR copies inside the loop (v_accvgpr_mov per MFMA), which is
+    // what made the earlier probe read the 16x16x32 rate low.  An accumulator
+    // is re-used 8 (16) MFMAs after its last write, far past the XDL latency;
+    // the s_nops after the loop cover the MFMA -> VALU read.
     if constexpr (SHAPE == 0) {
-        f32x16 c0 = {}, c1 = {}, c2 = {}, c3 = {};
+        f32x16 c[4] = {};
         for (int i = 0; i < iters; ++i) {
-            c0 = mfma32x32x16<bf16_t>(a, b, c0);
-            c1 = mfma32x32x16<bf16_t>(b, a, c1);
-            c2 = mfma32x32x16<bf16_t>(a, a, c2);
-            c3 = mfma32x32x16<bf16_t>(b, b, c3);
-        }
 #pragma unroll
-        for (int r = 0; r < 16; ++r) s += c0[r] + c1[r] + c2[r] + c3[r];
+            for (int j = 0; j < 8; ++j) {
+                const i32x4 x = (j & 1) ? b : a, y = ((j >> 1) ^ (j >> 2)) & 1 ? b : a;
+                asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c[j & 3]) : "v"(x), "v"(y));
+            }
+        }
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]));
+        asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1), "=s"(r1)::"memory");
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s += c[j][r];
     } else {
-        f32x4 c0 = {}, c1 = {}, c2 = {}, c3 = {};
+        f32x4 c[16] = {};
         for (int i = 0; i < iters; ++i) {
-            c0 = mfma16x16x32<bf16_t>(a, b, c0);
-            c1 = mfma16x16x32<bf16_t>(b, a, c1);
-            c2 = mfma16x16x32<bf16_t>(a, a, c2);
-            c3 = mfma16x16x32<bf16_t>(b, b, c3);
-        }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) s += c0[r] + c1[r] + c2[r] + c3[r];
+            for (int j = 0; j < 16; ++j) {
+                const i32x4 x = (j & 1) ? b : a, y = (j & 2) ? b : a;
+                asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c[j]) : "v"(x), "v"(y));
+            }
+        }
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]),
+                     "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]), "+v"(c[8]), "+v"(c[9]), "+v"(c[10]),
+                     "+v"(c[11]), "+v"(c[12]), "+v"(c[13]), "+v"(c[14]), "+v"(c[15]));
+        asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1), "=s"(r1)::"memory");
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s += c[j][r];
     }
     out[blockIdx.x * 256 + threadIdx.x] = s;
+    if (clocks != nullptr && (threadIdx.x & 63) == 0) {
+        const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+        clocks[2 * w] = t1 - t0;
+        clocks[2 * w + 1] = r1 - r0;
+    }
 }
 
 __global__ __launch_bounds__(256) void hbm_read_probe(const i32x4* __restrict__ src, int64_t n16,
@@ -126,14 +156,17 @@ extern "C" int pli_hbm_read_probe(const void* buf, int64_t bytes, uint32_t* out,
     return launch_status("hbm_read_probe");
 }
 
-extern "C" int pli_mfma_probe(float* out, int blocks, int iters, int shape, void* stream) {
+extern "C" int pli_mfma_probe(float* out, uint64_t* clocks, int blocks, int iters, int shape, void* stream) {
     using namespace pli;
     clear_error();
     PLI_REQUIRE(out != nullptr, "pli_mfma_probe: null output");
     PLI_REQUIRE(blocks > 0 && iters > 0 && (shape == 0 || shape == 1),
                 "pli_mfma_probe: bad blocks %d / iters %d / shape %d", blocks, iters, shape);
     hipStream_t s = (hipStream_t)stream;
-    if (shape == 0) hipLaunchKernelGGL((mfma_probe<0>), dim3(blocks), dim3(256), 0, s, out, iters);
-    else hipLaunchKernelGGL((mfma_probe<1>), dim3(blocks), dim3(256), 0, s, out, iters);
+    // 96 KiB of (unused) LDS per workgroup: one workgroup per CU, so one wave per SIMD
+    constexpr size_t kLds = 96 * 1024;
+    auto* ck = reinterpret_cast<unsigned long long*>(clocks);
+    if (shape == 0) hipLaunchKernelGGL((mfma_probe<0>), dim3(blocks), dim3(256), kLds, s, out, ck, iters);
+    else hipLaunchKernelGGL((mfma_probe<1>), dim3(blocks), dim3(256), kLds, s, out, ck, iters);
     return launch_status("mfma_probe");
 }

@@ -1,6 +1,7 @@
 // C ABI glue of libpli_hip.so: version string and thread-local errors.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 
@@ -26,6 +27,25 @@ int launch_status(const char* what) {
         return int(e);
     }
     return PLI_OK;
+}
+
+// CUs of the stream's device, looked up once per device id (a CPX-partitioned
+// or second device of the process gets its own count); 256 if the runtime
+// cannot say
+int cu_count(hipStream_t stream) {
+    static std::atomic<int> cache[64];
+    hipDevice_t dev = 0;
+    if (hipStreamGetDevice(stream, &dev) != hipSuccess) {
+        int d = 0;
+        if (hipGetDevice(&d) != hipSuccess) return 256;
+        dev = d;
+    }
+    if (dev < 0 || dev >= 64) return 256;
+    int n = cache[dev].load(std::memory_order_relaxed);
+    if (n > 0) return n;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev].store(n, std::memory_order_relaxed);
+    return n;
 }
 
 }  // namespace pli

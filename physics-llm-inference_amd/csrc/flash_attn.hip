@@ -523,6 +523,9 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
 //  71: attn_fwd_v12 persistent (one workgroup per CU walking its XCD's
 //      blocks, the K/V stream and the next block's Q across block seams) --
 //      the DEFAULT where 70 applies (1181 vs 1082 TF/s for 55)
+//  72: variant 71 with the defer-max threshold at 0 (a rescale whenever a
+//      tile raises a row's max): tests only, the threshold sweep of
+//      cdna_hip_programming.md rule 26 (72 and 71 agree to rounding)
 constexpr int kDefaultVariant = 71;
 // causal: the 4-wave workgroups of 60 -- 128-row blocks balance the
 // triangular work better and the two workgroups per CU drift apart
@@ -533,18 +536,25 @@ template <typename T, int D>
 int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int H,
                 int group, int Nq, int Nk, const AttnStrides& st, float scale,
                 int causal, hipStream_t stream, int variant) {
-    if (variant == 70 || variant == 71) {
+    // the MFMA bodies' defer-max sets m from the raw score max times c =
+    // scale*log2(e): only for c > 0 is that the row's largest scaled score
+    // (c <= 0 would make exp2(s*c - m) >= 1 and overflow); zero or negative
+    // scales never get here (the generic kernel's max is of the scaled scores).
+    // v7 / v10 also prescale Q by c, so c > 1 could overflow fp16 Q.
+    const float c_log2 = scale * 1.4426950408889634f;
+    const bool c_ok = c_log2 > 0.f && c_log2 <= 1.f;
+    if (variant == 70 || variant == 71 || variant == 72) {
         const bool bf = std::is_same<T, bf16_t>::value;
-        if (attn_v12_ok(D, bf ? 1 : 0, causal, Nk) && scale * 1.4426950408889634f <= 1.f) {
+        if (attn_v12_ok(D, bf ? 1 : 0, causal, Nk) && c_ok) {
             const V7Strides s7{st.qb, st.qh, st.qn, st.kb, st.kh, st.kn,
                                st.vb, st.vh, st.vn, st.ob, st.oh, st.on};
-            return launch_attn_v12(q, k, v, o, B, H, group, Nq, Nk, s7, scale, stream, variant == 71);
+            return launch_attn_v12(q, k, v, o, B, H, group, Nq, Nk, s7, scale, stream, variant != 70,
+                                   variant == 72 ? 0.f : 8.f);
         }
         variant = 55;
     }
     if (variant == 50 || variant == 51 || variant == 54 || variant == 55 || variant == 60) {
-        // v7 prescales Q by scale*log2(e); above 1 that could overflow fp16 Q
-        if (scale * 1.4426950408889634f <= 1.f) {
+        if (c_ok) {
             const V7Strides s7{st.qb, st.qh, st.qn, st.kb, st.kh, st.kn,
                                st.vb, st.vh, st.vn, st.ob, st.oh, st.on};
             return launch_attn_v7(q, k, v, o, B, H, group, Nq, Nk, D, s7, scale, causal,
@@ -618,7 +628,8 @@ extern "C" int pli_flash_attn_fwd_variant(const void* q, const void* k, const vo
     // n_kv == 0 (softmax over no keys) goes to the generic kernel, which
     // defines the output as zeros.
     bool vec = (dtype == PLI_BF16 || dtype == PLI_F16) && (head_dim == 64 || head_dim == 128) &&
-               aligned16(q) && aligned16(k) && aligned16(v) && aligned16(o) && n_kv > 0;
+               aligned16(q) && aligned16(k) && aligned16(v) && aligned16(o) && n_kv > 0 &&
+               scale > 0.f;  // the MFMA kernels' running max assumes a positive scale (launch_mfma)
     for (int i = 0; i < 12; ++i) {
         const bool inner = (i % 3) == 2;
         vec = vec && (strides[i] % 8 == 0) && (!inner || strides[i] >= head_dim);

@@ -111,14 +111,17 @@ __device__ __forceinline__ float v12_xor32_sum(float x) {
 }
 
 typedef __attribute__((ext_vector_type(2))) float v12f2;
-constexpr float V12_THR = 8.f;
+// defer-max threshold THR (log2 units, a template argument so the shipped
+// instantiation's register allocation is not touched): the shipped kernel
+// runs 8; variant 72 (tests only) runs 0, a rescale whenever a tile raises a
+// row's max
 
 #ifdef PLI_FLASH_STAMPS
 // diagnostic build only (tools/build_diag.sh): per-segment s_memtime sums
 __device__ unsigned long long g_v12_stamps[16];
 #endif
 
-template <bool STAMP = false>
+template <bool STAMP = false, int THR = 8>
 __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
     uint16_t* __restrict__ o, int H, int group, int Nq, int Nk, V7Strides st, float c, int qblocks,
@@ -438,7 +441,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     // l, recompute S from the LDS copy of K in slot sk, redo exps and P; block
     // B's slices 8..15, still to come, then use the new m)
     auto settle = [&](i32x4 (&Pc)[2][2][2], int sk) __attribute__((always_inline)) {
-        const bool upA = mxA * c > mA + V12_THR, upB = mxB * c > mB + V12_THR;
+        const bool upA = mxA * c > mA + (float)THR, upB = mxB * c > mB + (float)THR;
         if (__builtin_expect(__builtin_amdgcn_ballot_w64(upA || upB) != 0, 0)) {
             asm volatile("s_nop 7\n\ts_nop 7" : "+v"(lA), "+v"(lB));
             const float nA = upA ? mxA * c : mA, nB = upB ? mxB * c : mB;
@@ -485,7 +488,8 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
 
     // tile t: S(t) and P(t) in Pc = P(t&1); PV of tile t-1 from Pv.  LDS ring
     // of 5 slots, stream tile u in slot u % 5: the DMA of the stream tile two
-    // ahead goes out during phase QA(t) into the slot of stream tile u-3,
+    // ahead goes out during phase QA(t) into the slot of stream tile u-3
+    // (= u+2-NBUF),
     // whose last reader (PV(u-3) in phase P(u-2)) every wave has passed at
     // barrier(u-1); the counted vmcnt(8) before barrier(u) retires tile u+1
     // and leaves u+2 in flight.  Across a block seam the stream continues
@@ -672,30 +676,30 @@ bool attn_v12_ok(int D, int is_bf16, int causal, int Nk) {
 }
 
 int launch_attn_v12(const void* q, const void* k, const void* v, void* o, int B, int H, int group, int Nq,
-                    int Nk, const V7Strides& st, float scale, hipStream_t stream, bool persistent) {
+                    int Nk, const V7Strides& st, float scale, hipStream_t stream, bool persistent, float thr) {
+    PLI_REQUIRE(thr == 0.f || thr == 8.f, "attn_fwd_v12: defer-max threshold %g not built", thr);
     const int qblocks = cdiv(Nq, 256);
     const int64_t nb = (int64_t)B * H * qblocks;
     PLI_REQUIRE(nb < (1ll << 31), "pli_flash_attn_fwd: grid too large");
     const float c = scale * 1.4426950408889634f;
-    // persistent: one workgroup per CU (the kernel holds 160 KiB of LDS and
-    // the whole register file), a multiple of 8 so each walks one XCD; the
-    // stream across block seams needs two tiles per block
+    // persistent: one workgroup per CU of the stream's device (the kernel
+    // holds 160 KiB of LDS and the whole register file), a multiple of 8 so
+    // each walks one XCD; the stream across block seams needs two tiles per
+    // block
     int grid = (int)nb;
     if (persistent && Nk >= 128) {
-        static int ncu = [] {
-            int dev = 0, n = 0;
-            if (hipGetDevice(&dev) != hipSuccess ||
-                hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-                n = 256;
-            return n;
-        }();
-        const int g = ncu / 8 * 8;
+        const int g = cu_count(stream) / 8 * 8;
         if (g >= 8 && nb > g) grid = g;
     }
-    hipLaunchKernelGGL(attn_fwd_v12<false>, dim3((unsigned)grid), dim3(256), 0, stream, (const uint16_t*)q,
-                       (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, H, group, Nq, Nk, st, c, qblocks,
-                       (int)nb);
-    return hipGetLastError() == hipSuccess ? PLI_OK : PLI_EINVAL;
+    if (thr == 0.f)
+        hipLaunchKernelGGL((attn_fwd_v12<false, 0>), dim3((unsigned)grid), dim3(256), 0, stream,
+                           (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, H, group,
+                           Nq, Nk, st, c, qblocks, (int)nb);
+    else
+        hipLaunchKernelGGL((attn_fwd_v12<false, 8>), dim3((unsigned)grid), dim3(256), 0, stream,
+                           (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, H, group,
+                           Nq, Nk, st, c, qblocks, (int)nb);
+    return launch_status("attn_fwd_v12");
 }
 
 }  // namespace pli

@@ -20,6 +20,7 @@ int launch_attn_v7(const void* q, const void* k, const void* v, void* o, int B, 
 // the accumulator file; bf16, D = 128, non-causal, Nk a multiple of 64
 bool attn_v12_ok(int D, int is_bf16, int causal, int Nk);
 int launch_attn_v12(const void* q, const void* k, const void* v, void* o, int B, int H, int group, int Nq,
-                    int Nk, const V7Strides& st, float scale, hipStream_t stream, bool persistent);
+                    int Nk, const V7Strides& st, float scale, hipStream_t stream, bool persistent,
+                    float thr = 8.f);
 
 }  // namespace pli

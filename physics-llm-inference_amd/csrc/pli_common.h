@@ -25,6 +25,8 @@ void clear_error();
 
 // Check the launch that was just enqueued.
 int launch_status(const char* what);
+// Compute units of the device `stream` runs on (cached per device id).
+int cu_count(hipStream_t stream);
 
 // ------------------------------------------------------------ vector types --
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;

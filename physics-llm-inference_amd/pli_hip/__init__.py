@@ -62,7 +62,7 @@ _SIGS = {
     "pli_moe_combine": [_vp, _c_i64, _vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_int, _c_int, _vp],
     "pli_scale_copy": [_vp, _vp, _c_i64, _c_int, _vp],
     "pli_gemm_naive": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_i64, _c_i64, _c_i64, _vp],
-    "pli_mfma_probe": [_vp, _c_int, _c_int, _c_int, _vp],
+    "pli_mfma_probe": [_vp, _vp, _c_int, _c_int, _c_int, _vp],
     "pli_hbm_read_probe": [_vp, _c_i64, _vp, _c_int, _c_int, _vp],
     "pli_softmax_rows": [_vp, _vp, _c_i64, _c_int, _c_int, _vp],
     "pli_online_softmax_with_output": [_vp, _vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_int, _vp],
@@ -705,15 +705,23 @@ def scale_copy(inp: torch.Tensor, out: torch.Tensor, stride: int = 1) -> torch.T
 
 
 # ------------------------------------------------------------------ softmax
-def mfma_probe(out: torch.Tensor, blocks: int, iters: int, shape: int = 0) -> torch.Tensor:
+def mfma_probe(out: torch.Tensor, blocks: int, iters: int, shape: int = 0,
+               clocks: torch.Tensor | None = None) -> torch.Tensor:
     """Launch the MFMA calibration kernel (pli_mfma_probe): ``blocks`` x 256
-    threads, ``iters`` rounds of four bf16 MFMAs per wave (shape 0:
-    32x32x16, 1: 16x16x32); FLOPs = blocks * 4 * iters * 4 * (32768 or 16384)."""
+    threads, one workgroup per CU, ``iters`` rounds of 262,144 bf16 MFMA FLOP
+    per wave (shape 0: 8 x 32x32x16, 1: 16 x 16x16x32); FLOPs = blocks * 4 *
+    iters * 262144.  ``clocks`` (int64, >= blocks * 8, optional) receives per
+    wave the s_memtime and s_memrealtime (100 MHz) ticks around the loop."""
     dev = _require_gpu(out)
     if out.dtype != torch.float32 or not out.is_contiguous() or out.numel() < blocks * 256:
         raise PliError("mfma_probe: out must be contiguous fp32 with >= blocks*256 elements")
+    if clocks is not None:
+        if _require_gpu(clocks) != dev:
+            raise PliError("mfma_probe: clocks on another device")
+        if clocks.dtype != torch.int64 or not clocks.is_contiguous() or clocks.numel() < blocks * 8:
+            raise PliError("mfma_probe: clocks must be contiguous int64 with >= blocks*8 elements")
     with _on_device(dev):
-        rc = lib().pli_mfma_probe(_ptr(out), int(blocks), int(iters), int(shape), _stream(dev))
+        rc = lib().pli_mfma_probe(_ptr(out), _ptr(clocks), int(blocks), int(iters), int(shape), _stream(dev))
     _check(rc, "pli_mfma_probe")
     return out
 
@@ -721,11 +729,16 @@ def mfma_probe(out: torch.Tensor, blocks: int, iters: int, shape: int = 0) -> to
 def hbm_read_probe(buf: torch.Tensor, out: torch.Tensor, blocks: int, mode: int = 0) -> torch.Tensor:
     """Stream ``buf`` (contiguous, 16-byte multiple) with non-temporal 16-byte
     loads, ``blocks`` x 256 threads (pli_hbm_read_probe; mode 0 grid-stride,
-    1 one contiguous slice per block); out: int32 >= blocks*256."""
+    1 one contiguous slice per block); out: contiguous int32 >= blocks*256 on
+    the same device."""
     dev = _require_gpu(buf)
+    if _require_gpu(out) != dev:
+        raise PliError("hbm_read_probe: out on another device")
     nbytes = buf.numel() * buf.element_size()
-    if not buf.is_contiguous() or nbytes % 16 or out.numel() < blocks * 256 or out.element_size() != 4:
-        raise PliError("hbm_read_probe: contiguous buffer of 16k bytes, 4-byte out >= blocks*256")
+    if not buf.is_contiguous() or nbytes % 16:
+        raise PliError("hbm_read_probe: buf must be contiguous with a multiple of 16 bytes")
+    if out.dtype != torch.int32 or not out.is_contiguous() or out.numel() < blocks * 256:
+        raise PliError("hbm_read_probe: out must be contiguous int32 with >= blocks*256 elements")
     with _on_device(dev):
         rc = lib().pli_hbm_read_probe(_ptr(buf), nbytes, _ptr(out), int(blocks), int(mode), _stream(dev))
     _check(rc, "pli_hbm_read_probe")

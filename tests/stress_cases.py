@@ -13,6 +13,12 @@ sides rebuild them bit for bit.
   units in tiles 3 and 9;
 * ``all``    -- Q scaled by 6: |scores| ~ 9 log2 units, the rescale branch in
   many tiles.
+* ``seam2`` / ``seam5`` -- GQA 40/8 (72/8) heads, Q scaled by 4 (peaky rows,
+  the rescale branch in several tiles), shaped so that the persistent flash
+  kernel (variant 71) walks more than one block per workgroup with blocks
+  of 2 (5) key tiles: its K/V stream crosses block seams, and N = 320 gives
+  a ragged last query block.  The reference flash has no GQA: its fixture
+  entry is computed on K/V repeated to the query heads (the same math).
 """
 from __future__ import annotations
 
@@ -20,10 +26,17 @@ import numpy as np
 
 from oracle.numerics import round_to_bf16, seeded_normal
 
-STRESS = ("spike", "first", "late", "all")
+STRESS = ("spike", "first", "late", "all", "seam2", "seam5")
 
 
 def stress_inputs(name: str):
+    if name in ("seam2", "seam5"):
+        B, H, Hkv, N = (4, 72, 8, 128) if name == "seam2" else (4, 40, 8, 320)
+        seed = 21 if name == "seam2" else 25
+        q = seeded_normal((B, H, N, 128), seed, "bf16") * np.float32(4.0)  # exact in bf16
+        k = seeded_normal((B, Hkv, N, 128), seed + 1, "bf16")
+        v = seeded_normal((B, Hkv, N, 128), seed + 2, "bf16")
+        return q, k, v
     if name == "spike":
         B, H, N, D = 1, 2, 512, 128
         q = seeded_normal((B, H, N, D), 7, "bf16")

@@ -112,6 +112,23 @@ def test_ch05_benchmarks_run_on_gpu():
     torch.testing.assert_close(triton_matmul(a, b), torch.matmul(a, b), rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize("m,n,k,blocks", [(64, 64, 64, (32, 32, 32)), (256, 256, 128, None),
+                                           (128, 64, 256, None)])
+def test_ch05_triton_matmul_reference_cases(m, n, k, blocks):
+    """The reference's TestTritonMatmul cases (/root/reference/ch05/test_ch05.py:117-136),
+    which skip forever there without Triton: 64^2 with 32-blocks, 256x128 @
+    128x256 and the non-square 128x256 @ 256x64, fp16, against torch.matmul
+    at the reference's rtol = atol = 1e-2 (the mirror runs the HIP GEMM)."""
+    from ch05 import triton_matmul
+    g = torch.Generator(device=DEV).manual_seed(m + n + k)
+    a = torch.randn(m, k, device=DEV, dtype=torch.float16, generator=g)
+    b = torch.randn(k, n, device=DEV, dtype=torch.float16, generator=g)
+    kw = {} if blocks is None else dict(block_m=blocks[0], block_n=blocks[1], block_k=blocks[2])
+    out = triton_matmul(a, b, **kw)
+    assert out.shape == (m, n) and out.dtype == torch.float16
+    torch.testing.assert_close(out, torch.matmul(a, b), rtol=1e-2, atol=1e-2)
+
+
 @pytest.mark.parametrize("m,n,k,trans_b,bias", [(128, 128, 32, False, False), (200, 136, 68, False, True),
                                                 (1, 300, 1024, True, True), (257, 129, 4, True, False),
                                                 (512, 384, 1000, True, True), (96, 4, 12, False, False)])

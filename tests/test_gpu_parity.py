@@ -106,7 +106,7 @@ def test_flash_vs_oracle(case):
 
 
 # every MFMA variant (alternates A/B-tested by tools/tune.py) on the MFMA-eligible cases
-MFMA_VARIANTS = (21, 50, 51, 54, 55, 60, 70, 71)
+MFMA_VARIANTS = (21, 50, 51, 54, 55, 60, 70, 71, 72)
 
 
 
@@ -474,9 +474,13 @@ def test_row_parallel_rccl_two_ranks():
     """HIP shard GEMM + dist.all_reduce over RCCL ("nccl" backend), 2 ranks
     on 2 GPUs: the all-reduced partials equal the full F.linear within the
     bf16 partial-rounding bound (tests/tp_rccl_worker.py)."""
+    import socket
     import subprocess
     import sys
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29517", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    with socket.socket() as sk:  # a free port: a stale listener on a fixed one would fail the rendezvous
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
     worker = os.path.join(os.path.dirname(__file__), "tp_rccl_worker.py")
     procs = [subprocess.Popen([sys.executable, worker, str(r), "2"], env=env) for r in range(2)]
     rcs = [p.wait(timeout=110) for p in procs]
@@ -568,5 +572,14 @@ def test_calibration_probes():
             assert got == want, (mode, blocks)
     for shape in (0, 1):
         o = torch.zeros(16 * 256, device=DEV, dtype=torch.float32)
-        pli_hip.mfma_probe(o, 16, 64, shape)
+        ck = torch.zeros(16 * 8, device=DEV, dtype=torch.int64)
+        pli_hip.mfma_probe(o, 16, 64, shape, clocks=ck)
         assert torch.isfinite(o).all() and (o != 0).any()
+        ck = ck.view(-1, 2).double().cpu()
+        assert (ck > 0).all(), "every wave stamps its loop"
+        ghz = ck[:, 0] / ck[:, 1] * 0.1
+        assert ((ghz > 0.3) & (ghz < 3.0)).all(), ghz
+    with pytest.raises(pli_hip.PliError):  # a CPU or non-int32 out is refused, not written
+        pli_hip.hbm_read_probe(buf, torch.zeros(256, dtype=torch.int32), 1, 0)
+    with pytest.raises(pli_hip.PliError):
+        pli_hip.hbm_read_probe(buf, torch.zeros(256, device=DEV, dtype=torch.float32), 1, 0)

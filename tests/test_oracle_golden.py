@@ -149,6 +149,9 @@ def test_stress_fixture_matches_inputs():
     from stress_cases import STRESS, stress_inputs
     g = load_golden("stress_flash.npz")
     for name in STRESS:
+        assert np.isfinite(float(g[f"{name}_ref_err"])) and float(g[f"{name}_ref_err"]) > 0
+        if f"{name}_ref_flash" not in g:  # large seam cases: error only (fixture size)
+            continue
         q, k, v = stress_inputs(name)
         ref = oatt.naive_attention(q, k, v)
         out = bf16_from_bits(g[f"{name}_ref_flash"]).astype(np.float64)
