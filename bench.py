@@ -116,6 +116,36 @@ def calibrate() -> dict:
                    "median over waves of s_memtime/s_memrealtime x 100 MHz"}
 
 
+def usable_cores() -> int:
+    """Cores this process can actually run on: the affinity mask, capped by
+    the cgroup CPU quota (cgroup v2 cpu.max / v1 cfs_quota) -- the GPU box
+    shows os.cpu_count() = 256 but grants one GPU's share of them, and
+    torch threads beyond the quota oversubscribe and stall."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                per = int(f.read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    if quota is not None:
+        n = min(n, max(1, int(quota)))
+    return max(1, n)
+
+
 def cpu_info() -> dict:
     """Host CPU as the CPU baselines ran on it: model name, os.cpu_count(),
     the cores this process may run on (cgroup/affinity) and torch threads."""
@@ -133,7 +163,7 @@ def cpu_info() -> dict:
     except (AttributeError, OSError):
         affinity = None
     return {"cpu_model": model, "os_cpu_count": os.cpu_count(), "affinity_cores": affinity,
-            "torch_threads": torch.get_num_threads()}
+            "usable_cores": usable_cores(), "torch_threads": torch.get_num_threads()}
 
 
 def bench_torch_sdpa(q, k, v, o, stream) -> dict:
@@ -414,12 +444,13 @@ def cpu_baseline(seconds: float = 15.0) -> dict:
     g = torch.Generator().manual_seed(0)
     q, k, v = (torch.randn(b, H, S, D, generator=g).to(torch.bfloat16) for _ in range(3))
     flops = 4 * b * H * S * S * D
-    # torch.set_num_threads(os.cpu_count()); the box may grant
-    # this process fewer cores than that (its CPU share), so the default
-    # thread count is timed too and the faster one is the baseline
+    # torch.set_num_threads(os.cpu_count()) -- capped at the
+    # cores the process may actually use (usable_cores: affinity and cgroup
+    # quota; 256 threads on a 16-core share stall in OpenMP barriers), and
+    # torch's default thread count timed beside it; the faster is the baseline
     default_threads = torch.get_num_threads()
     tried, best = {}, None
-    for threads in sorted({os.cpu_count() or 1, default_threads}, reverse=True):
+    for threads in sorted({usable_cores(), default_threads}, reverse=True):
         torch.set_num_threads(threads)
         flash_tile_loop_torch(q[:, :2], k[:, :2], v[:, :2])  # warm
         times, t_end = [], time.perf_counter() + seconds / 2
@@ -440,7 +471,8 @@ def cpu_baseline(seconds: float = 15.0) -> dict:
             "sample": f"reference tile loop (ch06/flash_attention.py:14-74 restated, oracle/attention.py) "
                       f"on torch CPU bf16, B=1 H=32 S=4096 D=128 = 1/8 of the workload, "
                       f"best of {n} runs ({sec:.2f} s each) at {threads} threads "
-                      f"(os.cpu_count() {os.cpu_count()} and the default {default_threads} tried)"}
+                      f"(usable cores {usable_cores()} of os.cpu_count() {os.cpu_count()}, and the default "
+                      f"{default_threads}, tried)"}
 
 
 def cpu_other(cores: int | None = None) -> dict:
@@ -647,7 +679,9 @@ def main():
 
     extra = {}
     measured_roof = {}
+    log(f"[bench] flash: {achieved:.1f} TF/s per launch ({kernel_ms:.3f} ms)")
     if not args.flash_only:
+        log("[bench] calibration")
         cal = calibrate()
         extra["calibration"] = cal
         # the flash kernel's QK^T / PV run on v_mfma_f32_32x32x16_bf16
@@ -674,16 +708,23 @@ def main():
         extra["flash_causal"] = {"ms": ms_c,
                                  "TFLOP/s": 4 * B * H * D * (S * (S + 1) // 2) / (ms_c * 1e-3) / 1e12,
                                  "kernel": CAUSAL_KERNEL}
+        log("[bench] torch sdpa comparison")
         extra["flash_torch_sdpa"] = bench_torch_sdpa(q, k, v, o, stream)
     if args.flash_only:
         pass
     elif not args.quick:
+        log("[bench] gemv")
         extra["gemv"] = bench_gemv(stream, 200)
+        log("[bench] decode attention")
         extra["decode_attn"] = bench_decode(stream, 20)
+        log("[bench] gemm")
         extra["gemm"] = bench_gemm(stream, 20)
+        log("[bench] tp gemm")
         extra["tp_gemm"] = bench_tp(stream, world, rank, 10)
         if world == 1:
+            log("[bench] decode step")
             extra["decode_step"] = bench_decode_step()
+            log("[bench] ch05 demo")
             extra["ch05_matmul_demo"] = bench_matmul_demo()
     else:
         extra["gemv"] = bench_gemv(stream, 200)
@@ -739,6 +780,7 @@ def main():
         **extra,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.quick:
+        log("[bench] cpu baseline")
         result["cpu_baseline"] = cpu_baseline()
         result["cpu_other"] = cpu_other(result["cpu_baseline"]["cores"])
     if rank == 0:

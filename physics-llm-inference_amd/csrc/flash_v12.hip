@@ -38,6 +38,14 @@
 #include "pli_common.h"
 #include "flash_v12_asm.h"
 
+// A/B switches (tools/build_v12_ab.sh); the defaults are the product
+#ifndef V12_DMA_IMM
+#define V12_DMA_IMM 1  // LDS-DMA pieces by instruction offset, one M0 write per 4 pieces
+#endif
+#ifndef V12_SLOT_INC
+#define V12_SLOT_INC 0  // 1: ring slots stepped incrementally (no modulo per use): spills (hipcc parks O in a0/a1)
+#endif
+
 namespace pli {
 namespace {
 
@@ -121,7 +129,9 @@ typedef __attribute__((ext_vector_type(2))) float v12f2;
 __device__ unsigned long long g_v12_stamps[16];
 #endif
 
-template <bool STAMP = false, int THR = 8>
+// STAMP (diagnostic build only): 0 none, 1 per-segment s_memtime sums, 2 the
+// in-kernel clock (s_memtime / s_memrealtime once at entry and exit)
+template <int STAMP = 0, int THR = 8>
 __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
     uint16_t* __restrict__ o, int H, int group, int Nq, int Nk, V7Strides st, float c, int qblocks,
@@ -153,7 +163,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     const int nt = Nk / KT;
     unsigned long long st_sum[14] = {}, st_last = 0;
     auto stamp = [&](int seg) __attribute__((always_inline)) {
-        if constexpr (STAMP) {
+        if constexpr (STAMP == 1) {
             unsigned long long now;
             __builtin_amdgcn_sched_barrier(0);
             asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(now)::"memory");
@@ -163,6 +173,9 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         }
     };
     stamp(-1);
+    unsigned long long clk_t0 = 0, clk_r0 = 0;
+    if constexpr (STAMP == 2)
+        asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(clk_t0), "=s"(clk_r0)::"memory");
 
     // ---- LDS-DMA plan (attn_fwd_v10's, 4 waves: 4 K + 4 V pieces per wave)
     auto fsw = [](int row) __attribute__((always_inline)) { return ((row & 3) << 2) | ((row >> 2) & 3); };
@@ -171,25 +184,55 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     for (int i = 0; i < PPW; ++i) {
         const int drow = 4 * (PPW * wave + i) + (lane >> 4);
         const int ch = (lane & 15) ^ fsw(drow);
-        koff[i] = (uint32_t)(drow * (int)st.kn + 8 * ch) * 2u;
-        voff[i] = (uint32_t)(drow * (int)st.vn + 8 * ch) * 2u;
+        // V12_DMA_IMM: piece i reaches its LDS quarter through the
+        // instruction offset i * 1024, which the hardware adds to the global
+        // address too -- bias the source offset by -i * 1024 (drow >= 4i and
+        // a row is >= 256 B, so the offset stays >= 0)
+        koff[i] = (uint32_t)(drow * (int)st.kn + 8 * ch) * 2u - (V12_DMA_IMM ? 1024u * i : 0u);
+        voff[i] = (uint32_t)(drow * (int)st.vn + 8 * ch) * 2u - (V12_DMA_IMM ? 1024u * i : 0u);
     }
+#if V12_DMA_IMM
+    // one M0 per group of four pieces (a tile's K or V quarter of this wave):
+    // piece 0 of a group writes M0, pieces 1-3 reach their LDS quarter by the
+    // instruction offset.  hipcc itself never touches M0 in this kernel (the
+    // CPU build test checks it), so M0 is not saved or restored.
+    auto dma_first = [&](const uint16_t* tbase, uint32_t off, uint32_t lds) __attribute__((always_inline)) {
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(lds), "v"(off),
+                     "s"(tbase) : "memory");
+    };
+    auto dma_next = [&](auto i_tag, const uint16_t* tbase, uint32_t off) __attribute__((always_inline)) {
+        asm volatile("global_load_lds_dwordx4 %0, %1 offset:%2" ::"v"(off), "s"(tbase),
+                     "n"(1024 * decltype(i_tag)::value) : "memory");
+    };
+#else
     auto dma = [&](const uint16_t* tbase, uint32_t off, uint32_t lds) __attribute__((always_inline)) {
         uint32_t keep;
         asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %3\n\t"
                      "s_mov_b32 m0, %0"
                      : "=&s"(keep) : "s"(lds), "v"(off), "s"(tbase) : "memory");
     };
+#endif
     const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
+    // DMA piece j of a tile: V12_DMA_IMM K pieces 0-3 then V pieces 0-3;
+    // else even j K piece j/2, odd j V piece j/2
+    auto dma_piece = [&](auto j_tag, const uint16_t* kt, const uint16_t* vt, uint32_t base) __attribute__((always_inline)) {
+        constexpr int j = decltype(j_tag)::value;
+#if V12_DMA_IMM
+        constexpr int i = j % 4;
+        const uint16_t* src = j < 4 ? kt : vt;
+        const uint32_t off = j < 4 ? koff[i] : voff[i];
+        if constexpr (i == 0) dma_first(src, off, base + (j < 4 ? 0 : IMG));
+        else dma_next(std::integral_constant<int, i>{}, src, off);
+#else
+        if constexpr (j % 2 == 0) dma(kt, koff[j / 2], base + (j / 2) * 1024);
+        else dma(vt, voff[j / 2], base + IMG + (j / 2) * 1024);
+#endif
+    };
     auto dma_tile = [&](int t, int slot) __attribute__((always_inline)) {
         const uint16_t* kt = kp + (int64_t)t * KT * st.kn;
         const uint16_t* vt = vp + (int64_t)t * KT * st.vn;
         const uint32_t base = lds0 + slot * BUFB + (PPW * wave) * 1024;
-#pragma unroll
-        for (int i = 0; i < PPW; ++i) {
-            dma(kt, koff[i], base + i * 1024);
-            dma(vt, voff[i], base + IMG + i * 1024);
-        }
+        sfor<8>([&](auto J) { dma_piece(J, kt, vt, base); });
     };
 
     // ---- tiles 0 and 1 in flight first, then the Q^T fragments (VGPRs;
@@ -321,13 +364,6 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
             opE(X1{}, std::integral_constant<int, i>{}, H1{});
             opCV(X1{}, std::integral_constant<int, i>{}, Pc);
         });
-    };
-
-    // DMA piece j of a tile (even: K piece j/2, odd: V piece j/2)
-    auto dma_piece = [&](auto j_tag, const uint16_t* kt, const uint16_t* vt, uint32_t base) __attribute__((always_inline)) {
-        constexpr int j = decltype(j_tag)::value;
-        if constexpr (j % 2 == 0) dma(kt, koff[j / 2], base + (j / 2) * 1024);
-        else dma(vt, voff[j / 2], base + IMG + (j / 2) * 1024);
     };
 
     // phase QA: block A's QK^T chains (16 MFMAs); beside them block B's slices
@@ -470,7 +506,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     // t: this block, the next block's tile 0 or 1 (persistent), or past the
     // last block a reload of tile nt-1 (keeps the vmcnt count constant)
     auto dma_src = [&](int t2, const uint16_t*& kt, const uint16_t*& vt) __attribute__((always_inline)) {
-        if (t2 < nt) {
+        if (__builtin_expect(t2 < nt, 1)) {
             kt = kp + (int64_t)t2 * KT * st.kn;
             vt = vp + (int64_t)t2 * KT * st.vn;
         } else if (has_next) {  // recomputed here: fewer scalars live through the block
@@ -494,16 +530,26 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     // barrier(u-1); the counted vmcnt(8) before barrier(u) retires tile u+1
     // and leaves u+2 in flight.  Across a block seam the stream continues
     // (the next block's tiles 0 and 1 are DMA'd by this block's last steps).
+    // V12_SLOT_INC: the step carries slot(t-1) in `sm1` and steps it by one
+    // (wrap at NBUF) instead of a modulo per use
+    int sm1 = 0;
+    auto inc_slot = [](int x) __attribute__((always_inline)) { return x == NBUF - 1 ? 0 : x + 1; };
     auto step = [&](int t, i32x4 (&Pc)[2][2][2], i32x4 (&Pv)[2][2][2]) __attribute__((always_inline)) {
+#if V12_SLOT_INC
+        const int s_m1 = sm1, s_0 = inc_slot(s_m1), s_p1 = inc_slot(s_0), s_p2 = inc_slot(s_p1);
+        sm1 = s_0;
+#else
+        const int s_m1 = slot(t - 1), s_0 = slot(t), s_p1 = slot(t + 1), s_p2 = slot(t + 2);
+#endif
         stamp(6);
         lgkm<0>();  // K(t) fragments in AGPR
         stamp(0);
         {
             const uint16_t *kt, *vt;
             dma_src(t + 2, kt, vt);
-            const uint32_t dbase = lds0 + (uint32_t)slot(t + 2) * BUFB + (PPW * wave) * 1024;
+            const uint32_t dbase = lds0 + (uint32_t)s_p2 * BUFB + (PPW * wave) * 1024;
             phaseQA(Pv, std::true_type{}, kt, vt, dbase);
-            phaseQB(Pv, Pc, std::true_type{}, slot(t - 1));
+            phaseQB(Pv, Pc, std::true_type{}, s_m1);
         }
         stamp(1);
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile t+1 (issued one step ago)
@@ -515,10 +561,9 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         // used) -- one instantiation, so no branch between phase QB's V^T reads
         // and their use here (at a branch hipcc may copy the not-yet-landed
         // fragment registers)
-        phaseP(slot(t - 1), Pv, Pc, slot(t + 1), std::true_type{}, std::true_type{}, std::true_type{},
-               std::true_type{});
+        phaseP(s_m1, Pv, Pc, s_p1, std::true_type{}, std::true_type{}, std::true_type{}, std::true_type{});
         stamp(4);
-        settle(Pc, slot(t));
+        settle(Pc, s_0);
         stamp(5);
     };
 
@@ -590,6 +635,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         }
 
         stamp(6);
+        sm1 = s0;  // slot(0): tile t-1 of the first step
         int t = 1;
         for (; t + 1 < nt; t += 2) {
             step(t, P1, P0);
@@ -657,11 +703,21 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     // the last DMA (a reload of tile nt-1) lands before the LDS is released
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #ifdef PLI_FLASH_STAMPS
-    if constexpr (STAMP) {
+    if constexpr (STAMP == 1) {
         stamp(7);
         if (lane == 0) {
 #pragma unroll
             for (int i = 0; i < 14; ++i) atomicAdd(&g_v12_stamps[i], st_sum[i]);
+            atomicAdd(&g_v12_stamps[14], (unsigned long long)nt * (unsigned long long)nblk);
+            atomicAdd(&g_v12_stamps[15], 1ull);
+        }
+    }
+    if constexpr (STAMP == 2) {
+        unsigned long long t1, r1;
+        asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1), "=s"(r1)::"memory");
+        if (lane == 0) {
+            atomicAdd(&g_v12_stamps[0], t1 - clk_t0);
+            atomicAdd(&g_v12_stamps[1], r1 - clk_r0);
             atomicAdd(&g_v12_stamps[14], (unsigned long long)nt * (unsigned long long)nblk);
             atomicAdd(&g_v12_stamps[15], 1ull);
         }
@@ -692,11 +748,11 @@ int launch_attn_v12(const void* q, const void* k, const void* v, void* o, int B,
         if (g >= 8 && nb > g) grid = g;
     }
     if (thr == 0.f)
-        hipLaunchKernelGGL((attn_fwd_v12<false, 0>), dim3((unsigned)grid), dim3(256), 0, stream,
+        hipLaunchKernelGGL((attn_fwd_v12<0, 0>), dim3((unsigned)grid), dim3(256), 0, stream,
                            (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, H, group,
                            Nq, Nk, st, c, qblocks, (int)nb);
     else
-        hipLaunchKernelGGL((attn_fwd_v12<false, 8>), dim3((unsigned)grid), dim3(256), 0, stream,
+        hipLaunchKernelGGL((attn_fwd_v12<0, 8>), dim3((unsigned)grid), dim3(256), 0, stream,
                            (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, H, group,
                            Nq, Nk, st, c, qblocks, (int)nb);
     return launch_status("attn_fwd_v12");
@@ -710,7 +766,7 @@ int launch_attn_v12(const void* q, const void* k, const void* v, void* o, int B,
 // (segments: tools/v12_stamps.py SEGS; 14 tiles, 15 waves;
 // check, 6 prologue + loop overhead, 7 epilogue; 8 tiles, 9 waves).
 extern "C" int pli_diag_v12_stamps(const void* q, const void* k, const void* v, void* o, int B, int H, int N,
-                                   unsigned long long* out, int grid) {
+                                   unsigned long long* out, int grid, int mode) {
     using namespace pli;
     const int64_t sn = 128, sh = (int64_t)N * 128, sb = (int64_t)H * N * 128;
     const V7Strides st{sb, sh, sn, sb, sh, sn, sb, sh, sn, sb, sh, sn};
@@ -718,9 +774,14 @@ extern "C" int pli_diag_v12_stamps(const void* q, const void* k, const void* v, 
     const float c = (1.f / sqrtf(128.f)) * 1.4426950408889634f;
     unsigned long long zero[16] = {0};
     hipMemcpyToSymbol(HIP_SYMBOL(g_v12_stamps), zero, sizeof(zero));
-    hipLaunchKernelGGL(attn_fwd_v12<true>, dim3(grid > 0 && grid < nb ? grid : nb), dim3(256), 0, 0,
-                       (const uint16_t*)q, (const uint16_t*)k,
-                       (const uint16_t*)v, (uint16_t*)o, H, 1, N, N, st, c, qblocks, nb);
+    const dim3 gr(grid > 0 && grid < nb ? grid : nb);
+    // mode 1: per-segment stamps; mode 2: entry / exit clock only (words 0, 1)
+    if (mode == 2)
+        hipLaunchKernelGGL((attn_fwd_v12<2, 8>), gr, dim3(256), 0, 0, (const uint16_t*)q, (const uint16_t*)k,
+                           (const uint16_t*)v, (uint16_t*)o, H, 1, N, N, st, c, qblocks, nb);
+    else
+        hipLaunchKernelGGL((attn_fwd_v12<1, 8>), gr, dim3(256), 0, 0, (const uint16_t*)q, (const uint16_t*)k,
+                           (const uint16_t*)v, (uint16_t*)o, H, 1, N, N, st, c, qblocks, nb);
     if (hipDeviceSynchronize() != hipSuccess) return -1;
     hipMemcpyFromSymbol(out, HIP_SYMBOL(g_v12_stamps), 16 * sizeof(unsigned long long));
     return 0;

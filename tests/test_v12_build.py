@@ -41,6 +41,10 @@ def test_v12_no_compiler_agpr_use_or_spill(tmp_path):
         if not in_asm and re.search(r"\bv_accvgpr_(read|write)|\bscratch_(load|store)|buffer_(load|store).*off, s\[0:3\]",
                                     line):
             own.append(line.strip())
-    assert not own, f"hipcc-generated AGPR/scratch accesses in attn_fwd_v12: {own[:8]}"
+        # the LDS-DMA asm leaves M0 set between pieces (one write per four
+        # pieces): nothing hipcc generates may read or write M0
+        if not in_asm and re.search(r"\bm0\b", line.split(";")[0]):
+            own.append(line.strip())
+    assert not own, f"hipcc-generated AGPR/scratch/M0 accesses in attn_fwd_v12: {own[:8]}"
     m = re.search(r"\.private_segment_fixed_size:\s+(\d+)", text)
     assert m and int(m.group(1)) == 0, "attn_fwd_v12 uses scratch"

@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""GPU box: interleaved in-process A/B of flash builds (cdna_hip_programming.md
+rule 24).  Every library in $LIBS (space-separated .so paths) is loaded with
+ctypes side by side; each round times $ITERS back-to-back launches of its
+pli_flash_attn_fwd_variant (variant $VARIANT, default -1 = the default
+kernel) on the bench config (random data), libraries interleaved, after a
+warm-up; prints the median / min TF/s per library and whether its output is
+bitwise equal to the first library's.  $CAUSAL=1 times the causal form."""
+import ctypes
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIBS = os.environ.get("LIBS", "tools/ab/libpli_base.so physics-llm-inference_amd/pli_hip/libpli_hip.so").split()
+ROUNDS, ITERS = int(os.environ.get("ROUNDS", "8")), int(os.environ.get("ITERS", "20"))
+VARIANT = int(os.environ.get("VARIANT", "-1"))
+CAUSAL = int(os.environ.get("CAUSAL", "0"))
+B, H, N, D = (int(x) for x in os.environ.get("SHAPE", "8,32,4096,128").split(","))
+libs = []
+for p in LIBS:
+    lib = ctypes.CDLL(os.path.join(ROOT, p) if not os.path.isabs(p) else p)
+    f = lib.pli_flash_attn_fwd_variant
+    f.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int] * 6 + [ctypes.c_void_p, ctypes.c_float, ctypes.c_int,
+                                                                 ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+    f.restype = ctypes.c_int
+    libs.append(f)
+g = torch.Generator(device="cuda").manual_seed(0)
+q, k, v = (torch.randn(B, H, N, D, device="cuda", dtype=torch.bfloat16, generator=g) for _ in range(3))
+outs = [torch.empty_like(q) for _ in libs]
+st = (ctypes.c_int64 * 12)(*(int(x) for t in (q, k, v, q) for x in t.stride()[:3]))
+stream = torch.cuda.current_stream()
+BF16 = 2  # PLI_BF16
+
+
+def call(i):
+    rc = libs[i](q.data_ptr(), k.data_ptr(), v.data_ptr(), outs[i].data_ptr(), B, H, H, N, N, D, st,
+                 D ** -0.5, CAUSAL, BF16, ctypes.c_void_p(stream.cuda_stream), VARIANT)
+    assert rc == 0, (LIBS[i], rc)
+
+
+pairs = N * (N + 1) // 2 if CAUSAL else N * N
+flops = 4 * B * H * D * pairs
+for i in range(len(libs)):
+    for _ in range(30):
+        call(i)
+torch.cuda.synchronize()
+res = {p: [] for p in LIBS}
+for r in range(ROUNDS):
+    for i, p in enumerate(LIBS):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record(stream)
+        for _ in range(ITERS):
+            call(i)
+        e.record(stream)
+        e.synchronize()
+        res[p].append(flops / (s.elapsed_time(e) / ITERS * 1e-3) / 1e12)
+for i, p in enumerate(LIBS):
+    print(json.dumps({"lib": p, "variant": VARIANT, "causal": CAUSAL, "TF/s_median": statistics.median(res[p]),
+                      "TF/s_min": min(res[p]), "TF/s_max": max(res[p]),
+                      "bitwise_eq_first": bool(torch.equal(outs[i], outs[0]))}), flush=True)
