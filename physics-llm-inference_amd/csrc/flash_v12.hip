@@ -42,6 +42,34 @@
 #ifndef V12_DMA_IMM
 #define V12_DMA_IMM 1  // LDS-DMA pieces by instruction offset, one M0 write per 4 pieces
 #endif
+// ablations (timing diagnostics only, results wrong): drop one kind of work
+#ifndef V12_ABL_DMA
+#define V12_ABL_DMA 0
+#endif
+#ifndef V12_ABL_EXP
+#define V12_ABL_EXP 0
+#endif
+#ifndef V12_ABL_KREAD
+#define V12_ABL_KREAD 0
+#endif
+#ifndef V12_ABL_SEL
+#define V12_ABL_SEL 0
+#endif
+#ifndef V12_ABL_SETTLE
+#define V12_ABL_SETTLE 0
+#endif
+#ifndef V12_ABL_BAR
+#define V12_ABL_BAR 0
+#endif
+#ifndef V12_FM_AHEAD
+#define V12_FM_AHEAD 1  // each slice's s*c - m a gap pair ahead of its exps
+#endif
+#ifndef V12_SETTLE2
+#define V12_SETTLE2 1  // defer-max decision on half-row maxes, no permlane on the common path
+#endif
+#ifndef V12_SEL8
+#define V12_SEL8 1  // both blocks' row-sum selector MFMAs in one asm statement
+#endif
 #ifndef V12_SLOT_INC
 #define V12_SLOT_INC 0  // 1: ring slots stepped incrementally (no modulo per use): spills (hipcc parks O in a0/a1)
 #endif
@@ -102,6 +130,20 @@ __device__ __forceinline__ void v12_sel4(f32x4& l, i32x4 sel, i32x4 p0, i32x4 p1
                  "v_mfma_f32_16x16x32_bf16 %0, %1, %3, %0\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %4, %0\n\t"
                  "v_mfma_f32_16x16x32_bf16 %0, %1, %5, %0\n\ts_nop 7\n\ts_nop 2"
                  : "+v"(l) : "v"(sel), "v"(p0), "v"(p1), "v"(p2), "v"(p3));
+}
+
+// both blocks' four selector MFMAs in one statement: block B's chain right
+// behind block A's (independent accumulators), one set of pads
+__device__ __forceinline__ void v12_sel8(f32x4& la, f32x4& lb, i32x4 sel, const i32x4 (&p)[2][2][2]) {
+    asm volatile("s_nop 2\n\tv_mfma_f32_16x16x32_bf16 %0, %2, %3, %0\n\t"
+                 "v_mfma_f32_16x16x32_bf16 %0, %2, %4, %0\n\tv_mfma_f32_16x16x32_bf16 %0, %2, %5, %0\n\t"
+                 "v_mfma_f32_16x16x32_bf16 %0, %2, %6, %0\n\t"
+                 "v_mfma_f32_16x16x32_bf16 %1, %2, %7, %1\n\t"
+                 "v_mfma_f32_16x16x32_bf16 %1, %2, %8, %1\n\tv_mfma_f32_16x16x32_bf16 %1, %2, %9, %1\n\t"
+                 "v_mfma_f32_16x16x32_bf16 %1, %2, %10, %1\n\ts_nop 7\n\ts_nop 2"
+                 : "+v"(la), "+v"(lb)
+                 : "v"(sel), "v"(p[0][0][0]), "v"(p[0][0][1]), "v"(p[0][1][0]), "v"(p[0][1][1]), "v"(p[1][0][0]),
+                   "v"(p[1][0][1]), "v"(p[1][1][0]), "v"(p[1][1][1]));
 }
 
 // MFMA results -> VALU reads: 8-pass XDL needs 12 wait states
@@ -306,10 +348,10 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     auto opE = [&](auto x_tag, auto i_tag, auto h_tag) __attribute__((always_inline)) {
         constexpr int X = decltype(x_tag)::value, i = decltype(i_tag)::value, h = decltype(h_tag)::value;
         if constexpr (h == 0) {
-            se[X][i % 4].x = __builtin_amdgcn_exp2f(sy[X][i % 4].x);
+            se[X][i % 4].x = V12_ABL_EXP ? sy[X][i % 4].x : __builtin_amdgcn_exp2f(sy[X][i % 4].x);
             asm volatile("" : "+v"(se[X][i % 4].x));
         } else {
-            se[X][i % 4].y = __builtin_amdgcn_exp2f(sy[X][i % 4].y);
+            se[X][i % 4].y = V12_ABL_EXP ? sy[X][i % 4].y : __builtin_amdgcn_exp2f(sy[X][i % 4].y);
             asm volatile("" : "+v"(se[X][i % 4].y));
         }
     };
@@ -329,11 +371,29 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     auto stream = [&](auto x_tag, auto i0_tag, auto g_tag, i32x4 (&Pc)[2][2][2]) __attribute__((always_inline)) {
         constexpr int g = decltype(g_tag)::value, I0 = decltype(i0_tag)::value, i = I0 + g / 2;
         if constexpr (g % 2 == 0) {
+#if V12_FM_AHEAD
+            // the FM of slice i was issued a gap pair earlier (by the caller
+            // for the stream's first slice): hipcc pads any instruction that
+            // reads an asm statement's result right after it with s_nop 0
+            // (it cannot tell the asm is no transcendental), so the exp
+            // never follows its own FM
+            opE(x_tag, std::integral_constant<int, i>{}, H0{});
+            if constexpr (g / 2 + 1 < 8) opFM(x_tag, std::integral_constant<int, i + 1>{});
+#else
             opFM(x_tag, std::integral_constant<int, i>{});
             opE(x_tag, std::integral_constant<int, i>{}, H0{});
+#endif
         } else {
             opE(x_tag, std::integral_constant<int, i>{}, H1{});
             if constexpr (g > 1) opCV(x_tag, std::integral_constant<int, i - 1>{}, Pc);
+        }
+    };
+    // V12_FM_AHEAD: the first slice's FM of a stream, ahead of the phase's
+    // first MFMA
+    auto prefm = [&](auto x_tag, auto i_tag) __attribute__((always_inline)) {
+        if constexpr (V12_FM_AHEAD) {
+            opFM(x_tag, i_tag);
+            __builtin_amdgcn_sched_barrier(0);
         }
     };
     // VALU-written P -> MFMA operands: pin P here and pad
@@ -372,12 +432,13 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     auto phaseQA = [&](i32x4 (&Pp)[2][2][2], auto sm_tag, const uint16_t* kt, const uint16_t* vt, uint32_t dbase)
         __attribute__((always_inline)) {
         constexpr bool SM = decltype(sm_tag)::value;
+        if constexpr (SM) prefm(X1{}, std::integral_constant<int, 8>{});
         sfor<16>([&](auto FF) {
             constexpr int F = FF;
             v12::qk1<F, 0>(S[0][F / 8]);
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (SM) stream(X1{}, std::integral_constant<int, 8>{}, FF, Pp);
-            if constexpr (F % 2 == 1) dma_piece(std::integral_constant<int, F / 2>{}, kt, vt, dbase);
+            if constexpr (F % 2 == 1 && !V12_ABL_DMA) dma_piece(std::integral_constant<int, F / 2>{}, kt, vt, dbase);
             __builtin_amdgcn_sched_barrier(0);
         });
     };
@@ -396,6 +457,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         constexpr bool SM = decltype(sm_tag)::value;
         const uint32_t vs = (uint32_t)sv * BUFB;
         mxA = -INFINITY;
+        if constexpr (SM) prefm(X0{}, std::integral_constant<int, 0>{});
         sfor<16>([&](auto FF) {
             constexpr int F = FF;
             v12::qk1<F, 1>(S[1][F / 8]);
@@ -424,6 +486,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         constexpr bool VPRE = decltype(vpre_tag)::value;  // d-block 0 fragments already issued (phase QB)
         const uint32_t vs = (uint32_t)sv * BUFB, ks = (uint32_t)sk * BUFB;
         mxB = -INFINITY;
+        if constexpr (SM) prefm(X0{}, std::integral_constant<int, 8>{});
         if constexpr (PV && !VPRE)
             sfor<4>([&](auto KS) { vread1(std::integral_constant<int, 0>{}, KS, vs); });
         sfor<4>([&](auto DBB) {
@@ -448,12 +511,13 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
                 // gaps 0..3: the next d-block's fragment j; gaps 4..7: K fragment
                 if constexpr (PV && j < 4 && db + 1 < 4)
                     vread1(std::integral_constant<int, db + 1>{}, std::integral_constant<int, j>{}, vs);
-                if constexpr (KR && j >= 4) v12::kread<4 * db + j - 4>(kaddr[(4 * db + j - 4) % 8] + ks);
+                if constexpr (KR && j >= 4 && !V12_ABL_KREAD) v12::kread<4 * db + j - 4>(kaddr[(4 * db + j - 4) % 8] + ks);
                 if constexpr (SM) {
                     if constexpr (slot == 0) opCV(X0{}, std::integral_constant<int, 7>{}, Pc);
                     if constexpr (slot % 2 == 1) opMX(X1{}, std::integral_constant<int, slot / 2>{});
                     if constexpr (slot < 16) {
                         stream(X0{}, std::integral_constant<int, 8>{}, std::integral_constant<int, slot>{}, Pc);
+                        if constexpr (V12_FM_AHEAD && slot == 14) opFM(X1{}, std::integral_constant<int, 0>{});
                     } else {
                         if constexpr (slot == 16) opCV(X0{}, std::integral_constant<int, 15>{}, Pc);
                         stream(X1{}, std::integral_constant<int, 0>{}, std::integral_constant<int, slot - 16>{}, Pc);
@@ -464,10 +528,16 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         });
         if constexpr (SM) opCV(X1{}, std::integral_constant<int, 7>{}, Pc);
         if constexpr (PV) {
-            v12_sel4(lA, sel, Pv[0][0][0], Pv[0][0][1], Pv[0][1][0], Pv[0][1][1]);
-            v12_sel4(lB, sel, Pv[1][0][0], Pv[1][0][1], Pv[1][1][0], Pv[1][1][1]);
+            if (!V12_ABL_SEL) {
+#if V12_SEL8
+                v12_sel8(lA, lB, sel, Pv);
+#else
+                v12_sel4(lA, sel, Pv[0][0][0], Pv[0][0][1], Pv[0][1][0], Pv[0][1][1]);
+                v12_sel4(lB, sel, Pv[1][0][0], Pv[1][0][1], Pv[1][1][0], Pv[1][1][1]);
+#endif
+            }
         }
-        if constexpr (SM) {
+        if constexpr (SM && !V12_SETTLE2) {
             mxA = v12_xor32_max(mxA);
             mxB = v12_xor32_max(mxB);
         }
@@ -477,10 +547,38 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     // l, recompute S from the LDS copy of K in slot sk, redo exps and P; block
     // B's slices 8..15, still to come, then use the new m)
     auto settle = [&](i32x4 (&Pc)[2][2][2], int sk) __attribute__((always_inline)) {
+#if V12_SETTLE2
+        // V12_SETTLE2: decided on each lane's HALF-row maxes (lanes l and
+        // l^32 hold the two key halves of a row): fl(x*c) is non-decreasing
+        // in x, so some half's max*c exceeds m + THR exactly when the full
+        // row's does -- the same decision with no permlane merge, two
+        // compares and one SGPR test; the merge runs on the rare path
+        // mxA / mxB are scaled in place (fl(max * c) = max of fl(half * c)),
+        // one temporary for the thresholds: the allocation has no room
+        float t;
+        uint64_t hit;
+        static_assert(THR == 0 || THR == 8, "threshold literal");
+#define V12_SETTLE_ASM(T)                                                                                      \
+    asm volatile("v_mul_f32 %0, %0, %4\n\tv_mul_f32 %1, %1, %4\n\tv_add_f32 %2, " T ", %5\n\t"              \
+                 "v_cmp_gt_f32_e64 %3, %0, %2\n\tv_add_f32 %2, " T ", %6\n\tv_cmp_gt_f32_e64 vcc, %1, %2\n\t" \
+                 "s_or_b64 %3, %3, vcc"                                                                        \
+                 : "+v"(mxA), "+v"(mxB), "=&v"(t), "=&s"(hit)                                                  \
+                 : "v"(c), "v"(mA), "v"(mB) : "vcc", "scc")
+        if constexpr (THR == 8) V12_SETTLE_ASM("0x41000000");
+        else V12_SETTLE_ASM("0");
+#undef V12_SETTLE_ASM
+        if (__builtin_expect(hit != 0, 0)) {
+            mxA = v12_xor32_max(mxA);  // now the full rows' scaled maxes
+            mxB = v12_xor32_max(mxB);
+            const bool upA = mxA > mA + (float)THR, upB = mxB > mB + (float)THR;
+            asm volatile("s_nop 7\n\ts_nop 7" : "+v"(lA), "+v"(lB));
+            const float nA = upA ? mxA : mA, nB = upB ? mxB : mB;
+#else
         const bool upA = mxA * c > mA + (float)THR, upB = mxB * c > mB + (float)THR;
         if (__builtin_expect(__builtin_amdgcn_ballot_w64(upA || upB) != 0, 0)) {
             asm volatile("s_nop 7\n\ts_nop 7" : "+v"(lA), "+v"(lB));
             const float nA = upA ? mxA * c : mA, nB = upB ? mxB * c : mB;
+#endif
             const float alA = __builtin_amdgcn_exp2f(mA - nA), alB = __builtin_amdgcn_exp2f(mB - nB);
             mA = nA;
             mB = nB;
@@ -554,7 +652,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         stamp(1);
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile t+1 (issued one step ago)
         stamp(2);
-        __syncthreads();
+        if (!V12_ABL_BAR) __syncthreads();
         stamp(3);
         asm volatile("s_nop 1" ::: "memory");  // P just written -> MFMA operands
         // K(t+1) fragments; past the last tile they read a stale slot (never
@@ -563,7 +661,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         // fragment registers)
         phaseP(s_m1, Pv, Pc, s_p1, std::true_type{}, std::true_type{}, std::true_type{}, std::true_type{});
         stamp(4);
-        settle(Pc, s_0);
+        if (!V12_ABL_SETTLE) settle(Pc, s_0);
         stamp(5);
     };
 
