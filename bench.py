@@ -382,6 +382,7 @@ def bench_tp(stream, world: int, rank: int, iters: int) -> dict:
                                  "torch_F.linear_TFLOP/s": fl / (t["torch"] * 1e-3) / 1e12}
             del xs, wsh
         out["shard_gemm_per_rank"] = shards
+        out["partial_rounding"] = partial_rounding_by_tp()
     if world > 1:
         def ar():
             dist.all_reduce(y)
@@ -402,6 +403,42 @@ def bench_tp(stream, world: int, rank: int, iters: int) -> dict:
                     "allreduce_busbw_GB/s": payload / (ms_ar * 1e-3) / 1e9 * bounds["bus_factor"],
                     "xgmi_mesh_bound_us": bounds["mesh_us"], "xgmi_ring_bound_us": bounds["ring_us"]})
     return out
+
+
+def partial_rounding_by_tp(M: int = 1024, N: int = 8192, K: int = 8192) -> dict:
+    """Error of the row-parallel sum against the f64 product by TP degree
+    (ch09 RowParallelLinear, all-reduce simulated on one GPU by summing the
+    tp shard partials in fp32): bf16 partials (each rank's output rounded,
+    the default) vs fp32 partials (reduce_dtype=torch.float32,
+    pli_gemm_f32out); the sum is rounded to bf16 once at the end.  Also the
+    TP-8 shard's fp32-output GEMM time beside the bf16 one at M = 8192."""
+    import pli_hip
+    g = torch.Generator(device="cuda").manual_seed(7)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16, generator=g)
+    w = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).to(torch.bfloat16)
+    ref = x.double() @ w.double().T
+    scale = ref.abs().mean().item()
+    res = {"workload": f"M={M} N={N} K={K} bf16, f64 reference", "mean_|ref|": scale}
+    for tp in (1, 2, 4, 8):
+        ks = K // tp
+        s16 = torch.zeros(M, N, device="cuda")
+        s32 = torch.zeros(M, N, device="cuda")
+        for r in range(tp):
+            xs, wsh = x[:, r * ks:(r + 1) * ks], w[:, r * ks:(r + 1) * ks]
+            s16 += pli_hip.gemm(xs, wsh, trans_b=True).float()
+            s32 += pli_hip.gemm_f32out(xs, wsh)
+        e16 = (s16.bfloat16().double() - ref).abs()
+        e32 = (s32.bfloat16().double() - ref).abs()
+        res[f"tp{tp}"] = {"bf16_partials_mean_err": e16.mean().item(), "bf16_partials_max_err": e16.max().item(),
+                          "fp32_partials_mean_err": e32.mean().item(), "fp32_partials_max_err": e32.max().item()}
+    xs = torch.randn(8192, K // 8, device="cuda", dtype=torch.bfloat16, generator=g)
+    ws = (torch.randn(N, K // 8, device="cuda", generator=g) * (K // 8) ** -0.5).to(torch.bfloat16)
+    y16 = torch.empty(8192, N, device="cuda", dtype=torch.bfloat16)
+    y32 = torch.empty(8192, N, device="cuda", dtype=torch.float32)
+    t = paired_time_ms({"bf16": lambda: pli_hip.gemm(xs, ws, trans_b=True, out=y16),
+                        "fp32": lambda: pli_hip.gemm_f32out(xs, ws, out=y32)}, 10, torch.cuda.current_stream())
+    res["tp8_shard_M8192_us"] = {"bf16_out": t["bf16"] * 1e3, "fp32_out": t["fp32"] * 1e3}
+    return res
 
 
 def bench_decode_step(batches=(1, 32), prompt: int = 512, steps: int = 32) -> dict:

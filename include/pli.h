@@ -94,6 +94,17 @@ int pli_gemm(const void* a, const void* b, void* c, const void* bias, int m,
              int dtype, void* stream);
 
 /*
+ * NT GEMM with an fp32 output: C[m, n] = A[m, k] * B[n, k]^T, A / B bf16 or
+ * fp16 (dtype), C fp32 contiguous (ldc = n), fp32 accumulate -- the
+ * row-parallel partial of ch09/tensor_parallel.py:66-68 kept in fp32 so the
+ * all-reduce sums unrounded partials (RowParallelLinear(reduce_dtype=
+ * torch.float32)).  K % 64 == 0, N % 32 == 0, 16-byte aligned rows: the LDS
+ * split-K kernel with one slice; other shapes a one-thread-per-output kernel.
+ */
+int pli_gemm_f32out(const void* a, const void* b, float* c, int m, int n, int k, int64_t lda,
+                    int64_t ldb, int dtype, void* stream);
+
+/*
  * pli_gemm with a caller-owned device workspace (16-byte aligned) of at least
  * pli_gemm_workspace_size(m, n, k, trans_b, dtype) bytes (0: none needed, the
  * call is pli_gemm).  Decode-batch / TP-shard NT shapes (16 < m <= 256) then

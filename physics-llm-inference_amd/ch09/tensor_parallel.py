@@ -49,6 +49,15 @@ def _shard_linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None) -
     return y.view(*lead, w.shape[0])
 
 
+def _shard_linear_f32(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """y = x W^T in fp32 (the unrounded partial); HIP pli_gemm_f32out on ROCm."""
+    lead = x.shape[:-1]
+    if not x.is_cuda:
+        return F.linear(x.float(), w.detach().float())
+    y = pli_hip.gemm_f32out(x.reshape(-1, x.shape[-1]), w.detach())
+    return y.view(*lead, w.shape[0])
+
+
 def tp_group_active(world_size: int, group=None) -> bool:
     """True when a process group of exactly ``world_size`` ranks exists."""
     return (world_size > 1 and dist.is_available() and dist.is_initialized()
@@ -75,14 +84,22 @@ class ColumnParallelLinear(nn.Module):
 
 
 class RowParallelLinear(nn.Module):
-    """Y = sum_r X_r W_r^T with W_r the rank's [out, in/ws] column block."""
+    """Y = sum_r X_r W_r^T with W_r the rank's [out, in/ws] column block.
+
+    ``reduce_dtype=torch.float32`` keeps each rank's partial in fp32 (HIP
+    ``pli_gemm_f32out`` on ROCm) through the all-reduce and rounds the sum to
+    the input dtype once; the default rounds every partial to the input dtype
+    first (the reference's F.linear output), so TP ranks stack that many
+    roundings (error by TP degree: bench.py ``tp_gemm.partial_rounding``)."""
 
     def __init__(self, in_features: int, out_features: int, world_size: int = 1, rank: int = 0,
-                 bias: bool = False, group=None):
+                 bias: bool = False, group=None, reduce_dtype: torch.dtype | None = None):
         super().__init__()
         self.world_size = world_size
         self.rank = rank
         self.group = group
+        assert reduce_dtype in (None, torch.float32), "reduce_dtype: None or torch.float32"
+        self.reduce_dtype = reduce_dtype
         assert in_features % world_size == 0
         self.in_features_per_partition = in_features // world_size
         self.weight = nn.Parameter(torch.empty(out_features, self.in_features_per_partition))
@@ -90,6 +107,11 @@ class RowParallelLinear(nn.Module):
         nn.init.kaiming_uniform_(self.weight)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.reduce_dtype is not None and x.dtype != self.reduce_dtype:
+            y = _shard_linear_f32(x, self.weight)  # reference ignores the bias (:66-68)
+            if tp_group_active(self.world_size, self.group):
+                dist.all_reduce(y, op=dist.ReduceOp.SUM, group=self.group)
+            return y.to(x.dtype)
         y = _shard_linear(x, self.weight, None)  # reference ignores the bias (:66-68)
         if tp_group_active(self.world_size, self.group):
             dist.all_reduce(y, op=dist.ReduceOp.SUM, group=self.group)

@@ -1762,7 +1762,7 @@ inline int splitk_slices(int M, int N, int K, int target, int max_m = 256) {
 template <typename T>
 int launch_splitk(const void* a, const void* b, void* c, const void* bias, int M, int N, int K,
                   int64_t lda, int64_t ldb, int64_t ldc, int ks, float* ws, hipStream_t s,
-                  bool lds = false, bool nb3 = false) {
+                  bool lds = false, bool nb3 = false, bool f32out = false) {
     const dim3 grid(cdiv(N, 128), ks, cdiv(M, 128)), block(256);
     const int mc = cdiv(min(M, 128), 32);
     const int kslice = K / ks;
@@ -1788,6 +1788,10 @@ int launch_splitk(const void* a, const void* b, void* c, const void* bias, int M
         else if (mc == 3) PLI_SK(3, PA, BI); \
         else PLI_SK(4, PA, BI);             \
     } while (0)
+    if (f32out) {  // one slice, the fp32 plane is the product (pli_gemm_f32out)
+        PLI_SK_MC(true, false);
+        return launch_status("gemm_splitk_lds_nt");
+    }
     if (ks > 1) {
         PLI_SK_MC(true, false);
         const int rc = launch_status("gemm_splitk_nt");
@@ -2254,6 +2258,62 @@ extern "C" int pli_gemm(const void* a, const void* b, void* c, const void* bias,
                         int k, int64_t lda, int64_t ldb, int64_t ldc, int trans_b, int dtype,
                         void* stream) {
     return pli_gemm_variant(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, dtype, stream, 0);
+}
+
+namespace pli {
+namespace {
+// fp32-output fallback for shapes the LDS kernel does not take: one thread
+// per output, fp32 accumulation in k order
+template <typename T>
+__global__ __launch_bounds__(256) void gemm_f32out_generic(const T* __restrict__ A, const T* __restrict__ Bm,
+                                                           float* __restrict__ C, int M, int N, int K,
+                                                           int64_t lda, int64_t ldb) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)M * N) return;
+    const int m = (int)(i / N), n = (int)(i % N);
+    const T* a = A + (int64_t)m * lda;
+    const T* b = Bm + (int64_t)n * ldb;
+    float acc = 0.f;
+    for (int k = 0; k < K; ++k) acc = fmaf(elem<T>::to_f32(a[k]), elem<T>::to_f32(b[k]), acc);
+    C[i] = acc;
+}
+}  // namespace
+}  // namespace pli
+
+// C[m][n] = sum_k A[m][k] B[n][k] (NT, the F.linear layout) with bf16 / fp16
+// inputs and an fp32 output, contiguous [m, n]: the row-parallel partial of
+// ch09/tensor_parallel.py:66-68 kept in fp32 for the all-reduce.  The LDS
+// split-K kernel of pli_gemm_ws with one slice writes its fp32 tile straight
+// to C; other shapes take a one-thread-per-output kernel.
+extern "C" int pli_gemm_f32out(const void* a, const void* b, float* c, int m, int n, int k, int64_t lda,
+                               int64_t ldb, int dtype, void* stream) {
+    using namespace pli;
+    clear_error();
+    PLI_REQUIRE(a && b && c, "pli_gemm_f32out: null pointer");
+    PLI_REQUIRE(m >= 0 && n >= 0 && k >= 0 && lda >= k && ldb >= k,
+                "pli_gemm_f32out: bad shape m=%d n=%d k=%d lda=%lld ldb=%lld", m, n, k, (long long)lda,
+                (long long)ldb);
+    PLI_REQUIRE(dtype == PLI_BF16 || dtype == PLI_F16, "pli_gemm_f32out: bf16 / fp16 inputs only (%d)", dtype);
+    if (m == 0 || n == 0) return PLI_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const bool lds = k % 64 == 0 && k > 0 && n % 32 == 0 && lda % 8 == 0 && ldb % 8 == 0 && al16(a) &&
+                     al16(b) && al16(c);
+    if (lds) {
+        if (dtype == PLI_BF16)
+            return launch_splitk<bf16_t>(a, b, nullptr, nullptr, m, n, k, lda, ldb, n, 1, c, s, true, false,
+                                         true);
+        return launch_splitk<f16_t>(a, b, nullptr, nullptr, m, n, k, lda, ldb, n, 1, c, s, true, false, true);
+    }
+    const int64_t total = (int64_t)m * n;
+    PLI_REQUIRE(total / 256 < (1ll << 31), "pli_gemm_f32out: grid too large");
+    const dim3 grid((unsigned)((total + 255) / 256));
+    if (dtype == PLI_BF16)
+        hipLaunchKernelGGL(gemm_f32out_generic<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)a, (const bf16_t*)b,
+                           c, m, n, k, lda, ldb);
+    else
+        hipLaunchKernelGGL(gemm_f32out_generic<f16_t>, grid, dim3(256), 0, s, (const f16_t*)a, (const f16_t*)b,
+                           c, m, n, k, lda, ldb);
+    return launch_status("gemm_f32out_generic");
 }
 
 // Grouped NT GEMM over experts (see gemm_grouped_nt): C[r] = X[gather[r]] W_e^T

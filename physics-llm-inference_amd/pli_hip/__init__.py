@@ -15,7 +15,7 @@ import torch
 
 __all__ = [
     "PliError", "lib", "library_path", "available", "DTYPE_CODE",
-    "flash_attn_fwd", "gemv", "gemm", "scale_copy", "mfma_probe", "hbm_read_probe", "softmax_rows",
+    "flash_attn_fwd", "gemv", "gemm", "gemm_f32out", "scale_copy", "mfma_probe", "hbm_read_probe", "softmax_rows",
     "online_softmax_with_output",
 ]
 
@@ -62,6 +62,7 @@ _SIGS = {
     "pli_moe_combine": [_vp, _c_i64, _vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_int, _c_int, _vp],
     "pli_scale_copy": [_vp, _vp, _c_i64, _c_int, _vp],
     "pli_gemm_naive": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_i64, _c_i64, _c_i64, _vp],
+    "pli_gemm_f32out": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_i64, _c_i64, _c_int, _vp],
     "pli_mfma_probe": [_vp, _vp, _c_int, _c_int, _c_int, _vp],
     "pli_hbm_read_probe": [_vp, _c_i64, _vp, _c_int, _c_int, _vp],
     "pli_softmax_rows": [_vp, _vp, _c_i64, _c_int, _c_int, _vp],
@@ -705,6 +706,29 @@ def scale_copy(inp: torch.Tensor, out: torch.Tensor, stride: int = 1) -> torch.T
 
 
 # ------------------------------------------------------------------ softmax
+def gemm_f32out(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """fp32 [m, n] = x [m, k] @ w [n, k]^T for bf16 / fp16 x, w (pli_gemm_f32out):
+    the row-parallel partial kept unrounded for the all-reduce."""
+    dev = _require_gpu(x, w)
+    if x.dim() != 2 or w.dim() != 2 or x.shape[1] != w.shape[1]:
+        raise PliError(f"gemm_f32out: x {tuple(x.shape)} and w {tuple(w.shape)} must be [m, k] and [n, k]")
+    if x.dtype not in (torch.bfloat16, torch.float16):
+        raise PliError("gemm_f32out: bf16 / fp16 inputs only")
+    x = x if x.stride(1) == 1 else x.contiguous()
+    w = w if w.stride(1) == 1 else w.contiguous()
+    m, k = x.shape
+    n = w.shape[0]
+    if out is None:
+        out = torch.empty(m, n, dtype=torch.float32, device=dev)
+    if out.dtype != torch.float32 or tuple(out.shape) != (m, n) or not out.is_contiguous() or out.device != dev:
+        raise PliError("gemm_f32out: out must be a contiguous fp32 [m, n] tensor on the inputs' device")
+    with _on_device(dev):
+        rc = lib().pli_gemm_f32out(_ptr(x), _ptr(w), _ptr(out), m, n, k, x.stride(0), w.stride(0),
+                                   _dtype_code(x), _stream(dev))
+    _check(rc, "pli_gemm_f32out")
+    return out
+
+
 def mfma_probe(out: torch.Tensor, blocks: int, iters: int, shape: int = 0,
                clocks: torch.Tensor | None = None) -> torch.Tensor:
     """Launch the MFMA calibration kernel (pli_mfma_probe): ``blocks`` x 256

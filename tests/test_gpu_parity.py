@@ -583,3 +583,41 @@ def test_calibration_probes():
         pli_hip.hbm_read_probe(buf, torch.zeros(256, dtype=torch.int32), 1, 0)
     with pytest.raises(pli_hip.PliError):
         pli_hip.hbm_read_probe(buf, torch.zeros(256, device=DEV, dtype=torch.float32), 1, 0)
+
+
+@pytest.mark.parametrize("m,n,k", [(512, 1024, 2048), (200, 96, 128), (33, 40, 72), (1, 64, 64)])
+def test_gemm_f32out_vs_f64(m, n, k):
+    """pli_gemm_f32out (NT, bf16 in, fp32 out): the LDS split-K route (K % 64,
+    N % 32) and the one-thread-per-output route, against the f64 product of
+    the same bf16 inputs; fp32 accumulation, so 1e-5 relative."""
+    import pli_hip
+    x, w = seeded_normal((m, k), 91, "bf16"), seeded_normal((n, k), 92, "bf16")
+    y = pli_hip.gemm_f32out(dev(x, "bf16"), dev(w, "bf16")).cpu().numpy().astype(np.float64)
+    ref = olin.linear(x, w)
+    assert y.dtype == np.float64 and np.abs(y - ref).max() <= 1e-5 * (np.abs(ref).max() + 1)
+
+
+@pytest.mark.parametrize("tp", [2, 4, 8])
+def test_row_parallel_fp32_partials_error_by_tp(tp):
+    """The TP row-parallel sum at tp shards of an 8192-wide layer (M = 256):
+    bf16 partials (the reference's F.linear per rank) stack tp roundings,
+    fp32 partials (reduce_dtype=torch.float32) round once.  Both within the
+    bf16 bound of the f64 product; fp32 partials no worse than bf16 ones."""
+    import pli_hip
+    M, N, K = 256, 8192, 8192
+    g = torch.Generator(device=DEV).manual_seed(tp)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16, generator=g)
+    w = (torch.randn(N, K, device=DEV, generator=g) * K ** -0.5).to(torch.bfloat16)
+    ref = x.double() @ w.double().T
+    ks = K // tp
+    s16 = torch.zeros(M, N, device=DEV, dtype=torch.float32)
+    s32 = torch.zeros(M, N, device=DEV, dtype=torch.float32)
+    for r in range(tp):
+        xs, wsh = x[:, r * ks:(r + 1) * ks], w[:, r * ks:(r + 1) * ks]
+        s16 += pli_hip.gemm(xs, wsh, trans_b=True).float()
+        s32 += pli_hip.gemm_f32out(xs, wsh)
+    e16 = (s16.to(torch.bfloat16).double() - ref).abs()
+    e32 = (s32.to(torch.bfloat16).double() - ref).abs()
+    bound = 1e-2 * (ref.abs() + 1)
+    assert (e16 <= bound).all() and (e32 <= bound).all()
+    assert e32.mean().item() <= e16.mean().item()

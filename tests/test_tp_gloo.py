@@ -44,13 +44,18 @@ def _worker(rank: int, world: int, port: int, out_dir: str):
             layer.weight.copy_(w[:, sl])
             y = layer(x[:, sl])
             y2 = row_parallel_forward_overlapped(x[:, sl], layer.weight, chunks=3)
+            # fp32 partials through the all-reduce (reduce_dtype), bf16 input
+            l32 = RowParallelLinear(K, N, world_size=world, rank=rank, reduce_dtype=torch.float32)
+            l32.weight.copy_(w[:, sl])
+            y3 = l32.to(torch.bfloat16)(x[:, sl].to(torch.bfloat16)).float()
         # TP MLP: every rank must end with the same full output
         torch.manual_seed(100 + rank)
         mlp = TensorParallelMLP(TensorParallelConfig(world_size=world, rank=rank, hidden_dim=16,
                                                      intermediate_dim=32))
         with torch.no_grad():
             ym = mlp(torch.ones(3, 16))
-        np.savez(os.path.join(out_dir, f"rank{rank}.npz"), y=y.numpy(), y2=y2.numpy(), ym=ym.numpy())
+        np.savez(os.path.join(out_dir, f"rank{rank}.npz"), y=y.numpy(), y2=y2.numpy(), ym=ym.numpy(),
+                 y3=y3.numpy())
     finally:
         dist.destroy_process_group()
 
@@ -68,3 +73,8 @@ def test_row_parallel_allreduce_gloo_world2(tmp_path):
         np.testing.assert_allclose(ri["y"], full, rtol=1e-5, atol=1e-5)
         np.testing.assert_allclose(ri["y2"], full, rtol=1e-5, atol=1e-5)
     np.testing.assert_array_equal(r[0]["ym"], r[1]["ym"])
+    # bf16 inputs, fp32 partials summed by the all-reduce, one rounding at the end
+    from oracle.numerics import round_to_bf16
+    full16 = linear(round_to_bf16(x), round_to_bf16(w))
+    for ri in r:
+        assert np.abs(ri["y3"] - full16).max() <= 2.0 ** -8 * (np.abs(full16).max() + 1)
