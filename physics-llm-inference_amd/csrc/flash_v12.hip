@@ -70,6 +70,9 @@
 #ifndef V12_SEL8
 #define V12_SEL8 1  // both blocks' row-sum selector MFMAs in one asm statement
 #endif
+#ifndef V12_UNROLL4
+#define V12_UNROLL4 0  // four steps per loop iteration (A/B)
+#endif
 #ifndef V12_SLOT_INC
 #define V12_SLOT_INC 0  // 1: ring slots stepped incrementally (no modulo per use): spills (hipcc parks O in a0/a1)
 #endif
@@ -735,6 +738,14 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         stamp(6);
         sm1 = s0;  // slot(0): tile t-1 of the first step
         int t = 1;
+#if V12_UNROLL4
+        for (; t + 3 < nt; t += 4) {
+            step(t, P1, P0);
+            step(t + 1, P0, P1);
+            step(t + 2, P1, P0);
+            step(t + 3, P0, P1);
+        }
+#endif
         for (; t + 1 < nt; t += 2) {
             step(t, P1, P0);
             step(t + 1, P0, P1);

@@ -19,7 +19,7 @@ LIBS = os.environ.get("LIBS", "tools/ab/libpli_base.so physics-llm-inference_amd
 ROUNDS, ITERS = int(os.environ.get("ROUNDS", "8")), int(os.environ.get("ITERS", "20"))
 VARIANT = int(os.environ.get("VARIANT", "-1"))
 CAUSAL = int(os.environ.get("CAUSAL", "0"))
-B, H, N, D = (int(x) for x in os.environ.get("SHAPE", "8,32,4096,128").split(","))
+SHAPES = [tuple(int(x) for x in sh.split(",")) for sh in os.environ.get("SHAPE", "8,32,4096,128").split(";")]
 libs = []
 for p in LIBS:
     lib = ctypes.CDLL(os.path.join(ROOT, p) if not os.path.isabs(p) else p)
@@ -28,37 +28,38 @@ for p in LIBS:
                                                                  ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
     f.restype = ctypes.c_int
     libs.append(f)
-g = torch.Generator(device="cuda").manual_seed(0)
-q, k, v = (torch.randn(B, H, N, D, device="cuda", dtype=torch.bfloat16, generator=g) for _ in range(3))
-outs = [torch.empty_like(q) for _ in libs]
-st = (ctypes.c_int64 * 12)(*(int(x) for t in (q, k, v, q) for x in t.stride()[:3]))
 stream = torch.cuda.current_stream()
 BF16 = 2  # PLI_BF16
+for (B, H, N, D) in SHAPES:
+    g = torch.Generator(device="cuda").manual_seed(0)
+    q, k, v = (torch.randn(B, H, N, D, device="cuda", dtype=torch.bfloat16, generator=g) for _ in range(3))
+    outs = [torch.empty_like(q) for _ in libs]
+    st = (ctypes.c_int64 * 12)(*(int(x) for t in (q, k, v, q) for x in t.stride()[:3]))
 
+    def call(i):
+        rc = libs[i](q.data_ptr(), k.data_ptr(), v.data_ptr(), outs[i].data_ptr(), B, H, H, N, N, D, st,
+                     D ** -0.5, CAUSAL, BF16, ctypes.c_void_p(stream.cuda_stream), VARIANT)
+        assert rc == 0, (LIBS[i], rc)
 
-def call(i):
-    rc = libs[i](q.data_ptr(), k.data_ptr(), v.data_ptr(), outs[i].data_ptr(), B, H, H, N, N, D, st,
-                 D ** -0.5, CAUSAL, BF16, ctypes.c_void_p(stream.cuda_stream), VARIANT)
-    assert rc == 0, (LIBS[i], rc)
-
-
-pairs = N * (N + 1) // 2 if CAUSAL else N * N
-flops = 4 * B * H * D * pairs
-for i in range(len(libs)):
-    for _ in range(30):
-        call(i)
-torch.cuda.synchronize()
-res = {p: [] for p in LIBS}
-for r in range(ROUNDS):
-    for i, p in enumerate(LIBS):
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record(stream)
-        for _ in range(ITERS):
+    pairs = N * (N + 1) // 2 if CAUSAL else N * N
+    flops = 4 * B * H * D * pairs
+    for i in range(len(libs)):
+        for _ in range(30):
             call(i)
-        e.record(stream)
-        e.synchronize()
-        res[p].append(flops / (s.elapsed_time(e) / ITERS * 1e-3) / 1e12)
-for i, p in enumerate(LIBS):
-    print(json.dumps({"lib": p, "variant": VARIANT, "causal": CAUSAL, "TF/s_median": statistics.median(res[p]),
-                      "TF/s_min": min(res[p]), "TF/s_max": max(res[p]),
-                      "bitwise_eq_first": bool(torch.equal(outs[i], outs[0]))}), flush=True)
+    torch.cuda.synchronize()
+    res = {p: [] for p in LIBS}
+    for r in range(ROUNDS):
+        for i, p in enumerate(LIBS):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record(stream)
+            for _ in range(ITERS):
+                call(i)
+            e.record(stream)
+            e.synchronize()
+            res[p].append(flops / (s.elapsed_time(e) / ITERS * 1e-3) / 1e12)
+    for i, p in enumerate(LIBS):
+        print(json.dumps({"lib": p, "shape": [B, H, N, D], "variant": VARIANT, "causal": CAUSAL,
+                          "TF/s_median": statistics.median(res[p]), "TF/s_min": min(res[p]),
+                          "TF/s_max": max(res[p]), "bitwise_eq_first": bool(torch.equal(outs[i], outs[0]))}),
+              flush=True)
+    del q, k, v, outs
