@@ -523,6 +523,8 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
 //  71: attn_fwd_v12 persistent (one workgroup per CU walking its XCD's
 //      blocks, the K/V stream and the next block's Q across block seams) --
 //      the DEFAULT where 70 applies (1181 vs 1082 TF/s for 55)
+//  73 / 74: attn_fwd_v12 causal (bottom-right, Nq <= Nk), one block per
+//      workgroup heaviest first / persistent with the balanced rotation
 //  72: variant 71 with the defer-max threshold at 0 (a rescale whenever a
 //      tile raises a row's max): tests only, the threshold sweep of
 //      cdna_hip_programming.md rule 26 (72 and 71 agree to rounding)
@@ -551,7 +553,16 @@ int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int
             return launch_attn_v12(q, k, v, o, B, H, group, Nq, Nk, s7, scale, stream, variant != 70,
                                    variant == 72 ? 0.f : 8.f);
         }
-        variant = 55;
+        variant = causal ? 60 : 55;
+    }
+    if (variant == 73 || variant == 74) {
+        const bool bf = std::is_same<T, bf16_t>::value;
+        if (causal && attn_v12_ok(D, bf ? 1 : 0, 0, Nk) && Nq <= Nk && c_ok) {
+            const V7Strides s7{st.qb, st.qh, st.qn, st.kb, st.kh, st.kn,
+                               st.vb, st.vh, st.vn, st.ob, st.oh, st.on};
+            return launch_attn_v12(q, k, v, o, B, H, group, Nq, Nk, s7, scale, stream, variant == 74, 8.f, true);
+        }
+        variant = causal ? 60 : 55;
     }
     if (variant == 50 || variant == 51 || variant == 54 || variant == 55 || variant == 60) {
         if (c_ok) {

@@ -176,7 +176,54 @@ __device__ unsigned long long g_v12_stamps[16];
 
 // STAMP (diagnostic build only): 0 none, 1 per-segment s_memtime sums, 2 the
 // in-kernel clock (s_memtime / s_memrealtime once at entry and exit)
-template <int STAMP = 0, int THR = 8>
+// causal mask of one 32x32 score half in place: element r sits at key
+// offset (r&3) + 8(r>>2) of the lane's key group; -inf unless offset <= lim.
+// Compare into VCC and select, element by element in asm: hipcc hoists no
+// compares (their SGPR masks would not fit beside the kernel's scalars).
+template <int R> __device__ __forceinline__ void v12_mask1(f32x16& s, int lim, float ninf) {
+    float e = s[R];
+    asm volatile("v_cmp_le_i32_e32 vcc, %1, %2\n\tv_cndmask_b32_e32 %0, %3, %0"
+                 : "+v"(e) : "n"((R & 3) + 8 * (R >> 2)), "v"(lim), "v"(ninf) : "vcc");
+    s[R] = e;
+}
+template <int... R>
+__device__ __forceinline__ void v12_mask_seq(f32x16& s, int lim, float ninf, std::integer_sequence<int, R...>) {
+    (v12_mask1<R>(s, lim, ninf), ...);
+}
+// (-inf comes in a VGPR: a literal beside the VCC read of v_cndmask_b32_e32
+// breaks gfx9's one-constant-bus rule)
+__device__ __forceinline__ void v12_mask_half(f32x16& s, int lim, float ninf) {
+    v12_mask_seq(s, lim, ninf, std::make_integer_sequence<int, 16>{});
+}
+
+// Causal block order.  Persistent (G = gridDim.x < nblocks; the launcher
+// checks G % 8 == 0, (G/8) % QB == 0, (BH/8) % ((G/8)/QB) == 0 and
+// nblocks % G == 0): workgroup i of XCD x (walk position l = L + G j) owns
+// head x*BH/8 + i/QB + j*(G/8)/QB and query block (i + j) % QB, so every
+// workgroup walks each query height exactly once (equal triangular work) and,
+// at every step, the QB workgroups of one group run all blocks of one head
+// together (its K/V shared in the XCD's L2).  One block per workgroup:
+// xcd_remap order, the heaviest query block of a head first.
+__device__ __forceinline__ void causal_block(int l, int G, int nblocks, int qb, int& bh, int& qblk) {
+    if (G < nblocks) {
+        const int x = l % 8, wg = (l / 8) % (G / 8), j = l / G;
+        const int per = (G / 8) / qb, hx = nblocks / qb / 8;
+        bh = x * hx + wg / qb + per * j;
+        qblk = (wg % qb + j) % qb;
+    } else {
+        const int lb = xcd_remap(l, nblocks);
+        bh = lb / qb;
+        qblk = qb - 1 - lb % qb;
+    }
+}
+
+// CAUSAL: the bottom-right mask of ch01/attention.py:66-67 / ch02's cached
+// prefill (row i sees keys j <= i + Nk - Nq; the launcher requires Nq <= Nk):
+// a block runs only the key tiles its last row sees, the scores of tiles from
+// the wave's first masked one on are masked in place (-inf) right after their
+// QK^T chains, and the persistent walk is the balanced rotation of
+// causal_block (every workgroup the same triangular share).
+template <int STAMP = 0, int THR = 8, bool CAUSAL = false>
 __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
     uint16_t* __restrict__ o, int H, int group, int Nq, int Nk, V7Strides st, float c, int qblocks,
@@ -194,8 +241,14 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     const uint16_t *qp = q, *kp = k, *vp = v;
     auto block_ptrs = [&](int l, int& bb, int& hh, int& r0, const uint16_t*& qq, const uint16_t*& kk,
                           const uint16_t*& vv) __attribute__((always_inline)) {
-        const int lb = xcd_remap(l, nblocks);
-        const int bh = lb / qblocks, qblk = lb % qblocks;
+        int bh, qblk;
+        if constexpr (CAUSAL) {
+            causal_block(l, (int)gridDim.x, nblocks, qblocks, bh, qblk);
+        } else {
+            const int lb = xcd_remap(l, nblocks);
+            bh = lb / qblocks;
+            qblk = lb % qblocks;
+        }
         bb = bh / H;
         hh = bh % H;
         const int hk = hh / group;
@@ -205,7 +258,13 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         vv = v + bb * st.vb + hk * st.vh;
     };
     block_ptrs(L, b, hq, q0, qp, kp, vp);
-    const int nt = Nk / KT;
+    // key tiles of the block (causal: those its last row sees) and the
+    // wave's first tile with a masked score
+    auto block_nt = [&](int r0) __attribute__((always_inline)) {
+        return CAUSAL ? min(Nk / KT, (r0 - 64 * wave + 256 + Nk - Nq + KT - 1) / KT) : Nk / KT;
+    };
+    int nt = block_nt(q0);
+    int tdiag = CAUSAL ? (q0 + Nk - Nq + 1) / KT : 1 << 30;
     unsigned long long st_sum[14] = {}, st_last = 0;
     auto stamp = [&](int seg) __attribute__((always_inline)) {
         if constexpr (STAMP == 1) {
@@ -549,7 +608,24 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     // defer-max decision for the tile in S (rare path: drain, rescale O and
     // l, recompute S from the LDS copy of K in slot sk, redo exps and P; block
     // B's slices 8..15, still to come, then use the new m)
-    auto settle = [&](i32x4 (&Pc)[2][2][2], int sk) __attribute__((always_inline)) {
+    // CAUSAL: block X's scores of tile t in place, key > row + Nk - Nq ->
+    // -inf (element r of half tt is key 64t + 32tt + (r&3) + 8(r>>2) + 4h32
+    // of row q0 + 32X + l32); the MFMA results are padded first
+    auto mask_block = [&](auto x_tag, int t) __attribute__((always_inline)) {
+        if constexpr (CAUSAL) {
+            constexpr int X = decltype(x_tag)::value;
+            asm volatile("s_nop 7\n\ts_nop 4" : "+v"(S[X][0]), "+v"(S[X][1]));
+            // the lane id re-derived here (opaque asm): nothing lane-dependent
+            // stays live through the loop for the mask
+            int ln;
+            asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+            const int base = (ln & 31) - 4 * (ln >> 5) + (q0 + 32 * X + Nk - Nq - KT * t);
+            const float ninf = -INFINITY;
+            v12_mask_half(S[X][0], base, ninf);
+            v12_mask_half(S[X][1], base - 32, ninf);
+        }
+    };
+    auto settle = [&](i32x4 (&Pc)[2][2][2], int sk, int t, bool msk) __attribute__((always_inline)) {
 #if V12_SETTLE2
         // V12_SETTLE2: decided on each lane's HALF-row maxes (lanes l and
         // l^32 hold the two key halves of a row): fl(x*c) is non-decreasing
@@ -558,14 +634,14 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         // compares and one SGPR test; the merge runs on the rare path
         // mxA / mxB are scaled in place (fl(max * c) = max of fl(half * c)),
         // one temporary for the thresholds: the allocation has no room
-        float t;
+        float tq;
         uint64_t hit;
         static_assert(THR == 0 || THR == 8, "threshold literal");
 #define V12_SETTLE_ASM(T)                                                                                      \
     asm volatile("v_mul_f32 %0, %0, %4\n\tv_mul_f32 %1, %1, %4\n\tv_add_f32 %2, " T ", %5\n\t"              \
                  "v_cmp_gt_f32_e64 %3, %0, %2\n\tv_add_f32 %2, " T ", %6\n\tv_cmp_gt_f32_e64 vcc, %1, %2\n\t" \
                  "s_or_b64 %3, %3, vcc"                                                                        \
-                 : "+v"(mxA), "+v"(mxB), "=&v"(t), "=&s"(hit)                                                  \
+                 : "+v"(mxA), "+v"(mxB), "=&v"(tq), "=&s"(hit)                                                  \
                  : "v"(c), "v"(mA), "v"(mB) : "vcc", "scc")
         if constexpr (THR == 8) V12_SETTLE_ASM("0x41000000");
         else V12_SETTLE_ASM("0");
@@ -597,6 +673,10 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
                     v12::qk_v<1, KK>(S[1][tt], kf);
                 });
             v12_sfence(S);
+            if (msk) {
+                mask_block(X0{}, t);
+                mask_block(X1{}, t);
+            }
             expo_cvt_all(Pc);
             pfence(Pc);
         }
@@ -635,7 +715,11 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     // (wrap at NBUF) instead of a modulo per use
     int sm1 = 0;
     auto inc_slot = [](int x) __attribute__((always_inline)) { return x == NBUF - 1 ? 0 : x + 1; };
+    // causal: from the wave's tdiag on, the scores are masked in place right
+    // after each block's QK^T chain (a uniform branch; compiled out of the
+    // non-causal kernel)
     auto step = [&](int t, i32x4 (&Pc)[2][2][2], i32x4 (&Pv)[2][2][2]) __attribute__((always_inline)) {
+        const bool msk = CAUSAL && t >= tdiag;
 #if V12_SLOT_INC
         const int s_m1 = sm1, s_0 = inc_slot(s_m1), s_p1 = inc_slot(s_0), s_p2 = inc_slot(s_p1);
         sm1 = s_0;
@@ -650,7 +734,9 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
             dma_src(t + 2, kt, vt);
             const uint32_t dbase = lds0 + (uint32_t)s_p2 * BUFB + (PPW * wave) * 1024;
             phaseQA(Pv, std::true_type{}, kt, vt, dbase);
+            if (msk) mask_block(X0{}, t);
             phaseQB(Pv, Pc, std::true_type{}, s_m1);
+            if (msk) mask_block(X1{}, t);
         }
         stamp(1);
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile t+1 (issued one step ago)
@@ -664,7 +750,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         // fragment registers)
         phaseP(s_m1, Pv, Pc, s_p1, std::true_type{}, std::true_type{}, std::true_type{}, std::true_type{});
         stamp(4);
-        if (!V12_ABL_SETTLE) settle(Pc, s_0);
+        if (!V12_ABL_SETTLE) settle(Pc, s_0, t, msk);
         stamp(5);
     };
 
@@ -714,6 +800,10 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
             phaseQB(P1, P0, std::false_type{}, 0);
         }
         asm volatile("s_nop 7\n\ts_nop 4" : "+v"(S[0][0]), "+v"(S[0][1]), "+v"(S[1][0]), "+v"(S[1][1]));
+        if (CAUSAL && 0 >= tdiag) {  // tile 0 holds the diagonal (first query block)
+            mask_block(X0{}, 0);
+            mask_block(X1{}, 0);
+        }
         stamp(11);
         if (nt > 1)
             phaseP(0, P1, P1, slot(1), std::false_type{}, std::false_type{}, std::true_type{}, std::false_type{});
@@ -808,6 +898,10 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         s0 = (s0 + nt) % NBUF;
         L += (int)gridDim.x;
         block_ptrs(L, b, hq, q0, qp, kp, vp);
+        if constexpr (CAUSAL) {
+            nt = block_nt(q0);
+            tdiag = (q0 + Nk - Nq + 1) / KT;
+        }
     }
     // the last DMA (a reload of tile nt-1) lands before the LDS is released
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -841,8 +935,10 @@ bool attn_v12_ok(int D, int is_bf16, int causal, int Nk) {
 }
 
 int launch_attn_v12(const void* q, const void* k, const void* v, void* o, int B, int H, int group, int Nq,
-                    int Nk, const V7Strides& st, float scale, hipStream_t stream, bool persistent, float thr) {
+                    int Nk, const V7Strides& st, float scale, hipStream_t stream, bool persistent, float thr,
+                    bool causal) {
     PLI_REQUIRE(thr == 0.f || thr == 8.f, "attn_fwd_v12: defer-max threshold %g not built", thr);
+    PLI_REQUIRE(!causal || (thr == 8.f && Nq <= Nk), "attn_fwd_v12: causal needs Nq <= Nk (THR 8)");
     const int qblocks = cdiv(Nq, 256);
     const int64_t nb = (int64_t)B * H * qblocks;
     PLI_REQUIRE(nb < (1ll << 31), "pli_flash_attn_fwd: grid too large");
@@ -850,20 +946,32 @@ int launch_attn_v12(const void* q, const void* k, const void* v, void* o, int B,
     // persistent: one workgroup per CU of the stream's device (the kernel
     // holds 160 KiB of LDS and the whole register file), a multiple of 8 so
     // each walks one XCD; the stream across block seams needs two tiles per
-    // block
+    // block.  Causal: only where the balanced rotation of causal_block tiles
+    // the blocks exactly (else one block per workgroup, heaviest first).
     int grid = (int)nb;
     if (persistent && Nk >= 128) {
         const int g = cu_count(stream) / 8 * 8;
         if (g >= 8 && nb > g) grid = g;
+        if (causal && grid < nb) {
+            const int64_t bh = nb / qblocks, w = g / 8;
+            const bool rot = w % qblocks == 0 && bh % 8 == 0 && (bh / 8) % (w / qblocks) == 0 && nb % g == 0;
+            if (!rot) grid = (int)nb;
+        }
     }
-    if (thr == 0.f)
-        hipLaunchKernelGGL((attn_fwd_v12<0, 0>), dim3((unsigned)grid), dim3(256), 0, stream,
-                           (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, H, group,
-                           Nq, Nk, st, c, qblocks, (int)nb);
+    const dim3 gr((unsigned)grid), blk(256);
+    const auto* qq = (const uint16_t*)q;
+    const auto* kk = (const uint16_t*)k;
+    const auto* vv = (const uint16_t*)v;
+    auto* oo = (uint16_t*)o;
+    if (causal)
+        hipLaunchKernelGGL((attn_fwd_v12<0, 8, true>), gr, blk, 0, stream, qq, kk, vv, oo, H, group, Nq, Nk, st, c,
+                           qblocks, (int)nb);
+    else if (thr == 0.f)
+        hipLaunchKernelGGL((attn_fwd_v12<0, 0>), gr, blk, 0, stream, qq, kk, vv, oo, H, group, Nq, Nk, st, c,
+                           qblocks, (int)nb);
     else
-        hipLaunchKernelGGL((attn_fwd_v12<0, 8>), dim3((unsigned)grid), dim3(256), 0, stream,
-                           (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, H, group,
-                           Nq, Nk, st, c, qblocks, (int)nb);
+        hipLaunchKernelGGL((attn_fwd_v12<0, 8>), gr, blk, 0, stream, qq, kk, vv, oo, H, group, Nq, Nk, st, c,
+                           qblocks, (int)nb);
     return launch_status("attn_fwd_v12");
 }
 

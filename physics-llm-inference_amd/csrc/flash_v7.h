@@ -21,6 +21,6 @@ int launch_attn_v7(const void* q, const void* k, const void* v, void* o, int B, 
 bool attn_v12_ok(int D, int is_bf16, int causal, int Nk);
 int launch_attn_v12(const void* q, const void* k, const void* v, void* o, int B, int H, int group, int Nq,
                     int Nk, const V7Strides& st, float scale, hipStream_t stream, bool persistent,
-                    float thr = 8.f);
+                    float thr = 8.f, bool causal = false);
 
 }  // namespace pli

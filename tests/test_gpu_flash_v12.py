@@ -36,18 +36,27 @@ def dev(a):
     return torch.from_numpy(np.ascontiguousarray(a)).to(DEV).to(torch.bfloat16)
 
 
-def torch_attention(q, k, v, dtype=torch.float64, heads_per_chunk=8):
+def torch_attention(q, k, v, dtype=torch.float64, heads_per_chunk=8, causal=False):
     """softmax(q k^T / sqrt(D)) v over [B,H,N,D] tensors in ``dtype`` on the
-    device, K/V heads shared by H/Hkv query heads (GQA, ch01/gqa.py:30-34)."""
+    device, K/V heads shared by H/Hkv query heads (GQA, ch01/gqa.py:30-34);
+    causal: the bottom-right mask (row i sees keys j <= i + Nk - Nq,
+    ch01/attention.py:66-67, ch02/cached_generation.py:85-91)."""
     B, H, Nq, D = q.shape
+    Nk = k.shape[2]
     g = H // k.shape[1]
     out = torch.empty(B, H, Nq, D, dtype=dtype, device=q.device)
+    if causal:
+        i = torch.arange(Nq, device=q.device)[:, None]
+        j = torch.arange(Nk, device=q.device)[None, :]
+        masked = j > i + (Nk - Nq)
     for b in range(B):
         for h0 in range(0, H, heads_per_chunk):
             hs = torch.arange(h0, min(H, h0 + heads_per_chunk), device=q.device)
             qq, kk, vv = q[b, hs].to(dtype), k[b, hs // g].to(dtype), v[b, hs // g].to(dtype)
-            p = torch.softmax(torch.matmul(qq, kk.transpose(-1, -2)) * D ** -0.5, dim=-1)
-            out[b, hs] = torch.matmul(p, vv)
+            sc = torch.matmul(qq, kk.transpose(-1, -2)) * D ** -0.5
+            if causal:
+                sc = sc.masked_fill(masked, float("-inf"))
+            out[b, hs] = torch.matmul(torch.softmax(sc, dim=-1), vv)
     return out
 
 
@@ -165,3 +174,62 @@ def test_flash_negative_and_zero_scale():
         out = pli_hip.flash_attn_fwd(dev(q), dev(k), dev(v), scale=scale).double().cpu().numpy()
         ref = oatt.naive_attention(q, k, v, scale=scale)
         assert np.isfinite(out).all() and np.abs(out - ref).max() <= 1e-2, f"scale {scale}"
+
+
+# causal v12 (variants 73: one block per workgroup, heaviest first; 74:
+# persistent, the balanced rotation of query heights where the shape admits
+# it).  (B, H, Hkv, Nq, Nk): the rotation (512 and 4096 blocks over 256
+# workgroups), a head count the rotation does not tile (one block per
+# workgroup), bottom-right with Nq < Nk (ragged), a single query row, one key
+# tile (the prologue's tile holds every diagonal)
+CAUSAL_SHAPES = [(4, 32, 8, 1024, 1024), (2, 32, 32, 2048, 2048), (3, 40, 8, 1024, 1024),
+                 (2, 8, 2, 300, 512), (1, 4, 4, 1, 128), (2, 4, 4, 64, 64), (1, 8, 8, 700, 768)]
+
+
+@pytest.mark.parametrize("qmul", (1, 4))
+@pytest.mark.parametrize("shape", CAUSAL_SHAPES, ids=lambda s: "b{}h{}kv{}q{}k{}".format(*s))
+def test_v12_causal_vs_f64_full_tensor(shape, qmul):
+    """Every output element of causal 73 / 74 against the f64 device
+    reference with the bottom-right mask; 73 and 74 bitwise equal (same
+    arithmetic per block, only the block order differs)."""
+    import pli_hip
+    q, k, v = inputs(shape, sum(shape) % 991)
+    q = q * qmul
+    ref = torch_attention(q, k, v, causal=True)
+    tol = 1e-2 if qmul == 1 else 2.0 ** -8 * v.abs().max().item()
+    outs = {}
+    for var in (73, 74):
+        outs[var] = pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=var)
+        err = max_err(outs[var], ref)
+        assert err <= tol, f"{shape} q*{qmul} causal variant {var}: max |err| {err:.4e} > {tol:.4e}"
+    assert torch.equal(outs[73], outs[74]), f"{shape}: 73 != 74"
+
+
+def test_v12_causal_full_config_all_heads():
+    """Causal at the bench config (B8 S4096 H32 D128, the persistent
+    rotation): all 256 heads, whole heads, against an fp32 torch attention
+    with the causal mask; the default causal path agrees within rounding."""
+    import pli_hip
+    B, H, N, D = 8, 32, 4096, 128
+    g = torch.Generator(device=DEV).manual_seed(5)
+    q, k, v = (torch.randn(B, H, N, D, device=DEV, dtype=torch.bfloat16, generator=g) for _ in range(3))
+    out = pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=74)
+    for b in range(B):
+        ref = torch_attention(q[b:b + 1], k[b:b + 1], v[b:b + 1], dtype=torch.float32, heads_per_chunk=4,
+                              causal=True)
+        err = max_err(out[b:b + 1], ref)
+        assert err <= 1e-2, f"causal batch {b}: max |err| {err:.4e} over its 32 heads"
+    dflt = pli_hip.flash_attn_fwd(q, k, v, causal=True)
+    assert_agree_to_rounding(dflt, out, v)
+
+
+def test_v12_causal_stress():
+    """The rescale branch on masked tiles: the stress inputs (spike / late /
+    all) through causal 74, against the f64 causal reference."""
+    import pli_hip
+    from stress_cases import stress_inputs
+    for name in ("spike", "late", "all", "seam5"):
+        q, k, v = (dev(x) for x in stress_inputs(name))
+        out = pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=74)
+        err = max_err(out, torch_attention(q, k, v, causal=True))
+        assert err <= 2.0 ** -8 * v.abs().max().item(), f"{name}: {err:.4e}"

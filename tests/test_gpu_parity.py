@@ -106,7 +106,7 @@ def test_flash_vs_oracle(case):
 
 
 # every MFMA variant (alternates A/B-tested by tools/tune.py) on the MFMA-eligible cases
-MFMA_VARIANTS = (21, 50, 51, 54, 55, 60, 70, 71, 72)
+MFMA_VARIANTS = (21, 50, 51, 54, 55, 60, 70, 71, 72, 73, 74)
 
 
 

@@ -17,7 +17,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIBS = os.environ.get("LIBS", "tools/ab/libpli_base.so physics-llm-inference_amd/pli_hip/libpli_hip.so").split()
 ROUNDS, ITERS = int(os.environ.get("ROUNDS", "8")), int(os.environ.get("ITERS", "20"))
-VARIANT = int(os.environ.get("VARIANT", "-1"))
+VARIANTS = [int(v) for v in os.environ.get("VARIANTS", os.environ.get("VARIANT", "-1")).split(",")]
 CAUSAL = int(os.environ.get("CAUSAL", "0"))
 SHAPES = [tuple(int(x) for x in sh.split(",")) for sh in os.environ.get("SHAPE", "8,32,4096,128").split(";")]
 libs = []
@@ -28,38 +28,42 @@ for p in LIBS:
                                                                  ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
     f.restype = ctypes.c_int
     libs.append(f)
+# (library, variant) arms, interleaved round by round
+arms = [(li, var) for li in range(len(LIBS)) for var in VARIANTS]
 stream = torch.cuda.current_stream()
 BF16 = 2  # PLI_BF16
 for (B, H, N, D) in SHAPES:
     g = torch.Generator(device="cuda").manual_seed(0)
     q, k, v = (torch.randn(B, H, N, D, device="cuda", dtype=torch.bfloat16, generator=g) for _ in range(3))
-    outs = [torch.empty_like(q) for _ in libs]
+    outs = [torch.empty_like(q) for _ in arms]
     st = (ctypes.c_int64 * 12)(*(int(x) for t in (q, k, v, q) for x in t.stride()[:3]))
 
-    def call(i):
-        rc = libs[i](q.data_ptr(), k.data_ptr(), v.data_ptr(), outs[i].data_ptr(), B, H, H, N, N, D, st,
-                     D ** -0.5, CAUSAL, BF16, ctypes.c_void_p(stream.cuda_stream), VARIANT)
-        assert rc == 0, (LIBS[i], rc)
+    def call(a):
+        li, var = arms[a]
+        rc = libs[li](q.data_ptr(), k.data_ptr(), v.data_ptr(), outs[a].data_ptr(), B, H, H, N, N, D, st,
+                      D ** -0.5, CAUSAL, BF16, ctypes.c_void_p(stream.cuda_stream), var)
+        assert rc == 0, (LIBS[li], var, rc)
 
     pairs = N * (N + 1) // 2 if CAUSAL else N * N
     flops = 4 * B * H * D * pairs
-    for i in range(len(libs)):
+    for a in range(len(arms)):
         for _ in range(30):
-            call(i)
+            call(a)
     torch.cuda.synchronize()
-    res = {p: [] for p in LIBS}
+    res = {a: [] for a in range(len(arms))}
     for r in range(ROUNDS):
-        for i, p in enumerate(LIBS):
+        for a in range(len(arms)):
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record(stream)
             for _ in range(ITERS):
-                call(i)
+                call(a)
             e.record(stream)
             e.synchronize()
-            res[p].append(flops / (s.elapsed_time(e) / ITERS * 1e-3) / 1e12)
-    for i, p in enumerate(LIBS):
-        print(json.dumps({"lib": p, "shape": [B, H, N, D], "variant": VARIANT, "causal": CAUSAL,
-                          "TF/s_median": statistics.median(res[p]), "TF/s_min": min(res[p]),
-                          "TF/s_max": max(res[p]), "bitwise_eq_first": bool(torch.equal(outs[i], outs[0]))}),
-              flush=True)
+            res[a].append(flops / (s.elapsed_time(e) / ITERS * 1e-3) / 1e12)
+    ref = outs[0].float()
+    for a, (li, var) in enumerate(arms):
+        print(json.dumps({"lib": LIBS[li], "shape": [B, H, N, D], "variant": var, "causal": CAUSAL,
+                          "TF/s_median": statistics.median(res[a]), "TF/s_min": min(res[a]),
+                          "TF/s_max": max(res[a]), "bitwise_eq_first": bool(torch.equal(outs[a], outs[0])),
+                          "max_diff_first": (outs[a].float() - ref).abs().max().item()}), flush=True)
     del q, k, v, outs
