@@ -47,7 +47,7 @@ PEAK_BF16_TFLOPS = 2516.6   # 256 CU x 4096 FLOP/clk x 2.4 GHz (dense)
 PEAK_HBM_GBPS = 8000.0      # HBM3E datasheet
 B, H, S, D = 8, 32, 4096, 128
 FLASH_KERNEL = "attn_fwd_v12 persistent (variant 71; bitwise = attn_fwd_v10 exact)"
-CAUSAL_KERNEL = "attn_fwd_v10<bf16,exact>, 4-wave workgroups (variant 60)"
+CAUSAL_KERNEL = "attn_fwd_v12 causal, persistent balanced rotation (variant 74)"
 
 
 def log(*a):

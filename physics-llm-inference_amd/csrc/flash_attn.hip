@@ -529,10 +529,12 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
 //      tile raises a row's max): tests only, the threshold sweep of
 //      cdna_hip_programming.md rule 26 (72 and 71 agree to rounding)
 constexpr int kDefaultVariant = 71;
-// causal: the 4-wave workgroups of 60 -- 128-row blocks balance the
-// triangular work better and the two workgroups per CU drift apart
-// (B8 S4096 H32 D128 bf16: 924 vs 834 TF/s; non-causal 1085 vs 1100)
-constexpr int kDefaultCausalVariant = 60;
+// causal: attn_fwd_v12 causal (74; one block per workgroup where the
+// balanced persistent rotation does not tile the shape), 60 where v12 does
+// not apply (fp16, D != 128, Nq > Nk, Nk % 64): B8 S4096 H32 D128 bf16 1002
+// (74) vs 945 (60) TF/s, B2 S8192 1098 vs 1013, B32 S2048 867 vs 830
+// (profiles/r03/flash/ab_causal.log)
+constexpr int kDefaultCausalVariant = 74;
 
 template <typename T, int D>
 int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int H,

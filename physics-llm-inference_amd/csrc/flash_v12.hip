@@ -197,8 +197,8 @@ __device__ __forceinline__ void v12_mask_half(f32x16& s, int lim, float ninf) {
 }
 
 // Causal block order.  Persistent (G = gridDim.x < nblocks; the launcher
-// checks G % 8 == 0, (G/8) % QB == 0, (BH/8) % ((G/8)/QB) == 0 and
-// nblocks % G == 0): workgroup i of XCD x (walk position l = L + G j) owns
+// checks G % 8 == 0, (G/8) % QB == 0, (BH/8) % ((G/8)/QB) == 0,
+// nblocks % G == 0 and (nblocks/G) % QB == 0): workgroup i of XCD x (walk position l = L + G j) owns
 // head x*BH/8 + i/QB + j*(G/8)/QB and query block (i + j) % QB, so every
 // workgroup walks each query height exactly once (equal triangular work) and,
 // at every step, the QB workgroups of one group run all blocks of one head
@@ -954,7 +954,12 @@ int launch_attn_v12(const void* q, const void* k, const void* v, void* o, int B,
         if (g >= 8 && nb > g) grid = g;
         if (causal && grid < nb) {
             const int64_t bh = nb / qblocks, w = g / 8;
-            const bool rot = w % qblocks == 0 && bh % 8 == 0 && (bh / 8) % (w / qblocks) == 0 && nb % g == 0;
+            // every workgroup must walk whole multiples of the QB query
+            // heights (a walk shorter than QB sees a run of light or heavy
+            // blocks: B2 H32 N8192 ran 813 vs 1098 TF/s one block per
+            // workgroup)
+            const bool rot = w % qblocks == 0 && bh % 8 == 0 && (bh / 8) % (w / qblocks) == 0 && nb % g == 0 &&
+                             (nb / g) % qblocks == 0;
             if (!rot) grid = (int)nb;
         }
     }

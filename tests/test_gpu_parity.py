@@ -143,7 +143,7 @@ PRESCALED = (50, 54)
 DEFAULT_VARIANT = 71
 
 
-DEFAULT_CAUSAL_VARIANT = 60
+DEFAULT_CAUSAL_VARIANT = 74
 
 
 def test_flash_default_variants():
