@@ -47,7 +47,7 @@ PEAK_BF16_TFLOPS = 2516.6   # 256 CU x 4096 FLOP/clk x 2.4 GHz (dense)
 PEAK_HBM_GBPS = 8000.0      # HBM3E datasheet
 B, H, S, D = 8, 32, 4096, 128
 FLASH_KERNEL = "attn_fwd_v12 persistent (variant 71; bitwise = attn_fwd_v10 exact)"
-CAUSAL_KERNEL = "attn_fwd_v12 causal, persistent balanced rotation (variant 74)"
+CAUSAL_KERNEL = "attn_fwd_v12 causal, persistent pair walk (variant 74)"
 
 
 def log(*a):
@@ -744,7 +744,8 @@ def main():
         ms_c = event_time_ms(lambda: pli_hip.flash_attn_fwd(q, k, v, causal=True, out=o), 5, stream)
         extra["flash_causal"] = {"ms": ms_c,
                                  "TFLOP/s": 4 * B * H * D * (S * (S + 1) // 2) / (ms_c * 1e-3) / 1e12,
-                                 "kernel": CAUSAL_KERNEL}
+                                 "kernel": CAUSAL_KERNEL,
+                                 "traffic": load_traffic("attn_fwd_v12 causal")}
         log("[bench] torch sdpa comparison")
         extra["flash_torch_sdpa"] = bench_torch_sdpa(q, k, v, o, stream)
     if args.flash_only:

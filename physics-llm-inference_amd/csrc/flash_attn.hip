@@ -524,16 +524,17 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
 //      blocks, the K/V stream and the next block's Q across block seams) --
 //      the DEFAULT where 70 applies (1181 vs 1082 TF/s for 55)
 //  73 / 74: attn_fwd_v12 causal (bottom-right, Nq <= Nk), one block per
-//      workgroup heaviest first / persistent with the balanced rotation
+//      workgroup heaviest first / persistent with the pair walk
 //  72: variant 71 with the defer-max threshold at 0 (a rescale whenever a
 //      tile raises a row's max): tests only, the threshold sweep of
 //      cdna_hip_programming.md rule 26 (72 and 71 agree to rounding)
 constexpr int kDefaultVariant = 71;
 // causal: attn_fwd_v12 causal (74; one block per workgroup where the
-// balanced persistent rotation does not tile the shape), 60 where v12 does
-// not apply (fp16, D != 128, Nq > Nk, Nk % 64): B8 S4096 H32 D128 bf16 1002
-// (74) vs 945 (60) TF/s, B2 S8192 1098 vs 1013, B32 S2048 867 vs 830
-// (profiles/r03/flash/ab_causal.log)
+// persistent pair walk does not tile the shape), 60 where v12 does not apply
+// (fp16, D != 128, Nq > Nk, Nk % 64): B8 S4096 H32 D128 bf16 1002 (74, the
+// first rotation walk) vs 945 (60) TF/s, B2 S8192 1098 vs 1013, B32 S2048 867
+// vs 830 (profiles/r03/flash/ab_causal.log); the pair walk: 1049 at B8 S4096,
+// 1154 at B2 S8192, 1223 at B1 H64 S16384 (ab_causal_pair.log)
 constexpr int kDefaultCausalVariant = 74;
 
 template <typename T, int D>

@@ -196,15 +196,34 @@ __device__ __forceinline__ void v12_mask_half(f32x16& s, int lim, float ninf) {
     v12_mask_seq(s, lim, ninf, std::make_integer_sequence<int, 16>{});
 }
 
-// Causal block order.  Persistent (G = gridDim.x < nblocks; the launcher
-// checks G % 8 == 0, (G/8) % QB == 0, (BH/8) % ((G/8)/QB) == 0,
-// nblocks % G == 0 and (nblocks/G) % QB == 0): workgroup i of XCD x (walk position l = L + G j) owns
-// head x*BH/8 + i/QB + j*(G/8)/QB and query block (i + j) % QB, so every
-// workgroup walks each query height exactly once (equal triangular work) and,
-// at every step, the QB workgroups of one group run all blocks of one head
-// together (its K/V shared in the XCD's L2).  One block per workgroup:
-// xcd_remap order, the heaviest query block of a head first.
+// Causal block order.  Persistent (G = gridDim.x < nblocks), the pair walk
+// (V12_CAUSAL_PAIR 2, the default; the launcher checks QB even, (G/8) %
+// (QB/2) == 0, BH % 8 == 0, (BH/8) % ((G/8)/(QB/2)) == 0, nblocks % G == 0
+// and nblocks/G even): workgroup i of XCD x owns, at pair step p = j/2 of its
+// walk (j = l / G), head x*BH/8 + i/(QB/2) + p*(G/8)/(QB/2) and runs query
+// block QB-1-a then a (a = i % (QB/2)) of it.  Every pair is the same work
+// (QB+1 key-tile heights), so the QB/2 workgroups of a head stay in step and
+// share its K/V in the XCD's L2 -- the long blocks read the same tile at the
+// same time, the short ones re-read tiles a few tile-times apart.  B8 H32
+// S4096: FETCH 1.33 GB per launch vs 3.94 for the rotation walk below
+// (V12_CAUSAL_PAIR 0: QB workgroups run all blocks of one head per step,
+// one query height each, but desynchronise as the heights differ), 1049 vs
+// 1016 TF/s (profiles/r03/flash/ab_causal_pair.log); short block first
+// (V12_CAUSAL_PAIR 1) read 1.9 GB.  One block per workgroup: xcd_remap order,
+// the heaviest query block of a head first.
+#ifndef V12_CAUSAL_PAIR
+#define V12_CAUSAL_PAIR 2
+#endif
 __device__ __forceinline__ void causal_block(int l, int G, int nblocks, int qb, int& bh, int& qblk) {
+#if V12_CAUSAL_PAIR
+    if (G < nblocks) {
+        const int x = l % 8, wg = (l / 8) % (G / 8), j = l / G, hq = qb / 2;
+        const int per = (G / 8) / hq, hx = nblocks / qb / 8, a = wg % hq;
+        bh = x * hx + wg / hq + per * (j >> 1);
+        qblk = ((j & 1) == (V12_CAUSAL_PAIR == 1 ? 1 : 0)) ? qb - 1 - a : a;
+        return;
+    }
+#endif
     if (G < nblocks) {
         const int x = l % 8, wg = (l / 8) % (G / 8), j = l / G;
         const int per = (G / 8) / qb, hx = nblocks / qb / 8;
@@ -221,8 +240,8 @@ __device__ __forceinline__ void causal_block(int l, int G, int nblocks, int qb, 
 // prefill (row i sees keys j <= i + Nk - Nq; the launcher requires Nq <= Nk):
 // a block runs only the key tiles its last row sees, the scores of tiles from
 // the wave's first masked one on are masked in place (-inf) right after their
-// QK^T chains, and the persistent walk is the balanced rotation of
-// causal_block (every workgroup the same triangular share).
+// QK^T chains, and the persistent walk is causal_block's pair walk (every
+// workgroup the same triangular share).
 template <int STAMP = 0, int THR = 8, bool CAUSAL = false>
 __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
@@ -946,20 +965,26 @@ int launch_attn_v12(const void* q, const void* k, const void* v, void* o, int B,
     // persistent: one workgroup per CU of the stream's device (the kernel
     // holds 160 KiB of LDS and the whole register file), a multiple of 8 so
     // each walks one XCD; the stream across block seams needs two tiles per
-    // block.  Causal: only where the balanced rotation of causal_block tiles
-    // the blocks exactly (else one block per workgroup, heaviest first).
+    // block.  Causal: only where causal_block's walk tiles the blocks exactly
+    // (else one block per workgroup, heaviest first).
     int grid = (int)nb;
     if (persistent && Nk >= 128) {
         const int g = cu_count(stream) / 8 * 8;
         if (g >= 8 && nb > g) grid = g;
         if (causal && grid < nb) {
             const int64_t bh = nb / qblocks, w = g / 8;
-            // every workgroup must walk whole multiples of the QB query
-            // heights (a walk shorter than QB sees a run of light or heavy
-            // blocks: B2 H32 N8192 ran 813 vs 1098 TF/s one block per
-            // workgroup)
+            // every workgroup must walk whole pairs (whole multiples of the QB
+            // query heights for the rotation: a walk shorter than QB sees a
+            // run of light or heavy blocks, B2 H32 N8192 ran 813 vs 1098 TF/s
+            // one block per workgroup)
+#if V12_CAUSAL_PAIR
+            const int hq = qblocks / 2;
+            const bool rot = qblocks % 2 == 0 && w % hq == 0 && bh % 8 == 0 && (bh / 8) % (w / hq) == 0 &&
+                             nb % g == 0 && (nb / g) % 2 == 0;
+#else
             const bool rot = w % qblocks == 0 && bh % 8 == 0 && (bh / 8) % (w / qblocks) == 0 && nb % g == 0 &&
                              (nb / g) % qblocks == 0;
+#endif
             if (!rot) grid = (int)nb;
         }
     }

@@ -177,12 +177,11 @@ def test_flash_negative_and_zero_scale():
 
 
 # causal v12 (variants 73: one block per workgroup, heaviest first; 74:
-# persistent, the balanced rotation of query heights where the shape admits
-# it).  (B, H, Hkv, Nq, Nk): the rotation (512 and 4096 blocks over 256
-# workgroups), a head count the rotation does not tile (one block per
-# workgroup), bottom-right with Nq < Nk (ragged), a single query row, one key
+# persistent, the pair walk of query heights where the shape admits it).
+# (B, H, Hkv, Nq, Nk): the pair walk (512 blocks over 256 workgroups at QB 4,
+# 8 and 16), a head count the walk does not tile (one block per workgroup), bottom-right with Nq < Nk (ragged), a single query row, one key
 # tile (the prologue's tile holds every diagonal)
-CAUSAL_SHAPES = [(4, 32, 8, 1024, 1024), (2, 32, 32, 2048, 2048), (3, 40, 8, 1024, 1024),
+CAUSAL_SHAPES = [(4, 32, 8, 1024, 1024), (2, 32, 32, 2048, 2048), (2, 16, 4, 4096, 4096), (3, 40, 8, 1024, 1024),
                  (2, 8, 2, 300, 512), (1, 4, 4, 1, 128), (2, 4, 4, 64, 64), (1, 8, 8, 700, 768)]
 
 
@@ -207,7 +206,7 @@ def test_v12_causal_vs_f64_full_tensor(shape, qmul):
 
 def test_v12_causal_full_config_all_heads():
     """Causal at the bench config (B8 S4096 H32 D128, the persistent
-    rotation): all 256 heads, whole heads, against an fp32 torch attention
+    pair walk): all 256 heads, whole heads, against an fp32 torch attention
     with the causal mask; the default causal path agrees within rounding."""
     import pli_hip
     B, H, N, D = 8, 32, 4096, 128

@@ -4,7 +4,8 @@ The kernel names its accumulator registers literally in inline asm (O, Q, K
 fragments in a[0:255]); hipcc does not know the Q fragments stay live between
 the asm statements, so if it ever runs short of VGPRs it parks values in
 those AGPRs (v_accvgpr_write/read of its own) and the Q fragments are
-silently corrupted -- every output row of one 32-row block wrong.  This
+silently corrupted -- every output row of one 32-row block wrong.
+$V12_DEFS adds -D switches (checking an A/B build before it goes to the GPU).  This
 compiles the file the way build.py does and checks that no instruction
 outside the asm statements touches an AGPR and that nothing spills.
 """
@@ -25,7 +26,7 @@ def test_v12_no_compiler_agpr_use_or_spill(tmp_path):
     out = tmp_path / "v12.s"
     cmd = [HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "-fno-honor-nans",
            "-I" + os.path.join(ROOT, "include"), "-I" + CSRC, "-S", "--cuda-device-only",
-           os.path.join(CSRC, "flash_v12.hip"), "-o", str(out)]
+           os.path.join(CSRC, "flash_v12.hip"), "-o", str(out)] + os.environ.get("V12_DEFS", "").split()
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     text = out.read_text()

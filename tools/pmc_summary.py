@@ -23,6 +23,12 @@ KERNELS = ("attn_fwd_v12", "attn_fwd_v10", "attn_fwd_v7", "gemm_f32_mfma", "gemm
            "gemm_smallm_nt", "scale_copy_vec")
 
 
+def label(k: str, name: str) -> str:
+    """Causal instantiations (template flag ``true``) share the name prefix
+    with the non-causal kernel; keep them apart."""
+    return k + " causal" if k.startswith("attn_fwd") and ", true>" in name else k
+
+
 def per_kernel(path_glob: str, counter: str) -> dict:
     """{(kernel, grid_size): [values]}"""
     vals = defaultdict(list)
@@ -34,7 +40,7 @@ def per_kernel(path_glob: str, counter: str) -> dict:
                 name = row["Kernel_Name"]
                 for k in KERNELS:
                     if k in name:
-                        vals[(k, int(row["Grid_Size"]))].append(float(row["Counter_Value"]))
+                        vals[(label(k, name), int(row["Grid_Size"]))].append(float(row["Counter_Value"]))
     return vals
 
 
@@ -45,7 +51,8 @@ def main():
     write = per_kernel(os.path.join(d, "pmc_WRITE_SIZE*", "**", "*counter_collection.csv"), "WRITE_SIZE")
     res = {}
     mean = lambda v: sum(v) / len(v) if v else 0.0  # noqa: E731
-    for k in KERNELS:
+    labels = sorted({kk for (kk, _) in set(fetch) | set(write)})
+    for k in labels:
         grids = sorted({g for (kk, g) in set(fetch) | set(write) if kk == k})
         if not grids:
             continue
