@@ -61,6 +61,12 @@
 #ifndef V12_ABL_BAR
 #define V12_ABL_BAR 0
 #endif
+#ifndef V12_ABL_OSTORE
+#define V12_ABL_OSTORE 0  // no O stores at block seams
+#endif
+#ifndef V12_ABL_QLOAD
+#define V12_ABL_QLOAD 0  // no Q reload at block seams (the first block's Q reused)
+#endif
 #ifndef V12_FM_AHEAD
 #define V12_FM_AHEAD 1  // each slice's s*c - m a gap pair ahead of its exps
 #endif
@@ -865,7 +871,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         // the next block's Q rows, in flight under this block's epilogue
         // (past the last block a reload of this block's: unconditional, so
         // the old fragments are not kept live through the block)
-        {
+        if (!V12_ABL_QLOAD) {
             int b2, h2, r2;
             const uint16_t *q2, *k2, *v2;
             block_ptrs(has_next ? L + (int)gridDim.x : L, b2, h2, r2, q2, k2, v2);
@@ -894,7 +900,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
             sfor<4>([&](auto DB) {
                 f32x16 a;
                 v12::o_read<X, DB>(a);
-                if (qr < Nq) {
+                if (qr < Nq && (!V12_ABL_OSTORE || !has_next)) {
                     uint16_t* op = o + b * st.ob + hq * st.oh + (int64_t)qr * st.on;
 #pragma unroll
                     for (int i = 0; i < 4; i += 2) {

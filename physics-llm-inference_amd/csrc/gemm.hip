@@ -24,6 +24,7 @@
 #include <type_traits>
 
 #include "gemm_f32.h"
+#include "gemm_w4v.h"
 #include "pli_common.h"
 
 namespace pli {
@@ -2203,6 +2204,9 @@ static int gemm_dispatch(const void* a, const void* b, void* c, const void* bias
     // grid of tiles so the block count is not tiny)
     // (fewer than 128 tiles of 256^2 leave CUs idle: the 128^2 tile's 4x grid
     // wins there, +20-60 % at 16-64 tiles, profiles/r01/gemm/tune_few_tiles.log)
+    // variant 40: gemm_w4v (gemm_w4v.hip), one wave per SIMD, 128x128 per wave
+    if (variant == 40 && vec && gemm_w4v_ok(m, n, k, lda, ldb, ldc, trans_b))
+        return launch_gemm_w4v(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, dtype == PLI_BF16, s, 4);
     const bool big = vec && k % G2K == 0 && m >= 2 * G2M && n >= 2 * G2N && variant != 1 &&
                      (variant != 0 || (int64_t)cdiv(m, G2M) * cdiv(n, G2N) >= 128);
     if (big || (vec && variant >= 2 && k % G2K == 0 && n >= 8)) {
