@@ -36,7 +36,11 @@
 
 #include "flash_v7.h"
 #include "pli_common.h"
+#ifdef V12_ASM_HDR
+#include V12_ASM_HDR  // timing diagnostics only (tools/gen_flash_v12.py V12_MFMA16)
+#else
 #include "flash_v12_asm.h"
+#endif
 
 // A/B switches (tools/build_v12_ab.sh); the defaults are the product
 #ifndef V12_DMA_IMM
