@@ -69,6 +69,9 @@
 #ifndef W4_ABL_NOB
 #define W4_ABL_NOB 0  // no B pieces
 #endif
+#ifndef W4_ABL_LINES
+#define W4_ABL_LINES 0  // A / NT-B pieces as 8 rows x 128 B (wrong data: DMA cost vs cache lines per piece)
+#endif
 #ifndef W4_EPI_LDS
 #define W4_EPI_LDS 1  // epilogue through LDS: 16-B row stores (else 8-B stores from the accumulators)
 #endif
@@ -140,8 +143,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w4v(const uint16_t* __restrict__ 
     uint32_t aoff[4], boff[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int row = 64 * wave + 16 * i + (lane >> 2);
-        const int c = (lane & 3) ^ (3 * ((row >> 3) & 1));
+        const int row = W4_ABL_LINES ? 64 * wave + 16 * i + (lane >> 3) : 64 * wave + 16 * i + (lane >> 2);
+        const int c = W4_ABL_LINES ? (lane & 7) : (lane & 3) ^ (3 * ((row >> 3) & 1));
         aoff[i] = (uint32_t)(((int64_t)(min(m0 + row, M - 1) - m0) * lda + 8 * c) * 2);
         if constexpr (TRANS_B) {
             boff[i] = (uint32_t)(((int64_t)(min(n0 + row, N - 1) - n0) * ldb + 8 * c) * 2);
@@ -170,7 +173,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4v(const uint16_t* __restrict__ 
     auto dma_piece = [&](auto j_tag, int s) __attribute__((always_inline)) {
         constexpr int j = decltype(j_tag)::value, i = j % 4;
         if (W4_ABL_DMAW0 && wave != 0) return;
-        const int sc = min(s, ks - 1);
+        const int sc = min(s, ks - (W4_ABL_LINES ? 2 : 1));  // (ABL_LINES pieces read 64 k: stay in bounds)
         const uint32_t slot = lds0 + (uint32_t)(s % NS) * SLOT + (uint32_t)wave * 4096 + (W4_DMA_IMM ? 0 : i * 1024);
         const uint16_t* src = j < 4 ? abase + sc * 32 : (TRANS_B ? bbase + sc * 32 : bbase + (int64_t)sc * 32 * ldb);
         const uint32_t off = j < 4 ? aoff[i] : boff[i];
