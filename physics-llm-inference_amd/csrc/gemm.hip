@@ -25,6 +25,7 @@
 
 #include "gemm_f32.h"
 #include "gemm_w4v.h"
+#include "gemm_w5.h"
 #include "pli_common.h"
 
 namespace pli {
@@ -2207,15 +2208,19 @@ static int gemm_dispatch(const void* a, const void* b, void* c, const void* bias
     // variant 40: gemm_w4v (gemm_w4v.hip), one wave per SIMD, 128x128 per wave
     if (variant == 40 && vec && gemm_w4v_ok(m, n, k, lda, ldb, ldc, trans_b))
         return launch_gemm_w4v(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, dtype == PLI_BF16, s, 4);
+    // variant 41: gemm_w5 (gemm_w5.hip), the same tile with K staged 64 deep
+    if (variant == 41 && vec && gemm_w5_ok(m, n, k, lda, ldb, ldc, trans_b))
+        return launch_gemm_w5(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, dtype == PLI_BF16, s, 4);
     const bool big = vec && k % G2K == 0 && m >= 2 * G2M && n >= 2 * G2N && variant != 1 &&
                      (variant != 0 || (int64_t)cdiv(m, G2M) * cdiv(n, G2N) >= 128);
-    // default for the large shapes since round 3: gemm_w4v, +5-15 % over the
-    // phased 8-wave tile on every shape measured (same process, NT / NN:
-    // 4096^3 1255 / 1213 vs 1199 / 1126 TF/s, 8192^3 1355 / 1326 vs 1271 / 1259,
-    // 8192^2 x 1024 1065 / 1032 vs 935 / 897, 4096 x 14336 x 4096 1253 / 1238
-    // vs 1187 / 1102; profiles/r03/gemm/ab_w4v_shapes.log)
-    if (variant == 0 && big && gemm_w4v_ok(m, n, k, lda, ldb, ldc, trans_b))
-        return launch_gemm_w4v(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, dtype == PLI_BF16, s, 4);
+    // default for the large shapes since round 3: gemm_w5 (one wave per SIMD,
+    // K staged 64 deep), +10-25 % over the round-2 phased 8-wave tile (variant
+    // 13) and at or past hipBLASLt on most shapes (same process, NT / NN TF/s:
+    // 4096^3 1422 / 1378 vs 1206 / 1175, torch 1400 / 1281; 8192^3 1536 / 1488
+    // vs 1344 / 1305, torch 1560 / 1391; profiles/r03/gemm/ab_w5.log).
+    // gemm_w4v (variant 40, K 32 deep) sits between them.
+    if (variant == 0 && big && gemm_w5_ok(m, n, k, lda, ldb, ldc, trans_b))
+        return launch_gemm_w5(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, dtype == PLI_BF16, s, 4);
     if (big || (vec && variant >= 2 && k % G2K == 0 && n >= 8)) {
         // variant 3: phased (SCHED 0); 5-8: phased with SCHED 1, 3, 5, 7;
         // 9-11: one-phase tile with grouped rasterization (group_m 4, 8, 16);

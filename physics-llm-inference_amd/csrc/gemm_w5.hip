@@ -1,0 +1,330 @@
+// gemm_w5: C = A B (+ bias) for bf16 / fp16, one wave per SIMD, K staged 64
+// deep (reference ch03/gemm_benchmark.py:35-49, ch05 / ch09 F.linear shapes;
+// gfx950).
+//
+// gemm_w4v's tile (256 x 256, 4 waves of 128 x 128 C^T in the accumulator
+// file, v_mfma_f32_16x16x32 named by gemm_w4v_asm.h), with the operands
+// staged 64 k deep instead of 32.  The w4v ablation (profiles/r03/gemm/)
+// put the LDS-DMA issue first among its costs (NT 8192^3: 1369 TF/s, 1700
+// with no DMA), and its cost follows the cache lines a piece touches: the
+// same 1 KiB piece as 8 rows x 128 B instead of 16 rows x 64 B ran 1495.
+// At 64 k a row of A (and of NT-B) is one 128-B line.
+//
+// LDS: two 64 KiB slots (A image then B image, 32 KiB each), step S in slot
+// S % 2.  Per step (128 MFMAs, two k32 halves):
+//   half 0: MFMAs on the (S, h0) fragments; in their gaps the (S, h1)
+//           fragments are read (16 reads);
+//   s_waitcnt vmcnt(0) + barrier: step S+1's pieces landed everywhere, and
+//           every wave is done reading slot S (its h1 fragments were the last);
+//   half 1: MFMAs on (S, h1); in their gaps the (S+1, h0) fragments are read
+//           from slot S+1 and the 16 DMA pieces of step S+2 go into slot S.
+// One barrier per 64 k (w4v: one per 32 k).  Past the last step the DMA
+// re-loads the last step into the dead slot (no branch in the MFMA stream).
+//
+// LDS images (per slot):
+//   A, NT-B: [256 rows][64 k] (128-B rows), 16-B chunk c of row r at
+//            c ^ ((r >> 1) & 7) (gemm_256's swizzle: conflict-free for the
+//            16-row x 16-B fragment read); a DMA piece = 8 rows x 128 B.
+//   NN-B:    [64 k][256 n] (512-B rows), chunk c of k-row k at c ^ fnn(k)
+//            (gemm.hip's g2_fnn), read transposed by ds_read_b64_tr_b16;
+//            a piece = 2 k-rows x 512 B.
+// Arithmetic: every output is one chain of MFMAs over K in increasing order,
+// 32 k per MFMA -- gemm_256's order, so outputs are bitwise those of that
+// kernel (and of gemm_w4v).
+#include "gemm_w5.h"
+
+#include <utility>
+
+#include "pli_common.h"
+#include "gemm_w4v_asm.h"
+
+// A/B switches (tools/build_ab.sh); the defaults are the product
+#ifndef W5_DMA_START
+#define W5_DMA_START 2  // half-1 gap of the first DMA piece
+#endif
+#ifndef W5_DMA_STRIDE
+#define W5_DMA_STRIDE 4  // gaps between DMA pieces
+#endif
+#ifndef W5_DMA_IMM
+#define W5_DMA_IMM 1  // one M0 write per 4 pieces, pieces 1-3 by instruction offset
+#endif
+#ifndef W5_ABL_DMA
+#define W5_ABL_DMA 0  // timing only: no DMA in the loop (results wrong)
+#endif
+
+namespace pli {
+namespace {
+
+template <int... I, class Fn>
+__device__ __forceinline__ void w5_for(std::integer_sequence<int, I...>, Fn&& fn) {
+    (fn(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class Fn> __device__ __forceinline__ void w5_sfor(Fn&& fn) {
+    w5_for(std::make_integer_sequence<int, N>{}, fn);
+}
+
+__device__ __forceinline__ void w5_tile(int lb, int tiles_m, int tiles_n, int group_m, int& tm, int& tn) {
+    const int width = group_m * tiles_n;
+    const int first = (lb / width) * group_m;
+    const int rows = min(tiles_m - first, group_m);
+    const int r = lb % width;
+    tm = first + r % rows;
+    tn = r / rows;
+}
+__device__ __forceinline__ int w5_fnn(int k) { return 2 * ((k & 3) | (((k >> 3) & 1) << 2)); }
+
+template <int OFF> __device__ __forceinline__ void w5_rd128(i32x4& d, uint32_t addr) {
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "n"(OFF));
+}
+struct W5Pair { i32x2 lo, hi; };
+// NN B^T fragment: two transposed reads, k rows +0..3 and +4..7 (2 KiB apart)
+template <int OFF> __device__ __forceinline__ void w5_rdtr(W5Pair& d, uint32_t addr) {
+    asm volatile("ds_read_b64_tr_b16 %0, %2 offset:%3\n\tds_read_b64_tr_b16 %1, %2 offset:%4"
+                 : "=&v"(d.lo), "=&v"(d.hi) : "v"(addr), "n"(OFF), "n"(OFF + 2048));
+}
+
+template <typename T, bool TRANS_B, bool BIAS>
+__global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bm,
+                                                  uint16_t* __restrict__ C, const uint16_t* __restrict__ bias,
+                                                  int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
+                                                  int tiles_n, int nblocks, int group_m) {
+    constexpr int IMG = 32768, SLOT = 2 * IMG;
+    using BFrag = std::conditional_t<TRANS_B, i32x4, W5Pair>;
+    __shared__ __attribute__((aligned(1024))) char smem[2 * SLOT];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wave >> 1, wc = wave & 1;
+    int tm, tn;
+    w5_tile(xcd_remap(blockIdx.x, nblocks), cdiv(M, 256), tiles_n, group_m, tm, tn);
+    const int m0 = tm * 256, n0 = tn * 256;
+    const int ks = K / 64;
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
+
+    // ---- LDS-DMA plan: wave w stages 8 KiB of each operand image per step
+    // (8 pieces of 1 KiB): A / NT-B rows 64w .. 64w+63 (8 rows x 128 B per
+    // piece), NN-B k-rows 16w .. 16w+15 (2 x 512 B per piece).  Per-lane byte
+    // offsets from the tile's base; rows past M / N re-read the last row
+    // (their outputs are never stored).
+    uint32_t aoff[8], boff[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int row = 64 * wave + 8 * i + (lane >> 3);
+        const int c = (lane & 7) ^ ((row >> 1) & 7);
+        aoff[i] = (uint32_t)(((int64_t)(min(m0 + row, M - 1) - m0) * lda + 8 * c) * 2);
+        if constexpr (TRANS_B) {
+            boff[i] = (uint32_t)(((int64_t)(min(n0 + row, N - 1) - n0) * ldb + 8 * c) * 2);
+        } else {
+            const int kr = 16 * wave + 2 * i + (lane >> 5);
+            const int cn = (lane & 31) ^ w5_fnn(kr);
+            boff[i] = (uint32_t)(((int64_t)kr * ldb + min(n0 + 8 * cn, N - 8) - n0) * 2);
+        }
+    }
+    const uint16_t* abase = A + (int64_t)m0 * lda;
+    const uint16_t* bbase = TRANS_B ? Bm + (int64_t)n0 * ldb : Bm + n0;
+    auto dma1 = [&](const uint16_t* src, uint32_t off, uint32_t lds) __attribute__((always_inline)) {
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(lds), "v"(off), "s"(src)
+                     : "memory");
+    };
+    // W5_DMA_IMM: piece i of a group of 4 reaches its LDS kilobyte through
+    // the instruction offset (i % 4) * 1024, which the hardware adds to the
+    // global address too -- the scalar base is biased by that much instead
+    auto dma_next = [&](auto i_tag, const uint16_t* src, uint32_t off) __attribute__((always_inline)) {
+        constexpr int i = decltype(i_tag)::value;
+        asm volatile("global_load_lds_dwordx4 %0, %1 offset:%2" ::"v"(off),
+                     "s"(reinterpret_cast<const char*>(src) - 1024 * i), "n"(1024 * i) : "memory");
+    };
+    // DMA piece j (0-7 A, 8-15 B) of K step s into slot s % 2 (past the last
+    // step: a reload of the last step)
+    auto dma_piece = [&](auto j_tag, int s) __attribute__((always_inline)) {
+        constexpr int j = decltype(j_tag)::value, i = j % 8;
+        const int sc = min(s, ks - 1);
+        const uint32_t slot = lds0 + (uint32_t)(s & 1) * SLOT + (j < 8 ? 0u : (uint32_t)IMG) +
+                              (uint32_t)wave * 8192 + (uint32_t)(W5_DMA_IMM ? (i / 4) * 4096 : i * 1024);
+        const uint16_t* src = j < 8 ? abase + sc * 64 : (TRANS_B ? bbase + sc * 64 : bbase + (int64_t)sc * 64 * ldb);
+        const uint32_t off = j < 8 ? aoff[i] : boff[i];
+        if constexpr (W5_DMA_IMM && i % 4 > 0) dma_next(std::integral_constant<int, i % 4>{}, src, off);
+        else dma1(src, off, slot);
+    };
+
+    // ---- fragment read addresses (slot 0, half 0; + slot * SLOT, halves by
+    // address (A / NT-B: the chunk XOR) or offset (NN-B: +16 KiB))
+    const int r16 = lane & 15, h4 = lane >> 4;
+    uint32_t a_rd[2], b_rd[TRANS_B ? 2 : 8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int ch = (4 * h + h4) ^ ((r16 >> 1) & 7);
+        a_rd[h] = lds0 + (uint32_t)((wr * 128 + r16) * 128 + (ch << 4));
+        if constexpr (TRANS_B) b_rd[h] = lds0 + IMG + (uint32_t)((wc * 128 + r16) * 128 + (ch << 4));
+    }
+    if constexpr (!TRANS_B) {
+        const int q = (lane >> 2) & 3, p = lane & 3, kr = 8 * h4 + q;
+#pragma unroll
+        for (int ni = 0; ni < 8; ++ni) {
+            const int c = wc * 16 + 2 * ni + (p >> 1);
+            b_rd[ni] = lds0 + IMG + (uint32_t)(kr * 512 + ((c ^ w5_fnn(kr)) << 4) + (p & 1) * 8);
+        }
+    }
+
+    i32x4 fa[2][8];
+    BFrag fb[2][8];
+    // fragment read I (0-7 A, 8-15 B) of half H of the step whose slot is at
+    // byte offset so, into buffer P (= H)
+    auto frag_read = [&](auto h_tag, auto i_tag, uint32_t so) __attribute__((always_inline)) {
+        constexpr int H = decltype(h_tag)::value, I = decltype(i_tag)::value;
+        if constexpr (I < 8) {
+            w5_rd128<I * 2048>(fa[H][I], a_rd[H] + so);
+        } else if constexpr (TRANS_B) {
+            w5_rd128<(I - 8) * 2048>(fb[H][I - 8], b_rd[H] + so);
+        } else {
+            w5_rdtr<H * 16384>(fb[H][I - 8], b_rd[I - 8] + so);
+        }
+    };
+    auto frag_wait = [&](auto p_tag) __attribute__((always_inline)) {
+        constexpr int P = decltype(p_tag)::value;
+        if constexpr (TRANS_B) {
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(fa[P][0]), "+v"(fa[P][1]), "+v"(fa[P][2]), "+v"(fa[P][3]), "+v"(fa[P][4]),
+                           "+v"(fa[P][5]), "+v"(fa[P][6]), "+v"(fa[P][7]), "+v"(fb[P][0]), "+v"(fb[P][1]),
+                           "+v"(fb[P][2]), "+v"(fb[P][3]), "+v"(fb[P][4]), "+v"(fb[P][5]), "+v"(fb[P][6]),
+                           "+v"(fb[P][7])::"memory");
+        } else {
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(fa[P][0]), "+v"(fa[P][1]), "+v"(fa[P][2]), "+v"(fa[P][3]), "+v"(fa[P][4]),
+                           "+v"(fa[P][5]), "+v"(fa[P][6]), "+v"(fa[P][7])::"memory");
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(fb[P][0].lo), "+v"(fb[P][0].hi), "+v"(fb[P][1].lo), "+v"(fb[P][1].hi),
+                           "+v"(fb[P][2].lo), "+v"(fb[P][2].hi), "+v"(fb[P][3].lo), "+v"(fb[P][3].hi),
+                           "+v"(fb[P][4].lo), "+v"(fb[P][4].hi), "+v"(fb[P][5].lo), "+v"(fb[P][5].hi),
+                           "+v"(fb[P][6].lo), "+v"(fb[P][6].hi), "+v"(fb[P][7].lo), "+v"(fb[P][7].hi)::"memory");
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto bop = [&](const BFrag& f) __attribute__((always_inline)) {
+        if constexpr (TRANS_B) return f;
+        else return i32x4{f.lo.x, f.lo.y, f.hi.x, f.hi.y};
+    };
+    // 64 MFMAs on buffer P, with fragment reads (RD: 16, half RH into buffer
+    // RH, slot offset rso) and (DMA) the 16 pieces of step ds in their gaps
+    auto half = [&](auto p_tag, auto rd_tag, auto rh_tag, uint32_t rso, auto dma_tag, int ds)
+        __attribute__((always_inline)) {
+        constexpr int P = decltype(p_tag)::value, RH = decltype(rh_tag)::value;
+        constexpr bool RD = decltype(rd_tag)::value, DMA = decltype(dma_tag)::value;
+        w5_sfor<64>([&](auto JJ) {
+            constexpr int J = JJ, ni = J / 8, mi = J % 8;
+            if constexpr (std::is_same_v<T, bf16_t>) w4v::mfma_bf16<J>(bop(fb[P][ni]), fa[P][mi]);
+            else w4v::mfma_f16<J>(bop(fb[P][ni]), fa[P][mi]);
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (RD && J < 16) frag_read(std::integral_constant<int, RH>{}, JJ, rso);
+            constexpr int D = J - W5_DMA_START;
+            if constexpr (DMA && !W5_ABL_DMA && D >= 0 && D % W5_DMA_STRIDE == 0 && D / W5_DMA_STRIDE < 16)
+                dma_piece(std::integral_constant<int, D / W5_DMA_STRIDE>{}, ds);
+            __builtin_amdgcn_sched_barrier(0);
+        });
+    };
+
+    // ---- prologue: accumulators 0, steps 0 and 1 in flight, (0, h0) fragments
+    w4v::acc_zero();
+    w5_sfor<16>([&](auto J) { dma_piece(J, 0); });
+    w5_sfor<16>([&](auto J) { dma_piece(J, 1); });
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // step 0 (this wave's pieces)
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    w5_sfor<16>([&](auto I) { frag_read(std::integral_constant<int, 0>{}, I, 0u); });
+    frag_wait(std::integral_constant<int, 0>{});
+
+    using Z = std::integral_constant<int, 0>;
+    using O = std::integral_constant<int, 1>;
+    auto step = [&](int s, auto more_tag) __attribute__((always_inline)) {
+        constexpr bool MORE = decltype(more_tag)::value;  // a step s+1 follows
+        const uint32_t so = (uint32_t)(s & 1) * SLOT, sn = (uint32_t)((s + 1) & 1) * SLOT;
+        half(Z{}, std::true_type{}, O{}, so, std::false_type{}, 0);
+        frag_wait(O{});
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // step s+1 landed (this wave's pieces)
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        half(O{}, more_tag, Z{}, sn, std::true_type{}, s + 2);
+        if constexpr (MORE) frag_wait(Z{});
+    };
+    int s = 0;
+    for (; s + 1 < ks; ++s) step(s, std::true_type{});
+    step(s, std::false_type{});
+
+    // ---- epilogue (gemm_w4v's): accumulator block (ni, mi) holds C[m][n..n+3]
+    // with m = m0 + 128 wr + 16 mi + (lane & 15), n = n0 + 128 wc + 16 ni +
+    // 4 (lane >> 4); each wave packs its 128 x 128 tile into its own 32 KiB of
+    // LDS ([row][256 B], chunk c of row r at c ^ (r & 15)) and stores whole
+    // 256-B row segments, 16 B per lane
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // dead-slot reloads landed
+    __builtin_amdgcn_s_barrier();                     // every wave is done with the ring
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");  // last MFMA -> accumulator reads
+    char* reg = smem + wave * 32768;
+    w5_sfor<64>([&](auto JJ) {
+        constexpr int J = JJ, ni = J / 8, mi = J % 8;
+        f32x4 v;
+        w4v::acc_read<J>(v);
+        const int n = n0 + 128 * wc + 16 * ni + 4 * h4;
+        if constexpr (BIAS) {
+            if (n < N) {
+                const i32x2 bb = *reinterpret_cast<const i32x2*>(bias + n);
+                v[0] += elem<T>::to_f32(T{(uint16_t)(bb.x & 0xffff)});
+                v[1] += elem<T>::to_f32(T{(uint16_t)((uint32_t)bb.x >> 16)});
+                v[2] += elem<T>::to_f32(T{(uint16_t)(bb.y & 0xffff)});
+                v[3] += elem<T>::to_f32(T{(uint16_t)((uint32_t)bb.y >> 16)});
+            }
+        }
+        const i32x2 pk = i32x2{(int)pack2<T>(v[0], v[1]), (int)pack2<T>(v[2], v[3])};
+        const int row = 16 * mi + r16, chunk = 2 * ni + (h4 >> 1);
+        *reinterpret_cast<i32x2*>(reg + row * 256 + ((chunk ^ r16) << 4) + (h4 & 1) * 8) = pk;
+    });
+    {
+        const int c = lane & 15;
+        const int n = n0 + 128 * wc + 8 * c;
+#pragma unroll 8
+        for (int it = 0; it < 32; ++it) {
+            const int row = 4 * it + h4;
+            const i32x4 v = *reinterpret_cast<const i32x4*>(reg + row * 256 + ((c ^ (row & 15)) << 4));
+            const int m = m0 + 128 * wr + row;
+            if (m < M && n < N) *reinterpret_cast<i32x4*>(C + (int64_t)m * ldc + n) = v;
+        }
+    }
+}
+
+}  // namespace
+
+bool gemm_w5_ok(int m, int n, int k, int64_t lda, int64_t ldb, int64_t ldc, int trans_b) {
+    (void)m;
+    (void)ldc;
+    // per-lane DMA offsets are 32-bit: 256 rows (NN: 64 k-rows) of the operand
+    return k >= 64 && k % 64 == 0 && n % 8 == 0 && n >= 8 && lda * 2 * 256 < (1ll << 31) &&
+           ldb * 2 * (trans_b ? 256 : 64) < (1ll << 31);
+}
+
+int launch_gemm_w5(const void* a, const void* b, void* c, const void* bias, int m, int n, int k, int64_t lda,
+                   int64_t ldb, int64_t ldc, int trans_b, int is_bf16, hipStream_t stream, int group_m) {
+    PLI_REQUIRE(gemm_w5_ok(m, n, k, lda, ldb, ldc, trans_b), "gemm_w5: shape m=%d n=%d k=%d not supported", m, n,
+                k);
+    PLI_REQUIRE(group_m >= 1, "gemm_w5: group_m must be >= 1");
+    const int tiles_m = cdiv(m, 256), tiles_n = cdiv(n, 256);
+    const int64_t nb = (int64_t)tiles_m * tiles_n;
+    PLI_REQUIRE(nb < (1ll << 31), "gemm_w5: grid too large");
+    const auto* A = (const uint16_t*)a;
+    const auto* B = (const uint16_t*)b;
+    auto* Cc = (uint16_t*)c;
+    const auto* bs = (const uint16_t*)bias;
+    const dim3 gr((unsigned)nb), blk(256);
+#define W5_LAUNCH(T, TB, BI)                                                                                        \
+    hipLaunchKernelGGL((gemm_w5<T, TB, BI>), gr, blk, 0, stream, A, B, Cc, bs, m, n, k, lda, ldb, ldc, tiles_n, \
+                       (int)nb, group_m)
+    if (is_bf16) {
+        if (trans_b) { if (bias) W5_LAUNCH(bf16_t, true, true); else W5_LAUNCH(bf16_t, true, false); }
+        else { if (bias) W5_LAUNCH(bf16_t, false, true); else W5_LAUNCH(bf16_t, false, false); }
+    } else {
+        if (trans_b) { if (bias) W5_LAUNCH(f16_t, true, true); else W5_LAUNCH(f16_t, true, false); }
+        else { if (bias) W5_LAUNCH(f16_t, false, true); else W5_LAUNCH(f16_t, false, false); }
+    }
+#undef W5_LAUNCH
+    return launch_status("gemm_w5");
+}
+
+}  // namespace pli

@@ -1,5 +1,6 @@
-"""gemm_w4v (csrc/gemm_w4v.hip; GEMM variant 40, the default route for large
-bf16 / fp16 shapes since round 3) against the f64 product of the same rounded
+"""gemm_w5 (csrc/gemm_w5.hip; GEMM variant 41, the default route for large
+bf16 / fp16 shapes since round 3: K staged 64 deep) and gemm_w4v
+(csrc/gemm_w4v.hip; variant 40, K 32 deep) against the f64 product of the same rounded
 inputs (reference ch03/gemm_benchmark.py:35-49 times torch.mm on these shapes;
 ch09/tensor_parallel.py:66-68 is the NT F.linear form) and bitwise against
 the 256-tile kernel (variant 2), which runs the same MFMA chains in the same
@@ -30,41 +31,46 @@ def _ref(a, b, tb, bias=None):
     return r + bias.double() if bias is not None else r
 
 
+@pytest.mark.parametrize("variant", [41, 40])
 @pytest.mark.parametrize("tb", [True, False], ids=["nt", "nn"])
 @pytest.mark.parametrize("m,n,k", [(512, 512, 64), (256, 256, 32), (300, 520, 96), (1000, 776, 4096),
-                                   (777, 1032, 160), (2048, 8192, 1024), (4096, 4096, 4096)])
-def test_w4v_vs_f64_and_v2(m, n, k, tb):
+                                   (777, 1032, 160), (2048, 8192, 1024), (4096, 4096, 4096), (264, 392, 128)])
+def test_w4v_vs_f64_and_v2(m, n, k, tb, variant):
     import pli_hip
+    if variant == 41 and k % 64:
+        pytest.skip("gemm_w5 takes K % 64 == 0")
     a, b = _inputs(m, n, k, tb, torch.bfloat16, m * 7 + n * 3 + k)
-    o = pli_hip.gemm(a, b, trans_b=tb, variant=40)
+    o = pli_hip.gemm(a, b, trans_b=tb, variant=variant)
     ref = _ref(a, b, tb)
     err = ((o.double() - ref).abs() / (ref.abs() + 1)).max().item()
-    assert err <= 1e-2, f"{m}x{n}x{k} tb={tb}: max rel err {err:.3e}"
+    assert err <= 1e-2, f"v{variant} {m}x{n}x{k} tb={tb}: max rel err {err:.3e}"
     if k % 64 == 0 and m >= 512 and n >= 512:
-        assert torch.equal(o, pli_hip.gemm(a, b, trans_b=tb, variant=2)), "w4v != gemm_256 (same chain order)"
+        assert torch.equal(o, pli_hip.gemm(a, b, trans_b=tb, variant=2)), f"v{variant} != gemm_256 (same chain order)"
 
 
+@pytest.mark.parametrize("variant", [41, 40])
 @pytest.mark.parametrize("tb", [True, False], ids=["nt", "nn"])
-def test_w4v_bias_fp16_and_default_route(tb):
+def test_w4v_bias_fp16_and_default_route(tb, variant):
     import pli_hip
     a, b = _inputs(1024, 1024, 512, tb, torch.float16, 5)
     bias = torch.randn(1024, device=DEV, dtype=torch.float16)
-    o = pli_hip.gemm(a, b, trans_b=tb, bias=bias, variant=40)
+    o = pli_hip.gemm(a, b, trans_b=tb, bias=bias, variant=variant)
     ref = _ref(a, b, tb, bias)
     err = ((o.double() - ref).abs() / (ref.abs() + 1)).max().item()
     assert err <= 4e-3, f"fp16 + bias tb={tb}: max rel err {err:.3e}"
-    # the default route takes gemm_w4v at this size (128+ tiles of 256^2)
+    # the default route takes gemm_w5 at this size (128+ tiles of 256^2)
     a, b = _inputs(4096, 2048, 1024, tb, torch.bfloat16, 6)
-    assert torch.equal(pli_hip.gemm(a, b, trans_b=tb), pli_hip.gemm(a, b, trans_b=tb, variant=40))
+    assert torch.equal(pli_hip.gemm(a, b, trans_b=tb), pli_hip.gemm(a, b, trans_b=tb, variant=variant))
 
 
+@pytest.mark.parametrize("variant", [41, 40])
 @pytest.mark.parametrize("tb", [True, False], ids=["nt", "nn"])
-def test_w4v_strided_leading_dims(tb):
+def test_w4v_strided_leading_dims(tb, variant):
     import pli_hip
     a, b = _inputs(600, 520, 256, tb, torch.bfloat16, 9, lda=384, ldb=392 if tb else 528)
     assert a.stride(0) == 384
     o = torch.empty(600, 536, device=DEV, dtype=torch.bfloat16)[:, :520]
-    pli_hip.gemm(a, b, trans_b=tb, out=o, variant=40)
+    pli_hip.gemm(a, b, trans_b=tb, out=o, variant=variant)
     ref = _ref(a, b, tb)
     err = ((o.double() - ref).abs() / (ref.abs() + 1)).max().item()
     assert err <= 1e-2, f"strided tb={tb}: max rel err {err:.3e}"

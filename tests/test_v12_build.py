@@ -1,4 +1,6 @@
-"""Build-time invariants of attn_fwd_v12 (csrc/flash_v12.hip), CPU only.
+"""Build-time invariants of the kernels that name accumulator registers
+literally: attn_fwd_v12 (csrc/flash_v12.hip), gemm_w4v and gemm_w5 (csrc/
+gemm_w4v.hip, gemm_w5.hip; C^T in a[0:255]), CPU only.
 
 The kernel names its accumulator registers literally in inline asm (O, Q, K
 fragments in a[0:255]); hipcc does not know the Q fragments stay live between
@@ -22,11 +24,14 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
-def test_v12_no_compiler_agpr_use_or_spill(tmp_path):
-    out = tmp_path / "v12.s"
-    cmd = [HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "-fno-honor-nans",
+@pytest.mark.parametrize("src", ["flash_v12.hip", "gemm_w4v.hip", "gemm_w5.hip"])
+def test_v12_no_compiler_agpr_use_or_spill(tmp_path, src):
+    out = tmp_path / "k.s"
+    flags = ["-fno-honor-nans"] if src == "flash_v12.hip" else []
+    defs = os.environ.get("V12_DEFS", "").split() if src == "flash_v12.hip" else []
+    cmd = [HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950"] + flags + [
            "-I" + os.path.join(ROOT, "include"), "-I" + CSRC, "-S", "--cuda-device-only",
-           os.path.join(CSRC, "flash_v12.hip"), "-o", str(out)] + os.environ.get("V12_DEFS", "").split()
+           os.path.join(CSRC, src), "-o", str(out)] + defs
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     text = out.read_text()
@@ -46,6 +51,6 @@ def test_v12_no_compiler_agpr_use_or_spill(tmp_path):
         # pieces): nothing hipcc generates may read or write M0
         if not in_asm and re.search(r"\bm0\b", line.split(";")[0]):
             own.append(line.strip())
-    assert not own, f"hipcc-generated AGPR/scratch/M0 accesses in attn_fwd_v12: {own[:8]}"
-    m = re.search(r"\.private_segment_fixed_size:\s+(\d+)", text)
-    assert m and int(m.group(1)) == 0, "attn_fwd_v12 uses scratch"
+    assert not own, f"hipcc-generated AGPR/scratch/M0 accesses in {src}: {own[:8]}"
+    sizes = [int(x) for x in re.findall(r"\.private_segment_fixed_size:\s+(\d+)", text)]
+    assert sizes and not any(sizes), f"{src}: a kernel uses scratch ({sizes})"
