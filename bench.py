@@ -47,6 +47,7 @@ PEAK_BF16_TFLOPS = 2516.6   # 256 CU x 4096 FLOP/clk x 2.4 GHz (dense)
 PEAK_HBM_GBPS = 8000.0      # HBM3E datasheet
 B, H, S, D = 8, 32, 4096, 128
 FLASH_KERNEL = "attn_fwd_v12 persistent (variant 71; bitwise = attn_fwd_v10 exact)"
+GEMM_KERNEL = "gemm_w5 (variant 41: 256x256 tile, one wave per SIMD, K staged 64 deep)"
 CAUSAL_KERNEL = "attn_fwd_v12 causal, persistent pair walk (variant 74)"
 
 
@@ -329,7 +330,7 @@ def bench_gemm(stream, iters: int) -> dict:
                        iters, stream)
     ms, ms_t = t["ours"], t["torch"]
     tf = 2 * n ** 3 / (ms * 1e-3) / 1e12
-    return {"workload": "ch05/ch03 GEMM 4096^3 bf16 NN", "us_per_launch": ms * 1e3,
+    return {"workload": "ch05/ch03 GEMM 4096^3 bf16 NN", "kernel": GEMM_KERNEL, "us_per_launch": ms * 1e3,
             "timing": f"events, median of 3 interleaved rounds of {iters} launches (ours / torch)",
             "TFLOP/s": tf, "torch_mm_TFLOP/s": 2 * n ** 3 / (ms_t * 1e-3) / 1e12,
             "roofline": {"bound": "mfma", "achieved": tf, "peak": PEAK_BF16_TFLOPS,

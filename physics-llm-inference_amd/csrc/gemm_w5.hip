@@ -48,6 +48,12 @@
 #ifndef W5_DMA_IMM
 #define W5_DMA_IMM 1  // one M0 write per 4 pieces, pieces 1-3 by instruction offset
 #endif
+#ifndef W5_RD_STRIDE
+#define W5_RD_STRIDE 1  // gaps between fragment reads
+#endif
+#ifndef W5_RING5
+#define W5_RING5 0  // 5 ring positions of 32 KiB (A and B images apart): A's DMA in half 0, B's in half 1
+#endif
 #ifndef W5_ABL_DMA
 #define W5_ABL_DMA 0  // timing only: no DMA in the loop (results wrong)
 #endif
@@ -90,7 +96,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A
                                                   int tiles_n, int nblocks, int group_m) {
     constexpr int IMG = 32768, SLOT = 2 * IMG;
     using BFrag = std::conditional_t<TRANS_B, i32x4, W5Pair>;
-    __shared__ __attribute__((aligned(1024))) char smem[2 * SLOT];
+    __shared__ __attribute__((aligned(1024))) char smem[W5_RING5 ? 5 * IMG : 2 * SLOT];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -134,13 +140,18 @@ __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A
         asm volatile("global_load_lds_dwordx4 %0, %1 offset:%2" ::"v"(off),
                      "s"(reinterpret_cast<const char*>(src) - 1024 * i), "n"(1024 * i) : "memory");
     };
-    // DMA piece j (0-7 A, 8-15 B) of K step s into slot s % 2 (past the last
+    // LDS byte offset of step s's A (x = 0) or B (x = 1) image: slot s % 2,
+    // or (W5_RING5) ring position (2s + x) % 5
+    auto img_off = [&](int s, int x) __attribute__((always_inline)) {
+        return W5_RING5 ? (uint32_t)((2 * s + x) % 5) * IMG : (uint32_t)(s & 1) * SLOT + (uint32_t)x * IMG;
+    };
+    // DMA piece j (0-7 A, 8-15 B) of K step s into its image (past the last
     // step: a reload of the last step)
     auto dma_piece = [&](auto j_tag, int s) __attribute__((always_inline)) {
         constexpr int j = decltype(j_tag)::value, i = j % 8;
         const int sc = min(s, ks - 1);
-        const uint32_t slot = lds0 + (uint32_t)(s & 1) * SLOT + (j < 8 ? 0u : (uint32_t)IMG) +
-                              (uint32_t)wave * 8192 + (uint32_t)(W5_DMA_IMM ? (i / 4) * 4096 : i * 1024);
+        const uint32_t slot = lds0 + img_off(s, j < 8 ? 0 : 1) + (uint32_t)wave * 8192 +
+                              (uint32_t)(W5_DMA_IMM ? (i / 4) * 4096 : i * 1024);
         const uint16_t* src = j < 8 ? abase + sc * 64 : (TRANS_B ? bbase + sc * 64 : bbase + (int64_t)sc * 64 * ldb);
         const uint32_t off = j < 8 ? aoff[i] : boff[i];
         if constexpr (W5_DMA_IMM && i % 4 > 0) dma_next(std::integral_constant<int, i % 4>{}, src, off);
@@ -155,29 +166,29 @@ __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A
     for (int h = 0; h < 2; ++h) {
         const int ch = (4 * h + h4) ^ ((r16 >> 1) & 7);
         a_rd[h] = lds0 + (uint32_t)((wr * 128 + r16) * 128 + (ch << 4));
-        if constexpr (TRANS_B) b_rd[h] = lds0 + IMG + (uint32_t)((wc * 128 + r16) * 128 + (ch << 4));
+        if constexpr (TRANS_B) b_rd[h] = lds0 + (uint32_t)((wc * 128 + r16) * 128 + (ch << 4));
     }
     if constexpr (!TRANS_B) {
         const int q = (lane >> 2) & 3, p = lane & 3, kr = 8 * h4 + q;
 #pragma unroll
         for (int ni = 0; ni < 8; ++ni) {
             const int c = wc * 16 + 2 * ni + (p >> 1);
-            b_rd[ni] = lds0 + IMG + (uint32_t)(kr * 512 + ((c ^ w5_fnn(kr)) << 4) + (p & 1) * 8);
+            b_rd[ni] = lds0 + (uint32_t)(kr * 512 + ((c ^ w5_fnn(kr)) << 4) + (p & 1) * 8);
         }
     }
 
     i32x4 fa[2][8];
     BFrag fb[2][8];
-    // fragment read I (0-7 A, 8-15 B) of half H of the step whose slot is at
-    // byte offset so, into buffer P (= H)
-    auto frag_read = [&](auto h_tag, auto i_tag, uint32_t so) __attribute__((always_inline)) {
+    // fragment read I (0-7 A, 8-15 B) of half H of the step whose A and B
+    // images sit at byte offsets sa, sb, into buffer P (= H)
+    auto frag_read = [&](auto h_tag, auto i_tag, uint32_t sa, uint32_t sb) __attribute__((always_inline)) {
         constexpr int H = decltype(h_tag)::value, I = decltype(i_tag)::value;
         if constexpr (I < 8) {
-            w5_rd128<I * 2048>(fa[H][I], a_rd[H] + so);
+            w5_rd128<I * 2048>(fa[H][I], a_rd[H] + sa);
         } else if constexpr (TRANS_B) {
-            w5_rd128<(I - 8) * 2048>(fb[H][I - 8], b_rd[H] + so);
+            w5_rd128<(I - 8) * 2048>(fb[H][I - 8], b_rd[H] + sb);
         } else {
-            w5_rdtr<H * 16384>(fb[H][I - 8], b_rd[I - 8] + so);
+            w5_rdtr<H * 16384>(fb[H][I - 8], b_rd[I - 8] + sb);
         }
     };
     auto frag_wait = [&](auto p_tag) __attribute__((always_inline)) {
@@ -205,20 +216,25 @@ __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A
         else return i32x4{f.lo.x, f.lo.y, f.hi.x, f.hi.y};
     };
     // 64 MFMAs on buffer P, with fragment reads (RD: 16, half RH into buffer
-    // RH, slot offset rso) and (DMA) the 16 pieces of step ds in their gaps
-    auto half = [&](auto p_tag, auto rd_tag, auto rh_tag, uint32_t rso, auto dma_tag, int ds)
+    // RH, image offsets rsa / rsb) and DMA pieces J0 .. J0+NJ-1 of step ds in
+    // their gaps
+    constexpr int DSTART = W5_RING5 ? 2 : W5_DMA_START, DSTRIDE = W5_RING5 ? 8 : W5_DMA_STRIDE;
+    auto half = [&](auto p_tag, auto rd_tag, auto rh_tag, uint32_t rsa, uint32_t rsb, auto j0_tag, auto nj_tag, int ds)
         __attribute__((always_inline)) {
         constexpr int P = decltype(p_tag)::value, RH = decltype(rh_tag)::value;
-        constexpr bool RD = decltype(rd_tag)::value, DMA = decltype(dma_tag)::value;
+        constexpr bool RD = decltype(rd_tag)::value;
+        constexpr int J0 = decltype(j0_tag)::value, NJ = decltype(nj_tag)::value;
         w5_sfor<64>([&](auto JJ) {
             constexpr int J = JJ, ni = J / 8, mi = J % 8;
             if constexpr (std::is_same_v<T, bf16_t>) w4v::mfma_bf16<J>(bop(fb[P][ni]), fa[P][mi]);
             else w4v::mfma_f16<J>(bop(fb[P][ni]), fa[P][mi]);
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (RD && J < 16) frag_read(std::integral_constant<int, RH>{}, JJ, rso);
-            constexpr int D = J - W5_DMA_START;
-            if constexpr (DMA && !W5_ABL_DMA && D >= 0 && D % W5_DMA_STRIDE == 0 && D / W5_DMA_STRIDE < 16)
-                dma_piece(std::integral_constant<int, D / W5_DMA_STRIDE>{}, ds);
+            if constexpr (RD && J % W5_RD_STRIDE == 0 && J / W5_RD_STRIDE < 16)
+                frag_read(std::integral_constant<int, RH>{}, std::integral_constant<int, J / W5_RD_STRIDE>{}, rsa,
+                          rsb);
+            constexpr int D = J - DSTART;
+            if constexpr (!W5_ABL_DMA && D >= 0 && D % DSTRIDE == 0 && D / DSTRIDE < NJ)
+                dma_piece(std::integral_constant<int, J0 + D / DSTRIDE>{}, ds);
             __builtin_amdgcn_sched_barrier(0);
         });
     };
@@ -230,20 +246,33 @@ __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A
     asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // step 0 (this wave's pieces)
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    w5_sfor<16>([&](auto I) { frag_read(std::integral_constant<int, 0>{}, I, 0u); });
+    w5_sfor<16>([&](auto I) { frag_read(std::integral_constant<int, 0>{}, I, img_off(0, 0), img_off(0, 1)); });
     frag_wait(std::integral_constant<int, 0>{});
 
     using Z = std::integral_constant<int, 0>;
     using O = std::integral_constant<int, 1>;
     auto step = [&](int s, auto more_tag) __attribute__((always_inline)) {
         constexpr bool MORE = decltype(more_tag)::value;  // a step s+1 follows
-        const uint32_t so = (uint32_t)(s & 1) * SLOT, sn = (uint32_t)((s + 1) & 1) * SLOT;
-        half(Z{}, std::true_type{}, O{}, so, std::false_type{}, 0);
+        using N0 = std::integral_constant<int, 0>;
+        using N8 = std::integral_constant<int, 8>;
+        using N16 = std::integral_constant<int, 16>;
+        // W5_RING5: step s+2's A pieces in half 0 (into B(s-1)'s dead ring
+        // position), its B pieces in half 1 (into A(s)'s); else all 16 in half 1
+        if constexpr (W5_RING5)
+            half(Z{}, std::true_type{}, O{}, img_off(s, 0), img_off(s, 1), N0{}, N8{}, s + 2);
+        else
+            half(Z{}, std::true_type{}, O{}, img_off(s, 0), img_off(s, 1), N0{}, N0{}, s + 2);
         frag_wait(O{});
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // step s+1 landed (this wave's pieces)
+        // step s+1 landed (this wave's pieces; RING5: step s+2's A pieces,
+        // issued in half 0, may stay in flight)
+        if constexpr (W5_RING5) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
-        half(O{}, more_tag, Z{}, sn, std::true_type{}, s + 2);
+        if constexpr (W5_RING5)
+            half(O{}, more_tag, Z{}, img_off(s + 1, 0), img_off(s + 1, 1), N8{}, N8{}, s + 2);
+        else
+            half(O{}, more_tag, Z{}, img_off(s + 1, 0), img_off(s + 1, 1), N0{}, N16{}, s + 2);
         if constexpr (MORE) frag_wait(Z{});
     };
     int s = 0;
@@ -304,6 +333,9 @@ int launch_gemm_w5(const void* a, const void* b, void* c, const void* bias, int 
                    int64_t ldb, int64_t ldc, int trans_b, int is_bf16, hipStream_t stream, int group_m) {
     PLI_REQUIRE(gemm_w5_ok(m, n, k, lda, ldb, ldc, trans_b), "gemm_w5: shape m=%d n=%d k=%d not supported", m, n,
                 k);
+#ifdef W5_GROUP_M
+    group_m = W5_GROUP_M;  // A/B builds only
+#endif
     PLI_REQUIRE(group_m >= 1, "gemm_w5: group_m must be >= 1");
     const int tiles_m = cdiv(m, 256), tiles_n = cdiv(n, 256);
     const int64_t nb = (int64_t)tiles_m * tiles_n;
