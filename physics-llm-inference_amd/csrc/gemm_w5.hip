@@ -40,7 +40,7 @@
 
 // A/B switches (tools/build_ab.sh); the defaults are the product
 #ifndef W5_DMA_START
-#define W5_DMA_START 2  // half-1 gap of the first DMA piece
+#define W5_DMA_START 0  // half-1 gap of the first DMA piece
 #endif
 #ifndef W5_DMA_STRIDE
 #define W5_DMA_STRIDE 4  // gaps between DMA pieces
@@ -49,7 +49,7 @@
 #define W5_DMA_IMM 1  // one M0 write per 4 pieces, pieces 1-3 by instruction offset
 #endif
 #ifndef W5_RD_STRIDE
-#define W5_RD_STRIDE 1  // gaps between fragment reads
+#define W5_RD_STRIDE 2  // gaps between fragment reads (with DMA start 0: 0-3 % over stride 1 / start 2, profiles/r03/gemm/ab_w5_ring5.log)
 #endif
 #ifndef W5_RING5
 #define W5_RING5 0  // 5 ring positions of 32 KiB (A and B images apart): A's DMA in half 0, B's in half 1
