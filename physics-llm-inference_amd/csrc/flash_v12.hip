@@ -181,7 +181,7 @@ typedef __attribute__((ext_vector_type(2))) float v12f2;
 
 #ifdef PLI_FLASH_STAMPS
 // diagnostic build only (tools/build_diag.sh): per-segment s_memtime sums
-__device__ unsigned long long g_v12_stamps[16];
+__device__ unsigned long long g_v12_stamps[24];
 #endif
 
 // STAMP (diagnostic build only): 0 none, 1 per-segment s_memtime sums, 2 the
@@ -294,7 +294,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     };
     int nt = block_nt(q0);
     int tdiag = CAUSAL ? (q0 + Nk - Nq + 1) / KT : 1 << 30;
-    unsigned long long st_sum[14] = {}, st_last = 0;
+    unsigned long long st_sum[20] = {}, st_last = 0;
     auto stamp = [&](int seg) __attribute__((always_inline)) {
         if constexpr (STAMP == 1) {
             unsigned long long now;
@@ -881,6 +881,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
             block_ptrs(has_next ? L + (int)gridDim.x : L, b2, h2, r2, q2, k2, v2);
             load_q(q2, r2);
         }
+        stamp(14);
 
         // ---- epilogue: block B's slices 8..15 and PV of the last tile, l, O
         // read-out and store.  The V^T addresses are made opaque here, or
@@ -891,10 +892,12 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         for (int db = 0; db < 4; ++db) asm volatile("" : "+v"(valo[db]), "+v"(vahi[db]));
         if ((nt - 1) & 1) { tailB(P1); pfence(P1); }
         else { tailB(P0); pfence(P0); }
+        stamp(15);
         if ((nt - 1) & 1)
             phaseP(slot(nt - 1), P1, P1, 0, std::true_type{}, std::false_type{}, std::false_type{}, std::false_type{});
         else
             phaseP(slot(nt - 1), P0, P0, 0, std::true_type{}, std::false_type{}, std::false_type{}, std::false_type{});
+        stamp(16);
         asm volatile("s_nop 15\n\ts_nop 7" : "+v"(lA), "+v"(lB));
         const float invA = [&] { const float l = v12_xor32_sum(lA[0]); return l > 0.f ? 1.f / l : 0.f; }();
         const float invB = [&] { const float l = v12_xor32_sum(lB[0]); return l > 0.f ? 1.f / l : 0.f; }();
@@ -920,9 +923,11 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
                 }
             });
         };
+        stamp(17);
         store(std::integral_constant<int, 0>{}, invA);
+        stamp(18);
         store(std::integral_constant<int, 1>{}, invB);
-        stamp(13);
+        stamp(19);
         if (!has_next) break;
         s0 = (s0 + nt) % NBUF;
         L += (int)gridDim.x;
@@ -939,9 +944,9 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         stamp(7);
         if (lane == 0) {
 #pragma unroll
-            for (int i = 0; i < 14; ++i) atomicAdd(&g_v12_stamps[i], st_sum[i]);
-            atomicAdd(&g_v12_stamps[14], (unsigned long long)nt * (unsigned long long)nblk);
-            atomicAdd(&g_v12_stamps[15], 1ull);
+            for (int i = 0; i < 20; ++i) atomicAdd(&g_v12_stamps[i], st_sum[i]);
+            atomicAdd(&g_v12_stamps[22], (unsigned long long)nt * (unsigned long long)nblk);
+            atomicAdd(&g_v12_stamps[23], 1ull);
         }
     }
     if constexpr (STAMP == 2) {
@@ -950,8 +955,8 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         if (lane == 0) {
             atomicAdd(&g_v12_stamps[0], t1 - clk_t0);
             atomicAdd(&g_v12_stamps[1], r1 - clk_r0);
-            atomicAdd(&g_v12_stamps[14], (unsigned long long)nt * (unsigned long long)nblk);
-            atomicAdd(&g_v12_stamps[15], 1ull);
+            atomicAdd(&g_v12_stamps[22], (unsigned long long)nt * (unsigned long long)nblk);
+            atomicAdd(&g_v12_stamps[23], 1ull);
         }
     }
 #endif
@@ -1019,8 +1024,8 @@ int launch_attn_v12(const void* q, const void* k, const void* v, void* o, int B,
 
 #ifdef PLI_FLASH_STAMPS
 // Diagnostic entry (tools/libpli_diag.so only): one stamped launch of
-// attn_fwd_v12 on contiguous [B,H,N,128] bf16, the 16 stamp words to `out`
-// (segments: tools/v12_stamps.py SEGS; 14 tiles, 15 waves;
+// attn_fwd_v12 on contiguous [B,H,N,128] bf16, the 24 stamp words to `out`
+// (segments 0-19: tools/v12_stamps.py SEGS; 22 tiles, 23 waves;
 // check, 6 prologue + loop overhead, 7 epilogue; 8 tiles, 9 waves).
 extern "C" int pli_diag_v12_stamps(const void* q, const void* k, const void* v, void* o, int B, int H, int N,
                                    unsigned long long* out, int grid, int mode) {
@@ -1029,7 +1034,7 @@ extern "C" int pli_diag_v12_stamps(const void* q, const void* k, const void* v, 
     const V7Strides st{sb, sh, sn, sb, sh, sn, sb, sh, sn, sb, sh, sn};
     const int qblocks = cdiv(N, 256), nb = B * H * qblocks;
     const float c = (1.f / sqrtf(128.f)) * 1.4426950408889634f;
-    unsigned long long zero[16] = {0};
+    unsigned long long zero[24] = {0};
     hipMemcpyToSymbol(HIP_SYMBOL(g_v12_stamps), zero, sizeof(zero));
     const dim3 gr(grid > 0 && grid < nb ? grid : nb);
     // mode 1: per-segment stamps; mode 2: entry / exit clock only (words 0, 1)
@@ -1040,7 +1045,7 @@ extern "C" int pli_diag_v12_stamps(const void* q, const void* k, const void* v, 
         hipLaunchKernelGGL((attn_fwd_v12<1, 8>), gr, dim3(256), 0, 0, (const uint16_t*)q, (const uint16_t*)k,
                            (const uint16_t*)v, (uint16_t*)o, H, 1, N, N, st, c, qblocks, nb);
     if (hipDeviceSynchronize() != hipSuccess) return -1;
-    hipMemcpyFromSymbol(out, HIP_SYMBOL(g_v12_stamps), 16 * sizeof(unsigned long long));
+    hipMemcpyFromSymbol(out, HIP_SYMBOL(g_v12_stamps), 24 * sizeof(unsigned long long));
     return 0;
 }
 #endif

@@ -42,9 +42,9 @@ for rep in range(2):
     e.record()
     e.synchronize()
     ms = s.elapsed_time(e) / 20
-    buf = (ctypes.c_ulonglong * 16)()
+    buf = (ctypes.c_ulonglong * 24)()
     assert lib.pli_diag_v12_stamps(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), B, H, N, buf, 256, 2) == 0
-    dt, dr, tiles, waves = buf[0], buf[1], buf[14], buf[15]
+    dt, dr, tiles, waves = buf[0], buf[1], buf[22], buf[23]
     ghz = dt / dr * 0.1
     per_wave_us = dr / waves / 100.0
     # every SIMD runs one wave; a wave-tile = 64 query rows x 64 keys
