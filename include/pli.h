@@ -330,13 +330,17 @@ int pli_attn_decode_dev(const void* q, const void* k, const void* v, void* o,
  *   60 attn_fwd_v10 exact in 4-wave workgroups (causal default), 70 / 71
  *   attn_fwd_v12 (one wave per SIMD, 64 rows per wave; 71 persistent =
  *   non-causal default for bf16 D = 128, bitwise equal to 55; other inputs
- *   take 55).  Prescaled variants round Q * scale * log2(e) to the 16-bit
- *   input type (2^-9 relative score error in bf16).
+ *   take 55); 72 = 71 with the defer-max threshold at 0 (tests); 73 / 74
+ *   attn_fwd_v12 causal, one block per workgroup / persistent pair walk
+ *   (74 = causal default).  Prescaled variants round Q * scale * log2(e) to
+ *   the 16-bit input type (2^-9 relative score error in bf16).
  * pli_gemm_variant / pli_gemm_ws_variant: 0 default; 1 128^2 tile; 2 256^2
  *   one-phase; 3 phased SCHED 0; 4 one-phase + setprio; 5-8 phased SCHED
  *   1/3/5/7; 9-11 grouped one-phase (group_m 4/8/16); 12-15 grouped phased
  *   (8/4/2/16); 20 mid-M; 21 small-M; 22/24 direct-load split-K; 25-29 LDS
- *   split-K (256/512/128 targets, 3-deep ring).
+ *   split-K (256/512/128 targets, 3-deep ring); 40 gemm_w4v (one wave per
+ *   SIMD, K 32 deep); 41 gemm_w5 (K 64 deep, LDS-DMA; the large-shape
+ *   default); 42 gemm_w6 (K 64 deep, staged through VGPRs).
  * pli_gemv_variant: 0-16 (rows per wave x 16-B chunks per lane x waves per
  *   block, gemv.hip), -1 default.
  * pli_attn_decode_variant: mode -1 default, 2/9/11/13 load-layout modes
