@@ -339,8 +339,7 @@ int pli_attn_decode_dev(const void* q, const void* k, const void* v, void* o,
  *   1/3/5/7; 9-11 grouped one-phase (group_m 4/8/16); 12-15 grouped phased
  *   (8/4/2/16); 20 mid-M; 21 small-M; 22/24 direct-load split-K; 25-29 LDS
  *   split-K (256/512/128 targets, 3-deep ring); 40 gemm_w4v (one wave per
- *   SIMD, K 32 deep); 41 gemm_w5 (K 64 deep, LDS-DMA; the large-shape
- *   default); 42 gemm_w6 (K 64 deep, staged through VGPRs).
+ *   SIMD, K 32 deep); 41 gemm_w5 (K 64 deep; the large-shape default).
  * pli_gemv_variant: 0-16 (rows per wave x 16-B chunks per lane x waves per
  *   block, gemv.hip), -1 default.
  * pli_attn_decode_variant: mode -1 default, 2/9/11/13 load-layout modes

@@ -26,7 +26,6 @@
 #include "gemm_f32.h"
 #include "gemm_w4v.h"
 #include "gemm_w5.h"
-#include "gemm_w6.h"
 #include "pli_common.h"
 
 namespace pli {
@@ -2212,9 +2211,6 @@ static int gemm_dispatch(const void* a, const void* b, void* c, const void* bias
     // variant 41: gemm_w5 (gemm_w5.hip), the same tile with K staged 64 deep
     if (variant == 41 && vec && gemm_w5_ok(m, n, k, lda, ldb, ldc, trans_b))
         return launch_gemm_w5(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, dtype == PLI_BF16, s, 4);
-    // variant 42: gemm_w6 (gemm_w6.hip), the same tile staged through VGPRs
-    if (variant == 42 && vec && gemm_w6_ok(m, n, k, lda, ldb, ldc, trans_b))
-        return launch_gemm_w6(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, dtype == PLI_BF16, s, 4);
     const bool big = vec && k % G2K == 0 && m >= 2 * G2M && n >= 2 * G2N && variant != 1 &&
                      (variant != 0 || (int64_t)cdiv(m, G2M) * cdiv(n, G2N) >= 128);
     // default for the large shapes since round 3: gemm_w5 (one wave per SIMD,

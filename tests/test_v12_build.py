@@ -24,7 +24,7 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
-@pytest.mark.parametrize("src", ["flash_v12.hip", "gemm_w4v.hip", "gemm_w5.hip", "gemm_w6.hip"])
+@pytest.mark.parametrize("src", ["flash_v12.hip", "gemm_w4v.hip", "gemm_w5.hip"])
 def test_v12_no_compiler_agpr_use_or_spill(tmp_path, src):
     out = tmp_path / "k.s"
     flags = ["-fno-honor-nans"] if src == "flash_v12.hip" else []
