@@ -47,6 +47,7 @@ PEAK_BF16_TFLOPS = 2516.6   # 256 CU x 4096 FLOP/clk x 2.4 GHz (dense)
 PEAK_HBM_GBPS = 8000.0      # HBM3E datasheet
 B, H, S, D = 8, 32, 4096, 128
 FLASH_KERNEL = "attn_fwd_v12 persistent (variant 71; bitwise = attn_fwd_v10 exact)"
+JSON_OUT = sys.stdout  # main() points it at the original stdout and sends fd 1 to stderr
 GEMM_KERNEL = "gemm_w5 (variant 41: 256x256 tile, one wave per SIMD, K staged 64 deep)"
 CAUSAL_KERNEL = "attn_fwd_v12 causal, persistent pair walk (variant 74)"
 
@@ -628,7 +629,7 @@ def selftest_main(args, world: int, rank: int) -> None:
                           "data": "SELFTEST: launcher rehearsal on CPU, not a measurement",
                           "ranks_seen": int(ranks_seen.item()),
                           "backend": dist.get_backend() if world > 1 else None,
-                          "config": {"workload": "selftest"}}), flush=True)
+                          "config": {"workload": "selftest"}}), file=JSON_OUT, flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -653,6 +654,12 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # one process asked for N GPUs: start the N ranks (nothing has touched the GPU yet)
         sys.exit(launch_ranks(args))
+    # stdout carries exactly the one JSON line: anything a library prints there
+    # (gloo's connection banner, runtime notices) goes to stderr instead
+    global JSON_OUT
+    JSON_OUT = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -823,7 +830,7 @@ def main():
         result["cpu_baseline"] = cpu_baseline()
         result["cpu_other"] = cpu_other(result["cpu_baseline"]["cores"])
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=JSON_OUT, flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
