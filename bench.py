@@ -335,7 +335,8 @@ def bench_gemm(stream, iters: int) -> dict:
             "timing": f"events, median of 3 interleaved rounds of {iters} launches (ours / torch)",
             "TFLOP/s": tf, "torch_mm_TFLOP/s": 2 * n ** 3 / (ms_t * 1e-3) / 1e12,
             "roofline": {"bound": "mfma", "achieved": tf, "peak": PEAK_BF16_TFLOPS,
-                         "unit": "TFLOP/s", "frac": tf / PEAK_BF16_TFLOPS}}
+                         "unit": "TFLOP/s", "frac": tf / PEAK_BF16_TFLOPS,
+                         "algorithmic_bytes": 3 * n * n * 2, "traffic": load_traffic("gemm_w5 nn")}}
 
 
 def bench_tp(stream, world: int, rank: int, iters: int) -> dict:
@@ -736,9 +737,12 @@ def main():
     if args.flash_only:
         args.quick, args.no_cpu_baseline = True, True
     # causal variant of the same workload (ch01 MHA semantics), reported only
-    for _ in range(2 if not args.flash_only else 0):
+    # (10 back-to-back warm-up launches, then 20 timed: the first launches
+    # after a change of kernel or an idle gap run slower)
+    for _ in range(10 if not args.flash_only else 0):
         pli_hip.flash_attn_fwd(q, k, v, causal=True, out=o)
     if not args.flash_only:
+        ms_c = event_time_ms(lambda: pli_hip.flash_attn_fwd(q, k, v, causal=True, out=o), 20, stream)
         # the reference's own timing style (sync per call, wall clock), next to the events
         wc = []
         for _ in range(5):
@@ -749,8 +753,7 @@ def main():
             wc.append(time.perf_counter() - t1)
         extra["flash_wallclock_ms"] = {"mean": sum(wc) / len(wc) * 1e3, "min": min(wc) * 1e3,
                                        "timing": "sync + perf_counter per call, 5 calls"}
-        ms_c = event_time_ms(lambda: pli_hip.flash_attn_fwd(q, k, v, causal=True, out=o), 5, stream)
-        extra["flash_causal"] = {"ms": ms_c,
+        extra["flash_causal"] = {"ms": ms_c, "timing": "events, 20 launches after 10 warm-up",
                                  "TFLOP/s": 4 * B * H * D * (S * (S + 1) // 2) / (ms_c * 1e-3) / 1e12,
                                  "kernel": CAUSAL_KERNEL,
                                  "traffic": load_traffic("attn_fwd_v12 causal")}

@@ -19,13 +19,15 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = ("attn_fwd_v12", "attn_fwd_v10", "attn_fwd_v7", "gemm_f32_mfma", "gemm_naive_f32", "hbm_read_probe", "attn_fwd_v2", "attn_decode_chunk", "attn_decode_combine", "gemv_vec", "gemm_mfma",
+KERNELS = ("gemm_w5", "attn_fwd_v12", "attn_fwd_v10", "attn_fwd_v7", "gemm_f32_mfma", "gemm_naive_f32", "hbm_read_probe", "attn_fwd_v2", "attn_decode_chunk", "attn_decode_combine", "gemv_vec", "gemm_mfma",
            "gemm_smallm_nt", "scale_copy_vec")
 
 
 def label(k: str, name: str) -> str:
     """Causal instantiations (template flag ``true``) share the name prefix
     with the non-causal kernel; keep them apart."""
+    if k == "gemm_w5":  # gemm_w5<T, TRANS_B, BIAS>: NT and NN apart
+        return k + (" nt" if ", true," in name else " nn")
     return k + " causal" if k.startswith("attn_fwd") and ", true>" in name else k
 
 
