@@ -83,6 +83,9 @@
 #ifndef V12_UNROLL4
 #define V12_UNROLL4 0  // four steps per loop iteration (A/B)
 #endif
+#ifndef V12_MF16SPLIT
+#define V12_MF16SPLIT 0  // timing only (with a V12_MF16SPLIT asm header): each loop MFMA as two 16x16x32, fillers between
+#endif
 #ifndef V12_SLOT_INC
 #define V12_SLOT_INC 0  // 1: ring slots stepped incrementally (no modulo per use): spills (hipcc parks O in a0/a1)
 #endif
@@ -526,9 +529,17 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         if constexpr (SM) prefm(X1{}, std::integral_constant<int, 8>{});
         sfor<16>([&](auto FF) {
             constexpr int F = FF;
+#if V12_MF16SPLIT
+            v12::qk1h<F, 0, 0>(S[0][F / 8]);
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (SM) stream(X1{}, std::integral_constant<int, 8>{}, FF, Pp);
+            __builtin_amdgcn_sched_barrier(0);
+            v12::qk1h<F, 0, 1>(S[0][F / 8]);
+#else
             v12::qk1<F, 0>(S[0][F / 8]);
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (SM) stream(X1{}, std::integral_constant<int, 8>{}, FF, Pp);
+#endif
             if constexpr (F % 2 == 1 && !V12_ABL_DMA) dma_piece(std::integral_constant<int, F / 2>{}, kt, vt, dbase);
             __builtin_amdgcn_sched_barrier(0);
         });
@@ -551,12 +562,26 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         if constexpr (SM) prefm(X0{}, std::integral_constant<int, 0>{});
         sfor<16>([&](auto FF) {
             constexpr int F = FF;
-            v12::qk1<F, 1>(S[1][F / 8]);
+#if V12_MF16SPLIT
+            v12::qk1h<F, 1, 0>(S[1][F / 8]);
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (SM) {
                 if constexpr (F == 0) opCV(X1{}, std::integral_constant<int, 15>{}, Pp);
                 if constexpr (F % 2 == 0) opMX(X0{}, std::integral_constant<int, F / 2>{});
                 else opMX(X0{}, std::integral_constant<int, 8 + F / 2>{});
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            v12::qk1h<F, 1, 1>(S[1][F / 8]);
+#else
+            v12::qk1<F, 1>(S[1][F / 8]);
+#endif
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (SM) {
+#if !V12_MF16SPLIT
+                if constexpr (F == 0) opCV(X1{}, std::integral_constant<int, 15>{}, Pp);
+                if constexpr (F % 2 == 0) opMX(X0{}, std::integral_constant<int, F / 2>{});
+                else opMX(X0{}, std::integral_constant<int, 8 + F / 2>{});
+#endif
                 stream(X0{}, std::integral_constant<int, 0>{}, FF, Pc);
                 if constexpr (F % 2 == 1 && F < 8)
                     vread1(std::integral_constant<int, 0>{}, std::integral_constant<int, F / 2>{}, vs);
@@ -594,6 +619,22 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
             }
             sfor<8>([&](auto JJ) {
                 constexpr int j = JJ, X = j / 4, k = j % 4, slot = 8 * db + j;
+#if V12_MF16SPLIT
+                if constexpr (PV) {
+                    const V12Frag& ff = vf[db & 1][k];
+                    v12::pv1h<X, db, 0>(i32x4{ff.lo.x, ff.lo.y, ff.hi.x, ff.hi.y}, Pv[X][k / 2][k & 1]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                if constexpr (PV && j < 4 && db + 1 < 4)
+                    vread1(std::integral_constant<int, db + 1>{}, std::integral_constant<int, j>{}, vs);
+                if constexpr (KR && j >= 4 && !V12_ABL_KREAD) v12::kread<4 * db + j - 4>(kaddr[(4 * db + j - 4) % 8] + ks);
+                __builtin_amdgcn_sched_barrier(0);
+                if constexpr (PV) {
+                    const V12Frag& ff = vf[db & 1][k];
+                    v12::pv1h<X, db, 1>(i32x4{ff.lo.x, ff.lo.y, ff.hi.x, ff.hi.y}, Pv[X][k / 2][k & 1]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#else
                 if constexpr (PV) {
                     const V12Frag& ff = vf[db & 1][k];
                     v12::pv1<X, db>(i32x4{ff.lo.x, ff.lo.y, ff.hi.x, ff.hi.y}, Pv[X][k / 2][k & 1]);
@@ -603,6 +644,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
                 if constexpr (PV && j < 4 && db + 1 < 4)
                     vread1(std::integral_constant<int, db + 1>{}, std::integral_constant<int, j>{}, vs);
                 if constexpr (KR && j >= 4 && !V12_ABL_KREAD) v12::kread<4 * db + j - 4>(kaddr[(4 * db + j - 4) % 8] + ks);
+#endif
                 if constexpr (SM) {
                     if constexpr (slot == 0) opCV(X0{}, std::integral_constant<int, 7>{}, Pc);
                     if constexpr (slot % 2 == 1) opMX(X1{}, std::integral_constant<int, slot / 2>{});
