@@ -726,16 +726,6 @@ def main():
     extra = {}
     measured_roof = {}
     log(f"[bench] flash: {achieved:.1f} TF/s per launch ({kernel_ms:.3f} ms)")
-    if not args.flash_only:
-        log("[bench] calibration")
-        cal = calibrate()
-        extra["calibration"] = cal
-        # the flash kernel's QK^T / PV run on v_mfma_f32_32x32x16_bf16
-        measured_roof = {"measured_peak": cal["mfma_32x32x16_TFLOP/s"],
-                         "measured_peak_kind": "pli_mfma_probe 32x32x16 (the kernel's shape)",
-                         "frac_of_measured": achieved / cal["mfma_32x32x16_TFLOP/s"]}
-    if args.flash_only:
-        args.quick, args.no_cpu_baseline = True, True
     # causal variant of the same workload (ch01 MHA semantics), reported only
     # (10 back-to-back warm-up launches, then 20 timed: the first launches
     # after a change of kernel or an idle gap run slower)
@@ -757,6 +747,17 @@ def main():
                                  "TFLOP/s": 4 * B * H * D * (S * (S + 1) // 2) / (ms_c * 1e-3) / 1e12,
                                  "kernel": CAUSAL_KERNEL,
                                  "traffic": load_traffic("attn_fwd_v12 causal")}
+    if not args.flash_only:
+        log("[bench] calibration")
+        cal = calibrate()
+        extra["calibration"] = cal
+        # the flash kernel's QK^T / PV run on v_mfma_f32_32x32x16_bf16
+        measured_roof = {"measured_peak": cal["mfma_32x32x16_TFLOP/s"],
+                         "measured_peak_kind": "pli_mfma_probe 32x32x16 (the kernel's shape)",
+                         "frac_of_measured": achieved / cal["mfma_32x32x16_TFLOP/s"]}
+    if args.flash_only:
+        args.quick, args.no_cpu_baseline = True, True
+    if not args.flash_only:
         log("[bench] torch sdpa comparison")
         extra["flash_torch_sdpa"] = bench_torch_sdpa(q, k, v, o, stream)
     if args.flash_only:
