@@ -2211,6 +2211,9 @@ static int gemm_dispatch(const void* a, const void* b, void* c, const void* bias
     // variant 41: gemm_w5 (gemm_w5.hip), the same tile with K staged 64 deep
     if (variant == 41 && vec && gemm_w5_ok(m, n, k, lda, ldb, ldc, trans_b))
         return launch_gemm_w5(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, dtype == PLI_BF16, s, 4);
+    // variant 43: gemm_w5 persistent (M, N multiples of 256)
+    if (variant == 43 && vec && m % 256 == 0 && n % 256 == 0 && gemm_w5_ok(m, n, k, lda, ldb, ldc, trans_b))
+        return launch_gemm_w5(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, dtype == PLI_BF16, s, 4, true);
     const bool big = vec && k % G2K == 0 && m >= 2 * G2M && n >= 2 * G2N && variant != 1 &&
                      (variant != 0 || (int64_t)cdiv(m, G2M) * cdiv(n, G2N) >= 128);
     // default for the large shapes since round 3: gemm_w5 (one wave per SIMD,
@@ -2219,8 +2222,16 @@ static int gemm_dispatch(const void* a, const void* b, void* c, const void* bias
     // 4096^3 1422 / 1378 vs 1206 / 1175, torch 1400 / 1281; 8192^3 1536 / 1488
     // vs 1344 / 1305, torch 1560 / 1391; profiles/r03/gemm/ab_w5.log).
     // gemm_w4v (variant 40, K 32 deep) sits between them.
-    if (variant == 0 && big && gemm_w5_ok(m, n, k, lda, ldb, ldc, trans_b))
-        return launch_gemm_w5(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, dtype == PLI_BF16, s, 4);
+    // Its persistent walk (variant 43, K stream continued across tiles) where
+    // M, N are multiples of 256 and K <= 4096: the per-tile prologue is a
+    // larger share there (8192^2 x 1024 NT / NN 1260 / 1188 vs 1180 / 1114,
+    // 16384 x 8192 x 1024 1320 / 1245 vs 1187 / 1163, hipBLASLt 1237 / 1083
+    // and 1284 / 1109); at K = 8192 the one-tile form is 0.5-2 % ahead
+    // (profiles/r03/gemm/ab_w5_persistent.log)
+    if (variant == 0 && big && gemm_w5_ok(m, n, k, lda, ldb, ldc, trans_b)) {
+        const bool persist = m % 256 == 0 && n % 256 == 0 && k <= 4096;
+        return launch_gemm_w5(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, dtype == PLI_BF16, s, 4, persist);
+    }
     if (big || (vec && variant >= 2 && k % G2K == 0 && n >= 8)) {
         // variant 3: phased (SCHED 0); 5-8: phased with SCHED 1, 3, 5, 7;
         // 9-11: one-phase tile with grouped rasterization (group_m 4, 8, 16);

@@ -89,21 +89,31 @@ template <int OFF> __device__ __forceinline__ void w5_rdtr(W5Pair& d, uint32_t a
                  : "=&v"(d.lo), "=&v"(d.hi) : "v"(addr), "n"(OFF), "n"(OFF + 2048));
 }
 
-template <typename T, bool TRANS_B, bool BIAS>
+// PERSIST (variant 43; M and N multiples of 256): one workgroup per CU walks
+// the tiles L, L + G, ... (G = gridDim.x, a multiple of 8: one XCD per walk);
+// the K stream continues across tiles (the last two steps of a tile DMA the
+// next tile's steps 0 and 1 into the ring, the slot parity follows a global
+// step count), and the epilogue stages through a separate 32 KiB region
+// (8 KiB per wave, four passes of 32 rows) so the ring keeps the next tile's
+// first steps.
+template <typename T, bool TRANS_B, bool BIAS, bool PERSIST = false>
 __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bm,
                                                   uint16_t* __restrict__ C, const uint16_t* __restrict__ bias,
                                                   int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
                                                   int tiles_n, int nblocks, int group_m) {
     constexpr int IMG = 32768, SLOT = 2 * IMG;
     using BFrag = std::conditional_t<TRANS_B, i32x4, W5Pair>;
-    __shared__ __attribute__((aligned(1024))) char smem[W5_RING5 ? 5 * IMG : 2 * SLOT];
+    static_assert(!(PERSIST && W5_RING5), "the persistent form uses the two-slot ring");
+    constexpr int EPI = 2 * SLOT;  // PERSIST: epilogue staging, 8 KiB per wave
+    __shared__ __attribute__((aligned(1024))) char smem[W5_RING5 ? 5 * IMG : (PERSIST ? 2 * SLOT + 32768 : 2 * SLOT)];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = wave >> 1, wc = wave & 1;
     int tm, tn;
-    w5_tile(xcd_remap(blockIdx.x, nblocks), cdiv(M, 256), tiles_n, group_m, tm, tn);
-    const int m0 = tm * 256, n0 = tn * 256;
+    int L = blockIdx.x;
+    w5_tile(xcd_remap(L, nblocks), cdiv(M, 256), tiles_n, group_m, tm, tn);
+    int m0 = tm * 256, n0 = tn * 256;
     const int ks = K / 64;
     const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
 
@@ -126,8 +136,13 @@ __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A
             boff[i] = (uint32_t)(((int64_t)kr * ldb + min(n0 + 8 * cn, N - 8) - n0) * 2);
         }
     }
+    // (PERSIST: M, N multiples of 256, so no row is clamped and the offsets
+    // above hold for every tile; only the bases move)
     const uint16_t* abase = A + (int64_t)m0 * lda;
     const uint16_t* bbase = TRANS_B ? Bm + (int64_t)n0 * ldb : Bm + n0;
+    const uint16_t *nabase = abase, *nbbase = bbase;  // PERSIST: the next tile's
+    bool has_next = false;
+    int gs = 0;  // PERSIST: global step count of this tile's step 0 (slot parity)
     auto dma1 = [&](const uint16_t* src, uint32_t off, uint32_t lds) __attribute__((always_inline)) {
         asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(lds), "v"(off), "s"(src)
                      : "memory");
@@ -143,16 +158,26 @@ __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A
     // LDS byte offset of step s's A (x = 0) or B (x = 1) image: slot s % 2,
     // or (W5_RING5) ring position (2s + x) % 5
     auto img_off = [&](int s, int x) __attribute__((always_inline)) {
-        return W5_RING5 ? (uint32_t)((2 * s + x) % 5) * IMG : (uint32_t)(s & 1) * SLOT + (uint32_t)x * IMG;
+        return W5_RING5 ? (uint32_t)((2 * s + x) % 5) * IMG : (uint32_t)((gs + s) & 1) * SLOT + (uint32_t)x * IMG;
     };
     // DMA piece j (0-7 A, 8-15 B) of K step s into its image (past the last
     // step: a reload of the last step)
     auto dma_piece = [&](auto j_tag, int s) __attribute__((always_inline)) {
         constexpr int j = decltype(j_tag)::value, i = j % 8;
-        const int sc = min(s, ks - 1);
         const uint32_t slot = lds0 + img_off(s, j < 8 ? 0 : 1) + (uint32_t)wave * 8192 +
                               (uint32_t)(W5_DMA_IMM ? (i / 4) * 4096 : i * 1024);
-        const uint16_t* src = j < 8 ? abase + sc * 64 : (TRANS_B ? bbase + sc * 64 : bbase + (int64_t)sc * 64 * ldb);
+        // past the last step: PERSIST with a next tile, that tile's step
+        // s - ks; else a reload of the last step
+        const uint16_t *ab = abase, *bb = bbase;
+        int sc = min(s, ks - 1);
+        if constexpr (PERSIST) {
+            if (s >= ks && has_next) {
+                ab = nabase;
+                bb = nbbase;
+                sc = s - ks;
+            }
+        }
+        const uint16_t* src = j < 8 ? ab + sc * 64 : (TRANS_B ? bb + sc * 64 : bb + (int64_t)sc * 64 * ldb);
         const uint32_t off = j < 8 ? aoff[i] : boff[i];
         if constexpr (W5_DMA_IMM && i % 4 > 0) dma_next(std::integral_constant<int, i % 4>{}, src, off);
         else dma1(src, off, slot);
@@ -240,6 +265,17 @@ __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A
     };
 
     // ---- prologue: accumulators 0, steps 0 and 1 in flight, (0, h0) fragments
+    // PERSIST: the next tile of this walk (its bases, for the stream's DMA)
+    auto next_tile = [&]() __attribute__((always_inline)) {
+        has_next = L + (int)gridDim.x < nblocks;
+        if (has_next) {
+            int tm2, tn2;
+            w5_tile(xcd_remap(L + (int)gridDim.x, nblocks), cdiv(M, 256), tiles_n, group_m, tm2, tn2);
+            nabase = A + (int64_t)(tm2 * 256) * lda;
+            nbbase = TRANS_B ? Bm + (int64_t)(tn2 * 256) * ldb : Bm + tn2 * 256;
+        }
+    };
+    if constexpr (PERSIST) next_tile();
     w4v::acc_zero();
     w5_sfor<16>([&](auto J) { dma_piece(J, 0); });
     w5_sfor<16>([&](auto J) { dma_piece(J, 1); });
@@ -275,21 +311,11 @@ __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A
             half(O{}, more_tag, Z{}, img_off(s + 1, 0), img_off(s + 1, 1), N0{}, N16{}, s + 2);
         if constexpr (MORE) frag_wait(Z{});
     };
-    int s = 0;
-    for (; s + 1 < ks; ++s) step(s, std::true_type{});
-    step(s, std::false_type{});
-
-    // ---- epilogue (gemm_w4v's): accumulator block (ni, mi) holds C[m][n..n+3]
-    // with m = m0 + 128 wr + 16 mi + (lane & 15), n = n0 + 128 wc + 16 ni +
-    // 4 (lane >> 4); each wave packs its 128 x 128 tile into its own 32 KiB of
-    // LDS ([row][256 B], chunk c of row r at c ^ (r & 15)) and stores whole
-    // 256-B row segments, 16 B per lane
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // dead-slot reloads landed
-    __builtin_amdgcn_s_barrier();                     // every wave is done with the ring
-    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");  // last MFMA -> accumulator reads
-    char* reg = smem + wave * 32768;
-    w5_sfor<64>([&](auto JJ) {
-        constexpr int J = JJ, ni = J / 8, mi = J % 8;
+    // accumulator block J = (ni, mi) -> packed bf16 / fp16 (bias added):
+    // C[m][n .. n+3], m = m0 + 128 wr + 16 mi + (lane & 15), n = n0 + 128 wc +
+    // 16 ni + 4 (lane >> 4)
+    auto acc_pack = [&](auto j_tag) __attribute__((always_inline)) {
+        constexpr int J = decltype(j_tag)::value, ni = J / 8;
         f32x4 v;
         w4v::acc_read<J>(v);
         const int n = n0 + 128 * wc + 16 * ni + 4 * h4;
@@ -302,21 +328,85 @@ __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A
                 v[3] += elem<T>::to_f32(T{(uint16_t)((uint32_t)bb.y >> 16)});
             }
         }
-        const i32x2 pk = i32x2{(int)pack2<T>(v[0], v[1]), (int)pack2<T>(v[2], v[3])};
-        const int row = 16 * mi + r16, chunk = 2 * ni + (h4 >> 1);
-        *reinterpret_cast<i32x2*>(reg + row * 256 + ((chunk ^ r16) << 4) + (h4 & 1) * 8) = pk;
-    });
-    {
-        const int c = lane & 15;
-        const int n = n0 + 128 * wc + 8 * c;
+        return i32x2{(int)pack2<T>(v[0], v[1]), (int)pack2<T>(v[2], v[3])};
+    };
+    for (;;) {
+        int s = 0;
+        for (; s + 1 < ks; ++s) step(s, std::true_type{});
+        step(s, std::false_type{});
+
+        if constexpr (!PERSIST) {
+            // ---- epilogue (gemm_w4v's): each wave packs its 128 x 128 tile
+            // into its own 32 KiB of LDS ([row][256 B], chunk c of row r at
+            // c ^ (r & 15)) and stores whole 256-B row segments, 16 B per lane
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // dead-slot reloads landed
+            __builtin_amdgcn_s_barrier();                     // every wave is done with the ring
+            asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");  // last MFMA -> accumulator reads
+            char* reg = smem + wave * 32768;
+            w5_sfor<64>([&](auto JJ) {
+                constexpr int J = JJ, ni = J / 8, mi = J % 8;
+                const i32x2 pk = acc_pack(JJ);
+                const int row = 16 * mi + r16, chunk = 2 * ni + (h4 >> 1);
+                *reinterpret_cast<i32x2*>(reg + row * 256 + ((chunk ^ r16) << 4) + (h4 & 1) * 8) = pk;
+            });
+            const int c = lane & 15;
+            const int n = n0 + 128 * wc + 8 * c;
 #pragma unroll 8
-        for (int it = 0; it < 32; ++it) {
-            const int row = 4 * it + h4;
-            const i32x4 v = *reinterpret_cast<const i32x4*>(reg + row * 256 + ((c ^ (row & 15)) << 4));
-            const int m = m0 + 128 * wr + row;
-            if (m < M && n < N) *reinterpret_cast<i32x4*>(C + (int64_t)m * ldc + n) = v;
+            for (int it = 0; it < 32; ++it) {
+                const int row = 4 * it + h4;
+                const i32x4 v = *reinterpret_cast<const i32x4*>(reg + row * 256 + ((c ^ (row & 15)) << 4));
+                const int m = m0 + 128 * wr + row;
+                if (m < M && n < N) *reinterpret_cast<i32x4*>(C + (int64_t)m * ldc + n) = v;
+            }
+            break;
+        } else {
+            // ---- epilogue through this wave's 8 KiB of the staging region,
+            // four passes of 32 rows (accumulator rows mi = 2p, 2p + 1); the
+            // ring keeps the next tile's steps 0 and 1.  M, N multiples of
+            // 256: every store is in bounds, 32 per wave.
+            asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");  // last MFMA -> accumulator reads
+            char* reg = smem + EPI + wave * 8192;
+            const int c = lane & 15;
+            const int n = n0 + 128 * wc + 8 * c;
+            w5_sfor<4>([&](auto PP) {
+                constexpr int pss = PP;
+                w5_sfor<16>([&](auto II) {
+                    constexpr int ni = II / 2, mi = 2 * pss + II % 2;
+                    const i32x2 pk = acc_pack(std::integral_constant<int, 8 * ni + mi>{});
+                    const int row = 16 * (II % 2) + r16, chunk = 2 * ni + (h4 >> 1);
+                    *reinterpret_cast<i32x2*>(reg + row * 256 + ((chunk ^ r16) << 4) + (h4 & 1) * 8) = pk;
+                });
+#pragma unroll
+                for (int it = 0; it < 8; ++it) {
+                    const int row = 4 * it + h4;
+                    const i32x4 v = *reinterpret_cast<const i32x4*>(reg + row * 256 + ((c ^ (row & 15)) << 4));
+                    const int m = m0 + 128 * wr + 32 * pss + row;
+                    *reinterpret_cast<i32x4*>(C + (int64_t)m * ldc + n) = v;
+                }
+            });
+            if (!has_next) break;
+            // ---- next tile: its steps 0 and 1 are in the ring (DMA'd by
+            // this tile's last two steps)
+            gs += ks;
+            L += (int)gridDim.x;
+            w5_tile(xcd_remap(L, nblocks), cdiv(M, 256), tiles_n, group_m, tm, tn);
+            m0 = tm * 256;
+            n0 = tn * 256;
+            abase = nabase;
+            bbase = nbbase;
+            next_tile();
+            w4v::acc_zero();
+            // step 0 landed: younger than its pieces are step 1's 16 and the
+            // epilogue's 32 stores
+            asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+            w5_sfor<16>([&](auto I) { frag_read(std::integral_constant<int, 0>{}, I, img_off(0, 0), img_off(0, 1)); });
+            frag_wait(std::integral_constant<int, 0>{});
         }
     }
+    // the last (reload) pieces land before the LDS is released
+    if constexpr (PERSIST) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 }  // namespace
@@ -330,7 +420,8 @@ bool gemm_w5_ok(int m, int n, int k, int64_t lda, int64_t ldb, int64_t ldc, int 
 }
 
 int launch_gemm_w5(const void* a, const void* b, void* c, const void* bias, int m, int n, int k, int64_t lda,
-                   int64_t ldb, int64_t ldc, int trans_b, int is_bf16, hipStream_t stream, int group_m) {
+                   int64_t ldb, int64_t ldc, int trans_b, int is_bf16, hipStream_t stream, int group_m,
+                   bool persistent) {
     PLI_REQUIRE(gemm_w5_ok(m, n, k, lda, ldb, ldc, trans_b), "gemm_w5: shape m=%d n=%d k=%d not supported", m, n,
                 k);
 #ifdef W5_GROUP_M
@@ -344,10 +435,24 @@ int launch_gemm_w5(const void* a, const void* b, void* c, const void* bias, int 
     const auto* B = (const uint16_t*)b;
     auto* Cc = (uint16_t*)c;
     const auto* bs = (const uint16_t*)bias;
-    const dim3 gr((unsigned)nb), blk(256);
-#define W5_LAUNCH(T, TB, BI)                                                                                        \
-    hipLaunchKernelGGL((gemm_w5<T, TB, BI>), gr, blk, 0, stream, A, B, Cc, bs, m, n, k, lda, ldb, ldc, tiles_n, \
-                       (int)nb, group_m)
+    // persistent (variant 43): one workgroup per CU of the stream's device,
+    // a multiple of 8 (each walk stays on one XCD); M, N multiples of 256
+    PLI_REQUIRE(!persistent || (m % 256 == 0 && n % 256 == 0), "gemm_w5 persistent: M, N must be multiples of 256");
+    int grid = (int)nb;
+    if (persistent) {
+        const int g = cu_count(stream) / 8 * 8;
+        if (g >= 8 && nb > g) grid = g;
+    }
+    const dim3 gr((unsigned)grid), blk(256);
+#define W5_LAUNCH(T, TB, BI)                                                                                         \
+    do {                                                                                                             \
+        if (persistent)                                                                                              \
+            hipLaunchKernelGGL((gemm_w5<T, TB, BI, true>), gr, blk, 0, stream, A, B, Cc, bs, m, n, k, lda, ldb, ldc, \
+                               tiles_n, (int)nb, group_m);                                                           \
+        else                                                                                                         \
+            hipLaunchKernelGGL((gemm_w5<T, TB, BI, false>), gr, blk, 0, stream, A, B, Cc, bs, m, n, k, lda, ldb,     \
+                               ldc, tiles_n, (int)nb, group_m);                                                      \
+    } while (0)
     if (is_bf16) {
         if (trans_b) { if (bias) W5_LAUNCH(bf16_t, true, true); else W5_LAUNCH(bf16_t, true, false); }
         else { if (bias) W5_LAUNCH(bf16_t, false, true); else W5_LAUNCH(bf16_t, false, false); }

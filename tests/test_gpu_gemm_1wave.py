@@ -31,14 +31,16 @@ def _ref(a, b, tb, bias=None):
     return r + bias.double() if bias is not None else r
 
 
-@pytest.mark.parametrize("variant", [41, 40])
+@pytest.mark.parametrize("variant", [41, 43, 40])
 @pytest.mark.parametrize("tb", [True, False], ids=["nt", "nn"])
 @pytest.mark.parametrize("m,n,k", [(512, 512, 64), (256, 256, 32), (300, 520, 96), (1000, 776, 4096),
                                    (777, 1032, 160), (2048, 8192, 1024), (4096, 4096, 4096), (264, 392, 128)])
 def test_w4v_vs_f64_and_v2(m, n, k, tb, variant):
     import pli_hip
-    if variant == 41 and k % 64:
+    if variant in (41, 43) and k % 64:
         pytest.skip("gemm_w5 takes K % 64 == 0")
+    if variant == 43 and (m % 256 or n % 256):
+        pytest.skip("the persistent gemm_w5 takes M, N multiples of 256")
     a, b = _inputs(m, n, k, tb, torch.bfloat16, m * 7 + n * 3 + k)
     o = pli_hip.gemm(a, b, trans_b=tb, variant=variant)
     ref = _ref(a, b, tb)
@@ -48,7 +50,7 @@ def test_w4v_vs_f64_and_v2(m, n, k, tb, variant):
         assert torch.equal(o, pli_hip.gemm(a, b, trans_b=tb, variant=2)), f"v{variant} != gemm_256 (same chain order)"
 
 
-@pytest.mark.parametrize("variant", [41, 40])
+@pytest.mark.parametrize("variant", [41, 43, 40])
 @pytest.mark.parametrize("tb", [True, False], ids=["nt", "nn"])
 def test_w4v_bias_fp16_and_default_route(tb, variant):
     import pli_hip
@@ -58,7 +60,9 @@ def test_w4v_bias_fp16_and_default_route(tb, variant):
     ref = _ref(a, b, tb, bias)
     err = ((o.double() - ref).abs() / (ref.abs() + 1)).max().item()
     assert err <= 4e-3, f"fp16 + bias tb={tb}: max rel err {err:.3e}"
-    # the default route takes gemm_w5 at this size (128+ tiles of 256^2)
+    # the default route takes gemm_w5 (persistent: M, N multiples of 256,
+    # K <= 4096) at this size (128+ tiles of 256^2); every variant here runs
+    # the same MFMA chains, so all agree bitwise
     a, b = _inputs(4096, 2048, 1024, tb, torch.bfloat16, 6)
     assert torch.equal(pli_hip.gemm(a, b, trans_b=tb), pli_hip.gemm(a, b, trans_b=tb, variant=variant))
 
@@ -74,3 +78,20 @@ def test_w4v_strided_leading_dims(tb, variant):
     ref = _ref(a, b, tb)
     err = ((o.double() - ref).abs() / (ref.abs() + 1)).max().item()
     assert err <= 1e-2, f"strided tb={tb}: max rel err {err:.3e}"
+
+
+@pytest.mark.parametrize("tb", [True, False], ids=["nt", "nn"])
+@pytest.mark.parametrize("m,n,k", [(8192, 8192, 1024), (16384, 4096, 64), (4608, 4096, 128)])
+def test_w5_persistent_walks_vs_f64(m, n, k, tb):
+    """Variant 43 with more tiles than CUs (every workgroup walks several
+    tiles, the K stream crossing tile seams; K = 64 is a one-step tile whose
+    prologue already prefetches the next tile): sampled rows vs f64, and
+    bitwise against the one-tile form (41)."""
+    import pli_hip
+    a, b = _inputs(m, n, k, tb, torch.bfloat16, m + n + k)
+    o = pli_hip.gemm(a, b, trans_b=tb, variant=43)
+    assert torch.equal(o, pli_hip.gemm(a, b, trans_b=tb, variant=41))
+    rows = torch.randperm(m, generator=torch.Generator().manual_seed(1))[:48].to(DEV)
+    ref = a[rows].double() @ (b.double().t() if tb else b.double())
+    err = ((o[rows].double() - ref).abs() / (ref.abs() + 1)).max().item()
+    assert err <= 1e-2, f"{m}x{n}x{k} tb={tb}: max rel err {err:.3e}"
