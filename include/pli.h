@@ -339,7 +339,9 @@ int pli_attn_decode_dev(const void* q, const void* k, const void* v, void* o,
  *   1/3/5/7; 9-11 grouped one-phase (group_m 4/8/16); 12-15 grouped phased
  *   (8/4/2/16); 20 mid-M; 21 small-M; 22/24 direct-load split-K; 25-29 LDS
  *   split-K (256/512/128 targets, 3-deep ring); 40 gemm_w4v (one wave per
- *   SIMD, K 32 deep); 41 gemm_w5 (K 64 deep; the large-shape default).
+ *   SIMD, K 32 deep); 41 gemm_w5 (K 64 deep), 43 gemm_w5 persistent walk
+ *   (M, N multiples of 256) -- 43 is the large-shape default for K <= 4096,
+ *   41 above.
  * pli_gemv_variant: 0-16 (rows per wave x 16-B chunks per lane x waves per
  *   block, gemv.hip), -1 default.
  * pli_attn_decode_variant: mode -1 default, 2/9/11/13 load-layout modes

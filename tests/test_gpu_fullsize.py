@@ -39,8 +39,8 @@ def gemm4096():
 
 # 1: 128^2 tile, 2: 256^2 one-phase, 3: phased SCHED 0, 4: setprio, 5-8:
 # phased SCHED 1/3/5/7, 9-11: grouped one-phase, 12-15: grouped phased,
-# 40: gemm_w4v, 41: gemm_w5 (the default for large shapes since round 3)
-@pytest.mark.parametrize("variant", [None, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 40, 41])
+# 40: gemm_w4v, 41: gemm_w5, 43: gemm_w5 persistent (41 / 43: the large-shape defaults since round 3)
+@pytest.mark.parametrize("variant", [None, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 40, 41, 43])
 @pytest.mark.parametrize("tb", [False, True])
 def test_gemm_variants_4096_cube(gemm4096, variant, tb):
     import pli_hip
@@ -51,7 +51,7 @@ def test_gemm_variants_4096_cube(gemm4096, variant, tb):
     _rows_close(c[rows], ref, f"4096^3 tb={tb} v{variant}")
 
 
-@pytest.mark.parametrize("variant", [None, 3, 7, 9, 13, 40, 41])
+@pytest.mark.parametrize("variant", [None, 3, 7, 9, 13, 40, 41, 43])
 def test_gemm_variants_8192_cube_nt(variant):
     """The ch09 TP=1 shape of the bench (x [8192, 8192] . W^T)."""
     import pli_hip
