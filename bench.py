@@ -48,7 +48,8 @@ PEAK_HBM_GBPS = 8000.0      # HBM3E datasheet
 B, H, S, D = 8, 32, 4096, 128
 FLASH_KERNEL = "attn_fwd_v12 persistent (variant 71; bitwise = attn_fwd_v10 exact)"
 JSON_OUT = sys.stdout  # main() points it at the original stdout and sends fd 1 to stderr
-GEMM_KERNEL = "gemm_w5 (variant 41: 256x256 tile, one wave per SIMD, K staged 64 deep)"
+GEMM_KERNEL = ("gemm_w5 (256x256 tile, one wave per SIMD, K staged 64 deep; variant 43, its persistent walk, "
+               "where M, N are multiples of 256 and 128 <= K <= 4096)")
 CAUSAL_KERNEL = "attn_fwd_v12 causal, persistent pair walk (variant 74)"
 
 

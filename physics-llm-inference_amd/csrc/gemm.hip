@@ -2223,13 +2223,13 @@ static int gemm_dispatch(const void* a, const void* b, void* c, const void* bias
     // vs 1344 / 1305, torch 1560 / 1391; profiles/r03/gemm/ab_w5.log).
     // gemm_w4v (variant 40, K 32 deep) sits between them.
     // Its persistent walk (variant 43, K stream continued across tiles) where
-    // M, N are multiples of 256 and K <= 4096: the per-tile prologue is a
+    // M, N are multiples of 256 and 128 <= K <= 4096: the per-tile prologue is a
     // larger share there (8192^2 x 1024 NT / NN 1260 / 1188 vs 1180 / 1114,
     // 16384 x 8192 x 1024 1320 / 1245 vs 1187 / 1163, hipBLASLt 1237 / 1083
     // and 1284 / 1109); at K = 8192 the one-tile form is 0.5-2 % ahead
     // (profiles/r03/gemm/ab_w5_persistent.log)
     if (variant == 0 && big && gemm_w5_ok(m, n, k, lda, ldb, ldc, trans_b)) {
-        const bool persist = m % 256 == 0 && n % 256 == 0 && k <= 4096;
+        const bool persist = m % 256 == 0 && n % 256 == 0 && k >= 128 && k <= 4096;
         return launch_gemm_w5(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, dtype == PLI_BF16, s, 4, persist);
     }
     if (big || (vec && variant >= 2 && k % G2K == 0 && n >= 8)) {

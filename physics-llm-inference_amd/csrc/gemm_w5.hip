@@ -171,10 +171,10 @@ __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A
         const uint16_t *ab = abase, *bb = bbase;
         int sc = min(s, ks - 1);
         if constexpr (PERSIST) {
-            if (s >= ks && has_next) {
+            if (s >= ks && has_next) {  // (ks >= 2: the launcher's condition)
                 ab = nabase;
                 bb = nbbase;
-                sc = s - ks;
+                sc = min(s - ks, ks - 1);
             }
         }
         const uint16_t* src = j < 8 ? ab + sc * 64 : (TRANS_B ? bb + sc * 64 : bb + (int64_t)sc * 64 * ldb);
@@ -438,6 +438,9 @@ int launch_gemm_w5(const void* a, const void* b, void* c, const void* bias, int 
     // persistent (variant 43): one workgroup per CU of the stream's device,
     // a multiple of 8 (each walk stays on one XCD); M, N multiples of 256
     PLI_REQUIRE(!persistent || (m % 256 == 0 && n % 256 == 0), "gemm_w5 persistent: M, N must be multiples of 256");
+    // the stream prefetches two steps past a tile, i.e. the next tile's
+    // steps 0 and 1: one-step tiles (K = 64) take the one-tile form
+    if (k < 128) persistent = false;
     int grid = (int)nb;
     if (persistent) {
         const int g = cu_count(stream) / 8 * 8;

@@ -81,11 +81,11 @@ def test_w4v_strided_leading_dims(tb, variant):
 
 
 @pytest.mark.parametrize("tb", [True, False], ids=["nt", "nn"])
-@pytest.mark.parametrize("m,n,k", [(8192, 8192, 1024), (16384, 4096, 64), (4608, 4096, 128)])
+@pytest.mark.parametrize("m,n,k", [(8192, 8192, 1024), (16384, 4096, 64), (16384, 4096, 128), (4608, 4096, 192)])
 def test_w5_persistent_walks_vs_f64(m, n, k, tb):
     """Variant 43 with more tiles than CUs (every workgroup walks several
-    tiles, the K stream crossing tile seams; K = 64 is a one-step tile whose
-    prologue already prefetches the next tile): sampled rows vs f64, and
+    tiles, the K stream crossing tile seams; K = 128 is the two-step
+    minimum, K = 64 takes the one-tile form): sampled rows vs f64, and
     bitwise against the one-tile form (41)."""
     import pli_hip
     a, b = _inputs(m, n, k, tb, torch.bfloat16, m + n + k)
