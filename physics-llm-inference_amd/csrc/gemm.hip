@@ -2325,6 +2325,14 @@ extern "C" int pli_gemm_f32out(const void* a, const void* b, float* c, int m, in
     hipStream_t s = (hipStream_t)stream;
     const bool lds = k % 64 == 0 && k > 0 && n % 32 == 0 && lda % 8 == 0 && ldb % 8 == 0 && al16(a) &&
                      al16(b) && al16(c);
+    // large shapes (128+ tiles of 256^2): gemm_w5 with its fp32 epilogue
+    // (persistent where M, N are multiples of 256 and 128 <= K <= 4096); the
+    // TP-8 shard at M 8192 ran 214 us on the split-K kernel below
+    if (lds && m >= 512 && n >= 512 && (int64_t)cdiv(m, 256) * cdiv(n, 256) >= 128 &&
+        gemm_w5_ok(m, n, k, lda, ldb, n, 1)) {
+        const bool persist = m % 256 == 0 && n % 256 == 0 && k >= 128 && k <= 4096;
+        return launch_gemm_w5(a, b, c, nullptr, m, n, k, lda, ldb, n, 1, dtype == PLI_BF16, s, 4, persist, true);
+    }
     if (lds) {
         if (dtype == PLI_BF16)
             return launch_splitk<bf16_t>(a, b, nullptr, nullptr, m, n, k, lda, ldb, n, 1, c, s, true, false,

@@ -10,9 +10,10 @@ namespace pli {
 // 16-bit operands (is_bf16: bf16, else fp16), K % 64 == 0, 16-byte aligned
 // rows and bases, N % 8 == 0; trans_b: B is [N, K] (F.linear), else [K, N]
 bool gemm_w5_ok(int m, int n, int k, int64_t lda, int64_t ldb, int64_t ldc, int trans_b);
-// persistent: variant 43's walk (M, N multiples of 256)
+// persistent: variant 43's walk (M, N multiples of 256); f32out: c is float
+// [m][ldc] (NT, no bias: pli_gemm_f32out)
 int launch_gemm_w5(const void* a, const void* b, void* c, const void* bias, int m, int n, int k, int64_t lda,
                    int64_t ldb, int64_t ldc, int trans_b, int is_bf16, hipStream_t stream, int group_m,
-                   bool persistent = false);
+                   bool persistent = false, bool f32out = false);
 
 }  // namespace pli

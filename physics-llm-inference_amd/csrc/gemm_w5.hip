@@ -96,13 +96,17 @@ template <int OFF> __device__ __forceinline__ void w5_rdtr(W5Pair& d, uint32_t a
 // step count), and the epilogue stages through a separate 32 KiB region
 // (8 KiB per wave, four passes of 32 rows) so the ring keeps the next tile's
 // first steps.
-template <typename T, bool TRANS_B, bool BIAS, bool PERSIST = false>
+// F32OUT (pli_gemm_f32out, the row-parallel fp32 partial): C is float
+// [M][ldc], stored straight from the accumulators (16 B per lane), no bias.
+template <typename T, bool TRANS_B, bool BIAS, bool PERSIST = false, bool F32OUT = false>
 __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bm,
-                                                  uint16_t* __restrict__ C, const uint16_t* __restrict__ bias,
+                                                  void* __restrict__ Cv, const uint16_t* __restrict__ bias,
                                                   int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
                                                   int tiles_n, int nblocks, int group_m) {
     constexpr int IMG = 32768, SLOT = 2 * IMG;
     using BFrag = std::conditional_t<TRANS_B, i32x4, W5Pair>;
+    static_assert(!(F32OUT && BIAS), "the fp32-output form has no bias");
+    uint16_t* C = reinterpret_cast<uint16_t*>(Cv);
     static_assert(!(PERSIST && W5_RING5), "the persistent form uses the two-slot ring");
     constexpr int EPI = 2 * SLOT;  // PERSIST: epilogue staging, 8 KiB per wave
     __shared__ __attribute__((aligned(1024))) char smem[W5_RING5 ? 5 * IMG : (PERSIST ? 2 * SLOT + 32768 : 2 * SLOT)];
@@ -330,12 +334,27 @@ __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A
         }
         return i32x2{(int)pack2<T>(v[0], v[1]), (int)pack2<T>(v[2], v[3])};
     };
+    // F32OUT: every accumulator block straight to C (float), 16 B per lane
+    auto store_f32 = [&]() __attribute__((always_inline)) {
+        asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");  // last MFMA -> accumulator reads
+        float* Cf = reinterpret_cast<float*>(Cv);
+        w5_sfor<64>([&](auto JJ) {
+            constexpr int J = JJ, ni = J / 8, mi = J % 8;
+            f32x4 v;
+            w4v::acc_read<J>(v);
+            const int m = m0 + 128 * wr + 16 * mi + r16, n = n0 + 128 * wc + 16 * ni + 4 * h4;
+            if (m < M && n < N) *reinterpret_cast<f32x4*>(Cf + (int64_t)m * ldc + n) = v;
+        });
+    };
     for (;;) {
         int s = 0;
         for (; s + 1 < ks; ++s) step(s, std::true_type{});
         step(s, std::false_type{});
 
-        if constexpr (!PERSIST) {
+        if constexpr (F32OUT && !PERSIST) {
+            store_f32();
+            break;
+        } else if constexpr (!PERSIST) {
             // ---- epilogue (gemm_w4v's): each wave packs its 128 x 128 tile
             // into its own 32 KiB of LDS ([row][256 B], chunk c of row r at
             // c ^ (r & 15)) and stores whole 256-B row segments, 16 B per lane
@@ -360,6 +379,9 @@ __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A
             }
             break;
         } else {
+            if constexpr (F32OUT) {
+                store_f32();  // 64 stores per wave (M, N multiples of 256)
+            } else {
             // ---- epilogue through this wave's 8 KiB of the staging region,
             // four passes of 32 rows (accumulator rows mi = 2p, 2p + 1); the
             // ring keeps the next tile's steps 0 and 1.  M, N multiples of
@@ -384,6 +406,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A
                     *reinterpret_cast<i32x4*>(C + (int64_t)m * ldc + n) = v;
                 }
             });
+            }
             if (!has_next) break;
             // ---- next tile: its steps 0 and 1 are in the ring (DMA'd by
             // this tile's last two steps)
@@ -397,8 +420,10 @@ __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A
             next_tile();
             w4v::acc_zero();
             // step 0 landed: younger than its pieces are step 1's 16 and the
-            // epilogue's 32 stores
-            asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+            // epilogue's 32 stores (F32OUT: 64 stores, more than vmcnt holds:
+            // vmcnt(63) still retires the oldest 16 + 16 + 1)
+            if constexpr (F32OUT) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
             w5_sfor<16>([&](auto I) { frag_read(std::integral_constant<int, 0>{}, I, img_off(0, 0), img_off(0, 1)); });
@@ -421,7 +446,8 @@ bool gemm_w5_ok(int m, int n, int k, int64_t lda, int64_t ldb, int64_t ldc, int 
 
 int launch_gemm_w5(const void* a, const void* b, void* c, const void* bias, int m, int n, int k, int64_t lda,
                    int64_t ldb, int64_t ldc, int trans_b, int is_bf16, hipStream_t stream, int group_m,
-                   bool persistent) {
+                   bool persistent, bool f32out) {
+    PLI_REQUIRE(!f32out || (trans_b && bias == nullptr), "gemm_w5: fp32 output is NT without bias");
     PLI_REQUIRE(gemm_w5_ok(m, n, k, lda, ldb, ldc, trans_b), "gemm_w5: shape m=%d n=%d k=%d not supported", m, n,
                 k);
 #ifdef W5_GROUP_M
@@ -449,7 +475,14 @@ int launch_gemm_w5(const void* a, const void* b, void* c, const void* bias, int 
     const dim3 gr((unsigned)grid), blk(256);
 #define W5_LAUNCH(T, TB, BI)                                                                                         \
     do {                                                                                                             \
-        if (persistent)                                                                                              \
+        if (f32out) {                                                                                                \
+            if (persistent)                                                                                          \
+                hipLaunchKernelGGL((gemm_w5<T, true, false, true, true>), gr, blk, 0, stream, A, B, c, nullptr, m, n, \
+                                   k, lda, ldb, ldc, tiles_n, (int)nb, group_m);                                    \
+            else                                                                                                     \
+                hipLaunchKernelGGL((gemm_w5<T, true, false, false, true>), gr, blk, 0, stream, A, B, c, nullptr, m,  \
+                                   n, k, lda, ldb, ldc, tiles_n, (int)nb, group_m);                                 \
+        } else if (persistent)                                                                                       \
             hipLaunchKernelGGL((gemm_w5<T, TB, BI, true>), gr, blk, 0, stream, A, B, Cc, bs, m, n, k, lda, ldb, ldc, \
                                tiles_n, (int)nb, group_m);                                                           \
         else                                                                                                         \

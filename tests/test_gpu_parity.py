@@ -597,6 +597,26 @@ def test_gemm_f32out_vs_f64(m, n, k):
     assert y.dtype == np.float64 and np.abs(y - ref).max() <= 1e-5 * (np.abs(ref).max() + 1)
 
 
+@pytest.mark.parametrize("m,n,k", [(4096, 4096, 1024), (4096, 8192, 8192), (2200, 4096, 512)])
+def test_gemm_f32out_large_w5(m, n, k):
+    """pli_gemm_f32out at sizes that take gemm_w5's fp32 epilogue (128+
+    tiles of 256^2; persistent for M, N multiples of 256 with K <= 4096, the
+    one-tile form at K 8192 and for a ragged M): sampled rows against the f64
+    product of the same bf16 inputs, fp32 accumulation so 1e-5 relative, and
+    bitwise equal to the bf16 product before its rounding (pli_gemm's bf16
+    output is the rounded fp32 result of the same MFMA chains)."""
+    import pli_hip
+    g = torch.Generator(device="cuda").manual_seed(m + n + k)
+    x = torch.randn(m, k, device="cuda", dtype=torch.bfloat16, generator=g)
+    w = torch.randn(n, k, device="cuda", dtype=torch.bfloat16, generator=g)
+    y = pli_hip.gemm_f32out(x, w)
+    assert y.dtype == torch.float32 and y.shape == (m, n)
+    rows = torch.randperm(m, generator=torch.Generator().manual_seed(3))[:32].to("cuda")
+    ref = x[rows].double() @ w.double().t()
+    assert (y[rows].double() - ref).abs().max().item() <= 1e-5 * (ref.abs().max().item() + 1)
+    assert torch.equal(y.to(torch.bfloat16), pli_hip.gemm(x, w, trans_b=True))
+
+
 @pytest.mark.parametrize("tp", [2, 4, 8])
 def test_row_parallel_fp32_partials_error_by_tp(tp):
     """The TP row-parallel sum at tp shards of an 8192-wide layer (M = 256):
