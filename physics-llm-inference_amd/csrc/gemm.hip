@@ -1927,7 +1927,8 @@ inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) =
 // ---- fused SwiGLU launches: h = silu(x Wg^T) * (x Wu^T)
 template <typename T>
 int launch_swiglu(const void* x, const void* wg, const void* wu, void* h, int M, int N, int K,
-                  int64_t ldx, int64_t ldwg, int64_t ldwu, int64_t ldh, bool vec, hipStream_t s) {
+                  int64_t ldx, int64_t ldwg, int64_t ldwu, int64_t ldh, bool vec, hipStream_t s,
+                  int variant = 0) {
     const auto* X = (const uint16_t*)x;
     const auto* G = (const uint16_t*)wg;
     const auto* U = (const uint16_t*)wu;
@@ -1958,6 +1959,13 @@ int launch_swiglu(const void* x, const void* wg, const void* wu, void* h, int M,
 #undef PLI_SMALLM_SW
         return launch_status("gemm_smallm_nt<swiglu>");
     }
+    // gemm_w5's SwiGLU form (one wave per SIMD, K 64 deep): variant 3 (the
+    // prefill default once measured; 4 forces the phased tile below)
+    constexpr bool W5_SWIGLU_DEFAULT = false;
+    if (vec && variant != 4 && (variant == 3 || (W5_SWIGLU_DEFAULT && M >= G2M && N >= 256)) && K % 64 == 0 &&
+        (variant == 3 || (int64_t)cdiv(M, G2M) * cdiv(N, 128) >= 96) && ldx * 2 * 256 < (1ll << 31) &&
+        ldwg * 2 * 128 < (1ll << 31) && ldwu * 2 * 128 < (1ll << 31))
+        return launch_gemm_w5_swiglu(x, wg, wu, h, M, N, K, ldx, ldwg, ldwu, ldh, std::is_same_v<T, bf16_t>, s);
     if (vec && M >= G2M && N >= 256 && K % G2K == 0 && (int64_t)cdiv(M, G2M) * cdiv(N, 128) >= 96) {
         // prefill sizes: the phased 256 x 128 tile (staggered schedule, grouped rasterization)
         const int tm = cdiv(M, G2M), tn = cdiv(N, 128);
@@ -2061,8 +2069,8 @@ static int swiglu_dispatch(const void* x, const void* wg, const void* wu, void* 
         return launch_splitk_swiglu<f16_t>(x, wg, wu, h, m, n, k, ldx, ldwg, ldwu, ldh, ks, (float*)ws, s);
     }
     switch (dtype) {
-        case PLI_BF16: return launch_swiglu<bf16_t>(x, wg, wu, h, m, n, k, ldx, ldwg, ldwu, ldh, vec, s);
-        case PLI_F16: return launch_swiglu<f16_t>(x, wg, wu, h, m, n, k, ldx, ldwg, ldwu, ldh, vec, s);
+        case PLI_BF16: return launch_swiglu<bf16_t>(x, wg, wu, h, m, n, k, ldx, ldwg, ldwu, ldh, vec, s, variant);
+        case PLI_F16: return launch_swiglu<f16_t>(x, wg, wu, h, m, n, k, ldx, ldwg, ldwu, ldh, vec, s, variant);
         default: return launch_swiglu<float>(x, wg, wu, h, m, n, k, ldx, ldwg, ldwu, ldh, false, s);
     }
 }

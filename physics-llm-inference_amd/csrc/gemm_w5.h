@@ -16,4 +16,9 @@ int launch_gemm_w5(const void* a, const void* b, void* c, const void* bias, int 
                    int64_t ldb, int64_t ldc, int trans_b, int is_bf16, hipStream_t stream, int group_m,
                    bool persistent = false, bool f32out = false);
 
+// h = silu(x Wg^T) * (x Wu^T) (pli_gemm_swiglu prefill): 256 x 128 output
+// tiles, K % 64 == 0, N % 8 == 0, 16-byte aligned rows and bases
+int launch_gemm_w5_swiglu(const void* x, const void* wg, const void* wu, void* h, int m, int n, int k, int64_t ldx,
+                          int64_t ldwg, int64_t ldwu, int64_t ldh, int is_bf16, hipStream_t stream);
+
 }  // namespace pli

@@ -98,14 +98,22 @@ template <int OFF> __device__ __forceinline__ void w5_rdtr(W5Pair& d, uint32_t a
 // first steps.
 // F32OUT (pli_gemm_f32out, the row-parallel fp32 partial): C is float
 // [M][ldc], stored straight from the accumulators (16 B per lane), no bias.
-template <typename T, bool TRANS_B, bool BIAS, bool PERSIST = false, bool F32OUT = false>
+// SWIGLU (pli_gemm_swiglu prefill; NT, no bias, one tile per workgroup):
+// C[m][n] = silu(A Bg^T) * (A Bu^T) on a 256 x 128 output tile -- the B image's
+// rows 0-127 are gate rows n0 .. n0+127 (Bm), rows 128-255 the same up rows
+// (Bu), so wave (wr, 1) holds the up values of wave (wr, 0)'s gate block; it
+// hands them over through LDS (fp32) and wave (wr, 0) stores silu(g) * u.
+template <typename T, bool TRANS_B, bool BIAS, bool PERSIST = false, bool F32OUT = false, bool SWIGLU = false>
 __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bm,
                                                   void* __restrict__ Cv, const uint16_t* __restrict__ bias,
                                                   int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
-                                                  int tiles_n, int nblocks, int group_m) {
+                                                  int tiles_n, int nblocks, int group_m,
+                                                  const uint16_t* __restrict__ Bu = nullptr, int64_t ldbu = 0) {
     constexpr int IMG = 32768, SLOT = 2 * IMG;
     using BFrag = std::conditional_t<TRANS_B, i32x4, W5Pair>;
     static_assert(!(F32OUT && BIAS), "the fp32-output form has no bias");
+    static_assert(!SWIGLU || (TRANS_B && !BIAS && !PERSIST && !F32OUT), "the SwiGLU form is NT, one tile");
+    constexpr int TN = SWIGLU ? 128 : 256;  // output columns per tile
     uint16_t* C = reinterpret_cast<uint16_t*>(Cv);
     static_assert(!(PERSIST && W5_RING5), "the persistent form uses the two-slot ring");
     constexpr int EPI = 2 * SLOT;  // PERSIST: epilogue staging, 8 KiB per wave
@@ -117,7 +125,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A
     int tm, tn;
     int L = blockIdx.x;
     w5_tile(xcd_remap(L, nblocks), cdiv(M, 256), tiles_n, group_m, tm, tn);
-    int m0 = tm * 256, n0 = tn * 256;
+    int m0 = tm * 256, n0 = tn * TN;
     const int ks = K / 64;
     const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
 
@@ -132,7 +140,10 @@ __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A
         const int row = 64 * wave + 8 * i + (lane >> 3);
         const int c = (lane & 7) ^ ((row >> 1) & 7);
         aoff[i] = (uint32_t)(((int64_t)(min(m0 + row, M - 1) - m0) * lda + 8 * c) * 2);
-        if constexpr (TRANS_B) {
+        if constexpr (SWIGLU) {  // waves 0-1: gate rows, waves 2-3: the same up rows
+            const int rb = row & 127;
+            boff[i] = (uint32_t)(((int64_t)(min(n0 + rb, N - 1) - n0) * (wave < 2 ? ldb : ldbu) + 8 * c) * 2);
+        } else if constexpr (TRANS_B) {
             boff[i] = (uint32_t)(((int64_t)(min(n0 + row, N - 1) - n0) * ldb + 8 * c) * 2);
         } else {
             const int kr = 16 * wave + 2 * i + (lane >> 5);
@@ -143,7 +154,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A
     // (PERSIST: M, N multiples of 256, so no row is clamped and the offsets
     // above hold for every tile; only the bases move)
     const uint16_t* abase = A + (int64_t)m0 * lda;
-    const uint16_t* bbase = TRANS_B ? Bm + (int64_t)n0 * ldb : Bm + n0;
+    const uint16_t* bbase = SWIGLU ? (wave < 2 ? Bm + (int64_t)n0 * ldb : Bu + (int64_t)n0 * ldbu)
+                            : TRANS_B ? Bm + (int64_t)n0 * ldb : Bm + n0;
     const uint16_t *nabase = abase, *nbbase = bbase;  // PERSIST: the next tile's
     bool has_next = false;
     int gs = 0;  // PERSIST: global step count of this tile's step 0 (slot parity)
@@ -351,7 +363,38 @@ __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A
         for (; s + 1 < ks; ++s) step(s, std::true_type{});
         step(s, std::false_type{});
 
-        if constexpr (F32OUT && !PERSIST) {
+        if constexpr (SWIGLU) {
+            // up (waves wc = 1) -> LDS as fp32, lane-private [block][lane];
+            // gate waves read their lane's up values and store silu(g) * u
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // dead-slot reloads landed
+            __builtin_amdgcn_s_barrier();                     // every wave is done with the ring
+            asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");  // last MFMA -> accumulator reads
+            f32x4* up = reinterpret_cast<f32x4*>(smem + wr * 65536);
+            if (wc == 1) {
+                w5_sfor<64>([&](auto JJ) {
+                    f32x4 v;
+                    w4v::acc_read<JJ>(v);
+                    up[JJ * 64 + lane] = v;
+                });
+            }
+            __syncthreads();
+            if (wc == 0) {
+                w5_sfor<64>([&](auto JJ) {
+                    constexpr int J = JJ, ni = J / 8, mi = J % 8;
+                    f32x4 g;
+                    w4v::acc_read<J>(g);
+                    const f32x4 u = up[J * 64 + lane];
+                    f32x4 h;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) h[r] = g[r] / (1.f + __expf(-g[r])) * u[r];  // gemm.hip silu_mul
+                    const int m = m0 + 128 * wr + 16 * mi + r16, n = n0 + 16 * ni + 4 * h4;
+                    if (m < M && n < N)
+                        *reinterpret_cast<i32x2*>(C + (int64_t)m * ldc + n) =
+                            i32x2{(int)pack2<T>(h[0], h[1]), (int)pack2<T>(h[2], h[3])};
+                });
+            }
+            break;
+        } else if constexpr (F32OUT && !PERSIST) {
             store_f32();
             break;
         } else if constexpr (!PERSIST) {
@@ -435,6 +478,26 @@ __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A
 }
 
 }  // namespace
+
+int launch_gemm_w5_swiglu(const void* x, const void* wg, const void* wu, void* h, int m, int n, int k, int64_t ldx,
+                          int64_t ldwg, int64_t ldwu, int64_t ldh, int is_bf16, hipStream_t stream) {
+    PLI_REQUIRE(k >= 64 && k % 64 == 0 && n % 8 == 0 && ldx * 2 * 256 < (1ll << 31) &&
+                    ldwg * 2 * 128 < (1ll << 31) && ldwu * 2 * 128 < (1ll << 31),
+                "gemm_w5 swiglu: shape m=%d n=%d k=%d not supported", m, n, k);
+    const int tiles_n = cdiv(n, 128);
+    const int64_t nb = (int64_t)cdiv(m, 256) * tiles_n;
+    PLI_REQUIRE(nb < (1ll << 31), "gemm_w5 swiglu: grid too large");
+    const auto* X = (const uint16_t*)x;
+    const auto* G = (const uint16_t*)wg;
+    const auto* U = (const uint16_t*)wu;
+    if (is_bf16)
+        hipLaunchKernelGGL((gemm_w5<bf16_t, true, false, false, false, true>), dim3((unsigned)nb), dim3(256), 0,
+                           stream, X, G, h, nullptr, m, n, k, ldx, ldwg, ldh, tiles_n, (int)nb, 4, U, ldwu);
+    else
+        hipLaunchKernelGGL((gemm_w5<f16_t, true, false, false, false, true>), dim3((unsigned)nb), dim3(256), 0,
+                           stream, X, G, h, nullptr, m, n, k, ldx, ldwg, ldh, tiles_n, (int)nb, 4, U, ldwu);
+    return launch_status("gemm_w5<swiglu>");
+}
 
 bool gemm_w5_ok(int m, int n, int k, int64_t lda, int64_t ldb, int64_t ldc, int trans_b) {
     (void)m;

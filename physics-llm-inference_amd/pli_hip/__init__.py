@@ -582,8 +582,8 @@ def gemm_swiglu(x: torch.Tensor, w_gate: torch.Tensor, w_up: torch.Tensor,
             w_up.stride(0), out.stride(0), _dtype_code(x))
     with _on_device(dev):
         wsb = lib().pli_gemm_swiglu_workspace_size(m, n, k, _dtype_code(x)) if split_k else 0
-        if wsb and variant is not None:
-            ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        if variant is not None:  # an explicit route (A/B, tests); no workspace when none is needed
+            ws = torch.empty(wsb, dtype=torch.uint8, device=dev) if wsb else None
             rc = lib().pli_gemm_swiglu_ws_variant(*head, _ptr(ws), wsb, _stream(dev), int(variant))
         elif wsb:
             ws = torch.empty(wsb, dtype=torch.uint8, device=dev)

@@ -108,3 +108,23 @@ def test_tp_mlp_on_gpu_matches_reference_and_bf16_tracks():
         yb = m.bfloat16()(x.cuda().bfloat16()).float().cpu().numpy()
     rel = np.linalg.norm(yb - g["TensorParallelMLP"]) / np.linalg.norm(g["TensorParallelMLP"])
     assert rel < 2e-2, rel
+
+
+@pytest.mark.parametrize("m,n,k", [(2048, 5632, 2048), (4096, 1792, 4096), (2100, 1376, 640)])
+def test_gemm_swiglu_w5_route_matches_phased(m, n, k):
+    """gemm_w5's SwiGLU form (variant 3) against the phased 256 x 128 tile
+    (variant 4, the prefill default): the same MFMA
+    chains in k order and the same silu(g) * u in fp32, so bitwise equal;
+    and sampled rows against the f64 oracle."""
+    import pli_hip
+    g = torch.Generator(device="cuda").manual_seed(m + n + k)
+    x = torch.randn(m, k, device="cuda", dtype=torch.bfloat16, generator=g)
+    wg = torch.randn(n, k, device="cuda", dtype=torch.bfloat16, generator=g) * k ** -0.5
+    wu = torch.randn(n, k, device="cuda", dtype=torch.bfloat16, generator=g) * k ** -0.5
+    h3 = pli_hip.gemm_swiglu(x, wg, wu, variant=3)
+    h4 = pli_hip.gemm_swiglu(x, wg, wu, variant=4)
+    assert torch.equal(h3, h4), f"max diff {(h3.float() - h4.float()).abs().max().item():.3e}"
+    rows = torch.randperm(m, generator=torch.Generator().manual_seed(5))[:24]
+    ref = swiglu(x[rows].float().cpu().numpy(), wg.float().cpu().numpy(), wu.float().cpu().numpy())
+    err = np.abs(h3[rows].float().cpu().numpy() - ref) / (np.abs(ref) + 1)
+    assert err.max() <= TOL["bf16"], f"max rel err {err.max():.3e}"
