@@ -3,7 +3,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/r3zn
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_gpu_swiglu.py -q -p no:cacheprovider --timeout 200 --timeout-method thread -rf > $O/pytest_swiglu.log 2>&1
+PLI_W5_SWIGLU_CHECK=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_swiglu.py -q -p no:cacheprovider --timeout 200 --timeout-method thread -rf > $O/pytest_swiglu.log 2>&1
 rc=$?; tail -4 $O/pytest_swiglu.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u - > $O/swiglu_timing.log 2>&1 <<'PY'
 import sys, os, json, statistics, torch
