@@ -28,6 +28,11 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+/* the library is built with -fvisibility=hidden: exactly the entry points
+ * declared here are exported */
+#if defined(__GNUC__) || defined(__clang__)
+#pragma GCC visibility push(default)
+#endif
 
 /* element types */
 enum {
@@ -98,8 +103,12 @@ int pli_gemm(const void* a, const void* b, void* c, const void* bias, int m,
  * fp16 (dtype), C fp32 contiguous (ldc = n), fp32 accumulate -- the
  * row-parallel partial of ch09/tensor_parallel.py:66-68 kept in fp32 so the
  * all-reduce sums unrounded partials (RowParallelLinear(reduce_dtype=
- * torch.float32)).  K % 64 == 0, N % 32 == 0, 16-byte aligned rows: the LDS
- * split-K kernel with one slice; other shapes a one-thread-per-output kernel.
+ * torch.float32)).  Shapes with at least 128 tiles of 256 x 256, K % 64 == 0,
+ * N % 8 == 0 and 256 rows of A and B addressable by a 32-bit offset take
+ * gemm_w5 with an fp32 epilogue (its persistent walk when M, N are multiples
+ * of 256 and K <= 4096); other K % 64 == 0, N % 32 == 0 shapes with 16-byte
+ * aligned rows the LDS split-K kernel with one slice; the rest a
+ * one-thread-per-output kernel.
  */
 int pli_gemm_f32out(const void* a, const void* b, float* c, int m, int n, int k, int64_t lda,
                     int64_t ldb, int dtype, void* stream);
@@ -346,8 +355,11 @@ int pli_attn_decode_dev(const void* q, const void* k, const void* v, void* o,
  *   block, gemv.hip), -1 default.
  * pli_attn_decode_variant: mode -1 default, 2/9/11/13 load-layout modes
  *   (decode_attn.hip); target_wgs 0 = automatic split.
- * pli_gemm_swiglu_ws_variant, pli_gemm_grouped_variant: 0 default, 1/2
- *   alternate routes (gemm.hip swiglu_dispatch / grouped_dispatch).
+ * pli_gemm_swiglu_ws_variant: 0 default, 1 split K wherever the split-K
+ *   route applies, 2 never split, 3 gemm_w5's SwiGLU tile (the prefill
+ *   default), 4 the phased 256 x 128 tile (3 and 4 never split).
+ * pli_gemm_grouped_variant: 0 default, 1/2 alternate routes (gemm.hip
+ *   grouped_dispatch).
  */
 int pli_flash_attn_fwd_variant(const void* q, const void* k, const void* v, void* o, int batch,
                                int heads, int kv_heads, int n_q, int n_kv, int head_dim,
@@ -375,6 +387,9 @@ int pli_gemm_grouped_variant(const void* x, const int32_t* gather, const void* c
                              int experts, int rows_bound, int n, int k, int64_t ldx, int64_t ldw,
                              int64_t ldc, int dtype, void* stream, int variant);
 
+#if defined(__GNUC__) || defined(__clang__)
+#pragma GCC visibility pop
+#endif
 #ifdef __cplusplus
 }
 #endif

@@ -25,7 +25,9 @@ BUILD = os.path.join(PKG, "build")
 LIB = os.path.join(PKG, "pli_hip", "libpli_hip.so")
 ARCH = os.environ.get("PLI_OFFLOAD_ARCH", "gfx950")
 
-CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I" + INCLUDE, "-I" + CSRC,
+# -fvisibility=hidden: only the entry points include/pli.h declares (inside its
+# visibility push(default)) are exported (tests/test_capi.py checks the set)
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", f"--offload-arch={ARCH}", "-I" + INCLUDE, "-I" + CSRC,
           "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
 # per-source extra flags.  flash_v7: no NaN ever reaches the softmax (masks
 # use -inf), so fmaxf on MFMA results folds into v_max3_f32 without the

@@ -1,9 +1,11 @@
 // attn_fwd_v12: flash-attention forward, one wave per SIMD, 64 query rows per
-// wave (reference ch06/flash_attention.py:14-74; gfx950, bf16, D = 128,
-// non-causal, Nk a multiple of 64 -- other cases take attn_fwd_v10).
+// wave (reference ch06/flash_attention.py:14-74; gfx950, bf16, D = 128, Nk a
+// multiple of 64; causal as a second instantiation -- other cases take
+// attn_fwd_v10).
 //
-// The structure of cdna_hip_programming.md's 4-wave persistent example,
-// without persistence: a workgroup is 4 waves x 64 rows (two 32-row blocks A
+// The structure of cdna_hip_programming.md's 4-wave persistent example: one
+// workgroup per CU walks blocks L, L + G, ... (G = the grid), each block 4
+// waves x 64 rows (two 32-row blocks A
 // and B per wave), one workgroup per CU, and each wave owns the whole
 // 512-entry register file.  O^T (128 registers), Q^T (64) and the K
 // fragments of one tile (64) live in the accumulator file, named literally
@@ -22,7 +24,8 @@
 // then the defer-max ballot of tile t (rare path: drain, rescale O and l,
 // recompute S(t) from the LDS copy of K(t), redo its exps and P).  One S
 // state, two P states (t even / odd).  K/V tiles arrive by LDS-DMA into a
-// 4-slot ring of XOR-swizzled images (attn_fwd_v10's layout), one tile ahead.
+// 5-slot ring of XOR-swizzled images (attn_fwd_v10's layout), two tiles
+// ahead; the stream continues across block seams.
 //
 // Arithmetic is attn_fwd_v10's (exact scaling, same MFMA chains and orders,
 // same defer-max rule per row), so outputs are bitwise those of variant 55.

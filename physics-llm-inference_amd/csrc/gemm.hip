@@ -1959,10 +1959,13 @@ int launch_swiglu(const void* x, const void* wg, const void* wu, void* h, int M,
 #undef PLI_SMALLM_SW
         return launch_status("gemm_smallm_nt<swiglu>");
     }
-    // gemm_w5's SwiGLU form (one wave per SIMD, K 64 deep): variant 3 (the
-    // prefill default once measured; 4 forces the phased tile below)
-    constexpr bool W5_SWIGLU_DEFAULT = false;
-    if (vec && variant != 4 && (variant == 3 || (W5_SWIGLU_DEFAULT && M >= G2M && N >= 256)) && K % 64 == 0 &&
+    // gemm_w5's SwiGLU form (one wave per SIMD, K 64 deep), the prefill
+    // default since round 4: bitwise the phased tile's output and faster on
+    // every measured shape (4096 x 14336 x 4096 1371 vs 1303 TF/s, 16384 x
+    // 14336 x 4096 1359 vs 1309, 4096 x 1792 x 4096 1305 vs 1185, 2048 x 5632
+    // x 2048 940 vs 922; profiles/r04/swiglu_w5.log).  Variant 3 forces it
+    // (ragged M / N are masked in its epilogue), 4 forces the phased tile.
+    if (vec && variant != 4 && (variant == 3 || (M >= G2M && N >= 256)) && K % 64 == 0 &&
         (variant == 3 || (int64_t)cdiv(M, G2M) * cdiv(N, 128) >= 96) && ldx * 2 * 256 < (1ll << 31) &&
         ldwg * 2 * 128 < (1ll << 31) && ldwu * 2 * 128 < (1ll << 31))
         return launch_gemm_w5_swiglu(x, wg, wu, h, M, N, K, ldx, ldwg, ldwu, ldh, std::is_same_v<T, bf16_t>, s);
@@ -2031,8 +2034,9 @@ extern "C" int pli_gemm_swiglu_ws(const void* x, const void* wg, const void* wu,
                            workspace_bytes);
 }
 
-// Not in pli.h: variant 1 = split K wherever the split-K route applies,
-// 2 = never split (A/B of the decode-batch routing)
+// variant 1 = split K wherever the split-K route applies, 2 = never split
+// (A/B of the decode-batch routing), 3 = gemm_w5's SwiGLU tile, 4 = the
+// phased 256 x 128 tile (3 and 4 never split)
 extern "C" int pli_gemm_swiglu_ws_variant(const void* x, const void* wg, const void* wu, void* h,
                                           int m, int n, int k, int64_t ldx, int64_t ldwg,
                                           int64_t ldwu, int64_t ldh, int dtype, void* workspace,
@@ -2061,7 +2065,8 @@ static int swiglu_dispatch(const void* x, const void* wg, const void* wu, void* 
     // decode batches (16 < m <= 256, K > 2048 or m > 128) with a workspace:
     // gate and up split-K planes in one LDS-staged launch, silu(g) * u in the
     // fixed-order reduce (profiles/r01/gemm/tune_swiglu_splitk.log)
-    const int ks = vec && variant != 2 ? swiglu_slices(m, n, k, variant == 1) : 0;
+    // (variants 2, 3 and 4 name a one-launch tile: never split)
+    const int ks = vec && variant != 2 && variant != 3 && variant != 4 ? swiglu_slices(m, n, k, variant == 1) : 0;
     if (ks > 0 && ws != nullptr && ws_bytes >= (size_t)2 * ks * m * n * sizeof(float)) {
         PLI_REQUIRE(((uintptr_t)ws & 15) == 0, "pli_gemm_swiglu_ws: workspace must be 16-byte aligned");
         if (dtype == PLI_BF16)

@@ -396,6 +396,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A
             break;
         } else if constexpr (F32OUT && !PERSIST) {
             store_f32();
+            // the last step's dead-slot reloads land before the LDS is released
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             break;
         } else if constexpr (!PERSIST) {
             // ---- epilogue (gemm_w4v's): each wave packs its 128 x 128 tile

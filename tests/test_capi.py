@@ -34,6 +34,19 @@ def test_library_exports_every_declared_symbol(built_lib):
         assert hasattr(lib, s), f"{s} declared in pli.h but not exported"
 
 
+def test_library_exports_exactly_the_header(built_lib):
+    """Built with -fvisibility=hidden: the dynamic symbol table holds the
+    pli.h entry points and nothing else of ours (no C++-internal pli::
+    functions); hipcc's per-translation-unit __hip_cuid_* markers aside."""
+    import shutil
+    import subprocess
+    nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    out = subprocess.run([nm, "-D", "--defined-only", built_lib], capture_output=True, text=True, check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+    ours = {s for s in exported if not s.startswith("__hip_cuid_")}
+    assert ours == set(declared_symbols()), sorted(ours ^ set(declared_symbols()))
+
+
 def test_version_and_error_strings(built_lib):
     import pli_hip
     L = pli_hip.lib()

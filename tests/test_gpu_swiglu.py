@@ -6,7 +6,6 @@ modules that use it.  Bound: |err| <= tol * (|ref| + 1) (the outputs grow
 like sqrt(K)); bf16 1e-2, fp16 4e-3, fp32 1e-4 as for pli_gemm."""
 from __future__ import annotations
 
-import os
 
 import numpy as np
 import pytest
@@ -112,16 +111,10 @@ def test_tp_mlp_on_gpu_matches_reference_and_bf16_tracks():
     assert rel < 2e-2, rel
 
 
-# flipped once tools/gpu_r3zn.sh (which sets PLI_W5_SWIGLU_CHECK=1) has run on hardware
-W5_SWIGLU_VALIDATED = bool(os.environ.get("PLI_W5_SWIGLU_CHECK"))
-
-
-@pytest.mark.skipif(not W5_SWIGLU_VALIDATED,
-                    reason="opt-in gemm_w5 SwiGLU form not yet run on hardware (GPU pool unavailable, round 3)")
 @pytest.mark.parametrize("m,n,k", [(2048, 5632, 2048), (4096, 1792, 4096), (2100, 1376, 640)])
 def test_gemm_swiglu_w5_route_matches_phased(m, n, k):
-    """gemm_w5's SwiGLU form (variant 3) against the phased 256 x 128 tile
-    (variant 4, the prefill default): the same MFMA
+    """gemm_w5's SwiGLU form (variant 3, the prefill default since round 4)
+    against the phased 256 x 128 tile (variant 4): the same MFMA
     chains in k order and the same silu(g) * u in fp32, so bitwise equal;
     and sampled rows against the f64 oracle."""
     import pli_hip
