@@ -528,6 +528,14 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
 //  72: variant 71 with the defer-max threshold at 0 (a rescale whenever a
 //      tile raises a row's max): tests only, the threshold sweep of
 //      cdna_hip_programming.md rule 26 (72 and 71 agree to rounding)
+//  80: attn_fwd_v13 (flash_v13.hip): 4 waves x 64 rows, one wave per SIMD,
+//      v_mfma_f32_16x16x32_bf16 (the shape the chip clocks higher under load),
+//      one generated instruction stream (tools/gen_flash_v13.py), persistent;
+//      defer-max on P itself (bf16, D = 128, non-causal, Nk % 64 == 0, Nk >=
+//      128; else 71)
+//  81: variant 80 with one block per workgroup
+//  82: variant 80 with mu = max * c - 1 (a rescale at nearly every tile whose
+//      max reaches the running max): tests only, exercises the rare path
 constexpr int kDefaultVariant = 71;
 // causal: attn_fwd_v12 causal (74; one block per workgroup where the
 // persistent pair walk does not tile the shape), 60 where v12 does not apply
@@ -548,6 +556,14 @@ int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int
     // v7 / v10 also prescale Q by c, so c > 1 could overflow fp16 Q.
     const float c_log2 = scale * 1.4426950408889634f;
     const bool c_ok = c_log2 > 0.f && c_log2 <= 1.f;
+    if (variant == 80 || variant == 81 || variant == 82) {
+        const bool bf = std::is_same<T, bf16_t>::value;
+        const V7Strides s7{st.qb, st.qh, st.qn, st.kb, st.kh, st.kn, st.vb, st.vh, st.vn, st.ob, st.oh, st.on};
+        if (attn_v13_ok(D, bf ? 1 : 0, causal, Nq, Nk, s7) && c_ok)
+            return launch_attn_v13(q, k, v, o, B, H, group, Nq, Nk, s7, scale, stream, variant != 81,
+                                   variant == 82 ? -1.f : 7.f);
+        variant = 71;
+    }
     if (variant == 70 || variant == 71 || variant == 72) {
         const bool bf = std::is_same<T, bf16_t>::value;
         if (attn_v12_ok(D, bf ? 1 : 0, causal, Nk) && c_ok) {

@@ -1,0 +1,131 @@
+// attn_fwd_v13: flash-attention forward on v_mfma_f32_16x16x32_bf16
+// (reference ch06/flash_attention.py:14-74; gfx950, bf16, D = 128,
+// non-causal, Nk a multiple of 64 and >= 128; other cases take v12 / v10).
+//
+// One wave per SIMD, 64 query rows per wave (4 q-blocks of 16), persistent
+// workgroups of 4 waves walking 256-row blocks.  The body is ONE generated
+// instruction stream (flash_v13_asm.h from tools/gen_flash_v13.py; the
+// layout, schedule and the reasons for them are in tools/v13/kernel.py): the
+// 16x16x32 MFMA shape holds a higher clock under load than 32x32x16 (DESIGN
+// 3.1), but its 16-cycle gaps leave 8 issue cycles each, so the softmax
+// stream, the fragment reads and the LDS-DMA are placed gap by gap, with the
+// hazard padding and wait counts computed by the generator (hipcc pads
+// nothing inside an asm statement).  tests/test_v13_emu.py runs the same
+// program in a CPU emulator; tests/test_gpu_flash_v13.py on the device.
+//
+// Differences from v12 a caller can see: none in the contract; numerically
+// P = bf16(exp2(s c - mu)) with mu = (row max) c + 7 (P <= 2^-7 when the max
+// is taken, checked < 2 per tile, i.e. the same THR 8 defer-max rule in
+// log2 units), l from the same rounded P on the matrix core, 1/l by v_rcp.
+#include <cstring>
+
+#include "flash_v7.h"
+#include "flash_v13_asm.h"
+#include "pli_common.h"
+
+namespace pli {
+namespace {
+
+// kernel argument block: 48 dwords, the layout of tools/v13/kernel.py
+// ARG_LAYOUT (the body reads it through the kernarg pointer)
+struct V13Args {
+    uint32_t w[48];
+};
+static_assert(sizeof(V13Args) == 192, "V13Args layout");
+
+enum : int {
+    A_Q = 0, A_K = 2, A_V = 4, A_O = 6, A_QB = 8, A_QH = 10, A_KB = 12, A_KH = 14, A_VB = 16, A_VH = 18,
+    A_OB = 20, A_OH = 22, A_QN = 24, A_KN, A_VN, A_ON, A_NQ, A_NT, A_QBLOCKS, A_NBLOCKS, A_MAGQ, A_SHQ,
+    A_MAGH, A_SHH, A_MAGG, A_SHG, A_H, A_XQ, A_XR, A_C, A_MUOFF, A_G, A_TBK, A_TBV, A_GROUP, A_PAD
+};
+static_assert(A_PAD == 47, "argument layout");
+
+__global__ __launch_bounds__(256, 1) void attn_fwd_v13(V13Args args) {
+    __shared__ __attribute__((aligned(1024))) char smem[163840];
+    (void)args;
+    const void* kp = (const void*)__builtin_amdgcn_kernarg_segment_ptr();
+    const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const unsigned wg = blockIdx.x;
+    asm volatile(PLI_V13_BODY::"s"(kp), "s"(wg), "s"(wave), "s"((unsigned)(uintptr_t)smem) : PLI_V13_CLOBBERS);
+}
+
+// floor(x / d) == ((x * m) >> 31) >> l for 0 <= x < 2^31 (Granlund-Montgomery,
+// N = 31: m = ceil(2^(31+l) / d) < 2^32 with l = ceil(log2 d))
+void magic31(uint32_t d, uint32_t& m, uint32_t& l) {
+    l = 0;
+    while ((1ull << l) < d) ++l;
+    const unsigned __int128 num = (unsigned __int128)1 << (31 + l);
+    m = (uint32_t)((num + d - 1) / d);
+}
+
+void put64(V13Args& a, int at, uint64_t v) {
+    a.w[at] = (uint32_t)v;
+    a.w[at + 1] = (uint32_t)(v >> 32);
+}
+
+}  // namespace
+
+bool attn_v13_ok(int D, int is_bf16, int causal, int Nq, int Nk, const V7Strides& st) {
+    if (D != 128 || !is_bf16 || causal || Nk < 128 || Nk % 64 != 0 || Nq < 1) return false;
+    // 32-bit per-lane offsets: a Q / O head's rows, a K / V tile
+    const int64_t q_ext = ((int64_t)Nq - 1) * st.qn * 2 + 256, o_ext = ((int64_t)Nq - 1) * st.on * 2 + 256;
+    const int64_t kv_tile = 64 * std::max(st.kn, st.vn) * 2;
+    if (q_ext >= (1ll << 32) || o_ext >= (1ll << 32) || kv_tile >= (1ll << 31)) return false;
+    for (int64_t s : {st.qb, st.qh, st.kb, st.kh, st.vb, st.vh, st.ob, st.oh, st.qn, st.kn, st.vn, st.on})
+        if (s < 0) return false;
+    return true;
+}
+
+int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B, int H, int group, int Nq,
+                    int Nk, const V7Strides& st, float scale, hipStream_t stream, bool persistent, float muoff) {
+    PLI_REQUIRE(attn_v13_ok(128, 1, 0, Nq, Nk, st), "attn_fwd_v13: shape not supported");
+    const int qblocks = cdiv(Nq, 256);
+    const int64_t nb = (int64_t)B * H * qblocks;
+    PLI_REQUIRE(nb < (1ll << 31) && nb > 0, "attn_fwd_v13: grid too large");
+    int grid = (int)nb;
+    if (persistent) {
+        const int g = cu_count(stream) / 8 * 8;
+        if (g >= 8 && nb > g) grid = g;
+    }
+    V13Args a;
+    std::memset(&a, 0, sizeof(a));
+    put64(a, A_Q, (uint64_t)(uintptr_t)q);
+    put64(a, A_K, (uint64_t)(uintptr_t)k);
+    put64(a, A_V, (uint64_t)(uintptr_t)v);
+    put64(a, A_O, (uint64_t)(uintptr_t)o);
+    put64(a, A_QB, (uint64_t)st.qb * 2);
+    put64(a, A_QH, (uint64_t)st.qh * 2);
+    put64(a, A_KB, (uint64_t)st.kb * 2);
+    put64(a, A_KH, (uint64_t)st.kh * 2);
+    put64(a, A_VB, (uint64_t)st.vb * 2);
+    put64(a, A_VH, (uint64_t)st.vh * 2);
+    put64(a, A_OB, (uint64_t)st.ob * 2);
+    put64(a, A_OH, (uint64_t)st.oh * 2);
+    a.w[A_QN] = (uint32_t)(st.qn * 2);
+    a.w[A_KN] = (uint32_t)(st.kn * 2);
+    a.w[A_VN] = (uint32_t)(st.vn * 2);
+    a.w[A_ON] = (uint32_t)(st.on * 2);
+    a.w[A_NQ] = (uint32_t)Nq;
+    a.w[A_NT] = (uint32_t)(Nk / 64);
+    a.w[A_QBLOCKS] = (uint32_t)qblocks;
+    a.w[A_NBLOCKS] = (uint32_t)nb;
+    magic31((uint32_t)qblocks, a.w[A_MAGQ], a.w[A_SHQ]);
+    magic31((uint32_t)H, a.w[A_MAGH], a.w[A_SHH]);
+    magic31((uint32_t)group, a.w[A_MAGG], a.w[A_SHG]);
+    a.w[A_H] = (uint32_t)H;
+    a.w[A_GROUP] = (uint32_t)group;
+    // XCD remap of the walk: lb = x * xq + min(x, xr) + (l >> 3), x = l & 7
+    // (identity when there are fewer than 8 blocks)
+    a.w[A_XQ] = nb < 8 ? 0u : (uint32_t)(nb >> 3);
+    a.w[A_XR] = nb < 8 ? 8u : (uint32_t)(nb & 7);
+    const float c = scale * 1.4426950408889634f;
+    std::memcpy(&a.w[A_C], &c, 4);
+    std::memcpy(&a.w[A_MUOFF], &muoff, 4);
+    a.w[A_G] = (uint32_t)grid;
+    a.w[A_TBK] = (uint32_t)(64 * st.kn * 2);
+    a.w[A_TBV] = (uint32_t)(64 * st.vn * 2);
+    hipLaunchKernelGGL(attn_fwd_v13, dim3((unsigned)grid), dim3(256), 0, stream, a);
+    return launch_status("attn_fwd_v13");
+}
+
+}  // namespace pli

@@ -1,0 +1,110 @@
+"""attn_fwd_v13 (variants 80 persistent, 81 one block per workgroup, 82 =
+80 with mu = max * c - 1, i.e. the rare rescale path at nearly every tile)
+against references that share none of its code (cdna_hip_programming.md
+§5.4 rule 26) -- the same checks as tests/test_gpu_flash_v12.py:
+
+* a float64 torch attention on the device over the WHOLE output tensor
+  (the reference's naive_attention, ch06/attention_memory.py:19-33, in f64)
+  at every persistent-seam shape, plain and with Q scaled by 4 (peaky rows
+  that take the rescale branch);
+* an fp32 torch attention per head over all 256 heads of the bench config
+  (B8 S4096 H32 D128);
+* the rescale sweep: 82 (rescale whenever a tile's max reaches the running
+  max) and the shipped 80 agree to rounding, on randn and on the
+  adversarial inputs of tests/stress_cases.py.
+
+Bounds as in the v12 file: 1e-2 absolute on randn inputs (north_star's bf16
+bound), 2^-8 * max|v| on the peaky inputs (P and output rounding).
+"""
+from __future__ import annotations
+
+import pytest
+import torch
+
+from test_gpu_flash_v12 import (DEV, NK64, SEAMS, assert_agree_to_rounding, dev, inputs, max_err,
+                                torch_attention)
+
+pytestmark = pytest.mark.gpu
+V13 = (80, 81, 82)
+# v13 needs Nk >= 128 (two key tiles: the K/V stream runs two tiles ahead)
+SHAPES = SEAMS + [(1, 2, 2, 1, 128), (2, 4, 4, 300, 128), (8, 36, 4, 256, 128), (1, 3, 1, 64, 256),
+                  (2, 2, 1, 200, 128)]
+
+
+@pytest.mark.parametrize("qmul", (1, 4))
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "b{}h{}kv{}q{}k{}".format(*s))
+def test_v13_vs_f64_full_tensor(shape, qmul):
+    """Every output element of 80 / 81 / 82 against the f64 device
+    reference; 80 and 81 (one vs many blocks per workgroup) bitwise equal."""
+    import pli_hip
+    q, k, v = inputs(shape, sum(shape) % 997)
+    q = q * qmul  # exact in bf16
+    ref = torch_attention(q, k, v)
+    tol = 1e-2 if qmul == 1 else 2.0 ** -8 * v.abs().max().item()
+    outs = {}
+    for var in V13:
+        outs[var] = pli_hip.flash_attn_fwd(q, k, v, variant=var)
+        err = max_err(outs[var], ref)
+        assert err <= tol, f"{shape} q*{qmul} variant {var}: max |err| {err:.4e} > {tol:.4e}"
+    assert torch.equal(outs[80], outs[81]), f"{shape}: 80 != 81"
+
+
+def test_v13_nk64_falls_back():
+    """Nk = 64 is below v13's two-tile stream: the variant routes to v12."""
+    import pli_hip
+    for shape in NK64[:2]:
+        q, k, v = inputs(shape, 7)
+        assert torch.equal(pli_hip.flash_attn_fwd(q, k, v, variant=80), pli_hip.flash_attn_fwd(q, k, v, variant=71))
+
+
+def test_v13_strided_bshd_views():
+    """q/k/v as [B,S,H,D] buffers through [B,H,S,D] views, O into a
+    transposed view: against the f64 reference and the contiguous call."""
+    import pli_hip
+    from oracle.numerics import seeded_normal
+    B, S, H, D = 2, 320, 8, 128
+    x = dev(seeded_normal((3, B, S, H, D), 41, "bf16"))
+    q, k, v = (x[i].transpose(1, 2) for i in range(3))
+    ref = torch_attention(q, k, v)
+    for var in V13:
+        o = torch.full((B, S, H, D), float("nan"), dtype=torch.bfloat16, device=DEV)
+        pli_hip.flash_attn_fwd(q, k, v, out=o.transpose(1, 2), variant=var)
+        err = max_err(o.transpose(1, 2), ref)
+        assert err <= 1e-2, f"variant {var}: strided max |err| {err:.4e}"
+        contig = pli_hip.flash_attn_fwd(q.contiguous(), k.contiguous(), v.contiguous(), variant=var)
+        assert torch.equal(o.transpose(1, 2), contig), f"variant {var}: strided != contiguous"
+
+
+@pytest.mark.parametrize("variant", (80, 82))
+def test_v13_full_config_all_heads(variant):
+    """B8 S4096 H32 D128 bf16: all 256 (batch, head) pairs against an fp32
+    torch attention per head; 82 within rounding of 80."""
+    import pli_hip
+    B, H, N, D = 8, 32, 4096, 128
+    g = torch.Generator(device=DEV).manual_seed(0)
+    q, k, v = (torch.randn(B, H, N, D, device=DEV, dtype=torch.bfloat16, generator=g) for _ in range(3))
+    out = pli_hip.flash_attn_fwd(q, k, v, variant=variant)
+    worst = 0.0
+    for b in range(B):
+        ref = torch_attention(q[b:b + 1], k[b:b + 1], v[b:b + 1], dtype=torch.float32, heads_per_chunk=4)
+        err = max_err(out[b:b + 1], ref)
+        worst = max(worst, err)
+        assert err <= 1e-2, f"batch {b}: max |err| {err:.4e} over its 32 heads"
+    print(f"variant {variant}: max |err| over all 256 heads {worst:.4e}")
+    if variant == 82:
+        assert_agree_to_rounding(out, pli_hip.flash_attn_fwd(q, k, v, variant=80), v)
+
+
+@pytest.mark.parametrize("name", ("spike", "first", "late", "all", "seam2", "seam5"))
+def test_v13_rescale_stress(name):
+    """The adversarial inputs (each forces the rescale branch at chosen
+    tiles): 80 against the f64 reference, and 82 within rounding of 80."""
+    import pli_hip
+    from stress_cases import stress_inputs
+    q, k, v = (dev(x) for x in stress_inputs(name))
+    if k.shape[2] < 128:
+        pytest.skip("v13 needs Nk >= 128")
+    out = pli_hip.flash_attn_fwd(q, k, v, variant=80)
+    err = max_err(out, torch_attention(q, k, v))
+    assert err <= 2.0 ** -8 * v.abs().max().item(), f"{name}: {err:.4e}"
+    assert_agree_to_rounding(pli_hip.flash_attn_fwd(q, k, v, variant=82), out, v)

@@ -1,0 +1,84 @@
+"""attn_fwd_v13's generated program on the CPU (no GPU): the instruction
+stream that csrc/flash_v13_asm.h holds is executed by tools/v13/emu.py and
+compared with a float64 attention (the reference's naive_attention,
+ch06/attention_memory.py:19-33) on bf16-rounded inputs.  This checks the
+operand maps, LDS image layouts, DMA offsets, K/V stream and ring, the
+persistent walk (grid smaller than the block count), GQA, BSHD strides,
+ragged Nq and the defer-max rescale path; the hazard / wait-count pass is
+checked for idempotence, and the committed header for staleness."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+from v13 import emu as E  # noqa: E402
+from v13 import run as R  # noqa: E402
+from v13.isa import analyse  # noqa: E402
+
+
+def f64_attention(q, k, v):
+    r = lambda x: E.bf16_to_f32(E.bf16_rne(x.astype(np.float32))).astype(np.float64)  # noqa: E731
+    qf, kf, vf = r(q), r(k), r(v)
+    g = q.shape[1] // k.shape[1]
+    kf, vf = np.repeat(kf, g, axis=1), np.repeat(vf, g, axis=1)
+    s = np.einsum("bhqd,bhkd->bhqk", qf, kf) / np.sqrt(q.shape[-1])
+    s -= s.max(-1, keepdims=True)
+    p = np.exp(s)
+    p /= p.sum(-1, keepdims=True)
+    return np.einsum("bhqk,bhkd->bhqd", p, vf)
+
+
+CASES = [  # (B, H, Hkv, Nq, Nk, grid, layout, muoff)
+    (1, 1, 1, 256, 128, None, "bhsd", 7.0),      # one block, two key tiles
+    (1, 2, 2, 256, 320, 1, "bhsd", 7.0),         # persistent: two blocks of five tiles on one workgroup
+    (2, 2, 1, 200, 128, 1, "bshd", 7.0),         # GQA, ragged Nq, BSHD strides, nt = 2 across seams
+    (1, 1, 1, 256, 256, None, "bhsd", -1.0),     # the rescale path at nearly every tile
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "b{}h{}kv{}q{}k{}g{}-{}-mu{}".format(*c))
+def test_v13_program_vs_f64(case):
+    B, H, Hkv, Nq, Nk, grid, lay, muoff = case
+    rng = np.random.default_rng(sum(case[:5]))
+    q = rng.standard_normal((B, H, Nq, 128))
+    k = rng.standard_normal((B, Hkv, Nk, 128))
+    v = rng.standard_normal((B, Hkv, Nk, 128))
+    o, em = R.run(q, k, v, grid=grid, layout=lay, muoff=muoff)
+    err = np.abs(o - f64_attention(q, k, v)).max()
+    assert err <= 1e-2, f"max |err| {err:.3e}"
+    if muoff < 0:
+        assert em.counts.get("v_sub_f32", 0) > 0, "the rescale path never ran"
+
+
+def test_v13_spike_rescale():
+    """a key that raises one row's max by far more than 8 (log2) at a late
+    tile: the rare path recomputes S, moves mu and rescales O and l"""
+    rng = np.random.default_rng(3)
+    q = rng.standard_normal((1, 1, 256, 128))
+    k = rng.standard_normal((1, 1, 256, 128))
+    v = rng.standard_normal((1, 1, 256, 128))
+    k[0, 0, 200] = 40.0 * q[0, 0].mean(0)
+    o, em = R.run(q, k, v)
+    assert em.counts.get("v_sub_f32", 0) > 0
+    err = np.abs(o - f64_attention(q, k, v)).max()
+    assert err <= 2.0 ** -8 * np.abs(v).max(), f"max |err| {err:.3e}"
+
+
+def test_v13_hazard_pass_is_idempotent():
+    """the committed program needs no further padding or waits"""
+    prog = R.program()
+    assert analyse(prog) == {}
+
+
+def test_v13_header_is_current():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_flash_v13.py"), "--check"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr

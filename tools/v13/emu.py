@@ -1,0 +1,509 @@
+"""CPU emulator for the generated attn_fwd_v13 program (test infrastructure).
+
+Executes the same `Ins` list that tools/gen_flash_v13.py prints for hipcc,
+one workgroup at a time: 4 waves x 64 lanes run in turn between s_barriers,
+LDS-DMA and loads complete at issue (s_waitcnt is a no-op here; the hazard /
+wait-count pass in tools/v13/isa.py is checked separately), every global and
+LDS access is bounds-checked.  What it proves: the operand maps, LDS image
+layouts, DMA offsets, stream / ring bookkeeping, persistent walk, softmax and
+defer-max logic and the epilogue produce the right output.  What it does not:
+timing, wait counts, races between waves inside one barrier interval.
+
+Semantics of the less common instructions, as this file implements them:
+  v_mfma_f32_16x16x32_bf16  A lane l: row l&15, k = 8(l>>4)+j (j-th bf16 of
+      the 4 registers, low half first); B lane l: col l&15, same k; C/D lane
+      l: col l&15, rows 4(l>>4)+r (register r)
+  ds_read_b64_tr_b16  per 16-lane group, lane 4q+p addresses row q, columns
+      4p..4p+3 of a 4 x 16 block; lane i gets column i, row q in element q
+  global_load_lds_dwordx4  global = sbase + voffset + offset, LDS = M0 +
+      offset + 16 * lane
+  v_permlane16_swap_b32 a, b  rows (16 lanes) 1, 3 of a <-> rows 0, 2 of b
+  v_permlane32_swap_b32 a, b  lanes 32-63 of a <-> lanes 0-31 of b
+"""
+from __future__ import annotations
+
+import struct
+
+import numpy as np
+
+from .isa import Neg, Reg
+
+LANES = 64
+M32 = 0xFFFFFFFF
+
+
+def f2u(x):
+    return np.asarray(x, dtype=np.float32).view(np.uint32)
+
+
+def u2f(x):
+    return np.asarray(x, dtype=np.uint32).view(np.float32)
+
+
+def bf16_rne(f32):
+    """f32 array -> bf16 bit patterns (uint32 holding 16 bits), RNE"""
+    u = f2u(f32).astype(np.uint64)
+    r = ((u >> 16) & 1) + 0x7FFF
+    out = ((u + r) >> 16) & 0xFFFF
+    nan = np.isnan(np.asarray(f32, dtype=np.float32))
+    out = np.where(nan, 0x7FC0, out)
+    return out.astype(np.uint32)
+
+
+def bf16_to_f32(b):
+    return u2f((np.asarray(b, dtype=np.uint32) & 0xFFFF) << 16)
+
+
+class Heap:
+    """flat device memory with bounds-checked accesses"""
+
+    BASE = 0x100000000
+
+    def __init__(self):
+        self.bufs = []  # (start, np.uint8 array)
+        self.next = self.BASE
+
+    def alloc(self, nbytes, data=None):
+        start = self.next
+        arr = np.zeros(nbytes, dtype=np.uint8)
+        if data is not None:
+            b = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else \
+                np.ascontiguousarray(data).view(np.uint8).ravel()
+            arr[:b.size] = b
+        self.bufs.append((start, arr))
+        self.next = (start + nbytes + 0xFFFF) & ~0xFFFF
+        self.next += 0x10000
+        return start
+
+    def find(self, addr, n):
+        for start, arr in self.bufs:
+            if start <= addr and addr + n <= start + arr.size:
+                return arr, addr - start
+        raise IndexError(f"global access out of bounds: {addr:#x} + {n}")
+
+    def read(self, addr, n):
+        arr, off = self.find(addr, n)
+        return arr[off:off + n]
+
+    def write(self, addr, data):
+        arr, off = self.find(addr, len(data))
+        arr[off:off + len(data)] = data
+
+    def view(self, start):
+        for s, arr in self.bufs:
+            if s == start:
+                return arr
+        raise KeyError(start)
+
+
+class Wave:
+    def __init__(self):
+        self.v = np.zeros((256, LANES), dtype=np.uint32)
+        self.a = np.zeros((256, LANES), dtype=np.uint32)
+        self.s = np.zeros(128, dtype=np.uint64)  # held as < 2^32
+        self.vcc = np.zeros(LANES, dtype=bool)
+        self.exec = np.ones(LANES, dtype=bool)
+        self.scc = 0
+        self.m0 = 0
+        self.pc = 0
+        self.done = False
+        self.count = 0
+
+
+class Emu:
+    def __init__(self, prog, heap, lds_bytes=163840, trace=False):
+        self.prog = [i for i in prog]
+        self.labels = {ins.ops[0]: k for k, ins in enumerate(self.prog) if ins.op == "label"}
+        self.heap = heap
+        self.lds = np.zeros(lds_bytes, dtype=np.uint8)
+        self.trace = trace
+        self.counts = {}
+
+    # ---- operand access ---------------------------------------------------
+    def vec(self, w, o):
+        """operand as a per-lane uint32 vector (one register)"""
+        if isinstance(o, Neg):
+            return f2u(-u2f(self.vec(w, o.r)))
+        if isinstance(o, Reg):
+            assert o.n == 1, o
+            if o.f == "v":
+                return w.v[o.i].copy()
+            if o.f == "a":
+                return w.a[o.i].copy()
+            if o.f == "s":
+                return np.full(LANES, int(w.s[o.i]) & M32, dtype=np.uint32)
+            if o.f == "m0":
+                return np.full(LANES, w.m0, dtype=np.uint32)
+            raise ValueError(o)
+        if isinstance(o, float):
+            return np.full(LANES, struct.unpack("<I", struct.pack("<f", o))[0], dtype=np.uint32)
+        if isinstance(o, int):
+            return np.full(LANES, o & M32, dtype=np.uint32)
+        raise ValueError(o)
+
+    def sc(self, w, o):
+        """scalar operand"""
+        if isinstance(o, Reg):
+            if o.f == "s":
+                if o.n == 1:
+                    return int(w.s[o.i]) & M32
+                return (int(w.s[o.i]) & M32) | ((int(w.s[o.i + 1]) & M32) << 32)
+            if o.f == "exec":
+                return int(np.packbits(w.exec[::-1]).view(">u8")[0]) if False else \
+                    sum(1 << k for k in range(LANES) if w.exec[k])
+            if o.f == "vcc":
+                return sum(1 << k for k in range(LANES) if w.vcc[k])
+            if o.f == "m0":
+                return w.m0
+            raise ValueError(o)
+        if isinstance(o, int):
+            return o & M32
+        raise ValueError(o)
+
+    def sset(self, w, o, val):
+        if o.f == "s":
+            if o.n == 1:
+                w.s[o.i] = val & M32
+            else:
+                assert o.n == 2
+                w.s[o.i] = val & M32
+                w.s[o.i + 1] = (val >> 32) & M32
+        elif o.f == "m0":
+            w.m0 = val & M32
+        elif o.f == "exec":
+            w.exec = np.array([(val >> k) & 1 for k in range(LANES)], dtype=bool)
+        elif o.f == "vcc":
+            w.vcc = np.array([(val >> k) & 1 for k in range(LANES)], dtype=bool)
+        else:
+            raise ValueError(o)
+
+    def vset(self, w, o, val, mask=None):
+        m = w.exec if mask is None else mask
+        assert o.n == 1
+        arr = w.v if o.f == "v" else w.a
+        arr[o.i] = np.where(m, np.asarray(val, dtype=np.uint32), arr[o.i])
+
+    def regs(self, w, o):
+        arr = w.v if o.f == "v" else w.a
+        return arr[o.i:o.i + o.n]
+
+    @staticmethod
+    def off(ins):
+        for part in ins.mods.split():
+            if part.startswith("offset:"):
+                return int(part[7:])
+        return 0
+
+    # ---- execution ----------------------------------------------------------
+    def run_wg(self, waves, max_steps=50_000_000):
+        """run a workgroup's waves to completion (barrier-synchronised)"""
+        steps = 0
+        while not all(w.done for w in waves):
+            progressed = False
+            for w in waves:
+                if w.done:
+                    continue
+                while not w.done:
+                    ins = self.prog[w.pc]
+                    if ins.op == "s_barrier":
+                        w.pc += 1
+                        w.at_barrier = True
+                        break
+                    self.step(w, ins)
+                    steps += 1
+                    progressed = True
+                    if steps > max_steps:
+                        raise RuntimeError("emulator step limit")
+                    if w.pc >= len(self.prog):
+                        w.done = True
+            # barrier release: every live wave waits at it
+            live = [w for w in waves if not w.done]
+            if live and not all(getattr(w, "at_barrier", False) for w in live):
+                if not progressed:
+                    raise RuntimeError("barrier deadlock")
+            for w in waves:
+                w.at_barrier = False
+        return steps
+
+    def step(self, w, ins):
+        op, o = ins.op, ins.ops
+        self.counts[op] = self.counts.get(op, 0) + 1
+        w.pc += 1
+        if op in ("label", "s_nop", "s_waitcnt"):
+            return
+        k = ins.kind()
+        if k == "mfma":
+            return self.mfma(w, ins)
+        if op.startswith("v_"):
+            return self.valu(w, ins)
+        if op.startswith("s_"):
+            return self.salu(w, ins)
+        if op.startswith("ds_"):
+            return self.ds(w, ins)
+        if op.startswith("global_"):
+            return self.vmem(w, ins)
+        raise NotImplementedError(op)
+
+    # ---- MFMA -------------------------------------------------------------
+    def mfma(self, w, ins):
+        d, a, b, c = ins.ops
+        ra, rb = self.regs(w, a), self.regs(w, b)
+        A = np.zeros((16, 32))
+        B = np.zeros((32, 16))
+        for l in range(LANES):
+            for j in range(8):
+                wa = int(ra[j // 2, l])
+                wb = int(rb[j // 2, l])
+                ha = (wa >> (16 * (j % 2))) & 0xFFFF
+                hb = (wb >> (16 * (j % 2))) & 0xFFFF
+                A[l % 16, 8 * (l // 16) + j] = float(bf16_to_f32(ha))
+                B[8 * (l // 16) + j, l % 16] = float(bf16_to_f32(hb))
+        D = A @ B
+        if isinstance(c, int):
+            assert c == 0
+            C = np.zeros((4, LANES))
+        else:
+            C = u2f(self.regs(w, c)).astype(np.float64)
+        out = np.zeros((4, LANES))
+        for l in range(LANES):
+            for r in range(4):
+                out[r, l] = C[r, l] + D[4 * (l // 16) + r, l % 16]
+        self.regs(w, d)[:] = f2u(out.astype(np.float32))
+
+    # ---- VALU -------------------------------------------------------------
+    def valu(self, w, ins):
+        op, o = ins.op, ins.ops
+        g = lambda x: self.vec(w, x)  # noqa: E731
+        gf = lambda x: u2f(self.vec(w, x))  # noqa: E731
+        if op == "v_mov_b32":
+            return self.vset(w, o[0], g(o[1]))
+        if op == "v_accvgpr_write_b32":
+            return self.vset(w, o[0], g(o[1]))
+        if op == "v_accvgpr_read_b32":
+            return self.vset(w, o[0], g(o[1]))
+        if op == "v_add_u32":
+            return self.vset(w, o[0], (g(o[1]).astype(np.uint64) + g(o[2])) & M32)
+        if op == "v_sub_u32":
+            return self.vset(w, o[0], (g(o[1]).astype(np.int64) - g(o[2])) & M32)
+        if op == "v_add3_u32":
+            return self.vset(w, o[0], (g(o[1]).astype(np.uint64) + g(o[2]) + g(o[3])) & M32)
+        if op == "v_and_b32":
+            return self.vset(w, o[0], g(o[1]) & g(o[2]))
+        if op == "v_or_b32":
+            return self.vset(w, o[0], g(o[1]) | g(o[2]))
+        if op == "v_or3_b32":
+            return self.vset(w, o[0], g(o[1]) | g(o[2]) | g(o[3]))
+        if op == "v_lshlrev_b32":
+            return self.vset(w, o[0], (g(o[2]).astype(np.uint64) << (g(o[1]) & 31)) & M32)
+        if op == "v_lshrrev_b32":
+            return self.vset(w, o[0], g(o[2]) >> (g(o[1]) & 31))
+        if op == "v_mul_lo_u32":
+            return self.vset(w, o[0], (g(o[1]).astype(np.uint64) * g(o[2])) & M32)
+        if op == "v_min_u32":
+            return self.vset(w, o[0], np.minimum(g(o[1]), g(o[2])))
+        if op == "v_mbcnt_lo_u32_b32":
+            lane = np.arange(LANES)
+            return self.vset(w, o[0], (np.minimum(lane, 32) + g(o[2])).astype(np.uint32))
+        if op == "v_mbcnt_hi_u32_b32":
+            lane = np.arange(LANES)
+            return self.vset(w, o[0], (np.maximum(lane - 32, 0) + g(o[2])).astype(np.uint32))
+        if op == "v_fma_f32":
+            r = (gf(o[1]).astype(np.float64) * gf(o[2]) + gf(o[3])).astype(np.float32)
+            return self.vset(w, o[0], f2u(r))
+        if op == "v_mul_f32":
+            return self.vset(w, o[0], f2u(gf(o[1]) * gf(o[2])))
+        if op == "v_add_f32":
+            return self.vset(w, o[0], f2u(gf(o[1]) + gf(o[2])))
+        if op == "v_sub_f32":
+            return self.vset(w, o[0], f2u(gf(o[1]) - gf(o[2])))
+        if op == "v_max_f32":
+            return self.vset(w, o[0], f2u(np.maximum(gf(o[1]), gf(o[2]))))
+        if op == "v_max3_f32":
+            return self.vset(w, o[0], f2u(np.maximum(np.maximum(gf(o[1]), gf(o[2])), gf(o[3]))))
+        if op == "v_exp_f32":
+            with np.errstate(over="ignore"):
+                return self.vset(w, o[0], f2u(np.exp2(gf(o[1]))))
+        if op == "v_rcp_f32":
+            with np.errstate(divide="ignore"):
+                return self.vset(w, o[0], f2u(np.float32(1.0) / gf(o[1])))
+        if op == "v_cvt_pk_bf16_f32":
+            lo, hi = bf16_rne(gf(o[1])), bf16_rne(gf(o[2]))
+            return self.vset(w, o[0], lo | (hi << 16))
+        if op in ("v_cmp_ne_u32_e32", "v_cmp_gt_u32_e32"):
+            a, b = g(o[1]), g(o[2])
+            r = (a != b) if op == "v_cmp_ne_u32_e32" else (a > b)
+            w.vcc = np.where(w.exec, r, False)
+            return
+        if op == "v_permlane16_swap_b32":
+            A_, B_ = o[0], o[1]
+            va, vb = g(A_), g(B_)
+            na, nb = va.copy(), vb.copy()
+            for row in (1, 3):
+                sa = slice(16 * row, 16 * row + 16)
+                sb = slice(16 * (row - 1), 16 * row)
+                na[sa], nb[sb] = vb[sb], va[sa]
+            full = np.ones(LANES, dtype=bool)
+            self.vset(w, A_, na, full)
+            self.vset(w, B_, nb, full)
+            return
+        if op == "v_permlane32_swap_b32":
+            A_, B_ = o[0], o[1]
+            va, vb = g(A_), g(B_)
+            na, nb = va.copy(), vb.copy()
+            na[32:], nb[:32] = vb[:32], va[32:]
+            full = np.ones(LANES, dtype=bool)
+            self.vset(w, A_, na, full)
+            self.vset(w, B_, nb, full)
+            return
+        raise NotImplementedError(op)
+
+    # ---- SALU ---------------------------------------------------------------
+    def salu(self, w, ins):
+        op, o = ins.op, ins.ops
+        g = lambda x: self.sc(w, x)  # noqa: E731
+        if op in ("s_mov_b32", "s_mov_b64"):
+            return self.sset(w, o[0], g(o[1]))
+        if op == "s_add_u32":
+            r = g(o[1]) + g(o[2])
+            w.scc = int(r > M32)
+            return self.sset(w, o[0], r & M32)
+        if op == "s_addc_u32":
+            r = g(o[1]) + g(o[2]) + w.scc
+            w.scc = int(r > M32)
+            return self.sset(w, o[0], r & M32)
+        if op == "s_sub_u32":
+            r = g(o[1]) - g(o[2])
+            w.scc = int(r < 0)
+            return self.sset(w, o[0], r & M32)
+        if op == "s_mul_i32":
+            a, b = g(o[1]), g(o[2])
+            a = a - (1 << 32) if a >= 1 << 31 else a
+            b = b - (1 << 32) if b >= 1 << 31 else b
+            return self.sset(w, o[0], (a * b) & M32)
+        if op == "s_mul_hi_u32":
+            return self.sset(w, o[0], ((g(o[1]) * g(o[2])) >> 32) & M32)
+        if op == "s_lshl_b32":
+            r = (g(o[1]) << (g(o[2]) & 31)) & M32
+            w.scc = int(r != 0)
+            return self.sset(w, o[0], r)
+        if op == "s_lshr_b32":
+            r = g(o[1]) >> (g(o[2]) & 31)
+            w.scc = int(r != 0)
+            return self.sset(w, o[0], r)
+        if op == "s_ashr_i32":
+            a = g(o[1])
+            a = a - (1 << 32) if a >= 1 << 31 else a
+            r = (a >> (g(o[2]) & 31)) & M32
+            w.scc = int(r != 0)
+            return self.sset(w, o[0], r)
+        if op == "s_and_b32":
+            r = g(o[1]) & g(o[2])
+            w.scc = int(r != 0)
+            return self.sset(w, o[0], r)
+        if op == "s_or_b32":
+            r = g(o[1]) | g(o[2])
+            w.scc = int(r != 0)
+            return self.sset(w, o[0], r)
+        if op == "s_min_u32":
+            a, b = g(o[1]), g(o[2])
+            w.scc = int(a < b)
+            return self.sset(w, o[0], min(a, b))
+        if op == "s_cmp_eq_u32":
+            w.scc = int(g(o[0]) == g(o[1]))
+            return
+        if op == "s_cmp_lt_u32":
+            w.scc = int(g(o[0]) < g(o[1]))
+            return
+        if op == "s_cmp_ge_u32":
+            w.scc = int(g(o[0]) >= g(o[1]))
+            return
+        if op in ("s_cselect_b32", "s_cselect_b64"):
+            return self.sset(w, o[0], g(o[1]) if w.scc else g(o[2]))
+        if op == "s_and_saveexec_b64":
+            old = g(Reg("exec"))
+            self.sset(w, o[0], old)
+            new = old & g(o[1])
+            w.scc = int(new != 0)
+            self.sset(w, Reg("exec"), new)
+            return
+        if op == "s_branch":
+            w.pc = self.labels[o[0]]
+            return
+        if op in ("s_cbranch_scc0", "s_cbranch_scc1", "s_cbranch_vccnz", "s_cbranch_vccz"):
+            take = {"s_cbranch_scc0": not w.scc, "s_cbranch_scc1": bool(w.scc),
+                    "s_cbranch_vccnz": bool((w.vcc & w.exec).any()),
+                    "s_cbranch_vccz": not bool((w.vcc & w.exec).any())}[op]
+            if take:
+                w.pc = self.labels[o[0]]
+            return
+        if op.startswith("s_load_dword"):
+            n = {"s_load_dwordx2": 2, "s_load_dwordx4": 4, "s_load_dwordx8": 8, "s_load_dwordx16": 16}[op]
+            base = g(o[1])
+            data = self.heap.read(base + int(o[2]), 4 * n).view(np.uint32)
+            for k in range(n):
+                w.s[o[0].i + k] = int(data[k])
+            return
+        raise NotImplementedError(op)
+
+    # ---- LDS ------------------------------------------------------------------
+    def lds_read(self, addr, n):
+        assert 0 <= addr and addr + n <= self.lds.size, f"LDS read out of bounds {addr}+{n}"
+        return self.lds[addr:addr + n]
+
+    def ds(self, w, ins):
+        op, o = ins.op, ins.ops
+        off = self.off(ins)
+        addr = self.vec(w, o[1]).astype(np.int64) + off
+        if op == "ds_read_b128":
+            dst = self.regs(w, o[0])
+            for l in range(LANES):
+                if w.exec[l]:
+                    dst[:, l] = self.lds_read(int(addr[l]), 16).view(np.uint32)
+            return
+        if op == "ds_read_b64_tr_b16":
+            assert w.exec.all()
+            dst = self.regs(w, o[0])
+            for grp in range(4):
+                for i in range(16):
+                    l = 16 * grp + i
+                    vals = []
+                    for q in range(4):
+                        src = 16 * grp + 4 * q + (i >> 2)
+                        a = int(addr[src]) + 2 * (i & 3)
+                        vals.append(int(self.lds_read(a, 2).view(np.uint16)[0]))
+                    dst[0, l] = vals[0] | (vals[1] << 16)
+                    dst[1, l] = vals[2] | (vals[3] << 16)
+            return
+        raise NotImplementedError(op)
+
+    # ---- global -----------------------------------------------------------------
+    def vmem(self, w, ins):
+        op, o = ins.op, ins.ops
+        off = self.off(ins)
+        if op == "global_load_lds_dwordx4":
+            assert w.exec.all()
+            voff = self.vec(w, o[0])
+            base = self.sc(w, o[1])
+            for l in range(LANES):
+                data = self.heap.read(base + int(voff[l]) + off, 16)
+                la = w.m0 + off + 16 * l
+                assert 0 <= la and la + 16 <= self.lds.size, f"LDS-DMA out of bounds {la}"
+                self.lds[la:la + 16] = data
+            return
+        if op == "global_load_dwordx4":
+            dst = self.regs(w, o[0])
+            voff = self.vec(w, o[1])
+            base = self.sc(w, o[2])
+            for l in range(LANES):
+                if w.exec[l]:
+                    dst[:, l] = self.heap.read(base + int(voff[l]) + off, 16).view(np.uint32)
+            return
+        if op == "global_store_dwordx4":
+            voff = self.vec(w, o[0])
+            src = self.regs(w, o[1])
+            base = self.sc(w, o[2])
+            for l in range(LANES):
+                if w.exec[l]:
+                    self.heap.write(base + int(voff[l]) + off, src[:, l].copy().view(np.uint8))
+            return
+        raise NotImplementedError(op)

@@ -1,0 +1,776 @@
+"""attn_fwd_v13: flash-attention forward on v_mfma_f32_16x16x32_bf16, one
+wave per SIMD, 64 query rows per wave (reference ch06/flash_attention.py:14-74;
+gfx950, bf16, D = 128, non-causal, Nk a multiple of 64 and >= 128).
+
+The whole kernel body is one generated instruction stream (this module
+builds it; tools/gen_flash_v13.py prints it into csrc/flash_v13_asm.h, and
+tools/v13/emu.py executes the same program on the CPU).
+
+Layout per wave (lane l: i = l & 15, g = l >> 4):
+  * S^T = K Q^T as 4 key-blocks kb x 4 query-blocks qb of 16 x 16
+    (v_mfma_f32_16x16x32_bf16, A = K fragment from LDS, B = Q^T fragment;
+    both in accumulator registers): lane (g, i) holds keys 16kb + 4g + r
+    (r = 0..3) of query 16qb + i.
+  * P = bf16(exp2(s * c - mu)) straight from S into the B operand of the PV
+    MFMA (key order permuted; the V^T operand is read with the same
+    permutation by two ds_read_b64_tr_b16 per fragment).
+  * O^T = V^T P^T as 8 d-blocks x 4 q-blocks in a[0:127]; the row sum l on
+    the matrix core (an all-ones A operand).
+  * Defer-max on P itself: mu = (row max) * c + 7 when a tile's max is
+    taken, so P <= 2^-7 right after; a tile is accepted while every P < 2,
+    which is bit 14 of each bf16 half (one v_or3_b32 per two words).  P >= 2
+    means the row max grew by 8 in log2 units (the THR 8 rule of v10/v12):
+    the rare path recomputes S from the LDS copy of K, moves mu, rescales O
+    and l and redoes the P it covers.
+  * K / V tiles arrive by LDS-DMA (1 KiB pieces, each 8 rows x one 128-B
+    line) into a 5-slot ring two tiles ahead.  The images are laid out so
+    that every fragment read is one base register + an immediate offset and
+    bank-conflict free (tools/v13/layout.py checks both).
+"""
+from __future__ import annotations
+
+from .isa import A, EXEC, Ins, M0, Neg, S, SCC, V, VCC, label
+
+MFMA = "v_mfma_f32_16x16x32_bf16"
+BF16_ONES = 0x3F803F80
+
+# ---------------------------------------------------------------- registers
+
+
+def S_(kb, qb):
+    return V(4 * (4 * qb + kb), 4)
+
+
+def P_(X, qb, kp):
+    return V(64 + 32 * X + 4 * (2 * qb + kp), 4)
+
+
+NVF = 3  # V^T fragment buffers (one d-block each)
+
+
+def VF(b, kp):
+    return V(128 + 8 * b + 4 * kp, 4)
+
+
+def VFh(b, kp, h):
+    return V(128 + 8 * b + 4 * kp + 2 * h, 2)
+
+
+def L_(qb):
+    return V(152 + 4 * qb, 4)
+
+
+ONES = V(168, 4)
+
+
+def MU(qb):
+    return V(172 + qb)
+
+
+def ACC(X):
+    return V(176 + X)
+
+
+VKL, VVL, VKA, VVA = V(178), V(179), V(180), V(181)
+
+
+def DMAK(j):
+    return V(182 + j)
+
+
+def DMAV(j):
+    return V(186 + j)
+
+
+def Y(k):
+    return V(190 + k)
+
+
+NY = 16
+
+
+def QOFF(qb):
+    return V(206 + qb)
+
+
+def OOFF(qb):
+    return V(210 + qb)
+
+
+LANE, VI, VG = V(214), V(215), V(216)
+
+
+def T(k):
+    assert 0 <= k < 38
+    return V(218 + k)  # even base: VGPR tuples must be 64-bit aligned
+
+
+def O_(db, qb):
+    return A(4 * (4 * db + qb), 4)
+
+
+def Q_(qb, ds):
+    return A(128 + 4 * (4 * qb + ds), 4)
+
+
+def K_(kb, ds):
+    return A(192 + 4 * (4 * ds + kb), 4)
+
+
+# SGPRs (hipcc keeps its own in s0..s15)
+sKA = S(16, 2)
+sWAVE, sL, sC, sMUOFF, sNT, sTBK, sTBV, sNQ, sG, sNBLK = (S(18 + k) for k in range(10))
+sCOH, sCQ0, sWKOFF = S(28, 2), S(30), S(31)
+sNQH, sNOH, sNQ0, sHASN = S(32, 2), S(34, 2), S(36), S(37)
+sNXK, sNXV, sNXIDX, sT = S(38, 2), S(40, 2), S(42), S(43)
+sDK, sDV, sDIDX = S(44, 2), S(46, 2), S(48)
+sSM1, sS0, sSP1, sSP2, sXR = S(49), S(50), S(51), S(52), S(53)
+sT0, sT1 = S(54), S(55)
+ARGS = 56  # block-parameter arguments: s56..s95 (dwords 0..39)
+
+
+def ARG(k, n=1):
+    return S(ARGS + k, n)
+
+
+sT2, sT3, sT4, sT5, sT6, sT7 = (S(96 + k) for k in range(6))
+SGPR_FIRST = 16
+SGPR_LAST = 101
+
+# kernel argument dwords (V13Args in csrc/flash_v13.hip)
+ARG_LAYOUT = ["q", "q_hi", "k", "k_hi", "v", "v_hi", "o", "o_hi",
+              "qb", "qb_hi", "qh", "qh_hi", "kb", "kb_hi", "kh", "kh_hi",
+              "vb", "vb_hi", "vh", "vh_hi", "ob", "ob_hi", "oh", "oh_hi",
+              "qn", "kn", "vn", "on", "nq", "nt", "qblocks", "nblocks",
+              "magq", "shq", "magh", "shh", "magg", "shg", "H", "xq",
+              "xr", "c", "muoff", "G", "tbk", "tbv", "group", "pad"]
+AI = {n: i for i, n in enumerate(ARG_LAYOUT)}
+
+SLOT = 32768  # one ring slot: K image (16 KiB) then V image (16 KiB)
+NSLOT = 5
+VIMG = 16384
+
+
+def I(op, *ops, mods="", note=""):
+    return Ins(op, *ops, mods=mods, note=note)
+
+
+def mfma(d, a, b, c):
+    return I(MFMA, d, a, b, c)
+
+
+# ---------------------------------------------------------------- scheduler
+
+
+class Fill:
+    """filler work for the gaps between MFMAs: a few instructions with an
+    issue cost (cycles), dependencies on other fills, an earliest gap and an
+    optional deadline gap"""
+    __slots__ = ("ins", "cost", "trans", "deps", "sep", "earliest", "deadline", "gap", "tag", "hard")
+
+    def __init__(self, ins, cost, trans=False, deps=(), sep=1, earliest=0, deadline=None, tag="", hard=False):
+        self.ins = ins if isinstance(ins, list) else [ins]
+        self.cost, self.trans, self.deps, self.sep = cost, trans, list(deps), sep
+        self.earliest, self.deadline, self.gap, self.tag = earliest, deadline, None, tag
+        self.hard = hard  # the deadline is a correctness bound (checked)
+
+
+def schedule(mfmas, fills, budget=8, gap_offset=0):
+    """place fills into the gaps after each MFMA (gap k follows MFMA k);
+    returns (instructions, unplaced fills).  Gap indices are shifted by
+    gap_offset for the fills' earliest/deadline/dependency bookkeeping, so
+    several phases can share one gap numbering."""
+    out = []
+    for k0, m in enumerate(mfmas):
+        k = k0 + gap_offset
+        out.append(m)
+        used, trans = 0, False
+        for f in fills:
+            if f.gap is not None or f.earliest > k:
+                continue
+            if any(d.gap is None or d.gap + f.sep > k for d in f.deps):
+                continue
+            forced = f.deadline is not None and f.deadline <= k
+            if not forced:
+                if f.trans and trans:
+                    continue
+                if used + f.cost > budget and not (used == 0 and f.cost > budget):
+                    continue
+            f.gap = k
+            out.extend(f.ins)
+            used += f.cost
+            trans = trans or f.trans
+    for f in fills:
+        if f.hard and (f.gap is None or f.gap > f.deadline):
+            raise RuntimeError(f"fill {f.tag} {f.ins[0]} missed its hard deadline {f.deadline} (gap {f.gap})")
+    left = [f for f in fills if f.gap is None]
+    return out, left
+
+
+def chain(ins_list, earliest=0, cost=None):
+    """fills that keep program order (each depends on the one before)"""
+    out, prev = [], None
+    for ins in ins_list:
+        c = cost(ins) if cost else (4 if ins.op.startswith("v_") else 2)
+        f = Fill(ins, c, deps=[prev] if prev else [], sep=0, earliest=earliest, tag="chain")
+        out.append(f)
+        prev = f
+    return out
+
+
+def drain(fills, k):
+    """emit unplaced fills in dependency order after the last gap k"""
+    out = []
+    pending = [f for f in fills if f.gap is None]
+    while pending:
+        progressed = False
+        for f in pending:
+            if all(d.gap is not None for d in f.deps):
+                f.gap = k
+                out.extend(f.ins)
+                progressed = True
+        pending = [f for f in pending if f.gap is None]
+        assert progressed, "fill dependency cycle"
+    return out
+
+
+# ---------------------------------------------------------------- pieces
+
+
+def qk_mfmas():
+    return [mfma(S_(kb, qb), K_(kb, ds), Q_(qb, ds), S_(kb, qb) if ds else 0)
+            for qb in range(4) for ds in range(4) for kb in range(4)]
+
+
+def qk_done_gap(kb, qb):
+    """QK phase gap after which S(kb, qb) is complete"""
+    return 16 * qb + 12 + kb
+
+
+def pv_mfmas(X):
+    out = []
+    for db in range(8):
+        for kp in range(2):
+            for qb in range(4):
+                out.append(mfma(O_(db, qb), VF(db % NVF, kp), P_(X, qb, kp), O_(db, qb)))
+        qb, kp = db % 4, db // 4
+        out.append(mfma(L_(qb), ONES, P_(X, qb, kp), L_(qb)))
+    return out
+
+
+def pv_first_gap(db):
+    return 9 * db
+
+
+def k_reads():
+    return [I("ds_read_b128", K_(kb, ds), VKA, mods=f"offset:{512 * (ds & 1) + 2048 * kb + 8192 * (ds >> 1)}")
+            for ds in range(4) for kb in range(4)]
+
+
+def v_reads(db):
+    b = db % NVF
+    return [I("ds_read_b64_tr_b16", VFh(b, kp, h), VVA,
+              mods=f"offset:{256 * (db & 1) + 512 * ((db >> 1) & 1) + 2048 * h + 4096 * kp + 8192 * (db >> 2)}")
+            for kp in range(2) for h in range(2)]
+
+
+def slice_list():
+    """softmax slices of one tile: (qb, kb, hh) in stream order"""
+    return [(qb, kb, hh) for qb in range(4) for kb in range(4) for hh in range(2)]
+
+
+def softmax_fills(X, slices, earliest_of, deadline_of=None, ytag=0, prev_cv=None):
+    """fills for the given slices of the tile in P state X: per slice two
+    v_fma_f32 (s * c - mu), two v_exp_f32, one v_cvt_pk_bf16_f32; one
+    v_or3_b32 per two slices into ACC(X).  Temporaries Y rotate over 8 slots
+    (a slot is reused once its cvt has issued)."""
+    fills, cvs = [], []
+    last_or = None
+    slot_cv = dict(prev_cv or {})
+    for n, (qb, kb, hh) in enumerate(slices):
+        slot = (ytag + n) % (NY // 2)
+        y0, y1 = Y(2 * slot), Y(2 * slot + 1)
+        s = S_(kb, qb)
+        deps = [slot_cv[slot]] if slot in slot_cv else []
+        fm = Fill([I("v_fma_f32", y0, s[2 * hh], sC, Neg(MU(qb))), I("v_fma_f32", y1, s[2 * hh + 1], sC, Neg(MU(qb)))],
+                  8, deps=deps, sep=0, earliest=earliest_of(qb, kb),
+                  deadline=deadline_of(qb, kb) if deadline_of else None, tag="fma",
+                  hard=deadline_of is not None)
+        e0 = Fill(I("v_exp_f32", y0, y0), 8, trans=True, deps=[fm], sep=1, tag="exp")
+        e1 = Fill(I("v_exp_f32", y1, y1), 8, trans=True, deps=[fm], sep=1, tag="exp")
+        w = P_(X, qb, kb >> 1)[2 * (kb & 1) + hh]
+        cv = Fill(I("v_cvt_pk_bf16_f32", w, y0, y1), 4, deps=[e0, e1], sep=1, tag="cvt")
+        slot_cv[slot] = cv
+        fills += [fm, e0, e1, cv]
+        cvs.append((cv, w))
+        if len(cvs) == 2:
+            (c0, w0), (c1, w1) = cvs
+            od = [c0, c1] + ([last_or] if last_or else [])
+            last_or = Fill(I("v_or3_b32", ACC(X), ACC(X), w0, w1), 4, deps=od, sep=1, tag="or")
+            fills.append(last_or)
+            cvs = []
+    assert not cvs
+    return fills, slot_cv, last_or
+
+
+# ---------------------------------------------------------------- SALU helpers
+
+
+def div_magic(out, x, mag, sh):
+    """out = x / d for x < 2^31 (mag, sh from the host: Granlund-Montgomery
+    with N = 31): ((x * mag) >> 31) >> sh"""
+    return [I("s_mul_hi_u32", sT6, x, mag), I("s_mul_i32", sT7, x, mag), I("s_lshl_b32", sT6, sT6, 1),
+            I("s_lshr_b32", sT7, sT7, 31), I("s_or_b32", sT6, sT6, sT7), I("s_lshr_b32", out, sT6, sh)]
+
+
+def mad64(out, base, x, st, y, st2):
+    """out = base + x * st + y * st2 (64-bit; x, y 32-bit unsigned)"""
+    c = []
+    for (m, stv, b) in ((x, st, base), (y, st2, out)):
+        c += [I("s_mul_i32", sT6, m, stv[0]), I("s_mul_hi_u32", sT7, m, stv[0]),
+              I("s_add_u32", out[0], b[0], sT6), I("s_addc_u32", out[1], b[1], sT7),
+              I("s_mul_i32", sT6, m, stv[1]), I("s_add_u32", out[1], out[1], sT6)]
+    return c
+
+
+def block_params(sx):
+    """block index sx -> sNQH, sNOH (Q / O heads), sNQ0 (the wave's first
+    row), the K head in sT0:sT1 and the V head in s96:s97; needs the
+    arguments in s56..s95.  sx is read by the first two instructions only
+    (it may be a scratch register the rest overwrites)."""
+    c = []
+    # xcd remap (each XCD walks a contiguous range): lb = x*xq + min(x, xr) + (l >> 3)
+    c += [I("s_and_b32", sT2, sx, 7), I("s_lshr_b32", sT3, sx, 3), I("s_mul_i32", sT4, sT2, ARG(AI["xq"])),
+          I("s_min_u32", sT2, sT2, sXR), I("s_add_u32", sT4, sT4, sT2), I("s_add_u32", sT4, sT4, sT3)]
+    # bh = lb / qblocks, qblk = lb - bh * qblocks
+    c += div_magic(sT5, sT4, ARG(AI["magq"]), ARG(AI["shq"]))
+    c += [I("s_mul_i32", sT2, sT5, ARG(AI["qblocks"])), I("s_sub_u32", sT2, sT4, sT2),
+          I("s_lshl_b32", sT2, sT2, 8), I("s_lshl_b32", sT3, sWAVE, 6), I("s_add_u32", sNQ0, sT2, sT3)]
+    # b = bh / H, h = bh - b * H, hk = h / group
+    c += div_magic(sT4, sT5, ARG(AI["magh"]), ARG(AI["shh"]))
+    c += [I("s_mul_i32", sT2, sT4, ARG(AI["H"])), I("s_sub_u32", sT3, sT5, sT2)]
+    c += div_magic(sT5, sT3, ARG(AI["magg"]), ARG(AI["shg"]))
+    # heads: b in sT4, h in sT3, hk in sT5
+    c += mad64(sNQH, ARG(AI["q"], 2), sT4, ARG(AI["qb"], 2), sT3, ARG(AI["qh"], 2))
+    c += mad64(sNOH, ARG(AI["o"], 2), sT4, ARG(AI["ob"], 2), sT3, ARG(AI["oh"], 2))
+    c += mad64(S(sT0.i, 2), ARG(AI["k"], 2), sT4, ARG(AI["kb"], 2), sT5, ARG(AI["kh"], 2))
+    c += mad64(S(sT2.i, 2), ARG(AI["v"], 2), sT4, ARG(AI["vb"], 2), sT5, ARG(AI["vh"], 2))
+    return c  # K head in sT0:sT1, V head in sT2:sT3
+
+
+def load_args():
+    return [I("s_load_dwordx16", ARG(0, 16), sKA, 0), I("s_load_dwordx16", ARG(16, 16), sKA, 64),
+            I("s_load_dwordx8", ARG(32, 8), sKA, 128), I("s_waitcnt", "lgkmcnt(0)")]
+
+
+# ---------------------------------------------------------------- DMA
+
+
+def dma_fills(slot_reg, earliest0=2, spacing=6):
+    """the 8 LDS-DMA pieces of the stream's next tile into slot slot_reg
+    (K pieces 4w..4w+3 of the K image, V pieces of the V image; one M0 write
+    per four), the stream switch before and the advance after"""
+    sw = Fill([I("s_cmp_eq_u32", sDIDX, sNT), I("s_cselect_b64", sDK, sNXK, sDK),
+               I("s_cselect_b64", sDV, sNXV, sDV), I("s_cselect_b32", sDIDX, sNXIDX, sDIDX)],
+              2, earliest=earliest0 - 1, tag="dmasw")
+    fills = [sw]
+    prev = sw
+    for j in range(8):
+        ins = []
+        if j == 0:
+            ins.append(I("s_add_u32", M0, slot_reg, sWKOFF))
+        if j == 4:
+            ins += [I("s_add_u32", M0, slot_reg, sWKOFF), I("s_add_u32", M0, M0, VIMG)]
+        src = sDK if j < 4 else sDV
+        off = DMAK(j) if j < 4 else DMAV(j - 4)
+        ins.append(I("global_load_lds_dwordx4", off, src, mods=f"offset:{1024 * (j % 4)}"))
+        f = Fill(ins, 12, deps=[prev], sep=1 if j else 0, earliest=earliest0 + spacing * j, tag="dma")
+        fills.append(f)
+        prev = f
+    adv = Fill([I("s_add_u32", sDK[0], sDK[0], sTBK), I("s_addc_u32", sDK[1], sDK[1], 0),
+                I("s_add_u32", sDV[0], sDV[0], sTBV), I("s_addc_u32", sDV[1], sDV[1], 0),
+                I("s_add_u32", sDIDX, sDIDX, 1)], 2, deps=[prev], sep=0, tag="dmaadv")
+    fills.append(adv)
+    return fills
+
+
+def dma_now(slot_reg):
+    """the same as straight-line code (prologue of the first block)"""
+    out = []
+    for f in dma_fills(slot_reg):
+        out += f.ins
+    return out
+
+
+def rotate_slots():
+    """slot(t-1) <- slot(t) <- slot(t+1) <- slot(t+2) <- slot(t+2) + 1"""
+    return [I("s_mov_b32", sSM1, sS0), I("s_mov_b32", sS0, sSP1), I("s_mov_b32", sSP1, sSP2),
+            I("s_add_u32", sSP2, sSP2, SLOT), I("s_cmp_ge_u32", sSP2, SLOT * NSLOT),
+            I("s_cselect_b32", sSP2, 0, sSP2)]
+
+
+# ---------------------------------------------------------------- softmax bits
+
+
+def row_max(qb, m, t1, t2):
+    """m = max over the row (query 16qb + i) of S(., qb): 16 values per lane,
+    then across the four lanes l, l^16, l^32, l^48"""
+    c = []
+    vals = [S_(kb, qb)[r] for kb in range(4) for r in range(4)]
+    c.append(I("v_max3_f32", m, vals[0], vals[1], vals[2]))
+    k = 3
+    while k + 1 < 16:
+        c.append(I("v_max3_f32", m, m, vals[k], vals[k + 1]))
+        k += 2
+    c.append(I("v_max_f32", m, m, vals[15]))
+    for sw in ("v_permlane32_swap_b32", "v_permlane16_swap_b32"):
+        c += [I("v_mov_b32", t1, m), I("v_mov_b32", t2, m), I(sw, t1, t2), I("v_max_f32", m, t1, t2)]
+    return c
+
+
+def exps_all(X, also_or=False):
+    """every P of the tile in S with the current mu (straight line)"""
+    c = []
+    for n, (qb, kb, hh) in enumerate(slice_list()):
+        y0, y1 = T(0 + 2 * (n % 8)), T(1 + 2 * (n % 8))
+        s = S_(kb, qb)
+        w = P_(X, qb, kb >> 1)[2 * (kb & 1) + hh]
+        c += [I("v_fma_f32", y0, s[2 * hh], sC, Neg(MU(qb))), I("v_fma_f32", y1, s[2 * hh + 1], sC, Neg(MU(qb))),
+              I("v_exp_f32", y0, y0), I("v_exp_f32", y1, y1), I("v_cvt_pk_bf16_f32", w, y0, y1)]
+        if also_or:
+            c.append(I("v_or_b32", ACC(X), ACC(X), w))
+    return c
+
+
+# ---------------------------------------------------------------- program
+
+
+class Gen:
+    def __init__(self, ndef=8, budget=8, dma_spacing=6, tag="%="):
+        self.ndef, self.budget, self.dma_spacing, self.tag = ndef, budget, dma_spacing, tag
+        self.prog = []
+        self.stats = {}
+
+    def L(self, name):
+        return f"v13_{name}_{self.tag}"
+
+    def emit(self, c):
+        self.prog.extend(c)
+
+    # ---- init ------------------------------------------------------------
+    def init(self, in_kernarg, in_wg, in_wave):
+        e = self.emit
+        e([I("s_mov_b64", sKA, in_kernarg), I("s_mov_b32", sL, in_wg), I("s_mov_b32", sWAVE, in_wave)])
+        e(load_args())
+        a = lambda n: ARG(AI[n])  # noqa: E731
+        # persistent scalars (xr/c/muoff/G/tbk/tbv are dwords 40.. -> second load)
+        # dwords 40..47 into s88..s95 for the copies below, then the block
+        # arguments (dwords 0..39) again
+        e([I("s_load_dwordx8", S(88, 8), sKA, 160), I("s_waitcnt", "lgkmcnt(0)")])
+        e([I("s_mov_b32", sXR, S(88)), I("s_mov_b32", sC, S(89)), I("s_mov_b32", sMUOFF, S(90)),
+           I("s_mov_b32", sG, S(91)), I("s_mov_b32", sTBK, S(92)), I("s_mov_b32", sTBV, S(93))])
+        e(load_args())
+        e([I("s_mov_b32", sNT, a("nt")), I("s_mov_b32", sNQ, a("nq")), I("s_mov_b32", sNBLK, a("nblocks")),
+           I("s_lshl_b32", sWKOFF, sWAVE, 12)])
+        # lane constants
+        e([I("v_mbcnt_lo_u32_b32", LANE, -1, 0), I("v_mbcnt_hi_u32_b32", LANE, -1, LANE),
+           I("v_and_b32", VI, 15, LANE), I("v_lshrrev_b32", VG, 4, LANE)])
+        t = [T(k) for k in range(12)]
+        # K read base: 16 (g&1) + 32 (i&7) + 256 (g>>1) + 1024 (i>>3)
+        e([I("v_and_b32", t[0], 1, VG), I("v_lshlrev_b32", t[0], 4, t[0]),
+           I("v_and_b32", t[1], 7, VI), I("v_lshlrev_b32", t[1], 5, t[1]), I("v_add_u32", t[0], t[0], t[1]),
+           I("v_lshrrev_b32", t[1], 1, VG), I("v_lshlrev_b32", t[1], 8, t[1]), I("v_add_u32", t[0], t[0], t[1]),
+           I("v_lshrrev_b32", t[1], 3, VI), I("v_lshlrev_b32", t[1], 10, t[1]), I("v_add_u32", VKL, t[0], t[1])])
+        # V read base: 8 i + 128 (g&1) + 1024 (g>>1) + 16384
+        e([I("v_lshlrev_b32", t[0], 3, VI), I("v_and_b32", t[1], 1, VG), I("v_lshlrev_b32", t[1], 7, t[1]),
+           I("v_add_u32", t[0], t[0], t[1]), I("v_lshrrev_b32", t[1], 1, VG), I("v_lshlrev_b32", t[1], 10, t[1]),
+           I("v_add_u32", t[0], t[0], t[1]), I("v_add_u32", VVL, VIMG, t[0])])
+        # DMA lane parts: row (L>>1)&7, chunk 4((L>>5)&1) + 2((L>>4)&1) + (L&1)
+        e([I("v_lshrrev_b32", t[2], 1, LANE), I("v_and_b32", t[2], 7, t[2]),          # laneRow
+           I("v_lshrrev_b32", t[3], 5, LANE), I("v_and_b32", t[3], 1, t[3]), I("v_lshlrev_b32", t[3], 2, t[3]),
+           I("v_lshrrev_b32", t[4], 4, LANE), I("v_and_b32", t[4], 1, t[4]), I("v_lshlrev_b32", t[4], 1, t[4]),
+           I("v_add_u32", t[3], t[3], t[4]), I("v_and_b32", t[4], 1, LANE), I("v_add_u32", t[3], t[3], t[4]),
+           I("v_lshlrev_b32", t[3], 4, t[3])])                                          # 16 * laneCh
+        for j in range(4):
+            # K piece pc = 4w + j: rowbase 16((pc>>1)&3) + 8(pc&1), chbase 8(pc>>3)
+            # V piece: rowbase 8(pc&7), chbase 8(pc>>3)
+            e([I("s_lshl_b32", sT2, sWAVE, 2), I("s_add_u32", sT2, sT2, j),             # pc
+               I("s_lshr_b32", sT3, sT2, 1), I("s_and_b32", sT3, sT3, 3), I("s_lshl_b32", sT3, sT3, 4),
+               I("s_and_b32", sT4, sT2, 1), I("s_lshl_b32", sT4, sT4, 3), I("s_add_u32", sT3, sT3, sT4),  # K rowbase
+               I("s_and_b32", sT4, sT2, 7), I("s_lshl_b32", sT4, sT4, 3),               # V rowbase
+               I("s_lshr_b32", sT5, sT2, 3), I("s_lshl_b32", sT5, sT5, 7),              # 16 * chbase
+               I("s_sub_u32", sT5, sT5, 1024 * j)])
+            for (rb, st, dst) in ((sT3, a("kn"), DMAK(j)), (sT4, a("vn"), DMAV(j))):
+                e([I("v_add_u32", t[5], rb, t[2]), I("v_mul_lo_u32", t[5], t[5], st),
+                   I("v_add_u32", t[5], t[5], t[3]), I("v_add_u32", dst, sT5, t[5])])
+        # ones selector, slots
+        e([I("v_mov_b32", ONES[k], BF16_ONES) for k in range(4)])
+        e([I("s_mov_b32", sS0, 0), I("s_mov_b32", sSP1, SLOT), I("s_mov_b32", sSP2, 2 * SLOT),
+           I("s_mov_b32", sSM1, 4 * SLOT)])
+
+    # ---- per-block scalar setup -----------------------------------------
+    def q_offsets(self, q0, qh):
+        """QOFF(qb) = min(q0 + 16 qb + i, Nq - 1) * qn + 16 g; Q loads"""
+        c = [I("s_sub_u32", sT0, sNQ, 1)]
+        for qb in range(4):
+            c += [I("v_add_u32", T(0), q0, VI), I("v_add_u32", T(0), 16 * qb, T(0)),
+                  I("v_min_u32", T(0), sT0, T(0)), I("v_mul_lo_u32", T(0), T(0), ARG(AI["qn"])),
+                  I("v_lshlrev_b32", T(1), 4, VG), I("v_add_u32", QOFF(qb), T(0), T(1))]
+        for qb in range(4):
+            for ds in range(4):
+                c.append(I("global_load_dwordx4", Q_(qb, ds), QOFF(qb), qh, mods=f"offset:{64 * ds}"))
+        return c
+
+    def next_params(self):
+        """sHASN = L + G < nblocks; if so the next block's params into sNQH,
+        sNOH, sNQ0, its K / V heads into sNXK / sNXV with sNXIDX = 0; else
+        the stream parks on the current block's last tile (sNXK = head + (nt
+        - 1) tile, sNXIDX = nt - 1).  Expects the current block's K / V heads
+        in sT0:sT1 / sT2:sT3 ... passed through sS registers by the caller."""
+        raise NotImplementedError
+
+    def block_setup_first(self):
+        """first block: params, DMA tiles 0 and 1, Q loads, next-block params"""
+        e = self.emit
+        e(block_params(sL))                          # current -> sNQH, sNOH, sNQ0, K/V heads in sT0.. / sT2..
+        e([I("s_mov_b64", sCOH, sNOH), I("s_mov_b32", sCQ0, sNQ0),
+           I("s_mov_b64", sDK, S(sT0.i, 2)), I("s_mov_b64", sDV, S(sT2.i, 2)), I("s_mov_b32", sDIDX, 0)])
+        e(self.q_offsets(sNQ0, sNQH))
+        e(self._next_params())
+        e(dma_now(sS0))
+        e(dma_now(sSP1))
+
+    def _next_params(self):
+        """(the stream pointer sDK / sDV is at some tile of the current
+        block with sDIDX its index: the current block's head is sDK - sDIDX
+        tiles)"""
+        skip = self.L(f"nonext{len(self.prog)}")
+        c = [I("s_add_u32", sT2, sL, sG), I("s_cmp_lt_u32", sT2, sNBLK), I("s_cselect_b32", sHASN, 1, 0)]
+        # parking place: the current block's last tile = sDK + (nt - 1 - sDIDX)
+        # tiles (signed: -1 when nt = 2 and both tiles were already issued)
+        c += [I("s_sub_u32", sT4, sNT, 1), I("s_sub_u32", sT4, sT4, sDIDX)]
+        for (dst, src, tb) in ((sNXK, sDK, sTBK), (sNXV, sDV, sTBV)):
+            c += [I("s_mul_i32", sT5, sT4, tb), I("s_ashr_i32", sT3, sT5, 31),
+                  I("s_add_u32", dst[0], src[0], sT5), I("s_addc_u32", dst[1], src[1], sT3)]
+        c += [I("s_sub_u32", sNXIDX, sNT, 1)]
+        c += [I("s_cmp_eq_u32", sHASN, 0), I("s_cbranch_scc1", skip)]
+        # the next block's index in s100 (block_params reads it first, then
+        # uses the register as division scratch)
+        c += [I("s_add_u32", S(100), sL, sG)]
+        c += block_params(S(100))
+        c += [I("s_mov_b64", sNXK, S(sT0.i, 2)), I("s_mov_b64", sNXV, S(sT2.i, 2)), I("s_mov_b32", sNXIDX, 0)]
+        c += [label(skip)]
+        return c
+
+    # ---- the tile loop ---------------------------------------------------
+    def block_body(self):
+        """O, l, mu zero; tile 0 (QK, exact max, P); the step loop; the tail;
+        the epilogue; the walk to the next block"""
+        e, Lb = self.emit, self.L
+        e([label(Lb("common"))])
+        e([I("v_accvgpr_write_b32", A(k), 0) for k in range(128)])
+        e([I("v_mov_b32", L_(qb)[r], 0) for qb in range(4) for r in range(4)])
+        e([I("v_mov_b32", ACC(0), 0), I("v_mov_b32", ACC(1), 0)])
+        e([I("s_waitcnt", "vmcnt(0)"), I("s_barrier")])
+        # tile 0: K(0) fragments, QK(0) with tile 2's DMA beside it
+        e([I("v_add_u32", VKA, sS0, VKL)])
+        e(k_reads())
+        fills = dma_fills(sSP2, earliest0=1, spacing=4)
+        body, left = schedule(qk_mfmas(), fills, self.budget)
+        e(body)
+        e(drain(left, 64))
+        # exact row max -> mu = max * c + muoff; P(0) into state 0
+        for qb in range(4):
+            e(row_max(qb, T(20 + qb), T(30), T(31)))
+            e([I("v_mul_f32", T(20 + qb), sC, T(20 + qb)), I("v_add_f32", MU(qb), sMUOFF, T(20 + qb))])
+        e(exps_all(0))
+        # tile 1 landed (tile 2 in flight): K(1) fragments
+        e([I("s_waitcnt", "vmcnt(8)"), I("s_barrier"), I("v_add_u32", VKA, sSP1, VKL)])
+        e(k_reads())
+        e([I("s_mov_b32", sT, 1)])
+        # steps t = 1 .. nt-1, two per iteration (P states 1 / 0)
+        e([label(Lb("loop"))])
+        self.step(1)
+        e([I("s_add_u32", sT, sT, 1), I("s_cmp_ge_u32", sT, sNT), I("s_cbranch_scc1", Lb("tail1"))])
+        self.step(0)
+        e([I("s_add_u32", sT, sT, 1), I("s_cmp_lt_u32", sT, sNT), I("s_cbranch_scc1", Lb("loop"))])
+        # tails: the last tile T = nt - 1 is in state (T & 1)
+        self.tail(0)
+        e([I("s_branch", Lb("epi"))])
+        e([label(Lb("tail1"))])
+        self.tail(1)
+        e([label(Lb("epi"))])
+        self.epilogue()
+
+    def deferred(self):
+        sl = slice_list()
+        return sl[len(sl) - self.ndef:], sl[:len(sl) - self.ndef]
+
+    def step(self, X):
+        """step t (state X = t & 1): QK(t) || the deferred slices of t-1,
+        tile t+2's DMA, V(t-1) d-blocks 0-1, softmax(t); the defer-max check
+        of t-1; barrier; PV(t-1) + row sums || K(t+1), V(t-1) d-blocks 2-7,
+        softmax(t)"""
+        e, Lb = self.emit, self.L
+        Xp = 1 - X
+        site = f"s{X}"
+        dfr, now = self.deferred()
+        e(rotate_slots())
+        e([I("v_add_u32", VVA, sSM1, VVL)])
+        # ---- QK phase
+        fills = []
+        # deferred slices of tile t-1 (they read S(., 3): before QK(t) overwrites it)
+        dl = lambda qb, kb: 16 * qb + kb - 1  # noqa: E731
+        f_def, cvd, last_or_prev = softmax_fills(Xp, dfr, lambda qb, kb: 0, dl, ytag=0)
+        fills += f_def
+        fills += dma_fills(sSP2, earliest0=1, spacing=self.dma_spacing)
+        # V(t-1) d-blocks 0, 1
+        for db in (0, 1):
+            for ins in v_reads(db):
+                fills.append(Fill(ins, 2, earliest=40 + 8 * db, tag="vread"))
+        # softmax(t), zero ACC(X) first
+        z = Fill(I("v_mov_b32", ACC(X), 0), 4, tag="zero")
+        fills.append(z)
+        f_now, cvn, last_or = softmax_fills(X, now, lambda qb, kb: qk_done_gap(kb, qb) + 3, ytag=len(dfr),
+                                            prev_cv=cvd)
+        for f in f_now:
+            if f.tag == "or" and not any(d.tag == "or" for d in f.deps):
+                f.deps.append(z)
+        fills += f_now
+        body, left = schedule(qk_mfmas(), fills, self.budget)
+        e(body)
+        # everything of tile t-1 must be done before its check
+        pend_prev = [f for f in left if f in f_def or f.tag.startswith("dma")]
+        e(drain(pend_prev, 63))
+        left = [f for f in left if f.gap is None]
+        # ---- defer-max check of tile t-1
+        e([I("v_and_b32", T(37), 0x40004000, ACC(Xp)), I("v_cmp_ne_u32_e32", VCC, 0, T(37)),
+           I("s_cbranch_vccnz", Lb(f"rare_{site}")), label(Lb(f"ret_{site}"))])
+        e([I("s_waitcnt", "vmcnt(8)"), I("s_barrier")])
+        # ---- PV phase
+        fills = left
+        ka = Fill(I("v_add_u32", VKA, sSP1, VKL), 4, tag="kaddr")
+        fills.insert(0, ka)
+        prev = ka
+        for n, ins in enumerate(k_reads()):
+            f = Fill(ins, 2, deps=[ka], sep=1, earliest=n // 2, deadline=40, tag="kread")
+            fills.insert(1 + n, f)
+        pv = pv_mfmas(Xp)
+        # V d-block db (2..7) reads: after d-block db-3's MFMAs (same buffer), well before db's
+        vr = []
+        for db in range(2, 8):
+            for ins in v_reads(db):
+                vr.append(Fill(ins, 2, earliest=pv_first_gap(db - 3) + 9 if db >= 3 else 0,
+                               deadline=pv_first_gap(db) - 6, tag="vread"))
+        fills = fills[:17] + vr + fills[17:]
+        body, left = schedule(pv, fills, self.budget)
+        e(body)
+        e(drain(left, 71))
+        self.rare_sites = getattr(self, "rare_sites", [])
+        self.rare_sites.append((site, Xp, True))
+
+    def tail(self, X):
+        """last tile T (state X): its deferred slices, its check, PV(T) with
+        the next block's Q loads beside it"""
+        e, Lb = self.emit, self.L
+        site = f"t{X}"
+        dfr, _ = self.deferred()
+        e(rotate_slots())
+        e([I("v_add_u32", VVA, sSM1, VVL)])
+        f_def, _, _ = softmax_fills(X, dfr, lambda qb, kb: 0, ytag=0)
+        e(drain(f_def, 0))
+        e([I("v_and_b32", T(37), 0x40004000, ACC(X)), I("v_cmp_ne_u32_e32", VCC, 0, T(37)),
+           I("s_cbranch_vccnz", Lb(f"rare_{site}")), label(Lb(f"ret_{site}"))])
+        e(v_reads(0) + v_reads(1))
+        fills = []
+        for db in range(2, 8):
+            for ins in v_reads(db):
+                fills.append(Fill(ins, 2, earliest=pv_first_gap(db - 3) + 9 if db >= 3 else 0,
+                                  deadline=pv_first_gap(db) - 6, tag="vread"))
+        # the next block's Q rows (or this block's again past the last block)
+        fills += chain(self.q_offsets(sNQ0, sNQH), earliest=4)
+        body, left = schedule(pv_mfmas(X), fills, self.budget)
+        e(body)
+        e(drain(left, 71))
+        self.rare_sites = getattr(self, "rare_sites", [])
+        self.rare_sites.append((site, X, False))
+
+    # ---- epilogue ---------------------------------------------------------
+    def epilogue(self):
+        e, Lb = self.emit, self.L
+        e([I("s_nop", 7), I("s_nop", 7)])
+        for qb in range(4):
+            e([I("v_rcp_f32", T(20 + qb), L_(qb)[0])])
+        for qb in range(4):
+            # O offsets and the row mask of this q-block
+            e([I("v_add_u32", T(24), sCQ0, VI), I("v_add_u32", T(24), 16 * qb, T(24)),
+               I("v_mul_lo_u32", T(25), T(24), ARG(AI["on"])),
+               I("v_and_b32", T(26), 1, VG), I("v_lshlrev_b32", T(26), 5, T(26)),
+               I("v_lshrrev_b32", T(27), 1, VG), I("v_lshlrev_b32", T(27), 4, T(27)),
+               I("v_add3_u32", OOFF(qb), T(25), T(26), T(27))])
+            for dbp in range(4):
+                w = 4 * dbp  # words T(w) .. T(w+3)
+                for half, db in enumerate((2 * dbp, 2 * dbp + 1)):
+                    for r in range(4):
+                        e([I("v_accvgpr_read_b32", T(28 + r), O_(db, qb)[r])])
+                    for r in range(4):
+                        e([I("v_mul_f32", T(28 + r), T(28 + r), T(20 + qb))])
+                    e([I("v_cvt_pk_bf16_f32", T(w + 2 * half), T(28), T(29)),
+                       I("v_cvt_pk_bf16_f32", T(w + 2 * half + 1), T(30), T(31))])
+                e([I("v_permlane16_swap_b32", T(w), T(w + 2)), I("v_permlane16_swap_b32", T(w + 1), T(w + 3))])
+            e([I("v_cmp_gt_u32_e32", VCC, sNQ, T(24)), I("s_and_saveexec_b64", S(sT2.i, 2), VCC)])
+            for dbp in range(4):
+                e([I("global_store_dwordx4", OOFF(qb), V(T(4 * dbp).i, 4), sCOH, mods=f"offset:{64 * dbp}")])
+            e([I("s_mov_b64", EXEC, S(sT2.i, 2))])
+        # next block
+        e([I("s_cmp_eq_u32", sHASN, 0), I("s_cbranch_scc1", Lb("end"))])
+        e([I("s_add_u32", sL, sL, sG), I("s_mov_b64", sCOH, sNOH), I("s_mov_b32", sCQ0, sNQ0)])
+        e(load_args())
+        e(self._next_params())
+        e([I("s_branch", Lb("common"))])
+
+    # ---- rare path --------------------------------------------------------
+    def rare(self, site, X, has_next):
+        """tile t (state X) raised some row's max by >= 8 (log2): recompute
+        S(t) from K(t) in slot sSM1, mu_new = max(mu, rowmax * c + muoff),
+        rescale O and l by exp2(mu - mu_new), redo P(t); then S(t+1) (slot
+        sS0) and every P(t+1) so far, ACC(t+1) from them"""
+        e, Lb = self.emit, self.L
+        e([label(Lb(f"rare_{site}"))])
+        e([I("s_nop", 7), I("s_nop", 7)])
+        for tile_slot, Xs, redo in ((sSM1, X, True), (sS0, 1 - X, has_next)):
+            if not redo:
+                continue
+            e([I("v_add_u32", T(36), tile_slot, VKL)])
+            e([I("ds_read_b128", K_(kb, ds), T(36), mods=f"offset:{512 * (ds & 1) + 2048 * kb + 8192 * (ds >> 1)}")
+               for ds in range(4) for kb in range(4)])
+            e(qk_mfmas())
+            if Xs == X:
+                for qb in range(4):
+                    m = T(20 + qb)
+                    e(row_max(qb, m, T(30), T(31)))
+                    e([I("v_mul_f32", m, sC, m), I("v_add_f32", m, sMUOFF, m), I("v_max_f32", m, m, MU(qb)),
+                       I("v_sub_f32", T(24), MU(qb), m), I("v_exp_f32", T(24), T(24)), I("v_mov_b32", MU(qb), m)])
+                    for db in range(8):
+                        for r in range(4):
+                            e([I("v_accvgpr_read_b32", T(25), O_(db, qb)[r]),
+                               I("v_mul_f32", T(25), T(25), T(24)),
+                               I("v_accvgpr_write_b32", O_(db, qb)[r], T(25))])
+                    e([I("v_mul_f32", L_(qb)[r], L_(qb)[r], T(24)) for r in range(4)])
+                e(exps_all(X))
+            else:
+                e([I("v_mov_b32", ACC(Xs), 0)])
+                e(exps_all(Xs, also_or=True))
+        e([I("v_mov_b32", ACC(X), 0), I("s_nop", 4), I("s_branch", Lb(f"ret_{site}"))])
+
+    # ---- whole kernel -----------------------------------------------------
+    def build(self, in_kernarg="%0", in_wg="%1", in_wave="%2"):
+        self.init(in_kernarg, in_wg, in_wave)
+        self.block_setup_first()
+        self.block_body()
+        e, Lb = self.emit, self.L
+        e([label(Lb("end")), I("s_waitcnt", "vmcnt(0)"), I("s_branch", Lb("exit"))])
+        for site, X, has_next in self.rare_sites:
+            self.rare(site, X, has_next)
+        e([label(Lb("exit"))])
+        return self.prog

@@ -1,0 +1,115 @@
+"""Host-side argument block of attn_fwd_v13 (the Python mirror of
+launch_attn_v13 in csrc/flash_v13.hip) and an emulator driver."""
+from __future__ import annotations
+
+import math
+import struct
+
+import numpy as np
+
+from . import emu as E
+from .isa import S, finalize
+from .kernel import AI, ARG_LAYOUT, Gen
+
+
+def magic(d: int):
+    """(m, l) with floor(x / d) == ((x * m) >> 31) >> l for 0 <= x < 2^31"""
+    assert d >= 1
+    l = 0
+    while (1 << l) < d:
+        l += 1
+    m = -(-(1 << (31 + l)) // d)
+    assert m < (1 << 32)
+    return m, l
+
+
+def args_for(qa, ka, va, oa, B, H, Hkv, Nq, Nk, strides_el, scale, G, muoff=7.0):
+    """the 48-dword argument block; strides_el: 12 element strides
+    (qb, qh, qn, kb, kh, kn, vb, vh, vn, ob, oh, on) of bf16 tensors"""
+    st = [2 * s for s in strides_el]
+    qblocks = -(-Nq // 256)
+    nblocks = B * H * qblocks
+    group = H // Hkv
+    d = dict.fromkeys(ARG_LAYOUT, 0)
+    for name, ptr in (("q", qa), ("k", ka), ("v", va), ("o", oa)):
+        d[name], d[name + "_hi"] = ptr & 0xFFFFFFFF, ptr >> 32
+    for name, val in (("qb", st[0]), ("qh", st[1]), ("kb", st[3]), ("kh", st[4]), ("vb", st[6]),
+                      ("vh", st[7]), ("ob", st[9]), ("oh", st[10])):
+        d[name], d[name + "_hi"] = val & 0xFFFFFFFF, val >> 32
+    d["qn"], d["kn"], d["vn"], d["on"] = st[2], st[5], st[8], st[11]
+    d["nq"], d["nt"], d["qblocks"], d["nblocks"] = Nq, Nk // 64, qblocks, nblocks
+    d["magq"], d["shq"] = magic(qblocks)
+    d["magh"], d["shh"] = magic(H)
+    d["magg"], d["shg"] = magic(group)
+    d["H"], d["group"] = H, group
+    if nblocks < 8:
+        d["xq"], d["xr"] = 0, 8
+    else:
+        d["xq"], d["xr"] = nblocks >> 3, nblocks & 7
+    d["c"] = struct.unpack("<I", struct.pack("<f", scale * 1.4426950408889634))[0]
+    d["muoff"] = struct.unpack("<I", struct.pack("<f", muoff))[0]
+    d["G"] = G
+    d["tbk"], d["tbv"] = 64 * st[5], 64 * st[8]
+    return np.array([d[n] for n in ARG_LAYOUT], dtype=np.uint32)
+
+
+_PROG = {}
+
+
+def program(**kw):
+    key = tuple(sorted(kw.items()))
+    if key not in _PROG:
+        g = Gen(tag="emu", **kw)
+        prog = g.build(in_kernarg=S(0, 2), in_wg=S(2), in_wave=S(3))
+        prog, _ = finalize(prog)
+        _PROG[key] = prog
+    return _PROG[key]
+
+
+def run(q, k, v, scale=None, grid=None, muoff=7.0, layout="bhsd", **kw):
+    """q [B,H,Nq,128], k / v [B,Hkv,Nk,128] float arrays (rounded to bf16) ->
+    O [B,H,Nq,128] float32 from the emulated kernel.  layout 'bshd' stores
+    the tensors as [B,S,H,D] (strided heads)."""
+    B, H, Nq, D = q.shape
+    Hkv, Nk = k.shape[1], k.shape[2]
+    assert D == 128 and Nk % 64 == 0 and Nk >= 128
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    heap = E.Heap()
+
+    def put(x, lay):
+        b16 = E.bf16_rne(np.asarray(x, dtype=np.float32)).astype(np.uint16)
+        if lay == "bshd":
+            b16 = np.ascontiguousarray(b16.transpose(0, 2, 1, 3))
+            Bx, Sx, Hx, Dx = b16.shape
+            strides = (Sx * Hx * Dx, Dx, Hx * Dx)
+        else:
+            Bx, Hx, Sx, Dx = b16.shape
+            strides = (Hx * Sx * Dx, Sx * Dx, Dx)
+        return heap.alloc(b16.nbytes + 256, b16.tobytes()), strides
+
+    qa, sq = put(q, layout)
+    ka, sk = put(k, layout)
+    va, sv = put(v, layout)
+    oa = heap.alloc(B * H * Nq * D * 2 + 256)
+    so = (Nq * H * D, D, H * D) if layout == "bshd" else (H * Nq * D, Nq * D, D)
+    qblocks = -(-Nq // 256)
+    nb = B * H * qblocks
+    G = nb if grid is None else grid
+    args = args_for(qa, ka, va, oa, B, H, Hkv, Nq, Nk, list(sq) + list(sk) + list(sv) + list(so), scale, G, muoff)
+    kaddr = heap.alloc(args.nbytes, args.tobytes())
+    prog = program(**kw)
+    em = E.Emu(prog, heap)
+    for wg in range(G):
+        waves = []
+        for wv in range(4):
+            w = E.Wave()
+            w.s[0], w.s[1], w.s[2], w.s[3] = kaddr & 0xFFFFFFFF, kaddr >> 32, wg, wv
+            waves.append(w)
+        em.lds[:] = 0
+        em.run_wg(waves)
+    raw = heap.view(oa)[:B * H * Nq * D * 2].view(np.uint16)
+    if layout == "bshd":
+        o = E.bf16_to_f32(raw.reshape(B, Nq, H, D).astype(np.uint32)).transpose(0, 2, 1, 3)
+    else:
+        o = E.bf16_to_f32(raw.reshape(B, H, Nq, D).astype(np.uint32))
+    return np.ascontiguousarray(o), em
