@@ -194,7 +194,8 @@ def schedule(mfmas, fills, budget=8, gap_offset=0):
             if not forced:
                 if f.trans and trans:
                     continue
-                if used + f.cost > budget and not (used == 0 and f.cost > budget):
+                if used + f.cost > budget and not (used == 0 and f.cost > budget) and \
+                        not (f.cost <= 2 and used + f.cost <= budget + 2):
                     continue
             f.gap = k
             out.extend(f.ins)
@@ -284,7 +285,7 @@ def softmax_fills(X, slices, earliest_of, deadline_of=None, ytag=0, prev_cv=None
     v_fma_f32 (s * c - mu), two v_exp_f32, one v_cvt_pk_bf16_f32; one
     v_or3_b32 per two slices into ACC(X).  Temporaries Y rotate over 8 slots
     (a slot is reused once its cvt has issued)."""
-    fills, cvs = [], []
+    fills, cvs, groups = [], [], []
     last_or = None
     slot_cv = dict(prev_cv or {})
     for n, (qb, kb, hh) in enumerate(slices):
@@ -292,16 +293,19 @@ def softmax_fills(X, slices, earliest_of, deadline_of=None, ytag=0, prev_cv=None
         y0, y1 = Y(2 * slot), Y(2 * slot + 1)
         s = S_(kb, qb)
         deps = [slot_cv[slot]] if slot in slot_cv else []
-        fm = Fill([I("v_fma_f32", y0, s[2 * hh], sC, Neg(MU(qb))), I("v_fma_f32", y1, s[2 * hh + 1], sC, Neg(MU(qb)))],
-                  8, deps=deps, sep=0, earliest=earliest_of(qb, kb),
-                  deadline=deadline_of(qb, kb) if deadline_of else None, tag="fma",
-                  hard=deadline_of is not None)
-        e0 = Fill(I("v_exp_f32", y0, y0), 8, trans=True, deps=[fm], sep=1, tag="exp")
-        e1 = Fill(I("v_exp_f32", y1, y1), 8, trans=True, deps=[fm], sep=1, tag="exp")
+        ea, dl = earliest_of(qb, kb), deadline_of(qb, kb) if deadline_of else None
+        f0 = Fill(I("v_fma_f32", y0, s[2 * hh], sC, Neg(MU(qb))), 4, deps=deps, sep=0, earliest=ea, deadline=dl,
+                  tag="fma", hard=dl is not None)
+        f1 = Fill(I("v_fma_f32", y1, s[2 * hh + 1], sC, Neg(MU(qb))), 4, deps=deps, sep=0, earliest=ea,
+                  deadline=dl, tag="fma", hard=dl is not None)
+        e0 = Fill(I("v_exp_f32", y0, y0), 8, trans=True, deps=[f0], sep=1, tag="exp")
+        e1 = Fill(I("v_exp_f32", y1, y1), 8, trans=True, deps=[f1], sep=1, tag="exp")
+        fm = f1
         w = P_(X, qb, kb >> 1)[2 * (kb & 1) + hh]
         cv = Fill(I("v_cvt_pk_bf16_f32", w, y0, y1), 4, deps=[e0, e1], sep=1, tag="cvt")
         slot_cv[slot] = cv
-        fills += [fm, e0, e1, cv]
+        fills += [f0, f1, e0, e1, cv]
+        groups.append([f0, f1, e0, e1, cv])
         cvs.append((cv, w))
         if len(cvs) == 2:
             (c0, w0), (c1, w1) = cvs
@@ -310,6 +314,7 @@ def softmax_fills(X, slices, earliest_of, deadline_of=None, ytag=0, prev_cv=None
             fills.append(last_or)
             cvs = []
     assert not cvs
+    softmax_fills.groups = groups  # per-slice fills of the last call
     return fills, slot_cv, last_or
 
 
@@ -384,7 +389,7 @@ def dma_fills(slot_reg, earliest0=2, spacing=6):
         src = sDK if j < 4 else sDV
         off = DMAK(j) if j < 4 else DMAV(j - 4)
         ins.append(I("global_load_lds_dwordx4", off, src, mods=f"offset:{1024 * (j % 4)}"))
-        f = Fill(ins, 12, deps=[prev], sep=1 if j else 0, earliest=earliest0 + spacing * j, tag="dma")
+        f = Fill(ins, 8, deps=[prev], sep=1 if j else 0, earliest=earliest0 + spacing * j, tag="dma")
         fills.append(f)
         prev = f
     adv = Fill([I("s_add_u32", sDK[0], sDK[0], sTBK), I("s_addc_u32", sDK[1], sDK[1], 0),
@@ -446,7 +451,7 @@ def exps_all(X, also_or=False):
 
 
 class Gen:
-    def __init__(self, ndef=8, budget=8, dma_spacing=6, tag="%="):
+    def __init__(self, ndef=4, budget=8, dma_spacing=6, tag="%="):
         self.ndef, self.budget, self.dma_spacing, self.tag = ndef, budget, dma_spacing, tag
         self.prog = []
         self.stats = {}
@@ -633,6 +638,7 @@ class Gen:
         fills.append(z)
         f_now, cvn, last_or = softmax_fills(X, now, lambda qb, kb: qk_done_gap(kb, qb) + 3, ytag=len(dfr),
                                             prev_cv=cvd)
+        now_groups = softmax_fills.groups
         for f in f_now:
             if f.tag == "or" and not any(d.tag == "or" for d in f.deps):
                 f.deps.append(z)
@@ -641,31 +647,36 @@ class Gen:
         e(body)
         # everything of tile t-1 must be done before its check
         pend_prev = [f for f in left if f in f_def or f.tag.startswith("dma")]
+        # a slice of tile t that has started finishes before the check: the
+        # rare path redoes every P of t from S, and a slice whose fma ran
+        # with the old mu must not write its P after that
+        for grp in now_groups:
+            if any(f.gap is not None for f in grp):
+                pend_prev += [f for f in grp if f.gap is None]
         e(drain(pend_prev, 63))
         left = [f for f in left if f.gap is None]
         # ---- defer-max check of tile t-1
         e([I("v_and_b32", T(37), 0x40004000, ACC(Xp)), I("v_cmp_ne_u32_e32", VCC, 0, T(37)),
            I("s_cbranch_vccnz", Lb(f"rare_{site}")), label(Lb(f"ret_{site}"))])
         e([I("s_waitcnt", "vmcnt(8)"), I("s_barrier")])
-        # ---- PV phase
+        # ---- PV phase (gaps numbered on from the QK phase's 64, so the
+        # leftover softmax keeps its dependency distances)
+        B0 = 64
         fills = left
-        ka = Fill(I("v_add_u32", VKA, sSP1, VKL), 4, tag="kaddr")
-        fills.insert(0, ka)
-        prev = ka
-        for n, ins in enumerate(k_reads()):
-            f = Fill(ins, 2, deps=[ka], sep=1, earliest=n // 2, deadline=40, tag="kread")
-            fills.insert(1 + n, f)
+        ka = Fill(I("v_add_u32", VKA, sSP1, VKL), 4, earliest=B0, tag="kaddr")
+        kr = [Fill(ins, 2, deps=[ka], sep=1, earliest=B0 + n // 2, deadline=B0 + 40, tag="kread")
+              for n, ins in enumerate(k_reads())]
         pv = pv_mfmas(Xp)
         # V d-block db (2..7) reads: after d-block db-3's MFMAs (same buffer), well before db's
         vr = []
         for db in range(2, 8):
             for ins in v_reads(db):
-                vr.append(Fill(ins, 2, earliest=pv_first_gap(db - 3) + 9 if db >= 3 else 0,
-                               deadline=pv_first_gap(db) - 6, tag="vread"))
-        fills = fills[:17] + vr + fills[17:]
-        body, left = schedule(pv, fills, self.budget)
+                vr.append(Fill(ins, 2, earliest=B0 + (pv_first_gap(db - 3) + 9 if db >= 3 else 0),
+                               deadline=B0 + pv_first_gap(db) - 6, tag="vread"))
+        fills = [ka] + kr + vr + fills
+        body, left = schedule(pv, fills, self.budget, gap_offset=B0)
         e(body)
-        e(drain(left, 71))
+        e(drain(left, B0 + 71))
         self.rare_sites = getattr(self, "rare_sites", [])
         self.rare_sites.append((site, Xp, True))
 
