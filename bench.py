@@ -101,12 +101,13 @@ def calibrate() -> dict:
     (graph-replayed over 24 rotated buffers, exactly like the GEMV leg), the
     copy kernel, and the MFMA probe of both bf16 shapes (one wave per SIMD,
     random operands, after a 2 s ramp, in-kernel clock stamped)."""
-    from ch03.roofline import (measure_hbm_bandwidth, measure_hbm_read_bandwidth,
+    from ch03.roofline import (measure_gemv_floor, measure_hbm_bandwidth, measure_hbm_read_bandwidth,
                                measure_hbm_read_bandwidth_sized, measure_mfma_peak_detail)
     m32 = measure_mfma_peak_detail("32x32x16")
     m16 = measure_mfma_peak_detail("16x16x32")
     return {"hbm_GB/s": measure_hbm_read_bandwidth(),
             "hbm_32MiB_per_launch": measure_hbm_read_bandwidth_sized(),
+            "gemv_floor": measure_gemv_floor(),
             "hbm_copy_GB/s": measure_hbm_bandwidth(),
             "mfma_32x32x16_TFLOP/s": m32["TFLOP/s"], "mfma_32x32x16_clock_GHz": m32["clock_GHz"],
             "mfma_16x16x32_TFLOP/s": m16["TFLOP/s"], "mfma_16x16x32_clock_GHz": m16["clock_GHz"],
@@ -791,6 +792,10 @@ def main():
             r.update({"measured_peak": sized, "measured_peak_kind": "hbm_32MiB_per_launch (size-matched)",
                       "frac_of_measured": r["achieved"] / sized,
                       "frac_of_streaming_read": r["achieved"] / cal["hbm_GB/s"]})
+            # the fitted floor: per-launch boundary + the GEMV's bytes at the streaming slope
+            fl = cal["gemv_floor"]
+            r.update({"floor_us": fl["floor_us"], "empty_launch_us": fl["empty_launch_us"],
+                      "frac_of_floor": fl["floor_us"] / extra["gemv"]["us_per_launch"]})
         if "decode_attn" in extra:
             r = extra["decode_attn"]["roofline"]
             r.update({"measured_peak": cal["hbm_GB/s"], "measured_peak_kind": "hbm read stream 2 x 1 GiB",

@@ -184,6 +184,77 @@ def measure_hbm_read_bandwidth_sized(nbytes: int = 33570816, copies: int = 24, r
             "how": f"{copies} buffers in turn, one HIP graph of {copies} launches, median of {reps} replays"}
 
 
+def _graph_probe_us(bufs, blocks: int, mode: int, reps: int) -> float:
+    """median us per launch of pli_hbm_read_probe over ``bufs`` in turn, the
+    launches captured in one HIP graph (the GEMV leg's timing)"""
+    import torch
+
+    import pli_hip
+
+    stream = torch.cuda.current_stream()
+    out = torch.empty(blocks * 256, device=bufs[0].device, dtype=torch.int32)
+    for b in bufs:
+        pli_hip.hbm_read_probe(b, out, blocks, mode)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for b in bufs:
+            pli_hip.hbm_read_probe(b, out, blocks, mode)
+    for _ in range(3):
+        g.replay()
+    times = []
+    for _ in range(reps):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record(stream)
+        g.replay()
+        e.record(stream)
+        e.synchronize()
+        times.append(s.elapsed_time(e) * 1e3 / len(bufs))
+    del g
+    return sorted(times)[len(times) // 2]
+
+
+def measure_gemv_floor(gemv_nbytes: int = 33570816, sizes_mib=(8, 32, 128, 512), grid_waves: int = 4096,
+                       reps: int = 8, device: str = "cuda") -> dict:
+    """The GEMV's measured floor: in graphs timed like the
+    ch03 GEMV leg,
+
+    * an (almost) empty launch with the GEMV's wave count (the read probe
+      over 16 bytes, ``grid_waves`` waves in 256-thread blocks): the
+      per-launch boundary ``empty_us``;
+    * the read probe at ``sizes_mib`` per launch (best layout each, buffers
+      rotated past the 256 MiB Infinity Cache), fitted as
+      ``us = a + bytes / slope``.
+
+    floor_us = a + gemv_nbytes / slope: what a launch that only streams the
+    GEMV's bytes costs on this part, boundary included."""
+    import numpy as np
+    import torch
+
+    tiny = [torch.ones(4, device=device, dtype=torch.int32) for _ in range(24)]
+    empty_us = _graph_probe_us(tiny, max(1, grid_waves // 4), 1, reps)
+    pts = []
+    for mib in sizes_mib:
+        nbytes = mib << 20
+        copies = max(2, -(-(768 << 20) // nbytes))
+        bufs = [torch.empty(nbytes // 4, device=device, dtype=torch.int32).fill_(i + 1) for i in range(copies)]
+        best = min(_graph_probe_us(bufs, MI355X_CUS * per_cu, mode, reps)
+                   for mode, per_cu in ((0, 8), (1, 4), (1, 8), (1, 16)))
+        pts.append((nbytes, best))
+        del bufs
+    x = np.array([p[0] for p in pts], dtype=np.float64)
+    y = np.array([p[1] for p in pts], dtype=np.float64)
+    slope_us_per_byte, a = np.polyfit(x, y, 1)
+    floor_us = a + gemv_nbytes * slope_us_per_byte
+    return {"empty_launch_us": empty_us, "fit_intercept_us": float(a),
+            "fit_GB/s": float(1e-3 / slope_us_per_byte),
+            "points": [{"bytes": int(b), "us": float(t), "GB/s": b / t * 1e-3} for b, t in pts],
+            "floor_us": float(floor_us), "floor_GB/s": gemv_nbytes / floor_us * 1e-3,
+            "how": "pli_hbm_read_probe in one HIP graph per size (buffers rotated past 256 MiB), best "
+                   "layout per size; least-squares us = a + bytes/slope; floor = a + GEMV bytes/slope; "
+                   f"empty launch = the probe over 16 B with {grid_waves} waves"}
+
+
 def measure_mfma_peak_detail(shape: str = "32x32x16", iters: int = 2048, reps: int = 5,
                              ramp_s: float = 2.0, device: str = "cuda") -> dict:
     """Achievable bf16 MFMA rate of one shape: ``pli_mfma_probe`` (one wave

@@ -72,6 +72,9 @@ def test_row_parallel_allreduce_gloo_world2(tmp_path):
     for ri in r:
         np.testing.assert_allclose(ri["y"], full, rtol=1e-5, atol=1e-5)
         np.testing.assert_allclose(ri["y2"], full, rtol=1e-5, atol=1e-5)
+        # the chunked, overlapped all-reduce is the same sum as the plain one:
+        # each row's partial is the same product, all-reduced once
+        np.testing.assert_array_equal(ri["y2"], ri["y"])
     np.testing.assert_array_equal(r[0]["ym"], r[1]["ym"])
     # bf16 inputs, fp32 partials summed by the all-reduce, one rounding at the end
     from oracle.numerics import round_to_bf16
