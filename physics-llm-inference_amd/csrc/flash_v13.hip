@@ -36,9 +36,9 @@ static_assert(sizeof(V13Args) == 192, "V13Args layout");
 enum : int {
     A_Q = 0, A_K = 2, A_V = 4, A_O = 6, A_QB = 8, A_QH = 10, A_KB = 12, A_KH = 14, A_VB = 16, A_VH = 18,
     A_OB = 20, A_OH = 22, A_QN = 24, A_KN, A_VN, A_ON, A_NQ, A_NT, A_QBLOCKS, A_NBLOCKS, A_MAGQ, A_SHQ,
-    A_MAGH, A_SHH, A_MAGG, A_SHG, A_H, A_XQ, A_XR, A_C, A_MUOFF, A_G, A_TBK, A_TBV, A_GROUP, A_PAD
+    A_MAGH, A_SHH, A_MAGG, A_SHG, A_H, A_XQ, A_XR, A_C, A_MUOFF, A_G, A_TBK, A_TBV, A_STAMP, A_STAMP_HI
 };
-static_assert(A_PAD == 47, "argument layout");
+static_assert(A_STAMP_HI == 47, "argument layout");
 
 __global__ __launch_bounds__(256, 1) void attn_fwd_v13(V13Args args) {
     __shared__ __attribute__((aligned(1024))) char smem[163840];
@@ -63,6 +63,21 @@ void put64(V13Args& a, int at, uint64_t v) {
     a.w[at + 1] = (uint32_t)(v >> 32);
 }
 
+#ifdef PLI_FLASH_STAMPS
+// diagnostic build only (tools/build_diag.sh): the same program with
+// s_memtime / s_memrealtime at each wave's entry and exit (8 dwords per wave
+// at args.stamp + 32 * (workgroup * 4 + wave))
+#include "flash_v13_stamp_asm.h"
+__global__ __launch_bounds__(256, 1) void attn_fwd_v13_stamp(V13Args args) {
+    __shared__ __attribute__((aligned(1024))) char smem[163840];
+    (void)args;
+    const void* kp = (const void*)__builtin_amdgcn_kernarg_segment_ptr();
+    const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const unsigned wg = blockIdx.x;
+    asm volatile(PLI_V13_STAMP_BODY::"s"(kp), "s"(wg), "s"(wave), "s"((unsigned)(uintptr_t)smem) : PLI_V13_CLOBBERS);
+}
+#endif
+
 }  // namespace
 
 bool attn_v13_ok(int D, int is_bf16, int causal, int Nq, int Nk, const V7Strides& st) {
@@ -77,7 +92,8 @@ bool attn_v13_ok(int D, int is_bf16, int causal, int Nq, int Nk, const V7Strides
 }
 
 int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B, int H, int group, int Nq,
-                    int Nk, const V7Strides& st, float scale, hipStream_t stream, bool persistent, float muoff) {
+                    int Nk, const V7Strides& st, float scale, hipStream_t stream, bool persistent, float muoff,
+                    uint32_t* stamps) {
     PLI_REQUIRE(attn_v13_ok(128, 1, 0, Nq, Nk, st), "attn_fwd_v13: shape not supported");
     const int qblocks = cdiv(Nq, 256);
     const int64_t nb = (int64_t)B * H * qblocks;
@@ -113,7 +129,6 @@ int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B,
     magic31((uint32_t)H, a.w[A_MAGH], a.w[A_SHH]);
     magic31((uint32_t)group, a.w[A_MAGG], a.w[A_SHG]);
     a.w[A_H] = (uint32_t)H;
-    a.w[A_GROUP] = (uint32_t)group;
     // XCD remap of the walk: lb = x * xq + min(x, xr) + (l >> 3), x = l & 7
     // (identity when there are fewer than 8 blocks)
     a.w[A_XQ] = nb < 8 ? 0u : (uint32_t)(nb >> 3);
@@ -124,8 +139,32 @@ int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B,
     a.w[A_G] = (uint32_t)grid;
     a.w[A_TBK] = (uint32_t)(64 * st.kn * 2);
     a.w[A_TBV] = (uint32_t)(64 * st.vn * 2);
+#ifdef PLI_FLASH_STAMPS
+    if (stamps) {
+        put64(a, A_STAMP, (uint64_t)(uintptr_t)stamps);
+        hipLaunchKernelGGL(attn_fwd_v13_stamp, dim3((unsigned)grid), dim3(256), 0, stream, a);
+        return launch_status("attn_fwd_v13_stamp");
+    }
+#else
+    (void)stamps;
+#endif
     hipLaunchKernelGGL(attn_fwd_v13, dim3((unsigned)grid), dim3(256), 0, stream, a);
     return launch_status("attn_fwd_v13");
 }
 
 }  // namespace pli
+
+#ifdef PLI_FLASH_STAMPS
+// Diagnostic entry (tools/libpli_diag.so only): one clock-stamped launch of
+// attn_fwd_v13 (persistent) on contiguous [B,H,N,128] bf16; stamps: 8 dwords
+// per wave (entry s_memtime lo/hi, s_memrealtime lo/hi, then the exit ones)
+extern "C" int pli_diag_v13_clock(const void* q, const void* k, const void* v, void* o, int B, int H, int N,
+                                  uint32_t* stamps) {
+    using namespace pli;
+    const int64_t sn = 128, sh = (int64_t)N * 128, sb = (int64_t)H * N * 128;
+    const V7Strides st{sb, sh, sn, sb, sh, sn, sb, sh, sn, sb, sh, sn};
+    const int rc = launch_attn_v13(q, k, v, o, B, H, 1, N, N, st, 1.f / sqrtf(128.f), 0, true, 7.f, stamps);
+    if (rc != 0 || hipDeviceSynchronize() != hipSuccess) return -1;
+    return 0;
+}
+#endif

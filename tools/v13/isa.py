@@ -134,7 +134,7 @@ class Ins:
             return "vmload"
         if op.startswith("global_store"):
             return "vmstore"
-        if op.startswith("s_load"):
+        if op.startswith("s_load") or op in ("s_memtime", "s_memrealtime"):
             return "smem"
         if op in ("s_nop",):
             return "nop"
@@ -188,6 +188,8 @@ class Ins:
         if k == "branch":
             return {"s_cbranch_scc0": ["scc"], "s_cbranch_scc1": ["scc"], "s_cbranch_vccz": ["vcc"],
                     "s_cbranch_vccnz": ["vcc"], "s_cbranch_execz": ["exec"]}.get(op, [])
+        if op == "v_writelane_b32":
+            return self.regs_of(o[1]) + self.regs_of(o[0])
         if k in ("vmstore",):
             r = []
             for x in o:

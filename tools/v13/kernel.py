@@ -98,6 +98,7 @@ def OOFF(qb):
 
 
 LANE, VI, VG = V(214), V(215), V(216)
+STAMPV = V(217)  # diagnostic build only
 
 
 def T(k):
@@ -143,7 +144,7 @@ ARG_LAYOUT = ["q", "q_hi", "k", "k_hi", "v", "v_hi", "o", "o_hi",
               "vb", "vb_hi", "vh", "vh_hi", "ob", "ob_hi", "oh", "oh_hi",
               "qn", "kn", "vn", "on", "nq", "nt", "qblocks", "nblocks",
               "magq", "shq", "magh", "shh", "magg", "shg", "H", "xq",
-              "xr", "c", "muoff", "G", "tbk", "tbv", "group", "pad"]
+              "xr", "c", "muoff", "G", "tbk", "tbv", "stamp", "stamp_hi"]
 AI = {n: i for i, n in enumerate(ARG_LAYOUT)}
 
 SLOT = 32768  # one ring slot: K image (16 KiB) then V image (16 KiB)
@@ -451,8 +452,9 @@ def exps_all(X, also_or=False):
 
 
 class Gen:
-    def __init__(self, ndef=4, budget=8, dma_spacing=6, tag="%="):
+    def __init__(self, ndef=4, budget=8, dma_spacing=6, tag="%=", stamp=False):
         self.ndef, self.budget, self.dma_spacing, self.tag = ndef, budget, dma_spacing, tag
+        self.stamp = stamp  # diagnostic build: s_memtime / s_memrealtime at entry and exit
         self.prog = []
         self.stats = {}
 
@@ -477,6 +479,12 @@ class Gen:
         e(load_args())
         e([I("s_mov_b32", sNT, a("nt")), I("s_mov_b32", sNQ, a("nq")), I("s_mov_b32", sNBLK, a("nblocks")),
            I("s_lshl_b32", sWKOFF, sWAVE, 12)])
+        if self.stamp:
+            # STAMP: lanes 0-3 of v217 = entry s_memtime / s_memrealtime, lane 8
+            # = this wave's record index (workgroup x 4 + wave)
+            e([I("s_memtime", S(96, 2)), I("s_memrealtime", S(98, 2)), I("s_waitcnt", "lgkmcnt(0)")])
+            e([I("v_writelane_b32", STAMPV, S(96 + k), k) for k in range(4)])
+            e([I("s_lshl_b32", sT6, sL, 2), I("s_add_u32", sT6, sT6, sWAVE), I("v_writelane_b32", STAMPV, sT6, 8)])
         # lane constants
         e([I("v_mbcnt_lo_u32_b32", LANE, -1, 0), I("v_mbcnt_hi_u32_b32", LANE, -1, LANE),
            I("v_and_b32", VI, 15, LANE), I("v_lshrrev_b32", VG, 4, LANE)])
@@ -780,7 +788,17 @@ class Gen:
         self.block_setup_first()
         self.block_body()
         e, Lb = self.emit, self.L
-        e([label(Lb("end")), I("s_waitcnt", "vmcnt(0)"), I("s_branch", Lb("exit"))])
+        e([label(Lb("end")), I("s_waitcnt", "vmcnt(0)")])
+        if self.stamp:
+            # exit stamps into lanes 4-7; lanes 0-7 stored at stamp + 32 * record
+            e([I("s_memtime", S(96, 2)), I("s_memrealtime", S(98, 2)), I("s_waitcnt", "lgkmcnt(0)")])
+            e([I("v_writelane_b32", STAMPV, S(96 + k), 4 + k) for k in range(4)])
+            e([I("v_readlane_b32", sT6, STAMPV, 8), I("s_load_dwordx2", S(96, 2), sKA, 4 * AI["stamp"]),
+               I("s_waitcnt", "lgkmcnt(0)"), I("s_lshl_b32", sT6, sT6, 5),
+               I("v_lshlrev_b32", T(0), 2, LANE), I("v_add_u32", T(0), sT6, T(0)),
+               I("s_mov_b64", EXEC, 0xFF), I("global_store_dword", T(0), STAMPV, S(96, 2)),
+               I("s_mov_b64", EXEC, -1), I("s_waitcnt", "vmcnt(0)")])
+        e([I("s_branch", Lb("exit"))])
         for site, X, has_next in self.rare_sites:
             self.rare(site, X, has_next)
         e([label(Lb("exit"))])
