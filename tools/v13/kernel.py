@@ -167,16 +167,23 @@ class Fill:
     """filler work for the gaps between MFMAs: a few instructions with an
     issue cost (cycles), dependencies on other fills, an earliest gap and an
     optional deadline gap"""
-    __slots__ = ("ins", "cost", "trans", "deps", "sep", "earliest", "deadline", "gap", "tag", "hard")
+    __slots__ = ("ins", "cost", "trans", "deps", "sep", "earliest", "deadline", "gap", "tag", "hard", "lds")
 
     def __init__(self, ins, cost, trans=False, deps=(), sep=1, earliest=0, deadline=None, tag="", hard=False):
         self.ins = ins if isinstance(ins, list) else [ins]
+        # LDS bytes this fill reads per wave (a gap of 16 cycles moves at most
+        # 1 KiB per wave when all four SIMDs read: 256 B/clk per CU)
+        self.lds = sum(1024 if i.op == "ds_read_b128" else 512 if i.op == "ds_read_b64_tr_b16" else 0
+                       for i in self.ins)
         self.cost, self.trans, self.deps, self.sep = cost, trans, list(deps), sep
         self.earliest, self.deadline, self.gap, self.tag = earliest, deadline, None, tag
         self.hard = hard  # the deadline is a correctness bound (checked)
 
 
-def schedule(mfmas, fills, budget=8, gap_offset=0):
+LDS_GAP = 1024  # LDS bytes per wave per 16-cycle gap (256 B/clk per CU, 4 waves)
+
+
+def schedule(mfmas, fills, budget=8, gap_offset=0, lds_gap=LDS_GAP):
     """place fills into the gaps after each MFMA (gap k follows MFMA k);
     returns (instructions, unplaced fills).  Gap indices are shifted by
     gap_offset for the fills' earliest/deadline/dependency bookkeeping, so
@@ -185,7 +192,7 @@ def schedule(mfmas, fills, budget=8, gap_offset=0):
     for k0, m in enumerate(mfmas):
         k = k0 + gap_offset
         out.append(m)
-        used, trans = 0, False
+        used, trans, lds = 0, False, 0
         for f in fills:
             if f.gap is not None or f.earliest > k:
                 continue
@@ -195,12 +202,15 @@ def schedule(mfmas, fills, budget=8, gap_offset=0):
             if not forced:
                 if f.trans and trans:
                     continue
+                if f.lds and lds + f.lds > lds_gap:
+                    continue
                 if used + f.cost > budget and not (used == 0 and f.cost > budget) and \
                         not (f.cost <= 2 and used + f.cost <= budget + 2):
                     continue
             f.gap = k
             out.extend(f.ins)
             used += f.cost
+            lds += f.lds
             trans = trans or f.trans
     for f in fills:
         if f.hard and (f.gap is None or f.gap > f.deadline):
