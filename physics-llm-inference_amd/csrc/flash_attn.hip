@@ -536,6 +536,9 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
 //  81: variant 80 with one block per workgroup
 //  82: variant 80 with mu = max * c - 1 (a rescale at nearly every tile whose
 //      max reaches the running max): tests only, exercises the rare path
+//  83 / 84: attn_fwd_v13c causal (bottom-right, Nq <= Nk, (Nk - Nq) % 64 ==
+//      0): 83 persistent (the pair walk where it tiles the grid), 84 one
+//      block per workgroup heaviest first; 85 = 83 with mu = max * c - 1
 constexpr int kDefaultVariant = 71;
 // causal: attn_fwd_v12 causal (74; one block per workgroup where the
 // persistent pair walk does not tile the shape), 60 where v12 does not apply
@@ -556,13 +559,14 @@ int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int
     // v7 / v10 also prescale Q by c, so c > 1 could overflow fp16 Q.
     const float c_log2 = scale * 1.4426950408889634f;
     const bool c_ok = c_log2 > 0.f && c_log2 <= 1.f;
-    if (variant == 80 || variant == 81 || variant == 82) {
+    if (variant >= 80 && variant <= 85) {
         const bool bf = std::is_same<T, bf16_t>::value;
+        const bool cv = variant >= 83;  // the causal forms
         const V7Strides s7{st.qb, st.qh, st.qn, st.kb, st.kh, st.kn, st.vb, st.vh, st.vn, st.ob, st.oh, st.on};
-        if (attn_v13_ok(D, bf ? 1 : 0, causal, Nq, Nk, s7) && c_ok)
-            return launch_attn_v13(q, k, v, o, B, H, group, Nq, Nk, s7, scale, stream, variant != 81,
-                                   variant == 82 ? -1.f : 7.f);
-        variant = 71;
+        if (cv == (causal != 0) && attn_v13_ok(D, bf ? 1 : 0, causal, Nq, Nk, s7) && c_ok)
+            return launch_attn_v13(q, k, v, o, B, H, group, Nq, Nk, s7, scale, stream, variant != 81 && variant != 84,
+                                   (variant == 82 || variant == 85) ? -1.f : 7.f, nullptr, causal != 0);
+        variant = causal ? 74 : 71;
     }
     if (variant == 70 || variant == 71 || variant == 72) {
         const bool bf = std::is_same<T, bf16_t>::value;

@@ -29,16 +29,16 @@ namespace {
 // kernel argument block: 48 dwords, the layout of tools/v13/kernel.py
 // ARG_LAYOUT (the body reads it through the kernarg pointer)
 struct V13Args {
-    uint32_t w[48];
+    uint32_t w[64];
 };
-static_assert(sizeof(V13Args) == 192, "V13Args layout");
+static_assert(sizeof(V13Args) == 256, "V13Args layout");
 
 enum : int {
     A_Q = 0, A_K = 2, A_V = 4, A_O = 6, A_QB = 8, A_QH = 10, A_KB = 12, A_KH = 14, A_VB = 16, A_VH = 18,
-    A_OB = 20, A_OH = 22, A_QN = 24, A_KN, A_VN, A_ON, A_NQ, A_NT, A_QBLOCKS, A_NBLOCKS, A_MAGQ, A_SHQ,
-    A_MAGH, A_SHH, A_MAGG, A_SHG, A_H, A_XQ, A_XR, A_C, A_MUOFF, A_G, A_TBK, A_TBV, A_STAMP, A_STAMP_HI
+    A_OB = 20, A_OH = 22, A_QN = 24, A_ON, A_NQ, A_NT, A_QBLOCKS, A_NBLOCKS, A_MAGQ, A_SHQ, A_MAGH, A_SHH,
+    A_MAGG, A_SHG, A_H, A_CW, A_HX, A_G, A_KN, A_VN, A_C, A_MUOFF, A_TBK, A_TBV, A_STAMP, A_STAMP_HI, A_OFFT
 };
-static_assert(A_STAMP_HI == 47, "argument layout");
+static_assert(A_G == 39 && A_OFFT == 48, "argument layout (tools/v13/kernel.py ARG_LAYOUT)");
 
 __global__ __launch_bounds__(256, 1) void attn_fwd_v13(V13Args args) {
     __shared__ __attribute__((aligned(1024))) char smem[163840];
@@ -47,6 +47,17 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v13(V13Args args) {
     const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const unsigned wg = blockIdx.x;
     asm volatile(PLI_V13_BODY::"s"(kp), "s"(wg), "s"(wave), "s"((unsigned)(uintptr_t)smem) : PLI_V13_CLOBBERS);
+}
+
+// causal (bottom-right mask): the same program with the masked step bodies
+// and the causal walks (tools/v13/kernel.py Gen(causal=True))
+__global__ __launch_bounds__(256, 1) void attn_fwd_v13c(V13Args args) {
+    __shared__ __attribute__((aligned(1024))) char smem[163840];
+    (void)args;
+    const void* kp = (const void*)__builtin_amdgcn_kernarg_segment_ptr();
+    const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const unsigned wg = blockIdx.x;
+    asm volatile(PLI_V13C_BODY::"s"(kp), "s"(wg), "s"(wave), "s"((unsigned)(uintptr_t)smem) : PLI_V13_CLOBBERS);
 }
 
 // floor(x / d) == ((x * m) >> 31) >> l for 0 <= x < 2^31 (Granlund-Montgomery,
@@ -81,7 +92,9 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v13_stamp(V13Args args) {
 }  // namespace
 
 bool attn_v13_ok(int D, int is_bf16, int causal, int Nq, int Nk, const V7Strides& st) {
-    if (D != 128 || !is_bf16 || causal || Nk < 128 || Nk % 64 != 0 || Nq < 1) return false;
+    if (D != 128 || !is_bf16 || Nk < 128 || Nk % 64 != 0 || Nq < 1) return false;
+    // causal: the bottom-right diagonal on 64-key tile boundaries
+    if (causal && (Nq > Nk || (Nk - Nq) % 64 != 0)) return false;
     // 32-bit per-lane offsets: a Q / O head's rows, a K / V tile
     const int64_t q_ext = ((int64_t)Nq - 1) * st.qn * 2 + 256, o_ext = ((int64_t)Nq - 1) * st.on * 2 + 256;
     const int64_t kv_tile = 64 * std::max(st.kn, st.vn) * 2;
@@ -93,8 +106,8 @@ bool attn_v13_ok(int D, int is_bf16, int causal, int Nq, int Nk, const V7Strides
 
 int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B, int H, int group, int Nq,
                     int Nk, const V7Strides& st, float scale, hipStream_t stream, bool persistent, float muoff,
-                    uint32_t* stamps) {
-    PLI_REQUIRE(attn_v13_ok(128, 1, 0, Nq, Nk, st), "attn_fwd_v13: shape not supported");
+                    uint32_t* stamps, bool causal) {
+    PLI_REQUIRE(attn_v13_ok(128, 1, causal, Nq, Nk, st), "attn_fwd_v13: shape not supported");
     const int qblocks = cdiv(Nq, 256);
     const int64_t nb = (int64_t)B * H * qblocks;
     PLI_REQUIRE(nb < (1ll << 31) && nb > 0, "attn_fwd_v13: grid too large");
@@ -102,6 +115,27 @@ int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B,
     if (persistent) {
         const int g = cu_count(stream) / 8 * 8;
         if (g >= 8 && nb > g) grid = g;
+    }
+    // causal walk: the pair walk where it tiles the grid exactly (query
+    // heights QB-1-a then a of one head per workgroup step, the QB/2
+    // workgroups of a head in step on one XCD; G/8 and QB/2 powers of two),
+    // else one block per workgroup, heaviest first
+    uint32_t cw = 0, hx = 0;
+    if (causal) {
+        const int64_t bh = nb / qblocks, w = grid / 8, hq = qblocks / 2;
+        auto pw2 = [](int64_t x) { return x > 0 && (x & (x - 1)) == 0; };
+        const bool pair = grid < nb && qblocks % 2 == 0 && hq > 0 && w % hq == 0 && bh % 8 == 0 &&
+                          (bh / 8) % (w / hq) == 0 && nb % grid == 0 && (nb / grid) % 2 == 0 && pw2(w) && pw2(hq);
+        if (pair) {
+            uint32_t lg8 = 0, lghq = 0;
+            while ((1ll << lg8) < w) ++lg8;
+            while ((1ll << lghq) < hq) ++lghq;
+            cw = 1u | (lg8 << 8) | (lghq << 16) | ((uint32_t)(w / hq) << 24);
+            hx = (uint32_t)(bh / 8);
+        } else {
+            cw = 2u;
+            grid = (int)nb;
+        }
     }
     V13Args a;
     std::memset(&a, 0, sizeof(a));
@@ -129,10 +163,9 @@ int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B,
     magic31((uint32_t)H, a.w[A_MAGH], a.w[A_SHH]);
     magic31((uint32_t)group, a.w[A_MAGG], a.w[A_SHG]);
     a.w[A_H] = (uint32_t)H;
-    // XCD remap of the walk: lb = x * xq + min(x, xr) + (l >> 3), x = l & 7
-    // (identity when there are fewer than 8 blocks)
-    a.w[A_XQ] = nb < 8 ? 0u : (uint32_t)(nb >> 3);
-    a.w[A_XR] = nb < 8 ? 8u : (uint32_t)(nb & 7);
+    a.w[A_CW] = cw;
+    a.w[A_HX] = hx;
+    a.w[A_OFFT] = causal ? (uint32_t)((Nk - Nq) / 64) : 0u;
     const float c = scale * 1.4426950408889634f;
     std::memcpy(&a.w[A_C], &c, 4);
     std::memcpy(&a.w[A_MUOFF], &muoff, 4);
@@ -148,6 +181,10 @@ int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B,
 #else
     (void)stamps;
 #endif
+    if (causal) {
+        hipLaunchKernelGGL(attn_fwd_v13c, dim3((unsigned)grid), dim3(256), 0, stream, a);
+        return launch_status("attn_fwd_v13c");
+    }
     hipLaunchKernelGGL(attn_fwd_v13, dim3((unsigned)grid), dim3(256), 0, stream, a);
     return launch_status("attn_fwd_v13");
 }
@@ -163,7 +200,7 @@ extern "C" int pli_diag_v13_clock(const void* q, const void* k, const void* v, v
     using namespace pli;
     const int64_t sn = 128, sh = (int64_t)N * 128, sb = (int64_t)H * N * 128;
     const V7Strides st{sb, sh, sn, sb, sh, sn, sb, sh, sn, sb, sh, sn};
-    const int rc = launch_attn_v13(q, k, v, o, B, H, 1, N, N, st, 1.f / sqrtf(128.f), 0, true, 7.f, stamps);
+    const int rc = launch_attn_v13(q, k, v, o, B, H, 1, N, N, st, 1.f / sqrtf(128.f), 0, true, 7.f, stamps, false);
     if (rc != 0 || hipDeviceSynchronize() != hipSuccess) return -1;
     return 0;
 }

@@ -22,7 +22,7 @@ bool attn_v12_ok(int D, int is_bf16, int causal, int Nk);
 bool attn_v13_ok(int D, int is_bf16, int causal, int Nq, int Nk, const V7Strides& st);
 int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B, int H, int group, int Nq,
                     int Nk, const V7Strides& st, float scale, hipStream_t stream, bool persistent, float muoff,
-                    uint32_t* stamps = nullptr);
+                    uint32_t* stamps = nullptr, bool causal = false);
 int launch_attn_v12(const void* q, const void* k, const void* v, void* o, int B, int H, int group, int Nq,
                     int Nk, const V7Strides& st, float scale, hipStream_t stream, bool persistent,
                     float thr = 8.f, bool causal = false);

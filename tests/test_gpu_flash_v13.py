@@ -108,3 +108,52 @@ def test_v13_rescale_stress(name):
     err = max_err(out, torch_attention(q, k, v))
     assert err <= 2.0 ** -8 * v.abs().max().item(), f"{name}: {err:.4e}"
     assert_agree_to_rounding(pli_hip.flash_attn_fwd(q, k, v, variant=82), out, v)
+
+
+# causal (bottom-right mask, (Nk - Nq) % 64 == 0): 83 persistent (pair walk
+# where it tiles the grid), 84 one block per workgroup heaviest first, 85 =
+# 83 with the rescale path at nearly every tile
+CAUSAL = [(4, 32, 8, 1024, 1024), (2, 32, 32, 2048, 2048), (2, 16, 4, 4096, 4096), (3, 40, 8, 1024, 1024),
+          (2, 8, 2, 256, 512), (1, 4, 4, 128, 128), (1, 8, 8, 704, 768), (2, 4, 2, 320, 320)]
+
+
+@pytest.mark.parametrize("qmul", (1, 4))
+@pytest.mark.parametrize("shape", CAUSAL, ids=lambda s: "b{}h{}kv{}q{}k{}".format(*s))
+def test_v13_causal_vs_f64_full_tensor(shape, qmul):
+    """Every output element of causal 83 / 84 / 85 against the f64 device
+    reference with the bottom-right mask; 83 and 84 bitwise equal."""
+    import pli_hip
+    q, k, v = inputs(shape, sum(shape) % 991)
+    q = q * qmul
+    ref = torch_attention(q, k, v, causal=True)
+    tol = 1e-2 if qmul == 1 else 2.0 ** -8 * v.abs().max().item()
+    outs = {}
+    for var in (83, 84, 85):
+        outs[var] = pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=var)
+        err = max_err(outs[var], ref)
+        assert err <= tol, f"{shape} q*{qmul} causal variant {var}: max |err| {err:.4e} > {tol:.4e}"
+    assert torch.equal(outs[83], outs[84]), f"{shape}: 83 != 84"
+
+
+def test_v13_causal_full_config_all_heads():
+    """Causal at the bench config: all 256 heads against an fp32 torch
+    attention with the mask; 85 within rounding of 83."""
+    import pli_hip
+    B, H, N, D = 8, 32, 4096, 128
+    g = torch.Generator(device=DEV).manual_seed(5)
+    q, k, v = (torch.randn(B, H, N, D, device=DEV, dtype=torch.bfloat16, generator=g) for _ in range(3))
+    out = pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=83)
+    for b in range(B):
+        ref = torch_attention(q[b:b + 1], k[b:b + 1], v[b:b + 1], dtype=torch.float32, heads_per_chunk=4,
+                              causal=True)
+        err = max_err(out[b:b + 1], ref)
+        assert err <= 1e-2, f"causal batch {b}: max |err| {err:.4e} over its 32 heads"
+    assert_agree_to_rounding(pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=85), out, v)
+
+
+def test_v13_causal_unaligned_offset_falls_back():
+    """Nk - Nq not a multiple of 64: the causal v13 variants route to v12."""
+    import pli_hip
+    q, k, v = inputs((2, 8, 2, 300, 512), 3)
+    assert torch.equal(pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=83),
+                       pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=74))

@@ -24,35 +24,40 @@ from v13 import run as R  # noqa: E402
 from v13.isa import analyse  # noqa: E402
 
 
-def f64_attention(q, k, v):
+def f64_attention(q, k, v, causal=False):
     r = lambda x: E.bf16_to_f32(E.bf16_rne(x.astype(np.float32))).astype(np.float64)  # noqa: E731
     qf, kf, vf = r(q), r(k), r(v)
     g = q.shape[1] // k.shape[1]
     kf, vf = np.repeat(kf, g, axis=1), np.repeat(vf, g, axis=1)
     s = np.einsum("bhqd,bhkd->bhqk", qf, kf) / np.sqrt(q.shape[-1])
+    if causal:  # bottom-right: row i sees keys j <= i + Nk - Nq (ch01/attention.py:66-67)
+        nq, nk = q.shape[2], k.shape[2]
+        s = np.where(np.arange(nk)[None, :] > np.arange(nq)[:, None] + nk - nq, -np.inf, s)
     s -= s.max(-1, keepdims=True)
     p = np.exp(s)
     p /= p.sum(-1, keepdims=True)
     return np.einsum("bhqk,bhkd->bhqd", p, vf)
 
 
-CASES = [  # (B, H, Hkv, Nq, Nk, grid, layout, muoff)
-    (1, 1, 1, 256, 128, None, "bhsd", 7.0),      # one block, two key tiles
-    (1, 2, 2, 256, 320, 1, "bhsd", 7.0),         # persistent: two blocks of five tiles on one workgroup
-    (2, 2, 1, 200, 128, 1, "bshd", 7.0),         # GQA, ragged Nq, BSHD strides, nt = 2 across seams
-    (1, 1, 1, 256, 256, None, "bhsd", -1.0),     # the rescale path at nearly every tile
+CASES = [  # (B, H, Hkv, Nq, Nk, grid, layout, muoff, causal)
+    (1, 1, 1, 256, 128, None, "bhsd", 7.0, False),      # one block, two key tiles
+    (1, 2, 2, 256, 320, 1, "bhsd", 7.0, False),         # persistent: two blocks of five tiles on one workgroup
+    (2, 2, 1, 200, 128, 1, "bshd", 7.0, False),         # GQA, ragged Nq, BSHD strides, nt = 2 across seams
+    (1, 1, 1, 256, 256, None, "bhsd", -1.0, False),     # the rescale path at nearly every tile
+    (1, 2, 1, 256, 512, None, "bhsd", 7.0, True),       # causal, Nq < Nk (diagonal offset 4 tiles)
+    (1, 1, 1, 512, 512, None, "bhsd", -1.0, True),      # causal, two blocks, rescales on masked tiles
 ]
 
 
-@pytest.mark.parametrize("case", CASES, ids=lambda c: "b{}h{}kv{}q{}k{}g{}-{}-mu{}".format(*c))
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "b{}h{}kv{}q{}k{}g{}-{}-mu{}-causal{}".format(*c))
 def test_v13_program_vs_f64(case):
-    B, H, Hkv, Nq, Nk, grid, lay, muoff = case
+    B, H, Hkv, Nq, Nk, grid, lay, muoff, causal = case
     rng = np.random.default_rng(sum(case[:5]))
     q = rng.standard_normal((B, H, Nq, 128))
     k = rng.standard_normal((B, Hkv, Nk, 128))
     v = rng.standard_normal((B, Hkv, Nk, 128))
-    o, em = R.run(q, k, v, grid=grid, layout=lay, muoff=muoff)
-    err = np.abs(o - f64_attention(q, k, v)).max()
+    o, em = R.run(q, k, v, grid=grid, layout=lay, muoff=muoff, causal=causal)
+    err = np.abs(o - f64_attention(q, k, v, causal)).max()
     assert err <= 1e-2, f"max |err| {err:.3e}"
     if muoff < 0:
         assert em.counts.get("v_sub_f32", 0) > 0, "the rescale path never ran"
@@ -74,8 +79,8 @@ def test_v13_spike_rescale():
 
 def test_v13_hazard_pass_is_idempotent():
     """the committed program needs no further padding or waits"""
-    prog = R.program()
-    assert analyse(prog) == {}
+    for causal in (False, True):
+        assert analyse(R.program(causal=causal)) == {}
 
 
 def test_v13_header_is_current():

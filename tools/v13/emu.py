@@ -329,11 +329,16 @@ class Emu:
         if op == "v_cvt_pk_bf16_f32":
             lo, hi = bf16_rne(gf(o[1])), bf16_rne(gf(o[2]))
             return self.vset(w, o[0], lo | (hi << 16))
-        if op in ("v_cmp_ne_u32_e32", "v_cmp_gt_u32_e32"):
+        if op in ("v_cmp_ne_u32_e32", "v_cmp_gt_u32_e32", "v_cmp_gt_i32_e32", "v_cmp_lt_i32_e32"):
             a, b = g(o[1]), g(o[2])
-            r = (a != b) if op == "v_cmp_ne_u32_e32" else (a > b)
+            if op.endswith("i32_e32"):
+                a, b = a.view(np.int32), b.view(np.int32)
+            r = {"v_cmp_ne_u32_e32": a != b, "v_cmp_gt_u32_e32": a > b, "v_cmp_gt_i32_e32": a > b,
+                 "v_cmp_lt_i32_e32": a < b}[op]
             w.vcc = np.where(w.exec, r, False)
             return
+        if op == "v_cndmask_b32_e32":
+            return self.vset(w, o[0], np.where(w.vcc, g(o[2]), g(o[1])))
         if op == "v_permlane16_swap_b32":
             A_, B_ = o[0], o[1]
             va, vb = g(A_), g(B_)
@@ -436,8 +441,12 @@ class Emu:
             if take:
                 w.pc = self.labels[o[0]]
             return
+        if op == "s_endpgm":
+            w.pc = len(self.prog)
+            return
         if op.startswith("s_load_dword"):
-            n = {"s_load_dwordx2": 2, "s_load_dwordx4": 4, "s_load_dwordx8": 8, "s_load_dwordx16": 16}[op]
+            n = {"s_load_dword": 1, "s_load_dwordx2": 2, "s_load_dwordx4": 4, "s_load_dwordx8": 8,
+                 "s_load_dwordx16": 16}[op]
             base = g(o[1])
             data = self.heap.read(base + int(o[2]), 4 * n).view(np.uint32)
             for k in range(n):

@@ -145,6 +145,8 @@ class Ins:
             return "branch"
         if op == "s_barrier":
             return "barrier"
+        if op == "s_endpgm":
+            return "end"
         if op.startswith("s_"):
             return "salu"
         raise ValueError(op)
@@ -164,7 +166,7 @@ class Ins:
 
     def writes(self):
         k, op, o = self.kind(), self.op, self.ops
-        if k in ("label", "nop", "wait", "barrier", "branch", "vmstore", "dma"):
+        if k in ("label", "nop", "wait", "barrier", "branch", "vmstore", "dma", "end"):
             return []
         if op.startswith("v_cmp_") and op.endswith("_e32"):
             return ["vcc"]
@@ -183,7 +185,7 @@ class Ins:
 
     def reads(self):
         k, op, o = self.kind(), self.op, self.ops
-        if k in ("label", "nop", "wait", "barrier"):
+        if k in ("label", "nop", "wait", "barrier", "end"):
             return []
         if k == "branch":
             return {"s_cbranch_scc0": ["scc"], "s_cbranch_scc1": ["scc"], "s_cbranch_vccz": ["vcc"],

@@ -90,11 +90,15 @@ NY = 16
 
 
 def QOFF(qb):
-    return V(206 + qb)
+    return V(250 + qb)  # = T(32 + qb): live only while the Q loads issue
 
 
 def OOFF(qb):
-    return V(210 + qb)
+    return V(234 + qb)  # = T(16 + qb): epilogue only
+
+
+TRI = V(206, 4)   # causal: the 16 x 16 diagonal block's C operand (0 / -inf)
+NINF = V(210, 4)  # causal: -inf (C operand of fully masked chains, cndmask source)
 
 
 LANE, VI, VG = V(214), V(215), V(216)
@@ -120,13 +124,13 @@ def K_(kb, ds):
 
 # SGPRs (hipcc keeps its own in s0..s15)
 sKA = S(16, 2)
-sWAVE, sL, sC, sMUOFF, sNT, sTBK, sTBV, sNQ, sG, sNBLK = (S(18 + k) for k in range(10))
-sCOH, sCQ0, sWKOFF = S(28, 2), S(30), S(31)
-sNQH, sNOH, sNQ0, sHASN = S(32, 2), S(34, 2), S(36), S(37)
-sNXK, sNXV, sNXIDX, sT = S(38, 2), S(40, 2), S(42), S(43)
-sDK, sDV, sDIDX = S(44, 2), S(46, 2), S(48)
-sSM1, sS0, sSP1, sSP2, sXR = S(49), S(50), S(51), S(52), S(53)
-sT0, sT1 = S(54), S(55)
+sWKOFF, sL, sC, sNT, sTBK, sTBV = S(18), S(19), S(20), S(21), S(22), S(23)  # sWKOFF = 4096 * wave
+sCOH, sCQ0, sOFFT = S(24, 2), S(26), S(27)
+sNQH, sNOH, sNQ0, sNXNT, sTD, sDNT = S(28, 2), S(30, 2), S(32), S(33), S(34), S(35)
+sNXK, sNXV, sNXIDX, sT = S(36, 2), S(38, 2), S(40), S(41)
+sDK, sDV, sDIDX = S(42, 2), S(44, 2), S(46)
+sSM1, sS0, sSP1, sSP2, sHASN = S(47), S(48), S(49), S(50), S(51)
+sT0, sT1, sT8, sRET = S(52), S(53), S(54), S(55)
 ARGS = 56  # block-parameter arguments: s56..s95 (dwords 0..39)
 
 
@@ -139,12 +143,16 @@ SGPR_FIRST = 16
 SGPR_LAST = 101
 
 # kernel argument dwords (V13Args in csrc/flash_v13.hip)
+# (dwords 0..39 are reloaded into s56..s95 at every block transition; 40..
+# are read at init or by a single s_load where needed)
 ARG_LAYOUT = ["q", "q_hi", "k", "k_hi", "v", "v_hi", "o", "o_hi",
               "qb", "qb_hi", "qh", "qh_hi", "kb", "kb_hi", "kh", "kh_hi",
               "vb", "vb_hi", "vh", "vh_hi", "ob", "ob_hi", "oh", "oh_hi",
-              "qn", "kn", "vn", "on", "nq", "nt", "qblocks", "nblocks",
-              "magq", "shq", "magh", "shh", "magg", "shg", "H", "xq",
-              "xr", "c", "muoff", "G", "tbk", "tbv", "stamp", "stamp_hi"]
+              "qn", "on", "nq", "nt", "qblocks", "nblocks", "magq", "shq",
+              "magh", "shh", "magg", "shg", "H", "cw", "hx", "G",
+              "kn", "vn", "c", "muoff", "tbk", "tbv", "stamp", "stamp_hi",
+              "offt", "pad1", "pad2", "pad3", "pad4", "pad5", "pad6", "pad7",
+              "pad8", "pad9", "pad10", "pad11", "pad12", "pad13", "pad14", "pad15"]
 AI = {n: i for i, n in enumerate(ARG_LAYOUT)}
 
 SLOT = 32768  # one ring slot: K image (16 KiB) then V image (16 KiB)
@@ -249,8 +257,18 @@ def drain(fills, k):
 # ---------------------------------------------------------------- pieces
 
 
-def qk_mfmas():
-    return [mfma(S_(kb, qb), K_(kb, ds), Q_(qb, ds), S_(kb, qb) if ds else 0)
+def qk_mfmas(mask=None):
+    """QK^T of one tile, q-block major.  mask (causal): the C operand of each
+    chain's first MFMA -- 'diag' (the wave's diagonal tile: 0 below the
+    diagonal blocks, the triangular pattern on them, -inf above), 'beyond'
+    (every score -inf: P = 0)"""
+    def c0(kb, qb):
+        if mask == "beyond" or (mask == "diag" and kb > qb):
+            return NINF
+        if mask == "diag" and kb == qb:
+            return TRI
+        return 0
+    return [mfma(S_(kb, qb), K_(kb, ds), Q_(qb, ds), S_(kb, qb) if ds else c0(kb, qb))
             for qb in range(4) for ds in range(4) for kb in range(4)]
 
 
@@ -349,19 +367,58 @@ def mad64(out, base, x, st, y, st2):
     return c
 
 
-def block_params(sx):
+def block_params(sx, causal=False, uid=0):
     """block index sx -> sNQH, sNOH (Q / O heads), sNQ0 (the wave's first
-    row), the K head in sT0:sT1 and the V head in s96:s97; needs the
-    arguments in s56..s95.  sx is read by the first two instructions only
-    (it may be a scratch register the rest overwrites)."""
+    row), sT8 (the block's key-tile count), the K head in sT0:sT1 (s52:s53)
+    and the V head in s96:s97; needs the arguments in s56..s95.  sx is read
+    by the first instructions only (it may be a scratch register the rest
+    overwrites).
+
+    Walk (non-causal): each XCD walks a contiguous range of blocks (the
+    xcd_remap of pli_common.h), lb = x * (nb >> 3) + min(x, nb & 7) + (l >> 3).
+    Causal (the cw argument's low byte): 1 = the pair walk of attn_fwd_v12
+    (workgroup i of XCD x runs query heights QB-1-a then a of one head, so
+    every workgroup does the same triangular work and the QB/2 workgroups of a
+    head share its K/V in L2); 2 = the remap walk, heaviest block of a head
+    first (one block per workgroup)."""
+    NB, QB, CW = ARG(AI["nblocks"]), ARG(AI["qblocks"]), ARG(AI["cw"])
     c = []
-    # xcd remap (each XCD walks a contiguous range): lb = x*xq + min(x, xr) + (l >> 3)
-    c += [I("s_and_b32", sT2, sx, 7), I("s_lshr_b32", sT3, sx, 3), I("s_mul_i32", sT4, sT2, ARG(AI["xq"])),
-          I("s_min_u32", sT2, sT2, sXR), I("s_add_u32", sT4, sT4, sT2), I("s_add_u32", sT4, sT4, sT3)]
-    # bh = lb / qblocks, qblk = lb - bh * qblocks
+    pair, done = f"v13_pair_{uid}_%=", f"v13_walked_{uid}_%="
+    if causal:
+        c += [I("s_and_b32", sT6, CW, 0xFF), I("s_cmp_eq_u32", sT6, 1), I("s_cbranch_scc1", pair)]
+    # the remap walk: lb in sT4, bh in sT5, qblk in sT2
+    c += [I("s_lshr_b32", sT4, NB, 3), I("s_and_b32", sT5, NB, 7), I("s_cmp_lt_u32", NB, 8),
+          I("s_cselect_b32", sT4, 0, sT4), I("s_cselect_b32", sT5, 8, sT5),
+          I("s_and_b32", sT2, sx, 7), I("s_lshr_b32", sT3, sx, 3), I("s_mul_i32", sT4, sT2, sT4),
+          I("s_min_u32", sT2, sT2, sT5), I("s_add_u32", sT4, sT4, sT2), I("s_add_u32", sT4, sT4, sT3)]
     c += div_magic(sT5, sT4, ARG(AI["magq"]), ARG(AI["shq"]))
-    c += [I("s_mul_i32", sT2, sT5, ARG(AI["qblocks"])), I("s_sub_u32", sT2, sT4, sT2),
-          I("s_lshl_b32", sT2, sT2, 8), I("s_lshl_b32", sT3, sWAVE, 6), I("s_add_u32", sNQ0, sT2, sT3)]
+    c += [I("s_mul_i32", sT2, sT5, QB), I("s_sub_u32", sT2, sT4, sT2)]
+    if causal:
+        # heaviest first: query height QB-1-r
+        c += [I("s_sub_u32", sT3, QB, 1), I("s_sub_u32", sT2, sT3, sT2), I("s_branch", done)]
+        # the pair walk: x = l & 7, l8 = l >> 3, j = l8 >> lgG8, wg = l8 mod G8,
+        # wgq = wg >> lghq, a = wg mod hq, bh = x hx + wgq + per (j >> 1),
+        # qblk = j odd ? a : QB-1-a
+        c += [label(pair),
+              I("s_and_b32", sT2, sx, 7), I("s_lshr_b32", sT3, sx, 3),
+              I("s_lshr_b32", sT6, CW, 8), I("s_and_b32", sT6, sT6, 0xFF),
+              I("s_lshr_b32", sT4, sT3, sT6), I("s_lshl_b32", sT5, sT4, sT6), I("s_sub_u32", sT5, sT3, sT5),
+              I("s_mul_i32", sT2, sT2, ARG(AI["hx"])),
+              I("s_lshr_b32", sT6, CW, 16), I("s_and_b32", sT6, sT6, 0xFF),
+              I("s_lshr_b32", sT3, sT5, sT6), I("s_lshl_b32", sT7, sT3, sT6), I("s_sub_u32", sT5, sT5, sT7),
+              I("s_add_u32", sT2, sT2, sT3),
+              I("s_lshr_b32", sT6, CW, 24), I("s_lshr_b32", sT7, sT4, 1), I("s_mul_i32", sT7, sT7, sT6),
+              I("s_add_u32", sT2, sT2, sT7),
+              I("s_sub_u32", sT6, QB, 1), I("s_sub_u32", sT6, sT6, sT5),
+              I("s_and_b32", sT4, sT4, 1), I("s_cselect_b32", sT4, sT5, sT6),
+              I("s_mov_b32", sT5, sT2), I("s_mov_b32", sT2, sT4), label(done)]
+        # key tiles the block's last row sees: min(nt, 4 qblk + 4 + off / 64)
+        c += [I("s_lshl_b32", sT8, sT2, 2), I("s_add_u32", sT8, sT8, 4), I("s_add_u32", sT8, sT8, sOFFT),
+              I("s_min_u32", sT8, sT8, ARG(AI["nt"]))]
+    else:
+        c += [I("s_mov_b32", sT8, ARG(AI["nt"]))]
+    # q0 = qblk * 256 + 64 * wave
+    c += [I("s_lshl_b32", sT2, sT2, 8), I("s_lshr_b32", sT3, sWKOFF, 6), I("s_add_u32", sNQ0, sT2, sT3)]
     # b = bh / H, h = bh - b * H, hk = h / group
     c += div_magic(sT4, sT5, ARG(AI["magh"]), ARG(AI["shh"]))
     c += [I("s_mul_i32", sT2, sT4, ARG(AI["H"])), I("s_sub_u32", sT3, sT5, sT2)]
@@ -371,7 +428,7 @@ def block_params(sx):
     c += mad64(sNOH, ARG(AI["o"], 2), sT4, ARG(AI["ob"], 2), sT3, ARG(AI["oh"], 2))
     c += mad64(S(sT0.i, 2), ARG(AI["k"], 2), sT4, ARG(AI["kb"], 2), sT5, ARG(AI["kh"], 2))
     c += mad64(S(sT2.i, 2), ARG(AI["v"], 2), sT4, ARG(AI["vb"], 2), sT5, ARG(AI["vh"], 2))
-    return c  # K head in sT0:sT1, V head in sT2:sT3
+    return c  # K head in sT0:sT1, V head in sT2:sT3, nt in sT8
 
 
 def load_args():
@@ -386,8 +443,9 @@ def dma_fills(slot_reg, earliest0=2, spacing=6):
     """the 8 LDS-DMA pieces of the stream's next tile into slot slot_reg
     (K pieces 4w..4w+3 of the K image, V pieces of the V image; one M0 write
     per four), the stream switch before and the advance after"""
-    sw = Fill([I("s_cmp_eq_u32", sDIDX, sNT), I("s_cselect_b64", sDK, sNXK, sDK),
-               I("s_cselect_b64", sDV, sNXV, sDV), I("s_cselect_b32", sDIDX, sNXIDX, sDIDX)],
+    sw = Fill([I("s_cmp_eq_u32", sDIDX, sDNT), I("s_cselect_b64", sDK, sNXK, sDK),
+               I("s_cselect_b64", sDV, sNXV, sDV), I("s_cselect_b32", sDIDX, sNXIDX, sDIDX),
+               I("s_cselect_b32", sDNT, sNXNT, sDNT)],
               2, earliest=earliest0 - 1, tag="dmasw")
     fills = [sw]
     prev = sw
@@ -458,15 +516,36 @@ def exps_all(X, also_or=False):
     return c
 
 
+def mask_tile(tile):
+    """causal, straight line (prologue and rare path): scores of the tile
+    whose index is in SGPR `tile` with key > row + off set to -inf.  Lane
+    (g, i) holds key 64 tile + 16 kb + 4 g + r of row q0 + 16 qb + i: masked
+    iff 16 (kb - qb) + r > lim = q0 + 64 (off - tile) + i - 4 g"""
+    lim = T(37)
+    c = [I("s_sub_u32", sT7, sOFFT, tile), I("s_lshl_b32", sT7, sT7, 6), I("s_add_u32", sT7, sT7, sCQ0),
+         I("v_add_u32", lim, sT7, VI), I("v_lshlrev_b32", T(36), 2, VG), I("v_sub_u32", lim, lim, T(36))]
+    for qb in range(4):
+        for kb in range(4):
+            for r in range(4):
+                c += [I("v_cmp_gt_i32_e32", VCC, 16 * (kb - qb) + r, lim),
+                      I("v_cndmask_b32_e32", S_(kb, qb)[r], S_(kb, qb)[r], NINF[0], VCC)]
+    return c
+
+
 # ---------------------------------------------------------------- program
 
 
 class Gen:
-    def __init__(self, ndef=4, budget=8, dma_spacing=6, tag="%=", stamp=False):
+    """the whole kernel program (list of Ins); causal=True builds the
+    bottom-right-masked kernel (attn_fwd_v13c)"""
+
+    def __init__(self, ndef=4, budget=8, dma_spacing=6, tag="%=", stamp=False, causal=False):
         self.ndef, self.budget, self.dma_spacing, self.tag = ndef, budget, dma_spacing, tag
         self.stamp = stamp  # diagnostic build: s_memtime / s_memrealtime at entry and exit
+        self.causal = causal
         self.prog = []
-        self.stats = {}
+        self.sites = []  # (site id, rare block name, return label)
+        self.uid = 0
 
     def L(self, name):
         return f"v13_{name}_{self.tag}"
@@ -474,27 +553,21 @@ class Gen:
     def emit(self, c):
         self.prog.extend(c)
 
+    def new_uid(self):
+        self.uid += 1
+        return self.uid
+
     # ---- init ------------------------------------------------------------
     def init(self, in_kernarg, in_wg, in_wave):
         e = self.emit
-        e([I("s_mov_b64", sKA, in_kernarg), I("s_mov_b32", sL, in_wg), I("s_mov_b32", sWAVE, in_wave)])
-        e(load_args())
-        a = lambda n: ARG(AI[n])  # noqa: E731
-        # persistent scalars (xr/c/muoff/G/tbk/tbv are dwords 40.. -> second load)
-        # dwords 40..47 into s88..s95 for the copies below, then the block
-        # arguments (dwords 0..39) again
-        e([I("s_load_dwordx8", S(88, 8), sKA, 160), I("s_waitcnt", "lgkmcnt(0)")])
-        e([I("s_mov_b32", sXR, S(88)), I("s_mov_b32", sC, S(89)), I("s_mov_b32", sMUOFF, S(90)),
-           I("s_mov_b32", sG, S(91)), I("s_mov_b32", sTBK, S(92)), I("s_mov_b32", sTBV, S(93))])
-        e(load_args())
-        e([I("s_mov_b32", sNT, a("nt")), I("s_mov_b32", sNQ, a("nq")), I("s_mov_b32", sNBLK, a("nblocks")),
-           I("s_lshl_b32", sWKOFF, sWAVE, 12)])
-        if self.stamp:
-            # STAMP: lanes 0-3 of v217 = entry s_memtime / s_memrealtime, lane 8
-            # = this wave's record index (workgroup x 4 + wave)
-            e([I("s_memtime", S(96, 2)), I("s_memrealtime", S(98, 2)), I("s_waitcnt", "lgkmcnt(0)")])
-            e([I("v_writelane_b32", STAMPV, S(96 + k), k) for k in range(4)])
-            e([I("s_lshl_b32", sT6, sL, 2), I("s_add_u32", sT6, sT6, sWAVE), I("v_writelane_b32", STAMPV, sT6, 8)])
+        e([I("s_mov_b64", sKA, in_kernarg), I("s_mov_b32", sL, in_wg), I("s_lshl_b32", sWKOFF, in_wave, 12)])
+        # dwords 40..47 (kn, vn, c, muoff, tbk, tbv, stamp) into s88..s95 first
+        e([I("s_load_dwordx8", S(88, 8), sKA, 4 * AI["kn"])])
+        if self.causal:
+            e([I("s_load_dword", sOFFT, sKA, 4 * AI["offt"])])
+        e([I("s_waitcnt", "lgkmcnt(0)")])
+        kn, vn = S(88), S(89)
+        e([I("s_mov_b32", sC, S(90)), I("s_mov_b32", sTBK, S(92)), I("s_mov_b32", sTBV, S(93))])
         # lane constants
         e([I("v_mbcnt_lo_u32_b32", LANE, -1, 0), I("v_mbcnt_hi_u32_b32", LANE, -1, LANE),
            I("v_and_b32", VI, 15, LANE), I("v_lshrrev_b32", VG, 4, LANE)])
@@ -517,24 +590,39 @@ class Gen:
         for j in range(4):
             # K piece pc = 4w + j: rowbase 16((pc>>1)&3) + 8(pc&1), chbase 8(pc>>3)
             # V piece: rowbase 8(pc&7), chbase 8(pc>>3)
-            e([I("s_lshl_b32", sT2, sWAVE, 2), I("s_add_u32", sT2, sT2, j),             # pc
+            e([I("s_lshr_b32", sT2, sWKOFF, 10), I("s_add_u32", sT2, sT2, j),           # pc = 4 wave + j
                I("s_lshr_b32", sT3, sT2, 1), I("s_and_b32", sT3, sT3, 3), I("s_lshl_b32", sT3, sT3, 4),
                I("s_and_b32", sT4, sT2, 1), I("s_lshl_b32", sT4, sT4, 3), I("s_add_u32", sT3, sT3, sT4),  # K rowbase
                I("s_and_b32", sT4, sT2, 7), I("s_lshl_b32", sT4, sT4, 3),               # V rowbase
                I("s_lshr_b32", sT5, sT2, 3), I("s_lshl_b32", sT5, sT5, 7),              # 16 * chbase
                I("s_sub_u32", sT5, sT5, 1024 * j)])
-            for (rb, st, dst) in ((sT3, a("kn"), DMAK(j)), (sT4, a("vn"), DMAV(j))):
+            for (rb, st, dst) in ((sT3, kn, DMAK(j)), (sT4, vn, DMAV(j))):
                 e([I("v_add_u32", t[5], rb, t[2]), I("v_mul_lo_u32", t[5], t[5], st),
                    I("v_add_u32", t[5], t[5], t[3]), I("v_add_u32", dst, sT5, t[5])])
-        # ones selector, slots
+        e(load_args())
+        if self.stamp:
+            # STAMP: lanes 0-3 of v217 = entry s_memtime / s_memrealtime, lane 8
+            # = this wave's record index (workgroup x 4 + wave)
+            e([I("s_memtime", S(96, 2)), I("s_memrealtime", S(98, 2)), I("s_waitcnt", "lgkmcnt(0)")])
+            e([I("v_writelane_b32", STAMPV, S(96 + k), k) for k in range(4)])
+            e([I("s_lshl_b32", sT6, sL, 2), I("s_lshr_b32", sT7, sWKOFF, 12), I("s_add_u32", sT6, sT6, sT7),
+               I("v_writelane_b32", STAMPV, sT6, 8)])
+        # ones selector, ring slots, causal mask operands
         e([I("v_mov_b32", ONES[k], BF16_ONES) for k in range(4)])
         e([I("s_mov_b32", sS0, 0), I("s_mov_b32", sSP1, SLOT), I("s_mov_b32", sSP2, 2 * SLOT),
            I("s_mov_b32", sSM1, 4 * SLOT)])
+        if self.causal:
+            e([I("v_mov_b32", NINF[k], 0xFF800000) for k in range(4)])
+            # diagonal block: key 4g + r of the block masked above query i
+            e([I("v_lshlrev_b32", T(0), 2, VG)])
+            for r in range(4):
+                e([I("v_add_u32", T(1), r, T(0)), I("v_cmp_lt_i32_e32", VCC, VI, T(1)),
+                   I("v_cndmask_b32_e32", TRI[r], 0, NINF[0], VCC)])
 
     # ---- per-block scalar setup -----------------------------------------
     def q_offsets(self, q0, qh):
         """QOFF(qb) = min(q0 + 16 qb + i, Nq - 1) * qn + 16 g; Q loads"""
-        c = [I("s_sub_u32", sT0, sNQ, 1)]
+        c = [I("s_sub_u32", sT0, ARG(AI["nq"]), 1)]
         for qb in range(4):
             c += [I("v_add_u32", T(0), q0, VI), I("v_add_u32", T(0), 16 * qb, T(0)),
                   I("v_min_u32", T(0), sT0, T(0)), I("v_mul_lo_u32", T(0), T(0), ARG(AI["qn"])),
@@ -544,53 +632,52 @@ class Gen:
                 c.append(I("global_load_dwordx4", Q_(qb, ds), QOFF(qb), qh, mods=f"offset:{64 * ds}"))
         return c
 
-    def next_params(self):
-        """sHASN = L + G < nblocks; if so the next block's params into sNQH,
-        sNOH, sNQ0, its K / V heads into sNXK / sNXV with sNXIDX = 0; else
-        the stream parks on the current block's last tile (sNXK = head + (nt
-        - 1) tile, sNXIDX = nt - 1).  Expects the current block's K / V heads
-        in sT0:sT1 / sT2:sT3 ... passed through sS registers by the caller."""
-        raise NotImplementedError
-
     def block_setup_first(self):
         """first block: params, DMA tiles 0 and 1, Q loads, next-block params"""
         e = self.emit
-        e(block_params(sL))                          # current -> sNQH, sNOH, sNQ0, K/V heads in sT0.. / sT2..
-        e([I("s_mov_b64", sCOH, sNOH), I("s_mov_b32", sCQ0, sNQ0),
-           I("s_mov_b64", sDK, S(sT0.i, 2)), I("s_mov_b64", sDV, S(sT2.i, 2)), I("s_mov_b32", sDIDX, 0)])
+        e(block_params(sL, self.causal, self.new_uid()))
+        e([I("s_mov_b64", sCOH, sNOH), I("s_mov_b32", sCQ0, sNQ0), I("s_mov_b32", sNT, sT8),
+           I("s_mov_b64", sDK, S(sT0.i, 2)), I("s_mov_b64", sDV, S(sT2.i, 2)), I("s_mov_b32", sDIDX, 0),
+           I("s_mov_b32", sDNT, sT8)])
         e(self.q_offsets(sNQ0, sNQH))
         e(self._next_params())
         e(dma_now(sS0))
         e(dma_now(sSP1))
 
     def _next_params(self):
-        """(the stream pointer sDK / sDV is at some tile of the current
-        block with sDIDX its index: the current block's head is sDK - sDIDX
-        tiles)"""
-        skip = self.L(f"nonext{len(self.prog)}")
-        c = [I("s_add_u32", sT2, sL, sG), I("s_cmp_lt_u32", sT2, sNBLK), I("s_cselect_b32", sHASN, 1, 0)]
-        # parking place: the current block's last tile = sDK + (nt - 1 - sDIDX)
-        # tiles (signed: -1 when nt = 2 and both tiles were already issued)
+        """sHASN = L + G < nblocks; if so the next block's params into sNQH,
+        sNOH, sNQ0, its K / V heads into sNXK / sNXV with sNXIDX = 0 and its
+        tile count in sNXNT; else the stream parks on the current block's
+        last tile (sNXK = its address, sNXIDX = nt - 1, sNXNT = nt).  The
+        stream pointer sDK / sDV is at tile sDIDX of the current block."""
+        skip = self.L(f"nonext{self.new_uid()}")
+        c = [I("s_add_u32", sT2, sL, ARG(AI["G"])), I("s_cmp_lt_u32", sT2, ARG(AI["nblocks"])),
+             I("s_cselect_b32", sHASN, 1, 0)]
+        # parking place: sDK + (nt - 1 - sDIDX) tiles (signed: -1 when nt = 2
+        # and both tiles were already issued)
         c += [I("s_sub_u32", sT4, sNT, 1), I("s_sub_u32", sT4, sT4, sDIDX)]
         for (dst, src, tb) in ((sNXK, sDK, sTBK), (sNXV, sDV, sTBV)):
             c += [I("s_mul_i32", sT5, sT4, tb), I("s_ashr_i32", sT3, sT5, 31),
                   I("s_add_u32", dst[0], src[0], sT5), I("s_addc_u32", dst[1], src[1], sT3)]
-        c += [I("s_sub_u32", sNXIDX, sNT, 1)]
+        c += [I("s_sub_u32", sNXIDX, sNT, 1), I("s_mov_b32", sNXNT, sNT)]
         c += [I("s_cmp_eq_u32", sHASN, 0), I("s_cbranch_scc1", skip)]
-        # the next block's index in s100 (block_params reads it first, then
-        # uses the register as division scratch)
-        c += [I("s_add_u32", S(100), sL, sG)]
-        c += block_params(S(100))
-        c += [I("s_mov_b64", sNXK, S(sT0.i, 2)), I("s_mov_b64", sNXV, S(sT2.i, 2)), I("s_mov_b32", sNXIDX, 0)]
+        # the next block's index in s101 (block_params reads it first)
+        c += [I("s_add_u32", sT7, sL, ARG(AI["G"]))]
+        c += block_params(sT7, self.causal, self.new_uid())
+        c += [I("s_mov_b64", sNXK, S(sT0.i, 2)), I("s_mov_b64", sNXV, S(sT2.i, 2)), I("s_mov_b32", sNXIDX, 0),
+              I("s_mov_b32", sNXNT, sT8)]
         c += [label(skip)]
         return c
 
     # ---- the tile loop ---------------------------------------------------
     def block_body(self):
-        """O, l, mu zero; tile 0 (QK, exact max, P); the step loop; the tail;
-        the epilogue; the walk to the next block"""
+        """O, l zero; tile 0 (QK, exact max, P); the step loop; the tail; the
+        epilogue; the walk to the next block"""
         e, Lb = self.emit, self.L
         e([label(Lb("common"))])
+        e([I("s_load_dword", sT8, sKA, 4 * AI["muoff"])])
+        if self.causal:
+            e([I("s_lshr_b32", sTD, sCQ0, 6), I("s_add_u32", sTD, sTD, sOFFT)])  # the wave's diagonal tile
         e([I("v_accvgpr_write_b32", A(k), 0) for k in range(128)])
         e([I("v_mov_b32", L_(qb)[r], 0) for qb in range(4) for r in range(4)])
         e([I("v_mov_b32", ACC(0), 0), I("v_mov_b32", ACC(1), 0)])
@@ -602,10 +689,12 @@ class Gen:
         body, left = schedule(qk_mfmas(), fills, self.budget)
         e(body)
         e(drain(left, 64))
+        if self.causal:
+            e(mask_tile(0))
         # exact row max -> mu = max * c + muoff; P(0) into state 0
         for qb in range(4):
             e(row_max(qb, T(20 + qb), T(30), T(31)))
-            e([I("v_mul_f32", T(20 + qb), sC, T(20 + qb)), I("v_add_f32", MU(qb), sMUOFF, T(20 + qb))])
+            e([I("v_mul_f32", T(20 + qb), sC, T(20 + qb)), I("v_add_f32", MU(qb), sT8, T(20 + qb))])
         e(exps_all(0))
         # tile 1 landed (tile 2 in flight): K(1) fragments
         e([I("s_waitcnt", "vmcnt(8)"), I("s_barrier"), I("v_add_u32", VKA, sSP1, VKL)])
@@ -613,9 +702,9 @@ class Gen:
         e([I("s_mov_b32", sT, 1)])
         # steps t = 1 .. nt-1, two per iteration (P states 1 / 0)
         e([label(Lb("loop"))])
-        self.step(1)
+        self.step_dispatch(1)
         e([I("s_add_u32", sT, sT, 1), I("s_cmp_ge_u32", sT, sNT), I("s_cbranch_scc1", Lb("tail1"))])
-        self.step(0)
+        self.step_dispatch(0)
         e([I("s_add_u32", sT, sT, 1), I("s_cmp_lt_u32", sT, sNT), I("s_cbranch_scc1", Lb("loop"))])
         # tails: the last tile T = nt - 1 is in state (T & 1)
         self.tail(0)
@@ -629,14 +718,42 @@ class Gen:
         sl = slice_list()
         return sl[len(sl) - self.ndef:], sl[:len(sl) - self.ndef]
 
-    def step(self, X):
+    def step_dispatch(self, X):
+        """causal: the wave's tiles below its diagonal run the plain step,
+        the diagonal tile the masked one, tiles past it the all -inf one (the
+        workgroup's last row sees them; this wave's rows do not)"""
+        if not self.causal:
+            self.step(X, None)
+            return
+        e, Lb = self.emit, self.L
+        u = self.new_uid()
+        n, d, cont = Lb(f"plain{u}"), Lb(f"diag{u}"), Lb(f"stepped{u}")
+        e([I("s_cmp_lt_u32", sT, sTD), I("s_cbranch_scc1", n), I("s_cmp_eq_u32", sT, sTD),
+           I("s_cbranch_scc1", d)])
+        self.step(X, "beyond")
+        e([I("s_branch", cont), label(n)])
+        self.step(X, None)
+        e([I("s_branch", cont), label(d)])
+        self.step(X, "diag")
+        e([label(cont)])
+
+    def check(self, Xc, rare_block):
+        """the defer-max check of the tile in P state Xc (some P >= 2: bit 14
+        of a bf16 half); the rare block returns to the label emitted here"""
+        e, Lb = self.emit, self.L
+        k = len(self.sites)
+        ret = Lb(f"ret{k}")
+        self.sites.append((k, rare_block, ret))
+        e([I("v_and_b32", T(37), 0x40004000, ACC(Xc)), I("v_cmp_ne_u32_e32", VCC, 0, T(37)),
+           I("s_mov_b32", sRET, k), I("s_cbranch_vccnz", Lb(rare_block)), label(ret)])
+
+    def step(self, X, mask):
         """step t (state X = t & 1): QK(t) || the deferred slices of t-1,
         tile t+2's DMA, V(t-1) d-blocks 0-1, softmax(t); the defer-max check
         of t-1; barrier; PV(t-1) + row sums || K(t+1), V(t-1) d-blocks 2-7,
         softmax(t)"""
-        e, Lb = self.emit, self.L
+        e = self.emit
         Xp = 1 - X
-        site = f"s{X}"
         dfr, now = self.deferred()
         e(rotate_slots())
         e([I("v_add_u32", VVA, sSM1, VVL)])
@@ -661,7 +778,7 @@ class Gen:
             if f.tag == "or" and not any(d.tag == "or" for d in f.deps):
                 f.deps.append(z)
         fills += f_now
-        body, left = schedule(qk_mfmas(), fills, self.budget)
+        body, left = schedule(qk_mfmas(mask), fills, self.budget)
         e(body)
         # everything of tile t-1 must be done before its check
         pend_prev = [f for f in left if f in f_def or f.tag.startswith("dma")]
@@ -674,8 +791,7 @@ class Gen:
         e(drain(pend_prev, 63))
         left = [f for f in left if f.gap is None]
         # ---- defer-max check of tile t-1
-        e([I("v_and_b32", T(37), 0x40004000, ACC(Xp)), I("v_cmp_ne_u32_e32", VCC, 0, T(37)),
-           I("s_cbranch_vccnz", Lb(f"rare_{site}")), label(Lb(f"ret_{site}"))])
+        self.check(Xp, f"rare_s{Xp}")
         e([I("s_waitcnt", "vmcnt(8)"), I("s_barrier")])
         # ---- PV phase (gaps numbered on from the QK phase's 64, so the
         # leftover softmax keeps its dependency distances)
@@ -695,21 +811,17 @@ class Gen:
         body, left = schedule(pv, fills, self.budget, gap_offset=B0)
         e(body)
         e(drain(left, B0 + 71))
-        self.rare_sites = getattr(self, "rare_sites", [])
-        self.rare_sites.append((site, Xp, True))
 
     def tail(self, X):
         """last tile T (state X): its deferred slices, its check, PV(T) with
         the next block's Q loads beside it"""
-        e, Lb = self.emit, self.L
-        site = f"t{X}"
+        e = self.emit
         dfr, _ = self.deferred()
         e(rotate_slots())
         e([I("v_add_u32", VVA, sSM1, VVL)])
         f_def, _, _ = softmax_fills(X, dfr, lambda qb, kb: 0, ytag=0)
         e(drain(f_def, 0))
-        e([I("v_and_b32", T(37), 0x40004000, ACC(X)), I("v_cmp_ne_u32_e32", VCC, 0, T(37)),
-           I("s_cbranch_vccnz", Lb(f"rare_{site}")), label(Lb(f"ret_{site}"))])
+        self.check(X, f"rare_t{X}")
         e(v_reads(0) + v_reads(1))
         fills = []
         for db in range(2, 8):
@@ -721,8 +833,6 @@ class Gen:
         body, left = schedule(pv_mfmas(X), fills, self.budget)
         e(body)
         e(drain(left, 71))
-        self.rare_sites = getattr(self, "rare_sites", [])
-        self.rare_sites.append((site, X, False))
 
     # ---- epilogue ---------------------------------------------------------
     def epilogue(self):
@@ -747,26 +857,27 @@ class Gen:
                     e([I("v_cvt_pk_bf16_f32", T(w + 2 * half), T(28), T(29)),
                        I("v_cvt_pk_bf16_f32", T(w + 2 * half + 1), T(30), T(31))])
                 e([I("v_permlane16_swap_b32", T(w), T(w + 2)), I("v_permlane16_swap_b32", T(w + 1), T(w + 3))])
-            e([I("v_cmp_gt_u32_e32", VCC, sNQ, T(24)), I("s_and_saveexec_b64", S(sT2.i, 2), VCC)])
+            e([I("v_cmp_gt_u32_e32", VCC, ARG(AI["nq"]), T(24)), I("s_and_saveexec_b64", S(sT2.i, 2), VCC)])
             for dbp in range(4):
                 e([I("global_store_dwordx4", OOFF(qb), V(T(4 * dbp).i, 4), sCOH, mods=f"offset:{64 * dbp}")])
             e([I("s_mov_b64", EXEC, S(sT2.i, 2))])
         # next block
         e([I("s_cmp_eq_u32", sHASN, 0), I("s_cbranch_scc1", Lb("end"))])
-        e([I("s_add_u32", sL, sL, sG), I("s_mov_b64", sCOH, sNOH), I("s_mov_b32", sCQ0, sNQ0)])
+        e([I("s_add_u32", sL, sL, ARG(AI["G"])), I("s_mov_b64", sCOH, sNOH), I("s_mov_b32", sCQ0, sNQ0),
+           I("s_mov_b32", sNT, sNXNT)])
         e(load_args())
         e(self._next_params())
         e([I("s_branch", Lb("common"))])
 
     # ---- rare path --------------------------------------------------------
-    def rare(self, site, X, has_next):
+    def rare(self, name, X, has_next):
         """tile t (state X) raised some row's max by >= 8 (log2): recompute
         S(t) from K(t) in slot sSM1, mu_new = max(mu, rowmax * c + muoff),
         rescale O and l by exp2(mu - mu_new), redo P(t); then S(t+1) (slot
-        sS0) and every P(t+1) so far, ACC(t+1) from them"""
+        sS0) and every P(t+1) so far, ACC(t+1) from them.  Returns to the
+        site whose id is in sRET."""
         e, Lb = self.emit, self.L
-        e([label(Lb(f"rare_{site}"))])
-        e([I("s_nop", 7), I("s_nop", 7)])
+        e([label(Lb(name)), I("s_nop", 7), I("s_nop", 7), I("s_load_dword", sT1, sKA, 4 * AI["muoff"])])
         for tile_slot, Xs, redo in ((sSM1, X, True), (sS0, 1 - X, has_next)):
             if not redo:
                 continue
@@ -774,11 +885,17 @@ class Gen:
             e([I("ds_read_b128", K_(kb, ds), T(36), mods=f"offset:{512 * (ds & 1) + 2048 * kb + 8192 * (ds >> 1)}")
                for ds in range(4) for kb in range(4)])
             e(qk_mfmas())
+            if self.causal:
+                if Xs == X:  # tile t = sT - 1
+                    e([I("s_sub_u32", sT0, sT, 1)])
+                    e(mask_tile(sT0))
+                else:
+                    e(mask_tile(sT))
             if Xs == X:
                 for qb in range(4):
                     m = T(20 + qb)
                     e(row_max(qb, m, T(30), T(31)))
-                    e([I("v_mul_f32", m, sC, m), I("v_add_f32", m, sMUOFF, m), I("v_max_f32", m, m, MU(qb)),
+                    e([I("v_mul_f32", m, sC, m), I("v_add_f32", m, sT1, m), I("v_max_f32", m, m, MU(qb)),
                        I("v_sub_f32", T(24), MU(qb), m), I("v_exp_f32", T(24), T(24)), I("v_mov_b32", MU(qb), m)])
                     for db in range(8):
                         for r in range(4):
@@ -790,7 +907,11 @@ class Gen:
             else:
                 e([I("v_mov_b32", ACC(Xs), 0)])
                 e(exps_all(Xs, also_or=True))
-        e([I("v_mov_b32", ACC(X), 0), I("s_nop", 4), I("s_branch", Lb(f"ret_{site}"))])
+        e([I("v_mov_b32", ACC(X), 0), I("s_nop", 4)])
+        for k, blk, ret in self.sites:
+            if blk == name:
+                e([I("s_cmp_eq_u32", sRET, k), I("s_cbranch_scc1", ret)])
+        e([I("s_endpgm")])  # unreachable: every site that branches here is listed above
 
     # ---- whole kernel -----------------------------------------------------
     def build(self, in_kernarg="%0", in_wg="%1", in_wave="%2"):
@@ -809,7 +930,8 @@ class Gen:
                I("s_mov_b64", EXEC, 0xFF), I("global_store_dword", T(0), STAMPV, S(96, 2)),
                I("s_mov_b64", EXEC, -1), I("s_waitcnt", "vmcnt(0)")])
         e([I("s_branch", Lb("exit"))])
-        for site, X, has_next in self.rare_sites:
-            self.rare(site, X, has_next)
+        for X in (0, 1):
+            self.rare(f"rare_s{X}", X, True)
+            self.rare(f"rare_t{X}", X, False)
         e([label(Lb("exit"))])
         return self.prog

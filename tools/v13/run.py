@@ -23,8 +23,21 @@ def magic(d: int):
     return m, l
 
 
-def args_for(qa, ka, va, oa, B, H, Hkv, Nq, Nk, strides_el, scale, G, muoff=7.0):
-    """the 48-dword argument block; strides_el: 12 element strides
+def pair_walk(nb, qblocks, G):
+    """(walk, lgG8, lghq, per, hx): the causal pair walk where it tiles the
+    grid exactly (launch_attn_v13's rule), else the remap walk"""
+    bh = nb // qblocks
+    w = G // 8
+    hq = qblocks // 2
+    pw2 = lambda x: x > 0 and (x & (x - 1)) == 0  # noqa: E731
+    if (G < nb and qblocks % 2 == 0 and hq > 0 and w % hq == 0 and bh % 8 == 0 and (bh // 8) % (w // hq) == 0
+            and nb % G == 0 and (nb // G) % 2 == 0 and pw2(w) and pw2(hq)):
+        return 1, w.bit_length() - 1, hq.bit_length() - 1, w // hq, bh // 8
+    return 2, 0, 0, 0, 0
+
+
+def args_for(qa, ka, va, oa, B, H, Hkv, Nq, Nk, strides_el, scale, G, muoff=7.0, causal=False):
+    """the argument block (ARG_LAYOUT); strides_el: 12 element strides
     (qb, qh, qn, kb, kh, kn, vb, vh, vn, ob, oh, on) of bf16 tensors"""
     st = [2 * s for s in strides_el]
     qblocks = -(-Nq // 256)
@@ -41,11 +54,12 @@ def args_for(qa, ka, va, oa, B, H, Hkv, Nq, Nk, strides_el, scale, G, muoff=7.0)
     d["magq"], d["shq"] = magic(qblocks)
     d["magh"], d["shh"] = magic(H)
     d["magg"], d["shg"] = magic(group)
-    d["H"], d["group"] = H, group
-    if nblocks < 8:
-        d["xq"], d["xr"] = 0, 8
-    else:
-        d["xq"], d["xr"] = nblocks >> 3, nblocks & 7
+    d["H"] = H
+    if causal:
+        walk, lg8, lghq, per, hx = pair_walk(nblocks, qblocks, G)
+        d["cw"] = walk | (lg8 << 8) | (lghq << 16) | (per << 24)
+        d["hx"] = hx
+        d["offt"] = (Nk - Nq) // 64
     d["c"] = struct.unpack("<I", struct.pack("<f", scale * 1.4426950408889634))[0]
     d["muoff"] = struct.unpack("<I", struct.pack("<f", muoff))[0]
     d["G"] = G
@@ -66,13 +80,14 @@ def program(**kw):
     return _PROG[key]
 
 
-def run(q, k, v, scale=None, grid=None, muoff=7.0, layout="bhsd", **kw):
+def run(q, k, v, scale=None, grid=None, muoff=7.0, layout="bhsd", causal=False, **kw):
     """q [B,H,Nq,128], k / v [B,Hkv,Nk,128] float arrays (rounded to bf16) ->
     O [B,H,Nq,128] float32 from the emulated kernel.  layout 'bshd' stores
     the tensors as [B,S,H,D] (strided heads)."""
     B, H, Nq, D = q.shape
     Hkv, Nk = k.shape[1], k.shape[2]
     assert D == 128 and Nk % 64 == 0 and Nk >= 128
+    assert not causal or (Nk - Nq >= 0 and (Nk - Nq) % 64 == 0)
     scale = 1.0 / math.sqrt(D) if scale is None else scale
     heap = E.Heap()
 
@@ -95,9 +110,12 @@ def run(q, k, v, scale=None, grid=None, muoff=7.0, layout="bhsd", **kw):
     qblocks = -(-Nq // 256)
     nb = B * H * qblocks
     G = nb if grid is None else grid
-    args = args_for(qa, ka, va, oa, B, H, Hkv, Nq, Nk, list(sq) + list(sk) + list(sv) + list(so), scale, G, muoff)
+    if causal and pair_walk(nb, qblocks, G)[0] != 1:
+        G = nb  # the remap walk runs one block per workgroup
+    args = args_for(qa, ka, va, oa, B, H, Hkv, Nq, Nk, list(sq) + list(sk) + list(sv) + list(so), scale, G, muoff,
+                    causal)
     kaddr = heap.alloc(args.nbytes, args.tobytes())
-    prog = program(**kw)
+    prog = program(causal=causal, **kw)
     em = E.Emu(prog, heap)
     for wg in range(G):
         waves = []
