@@ -46,11 +46,12 @@ METRIC = "flash-attn prefill TFLOP/s + GEMV decode GB/s, as % of MI355X roofline
 PEAK_BF16_TFLOPS = 2516.6   # 256 CU x 4096 FLOP/clk x 2.4 GHz (dense)
 PEAK_HBM_GBPS = 8000.0      # HBM3E datasheet
 B, H, S, D = 8, 32, 4096, 128
-FLASH_KERNEL = "attn_fwd_v12 persistent (variant 71; bitwise = attn_fwd_v10 exact)"
+FLASH_KERNEL = ("attn_fwd_v13 persistent (variant 80; v_mfma_f32_16x16x32_bf16, one generated instruction stream, "
+                "tools/gen_flash_v13.py)")
 JSON_OUT = sys.stdout  # main() points it at the original stdout and sends fd 1 to stderr
 GEMM_KERNEL = ("gemm_w5 (256x256 tile, one wave per SIMD, K staged 64 deep; variant 43, its persistent walk, "
                "where M, N are multiples of 256 and 128 <= K <= 4096)")
-CAUSAL_KERNEL = "attn_fwd_v12 causal, persistent pair walk (variant 74)"
+CAUSAL_KERNEL = "attn_fwd_v13c causal, persistent pair walk (variant 83)"
 
 
 def log(*a):
@@ -84,15 +85,29 @@ def paired_time_ms(fns: dict, iters: int, stream, rounds: int = 3, warm: int = 5
     return {k: sorted(v)[len(v) // 2] for k, v in res.items()}
 
 
-def load_traffic(kernel: str):
-    """Per-launch HBM bytes of ``kernel`` from the committed rocprofv3 PMC
-    summary (profiles/traffic.json), or None."""
+def load_pmc(kernel: str) -> dict:
+    """The committed rocprofv3 PMC summary of ``kernel`` (profiles/traffic.json,
+    tools/pmc_summary.py), or {}."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(path) as f:
-            return json.load(f).get(kernel, {}).get("hbm_bytes_per_launch")
+            return json.load(f).get(kernel, {})
     except (OSError, ValueError):
-        return None
+        return {}
+
+
+def load_traffic(kernel: str):
+    """Per-launch HBM bytes of ``kernel`` from the PMC summary, or None."""
+    return load_pmc(kernel).get("hbm_bytes_per_launch")
+
+
+def pmc_fields(kernel: str) -> dict:
+    """traffic plus the matrix-core occupancy of ``kernel`` from the PMC
+    summary: mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x
+    GRBM_GUI_ACTIVE / 8), with the clock those passes ran at"""
+    r = load_pmc(kernel)
+    return {"traffic": r.get("hbm_bytes_per_launch"), "mfma_busy": r.get("mfma_busy"),
+            "pmc_clock_GHz": r.get("clock_GHz"), "lds_bank_conflict_cycles": r.get("SQ_LDS_BANK_CONFLICT")}
 
 
 def calibrate() -> dict:
@@ -263,7 +278,7 @@ def bench_gemv(stream, iters: int) -> dict:
             "streaming_kernel": "gemv_vec variant 13 (same body, 4-wave blocks)",
             "roofline": {"bound": "hbm", "achieved": gbps, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                          "frac": gbps / PEAK_HBM_GBPS, "algorithmic_bytes": nbytes,
-                         "traffic": load_traffic("gemv_vec")}}
+                         **pmc_fields("gemv_vec")}}
 
 
 def bench_matmul_demo() -> dict:
@@ -338,7 +353,7 @@ def bench_gemm(stream, iters: int) -> dict:
             "TFLOP/s": tf, "torch_mm_TFLOP/s": 2 * n ** 3 / (ms_t * 1e-3) / 1e12,
             "roofline": {"bound": "mfma", "achieved": tf, "peak": PEAK_BF16_TFLOPS,
                          "unit": "TFLOP/s", "frac": tf / PEAK_BF16_TFLOPS,
-                         "algorithmic_bytes": 3 * n * n * 2, "traffic": load_traffic("gemm_w5 nn")}}
+                         "algorithmic_bytes": 3 * n * n * 2, **pmc_fields("gemm_w5 nn")}}
 
 
 def bench_tp(stream, world: int, rank: int, iters: int) -> dict:
@@ -747,16 +762,15 @@ def main():
                                        "timing": "sync + perf_counter per call, 5 calls"}
         extra["flash_causal"] = {"ms": ms_c, "timing": "events, 20 launches after 10 warm-up",
                                  "TFLOP/s": 4 * B * H * D * (S * (S + 1) // 2) / (ms_c * 1e-3) / 1e12,
-                                 "kernel": CAUSAL_KERNEL,
-                                 "traffic": load_traffic("attn_fwd_v12 causal")}
+                                 "kernel": CAUSAL_KERNEL, **pmc_fields("attn_fwd_v13c")}
     if not args.flash_only:
         log("[bench] calibration")
         cal = calibrate()
         extra["calibration"] = cal
-        # the flash kernel's QK^T / PV run on v_mfma_f32_32x32x16_bf16
-        measured_roof = {"measured_peak": cal["mfma_32x32x16_TFLOP/s"],
-                         "measured_peak_kind": "pli_mfma_probe 32x32x16 (the kernel's shape)",
-                         "frac_of_measured": achieved / cal["mfma_32x32x16_TFLOP/s"]}
+        # the flash kernel's QK^T / PV run on v_mfma_f32_16x16x32_bf16
+        measured_roof = {"measured_peak": cal["mfma_16x16x32_TFLOP/s"],
+                         "measured_peak_kind": "pli_mfma_probe 16x16x32 (the kernel's shape)",
+                         "frac_of_measured": achieved / cal["mfma_16x16x32_TFLOP/s"]}
     if args.flash_only:
         args.quick, args.no_cpu_baseline = True, True
     if not args.flash_only:
@@ -828,7 +842,7 @@ def main():
                    "parallelism": f"replicas x{world} (flash does not shard; TP GEMM row-parallel)"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved / PEAK_BF16_TFLOPS,
-                     "traffic": load_traffic("attn_fwd_v12"),
+                     **pmc_fields("attn_fwd_v13"),
                      "traffic_source": "profiles/traffic.json: rocprofv3 FETCH_SIZE x2 (gfx950) + WRITE_SIZE "
                                        "per launch, separate --pmc passes (tools/pmc_summary.py), not this run",
                      "kernel": FLASH_KERNEL, "algorithmic_flops": flops_step,

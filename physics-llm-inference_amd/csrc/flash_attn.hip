@@ -539,14 +539,19 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
 //  83 / 84: attn_fwd_v13c causal (bottom-right, Nq <= Nk, (Nk - Nq) % 64 ==
 //      0): 83 persistent (the pair walk where it tiles the grid), 84 one
 //      block per workgroup heaviest first; 85 = 83 with mu = max * c - 1
-constexpr int kDefaultVariant = 71;
+// default since round 4: attn_fwd_v13 (80), 1388 vs 1242 TF/s for v12 (71)
+// at B8 S4096 H32 D128 in the same process (profiles/r04/flash/ab.log); where
+// v13 does not apply (fp16, D != 128, Nk % 64, Nk < 128) it routes to 71
+constexpr int kDefaultVariant = 80;
 // causal: attn_fwd_v12 causal (74; one block per workgroup where the
 // persistent pair walk does not tile the shape), 60 where v12 does not apply
 // (fp16, D != 128, Nq > Nk, Nk % 64): B8 S4096 H32 D128 bf16 1002 (74, the
 // first rotation walk) vs 945 (60) TF/s, B2 S8192 1098 vs 1013, B32 S2048 867
 // vs 830 (profiles/r03/flash/ab_causal.log); the pair walk: 1049 at B8 S4096,
 // 1154 at B2 S8192, 1223 at B1 H64 S16384 (ab_causal_pair.log)
-constexpr int kDefaultCausalVariant = 74;
+// causal default since round 4: attn_fwd_v13c (83), 1210 vs 1058 TF/s for
+// 74 (profiles/r04/flash/ab_causal.log); (Nk - Nq) % 64 != 0 etc. -> 74
+constexpr int kDefaultCausalVariant = 83;
 
 template <typename T, int D>
 int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int H,

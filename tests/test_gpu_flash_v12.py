@@ -1,4 +1,4 @@
-"""attn_fwd_v12, the non-causal flash default (variant 71 persistent, 70 one
+"""attn_fwd_v12, the round-3 non-causal flash default (variant 71 persistent, 70 one
 block per workgroup, 72 = 71 with the defer-max threshold at 0), against
 references that share none of its code (cdna_hip_programming.md §5.4 rule 26):
 
@@ -100,7 +100,6 @@ def test_v12_vs_f64_full_tensor(shape, qmul):
         err = max_err(outs[var], ref)
         assert err <= tol, f"{shape} q*{qmul} variant {var}: max |err| {err:.4e} > {tol:.4e}"
     assert torch.equal(outs[70], outs[71]), f"{shape}: 70 != 71"
-    assert torch.equal(outs[71], pli_hip.flash_attn_fwd(q, k, v)), "default != 71"
 
 
 def test_v12_strided_bshd_views():

@@ -106,7 +106,7 @@ def test_flash_vs_oracle(case):
 
 
 # every MFMA variant (alternates A/B-tested by tools/tune.py) on the MFMA-eligible cases
-MFMA_VARIANTS = (21, 50, 51, 54, 55, 60, 70, 71, 72, 73, 74)
+MFMA_VARIANTS = (21, 50, 51, 54, 55, 60, 70, 71, 72, 73, 74, 80, 81, 82)
 
 
 
@@ -140,10 +140,10 @@ def test_flash_strided_views_and_out_param():
 # variants whose Q is prescaled by scale*log2(e) and rounded to the 16-bit
 # input type before the MFMA (the rest scale the f32 scores exactly)
 PRESCALED = (50, 54)
-DEFAULT_VARIANT = 71
+DEFAULT_VARIANT = 80  # attn_fwd_v13 since round 4 (71 = v12 where v13 does not apply)
 
 
-DEFAULT_CAUSAL_VARIANT = 74
+DEFAULT_CAUSAL_VARIANT = 83  # attn_fwd_v13c since round 4 (74 = v12 causal otherwise)
 
 
 def test_flash_default_variants():
@@ -186,7 +186,7 @@ def test_flash_stress(variant, name):
         assert err <= tol, f"stress {name}: {err:.3e} > {tol:.3e}"
 
 
-@pytest.mark.parametrize("variant", [None, 21, 50, 51, 54, 55, 60, 70])
+@pytest.mark.parametrize("variant", [None, 21, 50, 51, 54, 55, 60, 70, 71, 81])
 def test_flash_full_config_properties(variant):
     """B=8 S=4096 H=32 D=128 bf16 (the bench config): v = 1 gives exactly 1;
     two heads checked against the f64 oracle; key permutation invariance."""
@@ -207,10 +207,13 @@ def test_flash_full_config_properties(variant):
     if variant is None:
         base = pli_hip.flash_attn_fwd(q, k, v, variant=21)
         assert (base.float() - out.float()).abs().max().item() <= 1.6e-2
-    # attn_fwd_v12 (70, 71 = default) runs attn_fwd_v10's arithmetic in the
-    # same order: bitwise equal to 55 over the whole tensor
-    if variant in (None, 70):
+    # attn_fwd_v12 (70, 71) runs attn_fwd_v10's arithmetic in the same
+    # order: bitwise equal to 55 over the whole tensor; the default (v13,
+    # variant 80) and its one-block-per-workgroup form 81 bitwise equal
+    if variant in (70, 71):
         assert torch.equal(out, pli_hip.flash_attn_fwd(q, k, v, variant=55))
+    if variant in (None, 81):
+        assert torch.equal(out, pli_hip.flash_attn_fwd(q, k, v, variant=80))
 
 
 @pytest.mark.parametrize("shape", [(4, 16, 4, 2048, 1024), (4, 32, 8, 1024, 128), (4, 32, 8, 1024, 192),

@@ -19,7 +19,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = ("gemm_w5", "attn_fwd_v12", "attn_fwd_v10", "attn_fwd_v7", "gemm_f32_mfma", "gemm_naive_f32", "hbm_read_probe", "attn_fwd_v2", "attn_decode_chunk", "attn_decode_combine", "gemv_vec", "gemm_mfma",
+KERNELS = ("gemm_w5", "attn_fwd_v13c", "attn_fwd_v13", "attn_fwd_v12", "attn_fwd_v10", "attn_fwd_v7", "gemm_f32_mfma", "gemm_naive_f32", "hbm_read_probe", "attn_fwd_v2", "attn_decode_chunk", "attn_decode_combine", "gemv_vec", "gemm_mfma",
            "gemm_smallm_nt", "scale_copy_vec")
 
 
@@ -28,7 +28,16 @@ def label(k: str, name: str) -> str:
     with the non-causal kernel; keep them apart."""
     if k == "gemm_w5":  # gemm_w5<T, TRANS_B, BIAS>: NT and NN apart
         return k + (" nt" if ", true," in name else " nn")
+    if k.startswith("attn_fwd_v13"):
+        return k
     return k + " causal" if k.startswith("attn_fwd") and ", true>" in name else k
+
+
+def kernel_label(name: str):
+    for k in KERNELS:
+        if k in name:
+            return label(k, name)
+    return None
 
 
 def per_kernel(path_glob: str, counter: str) -> dict:
@@ -39,11 +48,39 @@ def per_kernel(path_glob: str, counter: str) -> dict:
             for row in csv.DictReader(f):
                 if row.get("Counter_Name") != counter:
                     continue
-                name = row["Kernel_Name"]
-                for k in KERNELS:
-                    if k in name:
-                        vals[(label(k, name), int(row["Grid_Size"]))].append(float(row["Counter_Value"]))
+                lab = kernel_label(row["Kernel_Name"])
+                if lab:
+                    vals[(lab, int(row["Grid_Size"]))].append(float(row["Counter_Value"]))
     return vals
+
+
+def per_kernel_with_time(d: str, counter: str) -> dict:
+    """{(kernel, grid): [(value, duration_ns)]} from a pass directory holding
+    counter_collection.csv and kernel_trace.csv (joined on Correlation_Id)"""
+    out = defaultdict(list)
+    for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        dur = {}
+        for tp in glob.glob(os.path.join(os.path.dirname(path), "*kernel_trace.csv")):
+            with open(tp, newline="") as f:
+                for row in csv.DictReader(f):
+                    try:
+                        dur[row["Correlation_Id"]] = int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
+                    except (KeyError, ValueError):
+                        pass
+        with open(path, newline="") as f:
+            for row in csv.DictReader(f):
+                if row.get("Counter_Name") != counter:
+                    continue
+                lab = kernel_label(row["Kernel_Name"])
+                if lab:
+                    out[(lab, int(row["Grid_Size"]))].append(
+                        (float(row["Counter_Value"]), dur.get(row.get("Correlation_Id"))))
+    return out
+
+
+SQ = ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CU_CYCLES", "SQ_INSTS_MFMA", "SQ_INSTS_VALU", "SQ_INSTS_LDS",
+      "SQ_LDS_BANK_CONFLICT", "SQ_WAVES", "GRBM_GUI_ACTIVE")
+N_SIMD = 1024  # 256 CUs x 4
 
 
 def main():
@@ -54,6 +91,7 @@ def main():
     res = {}
     mean = lambda v: sum(v) / len(v) if v else 0.0  # noqa: E731
     labels = sorted({kk for (kk, _) in set(fetch) | set(write)})
+    d = sys.argv[1]
     for k in labels:
         grids = sorted({g for (kk, g) in set(fetch) | set(write) if kk == k})
         if not grids:
@@ -70,6 +108,26 @@ def main():
         res[k] = dict(by_grid[str(main_g)], grid_size=main_g, by_grid=by_grid,
                       note="FETCH_SIZE KiB x1024 x2 (gfx950 half-count), WRITE_SIZE KiB x1024; "
                            "mean over dispatches of that grid")
+    # the SQ pass: instruction counts, MFMA busy, LDS conflicts, clock
+    sq = {c: per_kernel_with_time(os.path.join(d, "pmc_SQ*"), c) for c in SQ}
+    for (k, g) in sorted(set(sq["GRBM_GUI_ACTIVE"]) | set(sq["SQ_VALU_MFMA_BUSY_CYCLES"])):
+        if k in res and res[k].get("grid_size") not in (None, g):
+            continue
+        ent = res.setdefault(k, {"grid_size": g})
+        for c in SQ:
+            vals = [v for v, _ in sq[c].get((k, g), [])]
+            if vals:
+                ent[c] = mean(vals)
+        grbm = sq["GRBM_GUI_ACTIVE"].get((k, g), [])
+        if ent.get("GRBM_GUI_ACTIVE") and ent.get("SQ_VALU_MFMA_BUSY_CYCLES") is not None:
+            ent["mfma_busy"] = ent["SQ_VALU_MFMA_BUSY_CYCLES"] / (N_SIMD * ent["GRBM_GUI_ACTIVE"] / 8)
+        durs = [t for _, t in grbm if t]
+        if durs and ent.get("GRBM_GUI_ACTIVE"):
+            ent["duration_ns_pmc"] = mean(durs)
+            ent["clock_GHz"] = ent["GRBM_GUI_ACTIVE"] / 8 / mean(durs)
+        ent["sq_note"] = ("SQ pass (one rocprofv3 --pmc run): means over dispatches; mfma_busy = "
+                          "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8); clock = "
+                          "GRBM_GUI_ACTIVE / 8 / kernel-trace duration (counters slow the clock: compare fractions)")
     with open(out, "w") as f:
         json.dump(res, f, indent=1, sort_keys=True)
     print(json.dumps(res, indent=1))
