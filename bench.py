@@ -101,13 +101,19 @@ def load_traffic(kernel: str):
     return load_pmc(kernel).get("hbm_bytes_per_launch")
 
 
-def pmc_fields(kernel: str) -> dict:
+def pmc_fields(kernel: str, kernel_ms: float | None = None) -> dict:
     """traffic plus the matrix-core occupancy of ``kernel`` from the PMC
     summary: mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x
-    GRBM_GUI_ACTIVE / 8), with the clock those passes ran at"""
+    GRBM_GUI_ACTIVE / 8), with the clock those passes ran at.  busy is a
+    ratio of cycles, so with this run's kernel time it gives the clock the
+    unprofiled kernel ran at: (busy cycles per SIMD / busy) / kernel time."""
     r = load_pmc(kernel)
-    return {"traffic": r.get("hbm_bytes_per_launch"), "mfma_busy": r.get("mfma_busy"),
-            "pmc_clock_GHz": r.get("clock_GHz"), "lds_bank_conflict_cycles": r.get("SQ_LDS_BANK_CONFLICT")}
+    out = {"traffic": r.get("hbm_bytes_per_launch"), "mfma_busy": r.get("mfma_busy"),
+           "pmc_clock_GHz": r.get("clock_GHz"), "lds_bank_conflict_cycles": r.get("SQ_LDS_BANK_CONFLICT")}
+    cyc, busy = r.get("mfma_busy_cycles_per_simd"), r.get("mfma_busy")
+    if kernel_ms and cyc and busy:
+        out["implied_clock_GHz"] = cyc / busy / (kernel_ms * 1e6)
+    return out
 
 
 def calibrate() -> dict:
@@ -353,7 +359,7 @@ def bench_gemm(stream, iters: int) -> dict:
             "TFLOP/s": tf, "torch_mm_TFLOP/s": 2 * n ** 3 / (ms_t * 1e-3) / 1e12,
             "roofline": {"bound": "mfma", "achieved": tf, "peak": PEAK_BF16_TFLOPS,
                          "unit": "TFLOP/s", "frac": tf / PEAK_BF16_TFLOPS,
-                         "algorithmic_bytes": 3 * n * n * 2, **pmc_fields("gemm_w5 nn")}}
+                         "algorithmic_bytes": 3 * n * n * 2, **pmc_fields("gemm_w5 nn", ms)}}
 
 
 def bench_tp(stream, world: int, rank: int, iters: int) -> dict:
@@ -762,7 +768,7 @@ def main():
                                        "timing": "sync + perf_counter per call, 5 calls"}
         extra["flash_causal"] = {"ms": ms_c, "timing": "events, 20 launches after 10 warm-up",
                                  "TFLOP/s": 4 * B * H * D * (S * (S + 1) // 2) / (ms_c * 1e-3) / 1e12,
-                                 "kernel": CAUSAL_KERNEL, **pmc_fields("attn_fwd_v13c")}
+                                 "kernel": CAUSAL_KERNEL, **pmc_fields("attn_fwd_v13c", ms_c)}
     if not args.flash_only:
         log("[bench] calibration")
         cal = calibrate()
@@ -842,7 +848,7 @@ def main():
                    "parallelism": f"replicas x{world} (flash does not shard; TP GEMM row-parallel)"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved / PEAK_BF16_TFLOPS,
-                     **pmc_fields("attn_fwd_v13"),
+                     **pmc_fields("attn_fwd_v13", kernel_ms),
                      "traffic_source": "profiles/traffic.json: rocprofv3 FETCH_SIZE x2 (gfx950) + WRITE_SIZE "
                                        "per launch, separate --pmc passes (tools/pmc_summary.py), not this run",
                      "kernel": FLASH_KERNEL, "algorithmic_flops": flops_step,

@@ -1,6 +1,7 @@
 // attn_fwd_v13: flash-attention forward on v_mfma_f32_16x16x32_bf16
-// (reference ch06/flash_attention.py:14-74; gfx950, bf16, D = 128,
-// non-causal, Nk a multiple of 64 and >= 128; other cases take v12 / v10).
+// (reference ch06/flash_attention.py:14-74; gfx950, bf16, D = 128, Nk a
+// multiple of 64 and >= 128; causal -- bottom-right, (Nk - Nq) % 64 == 0 --
+// as the second program attn_fwd_v13c; other cases take v12 / v10).
 //
 // One wave per SIMD, 64 query rows per wave (4 q-blocks of 16), persistent
 // workgroups of 4 waves walking 256-row blocks.  The body is ONE generated
@@ -20,13 +21,17 @@
 #include <cstring>
 
 #include "flash_v7.h"
+#ifdef PLI_V13_AB_HEADER  // timing-only A/B builds (tools/build_v13_ab.sh)
+#include PLI_V13_AB_HEADER
+#else
 #include "flash_v13_asm.h"
+#endif
 #include "pli_common.h"
 
 namespace pli {
 namespace {
 
-// kernel argument block: 48 dwords, the layout of tools/v13/kernel.py
+// kernel argument block: 64 dwords, the layout of tools/v13/kernel.py
 // ARG_LAYOUT (the body reads it through the kernarg pointer)
 struct V13Args {
     uint32_t w[64];

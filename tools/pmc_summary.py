@@ -16,6 +16,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
@@ -26,8 +27,9 @@ KERNELS = ("gemm_w5", "attn_fwd_v13c", "attn_fwd_v13", "attn_fwd_v12", "attn_fwd
 def label(k: str, name: str) -> str:
     """Causal instantiations (template flag ``true``) share the name prefix
     with the non-causal kernel; keep them apart."""
-    if k == "gemm_w5":  # gemm_w5<T, TRANS_B, BIAS>: NT and NN apart
-        return k + (" nt" if ", true," in name else " nn")
+    if k == "gemm_w5":  # gemm_w5<T, TRANS_B, BIAS, ...>: NT and NN apart by the first flag
+        m = re.search(r"gemm_w5<[^,<>]+, (true|false)", name)
+        return k + (" nt" if m and m.group(1) == "true" else " nn")
     if k.startswith("attn_fwd_v13"):
         return k
     return k + " causal" if k.startswith("attn_fwd") and ", true>" in name else k
@@ -121,8 +123,11 @@ def main():
         grbm = sq["GRBM_GUI_ACTIVE"].get((k, g), [])
         if ent.get("GRBM_GUI_ACTIVE") and ent.get("SQ_VALU_MFMA_BUSY_CYCLES") is not None:
             ent["mfma_busy"] = ent["SQ_VALU_MFMA_BUSY_CYCLES"] / (N_SIMD * ent["GRBM_GUI_ACTIVE"] / 8)
+            # per-SIMD MFMA busy cycles per launch: with a live kernel time the
+            # bench turns this into the unprofiled clock (busy is a cycle ratio)
+            ent["mfma_busy_cycles_per_simd"] = ent["SQ_VALU_MFMA_BUSY_CYCLES"] / N_SIMD
         durs = [t for _, t in grbm if t]
-        if durs and ent.get("GRBM_GUI_ACTIVE"):
+        if durs and ent.get("GRBM_GUI_ACTIVE") and mean(durs) >= 1e5:  # (short launches: dispatch dominates)
             ent["duration_ns_pmc"] = mean(durs)
             ent["clock_GHz"] = ent["GRBM_GUI_ACTIVE"] / 8 / mean(durs)
         ent["sq_note"] = ("SQ pass (one rocprofv3 --pmc run): means over dispatches; mfma_busy = "

@@ -1,6 +1,7 @@
 """attn_fwd_v13: flash-attention forward on v_mfma_f32_16x16x32_bf16, one
 wave per SIMD, 64 query rows per wave (reference ch06/flash_attention.py:14-74;
-gfx950, bf16, D = 128, non-causal, Nk a multiple of 64 and >= 128).
+gfx950, bf16, D = 128, Nk a multiple of 64 and >= 128; causal -- bottom-right,
+(Nk - Nq) % 64 == 0 -- as the second program, Gen(causal=True)).
 
 The whole kernel body is one generated instruction stream (this module
 builds it; tools/gen_flash_v13.py prints it into csrc/flash_v13_asm.h, and
@@ -190,6 +191,12 @@ class Fill:
 
 LDS_GAP = 1024  # LDS bytes per wave per 16-cycle gap (256 B/clk per CU, 4 waves)
 
+# timing-only A/B knobs (tools/build_v13_ab.sh; Gen(abl=..., dma_cost=...)):
+# ABL "dma" drops the LDS-DMA loads, "exp" turns v_exp_f32 into v_mov_b32,
+# "check" drops the defer-max branch -- results wrong, timing only
+ABL = set()
+DMA_COST = 8
+
 
 def schedule(mfmas, fills, budget=8, gap_offset=0, lds_gap=LDS_GAP):
     """place fills into the gaps after each MFMA (gap k follows MFMA k);
@@ -327,8 +334,12 @@ def softmax_fills(X, slices, earliest_of, deadline_of=None, ytag=0, prev_cv=None
                   tag="fma", hard=dl is not None)
         f1 = Fill(I("v_fma_f32", y1, s[2 * hh + 1], sC, Neg(MU(qb))), 4, deps=deps, sep=0, earliest=ea,
                   deadline=dl, tag="fma", hard=dl is not None)
-        e0 = Fill(I("v_exp_f32", y0, y0), 8, trans=True, deps=[f0], sep=1, tag="exp")
-        e1 = Fill(I("v_exp_f32", y1, y1), 8, trans=True, deps=[f1], sep=1, tag="exp")
+        if "exp" in ABL:
+            e0 = Fill(I("v_mov_b32", y0, y0), 4, deps=[f0], sep=1, tag="exp")
+            e1 = Fill(I("v_mov_b32", y1, y1), 4, deps=[f1], sep=1, tag="exp")
+        else:
+            e0 = Fill(I("v_exp_f32", y0, y0), 8, trans=True, deps=[f0], sep=1, tag="exp")
+            e1 = Fill(I("v_exp_f32", y1, y1), 8, trans=True, deps=[f1], sep=1, tag="exp")
         fm = f1
         w = P_(X, qb, kb >> 1)[2 * (kb & 1) + hh]
         cv = Fill(I("v_cvt_pk_bf16_f32", w, y0, y1), 4, deps=[e0, e1], sep=1, tag="cvt")
@@ -457,8 +468,9 @@ def dma_fills(slot_reg, earliest0=2, spacing=6):
             ins += [I("s_add_u32", M0, slot_reg, sWKOFF), I("s_add_u32", M0, M0, VIMG)]
         src = sDK if j < 4 else sDV
         off = DMAK(j) if j < 4 else DMAV(j - 4)
-        ins.append(I("global_load_lds_dwordx4", off, src, mods=f"offset:{1024 * (j % 4)}"))
-        f = Fill(ins, 8, deps=[prev], sep=1 if j else 0, earliest=earliest0 + spacing * j, tag="dma")
+        if "dma" not in ABL:
+            ins.append(I("global_load_lds_dwordx4", off, src, mods=f"offset:{1024 * (j % 4)}"))
+        f = Fill(ins, DMA_COST, deps=[prev], sep=1 if j else 0, earliest=earliest0 + spacing * j, tag="dma")
         fills.append(f)
         prev = f
     adv = Fill([I("s_add_u32", sDK[0], sDK[0], sTBK), I("s_addc_u32", sDK[1], sDK[1], 0),
@@ -539,8 +551,12 @@ class Gen:
     """the whole kernel program (list of Ins); causal=True builds the
     bottom-right-masked kernel (attn_fwd_v13c)"""
 
-    def __init__(self, ndef=4, budget=8, dma_spacing=6, tag="%=", stamp=False, causal=False):
+    def __init__(self, ndef=4, budget=8, dma_spacing=6, tag="%=", stamp=False, causal=False, abl=(), dma_cost=8):
+        global DMA_COST
         self.ndef, self.budget, self.dma_spacing, self.tag = ndef, budget, dma_spacing, tag
+        ABL.clear()
+        ABL.update(abl)
+        DMA_COST = dma_cost
         self.stamp = stamp  # diagnostic build: s_memtime / s_memrealtime at entry and exit
         self.causal = causal
         self.prog = []
@@ -744,6 +760,9 @@ class Gen:
         k = len(self.sites)
         ret = Lb(f"ret{k}")
         self.sites.append((k, rare_block, ret))
+        if "check" in ABL:
+            e([label(ret)])
+            return
         e([I("v_and_b32", T(37), 0x40004000, ACC(Xc)), I("v_cmp_ne_u32_e32", VCC, 0, T(37)),
            I("s_mov_b32", sRET, k), I("s_cbranch_vccnz", Lb(rare_block)), label(ret)])
 
