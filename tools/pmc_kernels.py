@@ -18,6 +18,18 @@ sys.path[:0] = [os.path.join(ROOT, "physics-llm-inference_amd"), ROOT]
 import pli_hip  # noqa: E402
 
 N_LAUNCH = int(os.environ.get("PMC_LAUNCHES", "3"))
+if os.environ.get("PMC_SET") == "causal":
+    # causal walks side by side: 83 (pair walk, persistent) and 84 (one block
+    # per workgroup, heaviest first) -- told apart by their grid sizes
+    g = torch.Generator(device="cuda").manual_seed(0)
+    q, k, v = (torch.randn(8, 32, 4096, 128, device="cuda", dtype=torch.bfloat16, generator=g) for _ in range(3))
+    o = torch.empty_like(q)
+    for _ in range(N_LAUNCH):
+        for var in (83, 84):
+            pli_hip.flash_attn_fwd(q, k, v, out=o, causal=True, variant=var)
+    torch.cuda.synchronize()
+    print("pmc workload done", flush=True)
+    sys.exit(0)
 g = torch.Generator(device="cuda").manual_seed(0)
 B, H, S, D = 8, 32, 4096, 128
 q, k, v = (torch.randn(B, H, S, D, device="cuda", dtype=torch.bfloat16, generator=g) for _ in range(3))

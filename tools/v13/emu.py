@@ -422,6 +422,12 @@ class Emu:
         if op == "s_cmp_ge_u32":
             w.scc = int(g(o[0]) >= g(o[1]))
             return
+        if op == "s_cmp_gt_u32":
+            w.scc = int(g(o[0]) > g(o[1]))
+            return
+        if op == "s_cmp_le_u32":
+            w.scc = int(g(o[0]) <= g(o[1]))
+            return
         if op in ("s_cselect_b32", "s_cselect_b64"):
             return self.sset(w, o[0], g(o[1]) if w.scc else g(o[2]))
         if op == "s_and_saveexec_b64":

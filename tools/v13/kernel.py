@@ -193,7 +193,9 @@ LDS_GAP = 1024  # LDS bytes per wave per 16-cycle gap (256 B/clk per CU, 4 waves
 
 # timing-only A/B knobs (tools/build_v13_ab.sh; Gen(abl=..., dma_cost=...)):
 # ABL "dma" drops the LDS-DMA loads, "exp" turns v_exp_f32 into v_mov_b32,
-# "check" drops the defer-max branch -- results wrong, timing only
+# "check" drops the defer-max branch; in the step loop only: "kread" / "vread"
+# drop the K / V fragment reads, "barrier" the per-step barrier, "soft" the
+# softmax stream -- results wrong, timing only
 ABL = set()
 DMA_COST = 8
 
@@ -781,18 +783,23 @@ class Gen:
         # deferred slices of tile t-1 (they read S(., 3): before QK(t) overwrites it)
         dl = lambda qb, kb: 16 * qb + kb - 1  # noqa: E731
         f_def, cvd, last_or_prev = softmax_fills(Xp, dfr, lambda qb, kb: 0, dl, ytag=0)
+        if "soft" in ABL:
+            f_def = []
         fills += f_def
         fills += dma_fills(sSP2, earliest0=1, spacing=self.dma_spacing)
         # V(t-1) d-blocks 0, 1
         for db in (0, 1):
             for ins in v_reads(db):
-                fills.append(Fill(ins, 2, earliest=40 + 8 * db, tag="vread"))
+                if "vread" not in ABL:
+                    fills.append(Fill(ins, 2, earliest=40 + 8 * db, tag="vread"))
         # softmax(t), zero ACC(X) first
         z = Fill(I("v_mov_b32", ACC(X), 0), 4, tag="zero")
         fills.append(z)
         f_now, cvn, last_or = softmax_fills(X, now, lambda qb, kb: qk_done_gap(kb, qb) + 3, ytag=len(dfr),
                                             prev_cv=cvd)
         now_groups = softmax_fills.groups
+        if "soft" in ABL:
+            f_now, now_groups = [], []
         for f in f_now:
             if f.tag == "or" and not any(d.tag == "or" for d in f.deps):
                 f.deps.append(z)
@@ -811,18 +818,18 @@ class Gen:
         left = [f for f in left if f.gap is None]
         # ---- defer-max check of tile t-1
         self.check(Xp, f"rare_s{Xp}")
-        e([I("s_waitcnt", "vmcnt(8)"), I("s_barrier")])
+        e([I("s_waitcnt", "vmcnt(8)")] + ([] if "barrier" in ABL else [I("s_barrier")]))
         # ---- PV phase (gaps numbered on from the QK phase's 64, so the
         # leftover softmax keeps its dependency distances)
         B0 = 64
         fills = left
         ka = Fill(I("v_add_u32", VKA, sSP1, VKL), 4, earliest=B0, tag="kaddr")
         kr = [Fill(ins, 2, deps=[ka], sep=1, earliest=B0 + n // 2, deadline=B0 + 40, tag="kread")
-              for n, ins in enumerate(k_reads())]
+              for n, ins in enumerate(k_reads())] if "kread" not in ABL else []
         pv = pv_mfmas(Xp)
         # V d-block db (2..7) reads: after d-block db-3's MFMAs (same buffer), well before db's
         vr = []
-        for db in range(2, 8):
+        for db in range(2 if "vread" not in ABL else 8, 8):
             for ins in v_reads(db):
                 vr.append(Fill(ins, 2, earliest=B0 + (pv_first_gap(db - 3) + 9 if db >= 3 else 0),
                                deadline=B0 + pv_first_gap(db) - 6, tag="vread"))
