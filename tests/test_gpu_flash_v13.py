@@ -111,8 +111,10 @@ def test_v13_rescale_stress(name):
 
 
 # causal (bottom-right mask, (Nk - Nq) % 64 == 0): 83 persistent (pair walk
-# where it tiles the grid), 84 one block per workgroup heaviest first, 85 =
-# 83 with the rescale path at nearly every tile
+# where it tiles the grid; the second block of each pair streams its key
+# tiles in the reversed order of tools/v13/kernel.py Gen.tile_of), 84 one
+# block per workgroup heaviest first (forward order), 85 = 83 with the
+# rescale path at nearly every tile
 CAUSAL = [(4, 32, 8, 1024, 1024), (2, 32, 32, 2048, 2048), (2, 16, 4, 4096, 4096), (3, 40, 8, 1024, 1024),
           (2, 8, 2, 256, 512), (1, 4, 4, 128, 128), (1, 8, 8, 704, 768), (2, 4, 2, 320, 320)]
 
@@ -121,7 +123,9 @@ CAUSAL = [(4, 32, 8, 1024, 1024), (2, 32, 32, 2048, 2048), (2, 16, 4, 4096, 4096
 @pytest.mark.parametrize("shape", CAUSAL, ids=lambda s: "b{}h{}kv{}q{}k{}".format(*s))
 def test_v13_causal_vs_f64_full_tensor(shape, qmul):
     """Every output element of causal 83 / 84 / 85 against the f64 device
-    reference with the bottom-right mask; 83 and 84 bitwise equal."""
+    reference with the bottom-right mask; 83 and 84 agree to rounding (the
+    same arithmetic per tile, key tiles summed in another order where the
+    pair walk reverses a block)."""
     import pli_hip
     q, k, v = inputs(shape, sum(shape) % 991)
     q = q * qmul
@@ -132,7 +136,7 @@ def test_v13_causal_vs_f64_full_tensor(shape, qmul):
         outs[var] = pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=var)
         err = max_err(outs[var], ref)
         assert err <= tol, f"{shape} q*{qmul} causal variant {var}: max |err| {err:.4e} > {tol:.4e}"
-    assert torch.equal(outs[83], outs[84]), f"{shape}: 83 != 84"
+    assert_agree_to_rounding(outs[83], outs[84], v)
 
 
 def test_v13_causal_full_config_all_heads():

@@ -380,6 +380,13 @@ class Emu:
             r = g(o[1]) - g(o[2])
             w.scc = int(r < 0)
             return self.sset(w, o[0], r & M32)
+        if op == "s_subb_u32":
+            r = g(o[1]) - g(o[2]) - w.scc
+            w.scc = int(r < 0)
+            return self.sset(w, o[0], r & M32)
+        if op == "s_bitcmp1_b32":
+            w.scc = (g(o[0]) >> (g(o[1]) & 31)) & 1
+            return
         if op == "s_mul_i32":
             a, b = g(o[1]), g(o[2])
             a = a - (1 << 32) if a >= 1 << 31 else a

@@ -131,6 +131,7 @@ sNQH, sNOH, sNQ0, sNXNT, sTD, sDNT = S(28, 2), S(30, 2), S(32), S(33), S(34), S(
 sNXK, sNXV, sNXIDX, sT = S(36, 2), S(38, 2), S(40), S(41)
 sDK, sDV, sDIDX = S(42, 2), S(44, 2), S(46)
 sSM1, sS0, sSP1, sSP2, sHASN = S(47), S(48), S(49), S(50), S(51)
+sDIR = sHASN  # causal: the current block's stream order (1 = reversed), see block_params
 sT0, sT1, sT8, sRET = S(52), S(53), S(54), S(55)
 ARGS = 56  # block-parameter arguments: s56..s95 (dwords 0..39)
 
@@ -380,7 +381,7 @@ def mad64(out, base, x, st, y, st2):
     return c
 
 
-def block_params(sx, causal=False, uid=0):
+def block_params(sx, causal=False, uid=0, rev=0):
     """block index sx -> sNQH, sNOH (Q / O heads), sNQ0 (the wave's first
     row), sT8 (the block's key-tile count), the K head in sT0:sT1 (s52:s53)
     and the V head in s96:s97; needs the arguments in s56..s95.  sx is read
@@ -408,7 +409,8 @@ def block_params(sx, causal=False, uid=0):
     c += [I("s_mul_i32", sT2, sT5, QB), I("s_sub_u32", sT2, sT4, sT2)]
     if causal:
         # heaviest first: query height QB-1-r
-        c += [I("s_sub_u32", sT3, QB, 1), I("s_sub_u32", sT2, sT3, sT2), I("s_branch", done)]
+        c += [I("s_sub_u32", sT3, QB, 1), I("s_sub_u32", sT2, sT3, sT2)] + \
+            ([I("s_mov_b32", sRET, 0)] if rev else []) + [I("s_branch", done)]
         # the pair walk: x = l & 7, l8 = l >> 3, j = l8 >> lgG8, wg = l8 mod G8,
         # wgq = wg >> lghq, a = wg mod hq, bh = x hx + wgq + per (j >> 1),
         # qblk = j odd ? a : QB-1-a
@@ -423,11 +425,14 @@ def block_params(sx, causal=False, uid=0):
               I("s_lshr_b32", sT6, CW, 24), I("s_lshr_b32", sT7, sT4, 1), I("s_mul_i32", sT7, sT7, sT6),
               I("s_add_u32", sT2, sT2, sT7),
               I("s_sub_u32", sT6, QB, 1), I("s_sub_u32", sT6, sT6, sT5),
-              I("s_and_b32", sT4, sT4, 1), I("s_cselect_b32", sT4, sT5, sT6),
+              I("s_and_b32", sT4, sT4, 1)] + ([I("s_cselect_b32", sRET, 1, 0)] if rev else []) + [
+              I("s_cselect_b32", sT4, sT5, sT6),
               I("s_mov_b32", sT5, sT2), I("s_mov_b32", sT2, sT4), label(done)]
         # key tiles the block's last row sees: min(nt, 4 qblk + 4 + off / 64)
         c += [I("s_lshl_b32", sT8, sT2, 2), I("s_add_u32", sT8, sT8, 4), I("s_add_u32", sT8, sT8, sOFFT),
               I("s_min_u32", sT8, sT8, ARG(AI["nt"]))]
+        if rev:  # reversed order (the second block of a pair) needs 4 tiles
+            c += [I("s_cmp_ge_u32", sT8, 4), I("s_cselect_b32", sRET, sRET, 0)]
     else:
         c += [I("s_mov_b32", sT8, ARG(AI["nt"]))]
     # q0 = qblk * 256 + 64 * wave
@@ -441,7 +446,16 @@ def block_params(sx, causal=False, uid=0):
     c += mad64(sNOH, ARG(AI["o"], 2), sT4, ARG(AI["ob"], 2), sT3, ARG(AI["oh"], 2))
     c += mad64(S(sT0.i, 2), ARG(AI["k"], 2), sT4, ARG(AI["kb"], 2), sT5, ARG(AI["kh"], 2))
     c += mad64(S(sT2.i, 2), ARG(AI["v"], 2), sT4, ARG(AI["vb"], 2), sT5, ARG(AI["vh"], 2))
-    return c  # K head in sT0:sT1, V head in sT2:sT3, nt in sT8
+    if causal and rev:
+        # reversed block: the stream starts at tile nt - 4 (see Gen.tile_of);
+        # the order rides in bit 16 of the tile count
+        fwd = f"v13_fwd_{uid}_%="
+        c += [I("s_cmp_eq_u32", sRET, 0), I("s_cbranch_scc1", fwd),
+              I("s_sub_u32", sT4, sT8, 4),
+              I("s_mul_i32", sT5, sT4, sTBK), I("s_add_u32", sT0, sT0, sT5), I("s_addc_u32", sT1, sT1, 0),
+              I("s_mul_i32", sT5, sT4, sTBV), I("s_add_u32", sT2, sT2, sT5), I("s_addc_u32", sT3, sT3, 0),
+              I("s_or_b32", sT8, sT8, 0x10000), label(fwd)]
+    return c  # K head in sT0:sT1, V head in sT2:sT3, nt in sT8 (causal: | reversed << 16)
 
 
 def load_args():
@@ -452,7 +466,7 @@ def load_args():
 # ---------------------------------------------------------------- DMA
 
 
-def dma_fills(slot_reg, earliest0=2, spacing=6):
+def dma_fills(slot_reg, earliest0=2, spacing=6, rev=False):
     """the 8 LDS-DMA pieces of the stream's next tile into slot slot_reg
     (K pieces 4w..4w+3 of the K image, V pieces of the V image; one M0 write
     per four), the stream switch before and the advance after"""
@@ -475,17 +489,31 @@ def dma_fills(slot_reg, earliest0=2, spacing=6):
         f = Fill(ins, DMA_COST, deps=[prev], sep=1 if j else 0, earliest=earliest0 + spacing * j, tag="dma")
         fills.append(f)
         prev = f
-    adv = Fill([I("s_add_u32", sDK[0], sDK[0], sTBK), I("s_addc_u32", sDK[1], sDK[1], 0),
-                I("s_add_u32", sDV[0], sDV[0], sTBV), I("s_addc_u32", sDV[1], sDV[1], 0),
-                I("s_add_u32", sDIDX, sDIDX, 1)], 2, deps=[prev], sep=0, tag="dmaadv")
+    if rev:
+        # causal: sDIDX bit 16 = the streamed block's order.  Reversed, the
+        # positions 0..3 are tiles nt-4 .. nt-1 and position p >= 4 is tile
+        # nt-1-p: the step into position p is +1, -4 (p = 4) or -1 tiles
+        adv = Fill([I("s_add_u32", sDIDX, sDIDX, 1), I("s_and_b32", sT2, sDIDX, 0xFFFF),
+                    I("s_cmp_eq_u32", sT2, 4), I("s_cselect_b32", sT3, -4, -1),
+                    I("s_cmp_lt_u32", sT2, 4), I("s_cselect_b32", sT3, 1, sT3),
+                    I("s_bitcmp1_b32", sDIDX, 16), I("s_cselect_b32", sT3, sT3, 1),
+                    I("s_mul_i32", sT2, sT3, sTBK), I("s_ashr_i32", sT4, sT2, 31),
+                    I("s_add_u32", sDK[0], sDK[0], sT2), I("s_addc_u32", sDK[1], sDK[1], sT4),
+                    I("s_mul_i32", sT2, sT3, sTBV), I("s_ashr_i32", sT4, sT2, 31),
+                    I("s_add_u32", sDV[0], sDV[0], sT2), I("s_addc_u32", sDV[1], sDV[1], sT4)],
+                   8, deps=[prev], sep=0, tag="dmaadv")
+    else:
+        adv = Fill([I("s_add_u32", sDK[0], sDK[0], sTBK), I("s_addc_u32", sDK[1], sDK[1], 0),
+                    I("s_add_u32", sDV[0], sDV[0], sTBV), I("s_addc_u32", sDV[1], sDV[1], 0),
+                    I("s_add_u32", sDIDX, sDIDX, 1)], 2, deps=[prev], sep=0, tag="dmaadv")
     fills.append(adv)
     return fills
 
 
-def dma_now(slot_reg):
+def dma_now(slot_reg, rev=False):
     """the same as straight-line code (prologue of the first block)"""
     out = []
-    for f in dma_fills(slot_reg):
+    for f in dma_fills(slot_reg, rev=rev):
         out += f.ins
     return out
 
@@ -553,8 +581,13 @@ class Gen:
     """the whole kernel program (list of Ins); causal=True builds the
     bottom-right-masked kernel (attn_fwd_v13c)"""
 
-    def __init__(self, ndef=4, budget=8, dma_spacing=6, tag="%=", stamp=False, causal=False, abl=(), dma_cost=8):
+    def __init__(self, ndef=4, budget=8, dma_spacing=6, tag="%=", stamp=False, causal=False, abl=(), dma_cost=8,
+                 rev=True):
         global DMA_COST
+        # causal: the second block of each pair streams its tiles in the
+        # reversed order of tile_of (its 8 workgroups then read every K/V
+        # tile at the same time)
+        self.rev = causal and rev
         self.ndef, self.budget, self.dma_spacing, self.tag = ndef, budget, dma_spacing, tag
         ABL.clear()
         ABL.update(abl)
@@ -653,7 +686,18 @@ class Gen:
     def block_setup_first(self):
         """first block: params, DMA tiles 0 and 1, Q loads, next-block params"""
         e = self.emit
-        e(block_params(sL, self.causal, self.new_uid()))
+        e(block_params(sL, self.causal, self.new_uid(), rev=int(self.rev)))
+        if self.rev:
+            e([I("s_mov_b64", sCOH, sNOH), I("s_mov_b32", sCQ0, sNQ0), I("s_and_b32", sNT, sT8, 0xFFFF),
+               I("s_lshr_b32", sDIR, sT8, 16),
+               I("s_mov_b64", sDK, S(sT0.i, 2)), I("s_mov_b64", sDV, S(sT2.i, 2)),
+               I("s_and_b32", sDIDX, sT8, 0xFFFF0000), I("s_mov_b32", sDNT, sT8)])
+            e(self.q_offsets(sNQ0, sNQH))
+            # the stream is at position 2 when the next block's params are made
+            e(dma_now(sS0, rev=True))
+            e(dma_now(sSP1, rev=True))
+            e(self._next_params())
+            return
         e([I("s_mov_b64", sCOH, sNOH), I("s_mov_b32", sCQ0, sNQ0), I("s_mov_b32", sNT, sT8),
            I("s_mov_b64", sDK, S(sT0.i, 2)), I("s_mov_b64", sDV, S(sT2.i, 2)), I("s_mov_b32", sDIDX, 0),
            I("s_mov_b32", sDNT, sT8)])
@@ -669,6 +713,21 @@ class Gen:
         last tile (sNXK = its address, sNXIDX = nt - 1, sNXNT = nt).  The
         stream pointer sDK / sDV is at tile sDIDX of the current block."""
         skip = self.L(f"nonext{self.new_uid()}")
+        if self.rev:
+            # (causal) park: the tile of stream position 1 of the current
+            # block (the stream is at position 2: one tile back in either
+            # order), a one-tile stream that repeats
+            c = [I("s_sub_u32", sNXK[0], sDK[0], sTBK), I("s_subb_u32", sNXK[1], sDK[1], 0),
+                 I("s_sub_u32", sNXV[0], sDV[0], sTBV), I("s_subb_u32", sNXV[1], sDV[1], 0),
+                 I("s_mov_b32", sNXIDX, 0), I("s_mov_b32", sNXNT, 1),
+                 I("s_add_u32", sT2, sL, ARG(AI["G"])), I("s_cmp_ge_u32", sT2, ARG(AI["nblocks"])),
+                 I("s_cbranch_scc1", skip),
+                 I("s_add_u32", sT7, sL, ARG(AI["G"]))]
+            c += block_params(sT7, self.causal, self.new_uid(), rev=1)
+            c += [I("s_mov_b64", sNXK, S(sT0.i, 2)), I("s_mov_b64", sNXV, S(sT2.i, 2)),
+                  I("s_and_b32", sNXIDX, sT8, 0xFFFF0000), I("s_mov_b32", sNXNT, sT8)]
+            c += [label(skip)]
+            return c
         c = [I("s_add_u32", sT2, sL, ARG(AI["G"])), I("s_cmp_lt_u32", sT2, ARG(AI["nblocks"])),
              I("s_cselect_b32", sHASN, 1, 0)]
         # parking place: sDK + (nt - 1 - sDIDX) tiles (signed: -1 when nt = 2
@@ -703,11 +762,14 @@ class Gen:
         # tile 0: K(0) fragments, QK(0) with tile 2's DMA beside it
         e([I("v_add_u32", VKA, sS0, VKL)])
         e(k_reads())
-        fills = dma_fills(sSP2, earliest0=1, spacing=4)
+        fills = dma_fills(sSP2, earliest0=1, spacing=4, rev=self.rev)
         body, left = schedule(qk_mfmas(), fills, self.budget)
         e(body)
         e(drain(left, 64))
-        if self.causal:
+        if self.rev:
+            e(self.tile_of(sT0, 0))
+            e(mask_tile(sT0))
+        elif self.causal:
             e(mask_tile(0))
         # exact row max -> mu = max * c + muoff; P(0) into state 0
         for qb in range(4):
@@ -736,6 +798,19 @@ class Gen:
         sl = slice_list()
         return sl[len(sl) - self.ndef:], sl[:len(sl) - self.ndef]
 
+    def tile_of(self, dst, pos):
+        """causal: the key tile at stream position pos (SGPR or 0) of the
+        current block: pos, or reversed (sDIR) nt-4+pos for pos < 4 and
+        nt-1-pos after (the diagonal group first -- every wave's first tile
+        then has an unmasked key in every row -- then down to tile 0)"""
+        if not self.rev:
+            return [I("s_mov_b32", dst, pos)]
+        if pos == 0:
+            return [I("s_sub_u32", sT2, sNT, 4), I("s_cmp_eq_u32", sDIR, 0), I("s_cselect_b32", dst, 0, sT2)]
+        return [I("s_add_u32", sT2, sNT, pos), I("s_sub_u32", sT2, sT2, 4), I("s_sub_u32", sT3, sNT, 1),
+                I("s_sub_u32", sT3, sT3, pos), I("s_cmp_lt_u32", pos, 4), I("s_cselect_b32", sT3, sT2, sT3),
+                I("s_cmp_eq_u32", sDIR, 0), I("s_cselect_b32", dst, pos, sT3)]
+
     def step_dispatch(self, X):
         """causal: the wave's tiles below its diagonal run the plain step,
         the diagonal tile the masked one, tiles past it the all -inf one (the
@@ -746,7 +821,11 @@ class Gen:
         e, Lb = self.emit, self.L
         u = self.new_uid()
         n, d, cont = Lb(f"plain{u}"), Lb(f"diag{u}"), Lb(f"stepped{u}")
-        e([I("s_cmp_lt_u32", sT, sTD), I("s_cbranch_scc1", n), I("s_cmp_eq_u32", sT, sTD),
+        tl = sT
+        if self.rev:
+            e(self.tile_of(sT0, sT))
+            tl = sT0
+        e([I("s_cmp_lt_u32", tl, sTD), I("s_cbranch_scc1", n), I("s_cmp_eq_u32", tl, sTD),
            I("s_cbranch_scc1", d)])
         self.step(X, "beyond")
         e([I("s_branch", cont), label(n)])
@@ -786,7 +865,7 @@ class Gen:
         if "soft" in ABL:
             f_def = []
         fills += f_def
-        fills += dma_fills(sSP2, earliest0=1, spacing=self.dma_spacing)
+        fills += dma_fills(sSP2, earliest0=1, spacing=self.dma_spacing, rev=self.rev)
         # V(t-1) d-blocks 0, 1
         for db in (0, 1):
             for ins in v_reads(db):
@@ -888,9 +967,15 @@ class Gen:
                 e([I("global_store_dwordx4", OOFF(qb), V(T(4 * dbp).i, 4), sCOH, mods=f"offset:{64 * dbp}")])
             e([I("s_mov_b64", EXEC, S(sT2.i, 2))])
         # next block
-        e([I("s_cmp_eq_u32", sHASN, 0), I("s_cbranch_scc1", Lb("end"))])
-        e([I("s_add_u32", sL, sL, ARG(AI["G"])), I("s_mov_b64", sCOH, sNOH), I("s_mov_b32", sCQ0, sNQ0),
-           I("s_mov_b32", sNT, sNXNT)])
+        if self.rev:
+            e([I("s_add_u32", sT2, sL, ARG(AI["G"])), I("s_cmp_ge_u32", sT2, ARG(AI["nblocks"])),
+               I("s_cbranch_scc1", Lb("end"))])
+            e([I("s_add_u32", sL, sL, ARG(AI["G"])), I("s_mov_b64", sCOH, sNOH), I("s_mov_b32", sCQ0, sNQ0),
+               I("s_and_b32", sNT, sNXNT, 0xFFFF), I("s_lshr_b32", sDIR, sNXNT, 16)])
+        else:
+            e([I("s_cmp_eq_u32", sHASN, 0), I("s_cbranch_scc1", Lb("end"))])
+            e([I("s_add_u32", sL, sL, ARG(AI["G"])), I("s_mov_b64", sCOH, sNOH), I("s_mov_b32", sCQ0, sNQ0),
+               I("s_mov_b32", sNT, sNXNT)])
         e(load_args())
         e(self._next_params())
         e([I("s_branch", Lb("common"))])
@@ -912,8 +997,13 @@ class Gen:
                for ds in range(4) for kb in range(4)])
             e(qk_mfmas())
             if self.causal:
-                if Xs == X:  # tile t = sT - 1
+                if Xs == X:  # tile at position sT - 1
                     e([I("s_sub_u32", sT0, sT, 1)])
+                    if self.rev:
+                        e(self.tile_of(sT0, sT0))
+                    e(mask_tile(sT0))
+                elif self.rev:
+                    e(self.tile_of(sT0, sT))
                     e(mask_tile(sT0))
                 else:
                     e(mask_tile(sT))
