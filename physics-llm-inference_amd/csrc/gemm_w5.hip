@@ -11,15 +11,18 @@
 // At 64 k a row of A (and of NT-B) is one 128-B line.
 //
 // LDS: two 64 KiB slots (A image then B image, 32 KiB each), step S in slot
-// S % 2.  Per step (128 MFMAs, two k32 halves):
-//   half 0: MFMAs on the (S, h0) fragments; in their gaps the (S, h1)
-//           fragments are read (16 reads);
-//   s_waitcnt vmcnt(0) + barrier: step S+1's pieces landed everywhere, and
-//           every wave is done reading slot S (its h1 fragments were the last);
+// S % 2.  Per step (128 MFMAs, two k32 halves; W5_SPLIT, the default):
+//   half 0: MFMAs on the (S, h0) fragments; in the first 16 gaps the (S, h1)
+//           fragments are read; after gap 24 they are waited for and the
+//           workgroup meets (every wave is done reading slot S), and 5 of
+//           step S+2's 16 DMA pieces go into slot S in gaps 28-56;
+//   s_waitcnt vmcnt(5) + barrier: step S+1's pieces landed everywhere;
 //   half 1: MFMAs on (S, h1); in their gaps the (S+1, h0) fragments are read
-//           from slot S+1 and the 16 DMA pieces of step S+2 go into slot S.
-// One barrier per 64 k (w4v: one per 32 k).  Past the last step the DMA
-// re-loads the last step into the dead slot (no branch in the MFMA stream).
+//           from slot S+1 and the other 11 DMA pieces of step S+2 issue.
+// (W5_SPLIT 0, round 3: all 16 pieces in half 1 beside the reads, one
+// barrier per step; the split is bitwise the same and 0.5-2 % faster,
+// profiles/r04/gemm/ab_w5_split.log.)  Past the last step the DMA re-loads
+// the last step into the dead slot (no branch in the MFMA stream).
 //
 // LDS images (per slot):
 //   A, NT-B: [256 rows][64 k] (128-B rows), 16-B chunk c of row r at
@@ -56,6 +59,13 @@
 #endif
 #ifndef W5_ABL_DMA
 #define W5_ABL_DMA 0  // timing only: no DMA in the loop (results wrong)
+#endif
+#ifndef W5_SPLIT
+// 1: the (S, h1) fragments are read in half 0's first 16 gaps, a barrier
+// after gap 24 frees slot S, and 5 of step S+2's DMA pieces go into half 0's
+// later gaps (11 stay in half 1): the pieces spread over 1.6 halves and the
+// half-0 ones meet no fragment read
+#define W5_SPLIT 1
 #endif
 
 namespace pli {
@@ -260,24 +270,39 @@ __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A
     // RH, image offsets rsa / rsb) and DMA pieces J0 .. J0+NJ-1 of step ds in
     // their gaps
     constexpr int DSTART = W5_RING5 ? 2 : W5_DMA_START, DSTRIDE = W5_RING5 ? 8 : W5_DMA_STRIDE;
-    auto half = [&](auto p_tag, auto rd_tag, auto rh_tag, uint32_t rsa, uint32_t rsb, auto j0_tag, auto nj_tag, int ds)
-        __attribute__((always_inline)) {
+    // RS: gaps between fragment reads, DS0 / DSTR: first gap and spacing of
+    // the DMA pieces, BAR: the gap after which the reads are waited for and
+    // the workgroup meets (-1: none)
+    auto half_x = [&](auto p_tag, auto rd_tag, auto rh_tag, uint32_t rsa, uint32_t rsb, auto j0_tag, auto nj_tag,
+                      int ds, auto rs_tag, auto ds0_tag, auto dstr_tag, auto bar_tag) __attribute__((always_inline)) {
         constexpr int P = decltype(p_tag)::value, RH = decltype(rh_tag)::value;
         constexpr bool RD = decltype(rd_tag)::value;
         constexpr int J0 = decltype(j0_tag)::value, NJ = decltype(nj_tag)::value;
+        constexpr int RS = decltype(rs_tag)::value, DS0 = decltype(ds0_tag)::value;
+        constexpr int DSTR = decltype(dstr_tag)::value, BAR = decltype(bar_tag)::value;
         w5_sfor<64>([&](auto JJ) {
             constexpr int J = JJ, ni = J / 8, mi = J % 8;
             if constexpr (std::is_same_v<T, bf16_t>) w4v::mfma_bf16<J>(bop(fb[P][ni]), fa[P][mi]);
             else w4v::mfma_f16<J>(bop(fb[P][ni]), fa[P][mi]);
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (RD && J % W5_RD_STRIDE == 0 && J / W5_RD_STRIDE < 16)
-                frag_read(std::integral_constant<int, RH>{}, std::integral_constant<int, J / W5_RD_STRIDE>{}, rsa,
-                          rsb);
-            constexpr int D = J - DSTART;
-            if constexpr (!W5_ABL_DMA && D >= 0 && D % DSTRIDE == 0 && D / DSTRIDE < NJ)
-                dma_piece(std::integral_constant<int, J0 + D / DSTRIDE>{}, ds);
+            if constexpr (RD && J % RS == 0 && J / RS < 16)
+                frag_read(std::integral_constant<int, RH>{}, std::integral_constant<int, J / RS>{}, rsa, rsb);
+            if constexpr (J == BAR) {
+                frag_wait(std::integral_constant<int, RH>{});
+                __builtin_amdgcn_s_barrier();
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            constexpr int D = J - DS0;
+            if constexpr (!W5_ABL_DMA && D >= 0 && D % DSTR == 0 && D / DSTR < NJ)
+                dma_piece(std::integral_constant<int, J0 + D / DSTR>{}, ds);
             __builtin_amdgcn_sched_barrier(0);
         });
+    };
+    auto half = [&](auto p_tag, auto rd_tag, auto rh_tag, uint32_t rsa, uint32_t rsb, auto j0_tag, auto nj_tag, int ds)
+        __attribute__((always_inline)) {
+        half_x(p_tag, rd_tag, rh_tag, rsa, rsb, j0_tag, nj_tag, ds, std::integral_constant<int, W5_RD_STRIDE>{},
+               std::integral_constant<int, DSTART>{}, std::integral_constant<int, DSTRIDE>{},
+               std::integral_constant<int, -1>{});
     };
 
     // ---- prologue: accumulators 0, steps 0 and 1 in flight, (0, h0) fragments
@@ -310,6 +335,20 @@ __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A
         using N16 = std::integral_constant<int, 16>;
         // W5_RING5: step s+2's A pieces in half 0 (into B(s-1)'s dead ring
         // position), its B pieces in half 1 (into A(s)'s); else all 16 in half 1
+        if constexpr (W5_SPLIT) {
+            using I = std::integral_constant<int, 1>;
+            half_x(Z{}, std::true_type{}, O{}, img_off(s, 0), img_off(s, 1), N0{}, std::integral_constant<int, 5>{},
+                   s + 2, I{}, std::integral_constant<int, 28>{}, std::integral_constant<int, 7>{},
+                   std::integral_constant<int, 24>{});
+            asm volatile("s_waitcnt vmcnt(5)" ::: "memory");  // step s+1 landed (5 of s+2's pieces in flight)
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+            half_x(O{}, more_tag, Z{}, img_off(s + 1, 0), img_off(s + 1, 1), std::integral_constant<int, 5>{},
+                   std::integral_constant<int, 11>{}, s + 2, std::integral_constant<int, W5_RD_STRIDE>{}, N0{},
+                   std::integral_constant<int, 6>{}, std::integral_constant<int, -1>{});
+            if constexpr (MORE) frag_wait(Z{});
+            return;
+        }
         if constexpr (W5_RING5)
             half(Z{}, std::true_type{}, O{}, img_off(s, 0), img_off(s, 1), N0{}, N8{}, s + 2);
         else

@@ -18,6 +18,19 @@ sys.path[:0] = [os.path.join(ROOT, "physics-llm-inference_amd"), ROOT]
 import pli_hip  # noqa: E402
 
 N_LAUNCH = int(os.environ.get("PMC_LAUNCHES", "3"))
+if os.environ.get("PMC_SET") == "gemm8k":
+    # TP=1 8192^3 NT: gemm_w5 (one-tile form at K = 8192) beside hipBLASLt
+    n = 8192
+    g = torch.Generator(device="cuda").manual_seed(0)
+    a = torch.randn(n, n, device="cuda", dtype=torch.bfloat16, generator=g)
+    w = torch.randn(n, n, device="cuda", dtype=torch.bfloat16, generator=g)
+    c = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
+    for _ in range(N_LAUNCH):
+        pli_hip.gemm(a, w, trans_b=True, out=c)
+        torch.nn.functional.linear(a, w)
+    torch.cuda.synchronize()
+    print("pmc workload done", flush=True)
+    sys.exit(0)
 if os.environ.get("PMC_SET") == "causal":
     # causal walks side by side: 83 (pair walk, persistent) and 84 (one block
     # per workgroup, heaviest first) -- told apart by their grid sizes

@@ -21,7 +21,7 @@ import sys
 from collections import defaultdict
 
 KERNELS = ("gemm_w5", "attn_fwd_v13c", "attn_fwd_v13", "attn_fwd_v12", "attn_fwd_v10", "attn_fwd_v7", "gemm_f32_mfma", "gemm_naive_f32", "hbm_read_probe", "attn_fwd_v2", "attn_decode_chunk", "attn_decode_combine", "gemv_vec", "gemm_mfma",
-           "gemm_smallm_nt", "scale_copy_vec")
+           "gemm_smallm_nt", "scale_copy_vec", "Cijk_")
 
 
 def label(k: str, name: str) -> str:
@@ -32,6 +32,8 @@ def label(k: str, name: str) -> str:
         return k + (" nt" if m and m.group(1) == "true" else " nn")
     if k.startswith("attn_fwd_v13"):
         return k
+    if k == "Cijk_":  # hipBLASLt (torch F.linear / mm), for comparison
+        return "hipblaslt " + name.split("_MT")[1].split("_")[0] if "_MT" in name else "hipblaslt"
     return k + " causal" if k.startswith("attn_fwd") and ", true>" in name else k
 
 
