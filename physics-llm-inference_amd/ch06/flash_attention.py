@@ -13,12 +13,13 @@ reference signature and return contract (a NEW tensor shaped like ``q`` in
 
 ``FlashAttentionConfig`` keeps its four fields (``:6-11``).  They are Triton
 launch knobs in the reference's design notes; on MI355X each one maps to a
-fixed property of the default HIP kernel, attn_fwd_v12 (``hip_tiling``
+fixed property of the default HIP kernel, attn_fwd_v13 (``hip_tiling``
 returns the mapping): ``block_q`` -> 256 query rows per workgroup (4 waves x
-64 rows, one wave per SIMD, one row per lane of the swapped QK^T),
-``block_k`` -> 64-key K/V tiles, ``num_warps`` -> 4 wave64s per workgroup,
-``num_stages`` -> a 5-slot LDS ring with K/V DMA'd two tiles ahead (causal,
-fp16 and D = 64 take attn_fwd_v10 / v7: 4 or 8 waves x 32 rows).  The GPU path ignores the requested values (results do not
+64 rows, one wave per SIMD, four 16-row q-blocks per wave on the 16x16x32
+MFMA), ``block_k`` -> 64-key K/V tiles, ``num_warps`` -> 4 wave64s per
+workgroup, ``num_stages`` -> a 5-slot LDS ring with K/V DMA'd two tiles
+ahead (causal bf16 D = 128 runs the same program with the mask,
+attn_fwd_v13c; fp16, D = 64 and Nk < 128 take attn_fwd_v12 / v10 / v7).  The GPU path ignores the requested values (results do not
 depend on the blocking; the kernel's tiles are set by the MFMA / LDS
 mapping); the CPU recurrence uses ``block_q``/``block_k`` as the reference
 does.  Non-positive or non-integer fields are rejected on both paths.  Softmax statistics are fp32 on both paths (the reference keeps
@@ -41,10 +42,10 @@ class FlashAttentionConfig:
     num_stages: int = 2
 
 
-# what each FlashAttentionConfig knob means on the HIP path (non-causal bf16
-# D=128: attn_fwd_v12 -- 256-row blocks of 4 waves x 64 rows, 64-key tiles,
-# a 5-slot LDS ring; causal / fp16 / other D run attn_fwd_v10 with 8 waves and
-# a 3-slot ring, or 4 waves and 2 slots for causal)
+# what each FlashAttentionConfig knob means on the HIP path (bf16 D=128,
+# causal or not: attn_fwd_v13 / v13c -- 256-row blocks of 4 waves x 64 rows,
+# 64-key tiles, a 5-slot LDS ring two tiles ahead; fp16 / other D / short Nk
+# run attn_fwd_v12 / v10 / v7)
 HIP_TILING = {"block_q": 256, "block_k": 64, "num_warps": 4, "num_stages": 5}
 
 

@@ -90,6 +90,17 @@ def Y(k):
 NY = 16
 
 
+def MUC(qb):
+    """QSCALE: -mu of q-block qb in all four words (the C operand of the
+    block's first QK MFMA); shares v190-205 with Y, which QSCALE leaves idle"""
+    return V(190 + 4 * qb, 4)
+
+
+def TRIMU(qb):
+    """QSCALE, causal diagonal step: TRI - mu of q-block qb (T(20+4qb) .. +3)"""
+    return V(238 + 4 * qb, 4)
+
+
 def QOFF(qb):
     return V(250 + qb)  # = T(32 + qb): live only while the Q loads issue
 
@@ -199,6 +210,10 @@ LDS_GAP = 1024  # LDS bytes per wave per 16-cycle gap (256 B/clk per CU, 4 waves
 # softmax stream -- results wrong, timing only
 ABL = set()
 DMA_COST = 8
+# QSCALE (Gen(qscale=True)): Q is scaled by c = scale * log2(e) once per
+# block (bf16, RNE) and -mu enters as the first QK MFMA's C operand, so the
+# softmax stream is exp2(S) in place + cvt: no v_fma_f32 per score
+QSCALE = [False]
 
 
 def schedule(mfmas, fills, budget=8, gap_offset=0, lds_gap=LDS_GAP):
@@ -267,7 +282,7 @@ def drain(fills, k):
 # ---------------------------------------------------------------- pieces
 
 
-def qk_mfmas(mask=None):
+def qk_mfmas(mask=None, muc=False):
     """QK^T of one tile, q-block major.  mask (causal): the C operand of each
     chain's first MFMA -- 'diag' (the wave's diagonal tile: 0 below the
     diagonal blocks, the triangular pattern on them, -inf above), 'beyond'
@@ -276,8 +291,8 @@ def qk_mfmas(mask=None):
         if mask == "beyond" or (mask == "diag" and kb > qb):
             return NINF
         if mask == "diag" and kb == qb:
-            return TRI
-        return 0
+            return TRIMU(qb) if muc else TRI
+        return MUC(qb) if muc else 0
     return [mfma(S_(kb, qb), K_(kb, ds), Q_(qb, ds), S_(kb, qb) if ds else c0(kb, qb))
             for qb in range(4) for ds in range(4) for kb in range(4)]
 
@@ -337,18 +352,34 @@ def softmax_fills(X, slices, earliest_of, deadline_of=None, ytag=0, prev_cv=None
                   tag="fma", hard=dl is not None)
         f1 = Fill(I("v_fma_f32", y1, s[2 * hh + 1], sC, Neg(MU(qb))), 4, deps=deps, sep=0, earliest=ea,
                   deadline=dl, tag="fma", hard=dl is not None)
-        if "exp" in ABL:
+        if QSCALE[0]:  # P = bf16(exp2(S)), S already c s - mu: in place, no temporaries
+            dle = None if dl is None else dl - 1
+            e0 = Fill(I("v_exp_f32", s[2 * hh], s[2 * hh]), 8, trans=True, sep=0, earliest=ea, deadline=dle,
+                      tag="exp", hard=dl is not None)
+            e1 = Fill(I("v_exp_f32", s[2 * hh + 1], s[2 * hh + 1]), 8, trans=True, sep=0, earliest=ea,
+                      deadline=dle, tag="exp", hard=dl is not None)
+            f0 = f1 = None
+            y0, y1 = s[2 * hh], s[2 * hh + 1]
+        elif "exp" in ABL:
             e0 = Fill(I("v_mov_b32", y0, y0), 4, deps=[f0], sep=1, tag="exp")
             e1 = Fill(I("v_mov_b32", y1, y1), 4, deps=[f1], sep=1, tag="exp")
+        elif "fma" in ABL:  # exp straight from S (no s * c - mu)
+            e0 = Fill(I("v_exp_f32", y0, s[2 * hh]), 8, trans=True, deps=deps, sep=0, earliest=ea, deadline=dl,
+                      tag="exp", hard=dl is not None)
+            e1 = Fill(I("v_exp_f32", y1, s[2 * hh + 1]), 8, trans=True, deps=deps, sep=0, earliest=ea, deadline=dl,
+                      tag="exp", hard=dl is not None)
+            f0 = f1 = None
         else:
             e0 = Fill(I("v_exp_f32", y0, y0), 8, trans=True, deps=[f0], sep=1, tag="exp")
             e1 = Fill(I("v_exp_f32", y1, y1), 8, trans=True, deps=[f1], sep=1, tag="exp")
         fm = f1
         w = P_(X, qb, kb >> 1)[2 * (kb & 1) + hh]
-        cv = Fill(I("v_cvt_pk_bf16_f32", w, y0, y1), 4, deps=[e0, e1], sep=1, tag="cvt")
+        cv = Fill(I("v_cvt_pk_bf16_f32", w, y0, y1), 4, deps=[e0, e1], sep=1, tag="cvt",
+                  deadline=dl if QSCALE[0] else None, hard=QSCALE[0] and dl is not None)
         slot_cv[slot] = cv
-        fills += [f0, f1, e0, e1, cv]
-        groups.append([f0, f1, e0, e1, cv])
+        grp = [f for f in (f0, f1, e0, e1, cv) if f is not None]
+        fills += grp
+        groups.append(grp)
         cvs.append((cv, w))
         if len(cvs) == 2:
             (c0, w0), (c1, w1) = cvs
@@ -544,15 +575,23 @@ def row_max(qb, m, t1, t2):
     return c
 
 
-def exps_all(X, also_or=False):
-    """every P of the tile in S with the current mu (straight line)"""
+def exps_all(X, also_or=False, shifted=False):
+    """every P of the tile in S with the current mu (straight line);
+    QSCALE: S = c s (C operand 0) unless shifted (S = c s - mu already)"""
     c = []
     for n, (qb, kb, hh) in enumerate(slice_list()):
         y0, y1 = T(0 + 2 * (n % 8)), T(1 + 2 * (n % 8))
         s = S_(kb, qb)
         w = P_(X, qb, kb >> 1)[2 * (kb & 1) + hh]
-        c += [I("v_fma_f32", y0, s[2 * hh], sC, Neg(MU(qb))), I("v_fma_f32", y1, s[2 * hh + 1], sC, Neg(MU(qb))),
-              I("v_exp_f32", y0, y0), I("v_exp_f32", y1, y1), I("v_cvt_pk_bf16_f32", w, y0, y1)]
+        if QSCALE[0] and shifted:
+            c += [I("v_exp_f32", y0, s[2 * hh]), I("v_exp_f32", y1, s[2 * hh + 1])]
+        elif QSCALE[0]:
+            c += [I("v_sub_f32", y0, s[2 * hh], MU(qb)), I("v_sub_f32", y1, s[2 * hh + 1], MU(qb)),
+                  I("v_exp_f32", y0, y0), I("v_exp_f32", y1, y1)]
+        else:
+            c += [I("v_fma_f32", y0, s[2 * hh], sC, Neg(MU(qb))), I("v_fma_f32", y1, s[2 * hh + 1], sC, Neg(MU(qb))),
+                  I("v_exp_f32", y0, y0), I("v_exp_f32", y1, y1)]
+        c += [I("v_cvt_pk_bf16_f32", w, y0, y1)]
         if also_or:
             c.append(I("v_or_b32", ACC(X), ACC(X), w))
     return c
@@ -582,8 +621,9 @@ class Gen:
     bottom-right-masked kernel (attn_fwd_v13c)"""
 
     def __init__(self, ndef=4, budget=8, dma_spacing=6, tag="%=", stamp=False, causal=False, abl=(), dma_cost=8,
-                 rev=True):
+                 rev=True, qscale=False):
         global DMA_COST
+        QSCALE[0] = bool(qscale)
         # causal: the second block of each pair streams its tiles in the
         # reversed order of tile_of (its 8 workgroups then read every K/V
         # tile at the same time)
@@ -759,6 +799,8 @@ class Gen:
         e([I("v_mov_b32", L_(qb)[r], 0) for qb in range(4) for r in range(4)])
         e([I("v_mov_b32", ACC(0), 0), I("v_mov_b32", ACC(1), 0)])
         e([I("s_waitcnt", "vmcnt(0)"), I("s_barrier")])
+        if QSCALE[0]:
+            e(self.q_prescale())
         # tile 0: K(0) fragments, QK(0) with tile 2's DMA beside it
         e([I("v_add_u32", VKA, sS0, VKL)])
         e(k_reads())
@@ -774,7 +816,11 @@ class Gen:
         # exact row max -> mu = max * c + muoff; P(0) into state 0
         for qb in range(4):
             e(row_max(qb, T(20 + qb), T(30), T(31)))
-            e([I("v_mul_f32", T(20 + qb), sC, T(20 + qb)), I("v_add_f32", MU(qb), sT8, T(20 + qb))])
+            if QSCALE[0]:  # S = c s already
+                e([I("v_add_f32", MU(qb), sT8, T(20 + qb))] +
+                  [I("v_sub_f32", MUC(qb)[r], 0, MU(qb)) for r in range(4)])
+            else:
+                e([I("v_mul_f32", T(20 + qb), sC, T(20 + qb)), I("v_add_f32", MU(qb), sT8, T(20 + qb))])
         e(exps_all(0))
         # tile 1 landed (tile 2 in flight): K(1) fragments
         e([I("s_waitcnt", "vmcnt(8)"), I("s_barrier"), I("v_add_u32", VKA, sSP1, VKL)])
@@ -797,6 +843,22 @@ class Gen:
     def deferred(self):
         sl = slice_list()
         return sl[len(sl) - self.ndef:], sl[:len(sl) - self.ndef]
+
+    def q_prescale(self):
+        """QSCALE: every Q word (two bf16) in the accumulator file times c,
+        rounded to bf16 (RNE); eight rotating temporaries"""
+        c = []
+        n = 0
+        for qb in range(4):
+            for ds in range(4):
+                for r in range(4):
+                    a = Q_(qb, ds)[r]
+                    t0, t1, t2 = T(3 * (n % 8)), T(3 * (n % 8) + 1), T(3 * (n % 8) + 2)
+                    c += [I("v_accvgpr_read_b32", t0, a), I("v_lshlrev_b32", t1, 16, t0),
+                          I("v_and_b32", t2, 0xFFFF0000, t0), I("v_mul_f32", t1, sC, t1), I("v_mul_f32", t2, sC, t2),
+                          I("v_cvt_pk_bf16_f32", t0, t1, t2), I("v_accvgpr_write_b32", a, t0)]
+                    n += 1
+        return c
 
     def tile_of(self, dst, pos):
         """causal: the key tile at stream position pos (SGPR or 0) of the
@@ -883,7 +945,9 @@ class Gen:
             if f.tag == "or" and not any(d.tag == "or" for d in f.deps):
                 f.deps.append(z)
         fills += f_now
-        body, left = schedule(qk_mfmas(mask), fills, self.budget)
+        if QSCALE[0] and mask == "diag":
+            e([I("v_add_f32", TRIMU(qb)[r], TRI[r], MUC(qb)[r]) for qb in range(4) for r in range(4)])
+        body, left = schedule(qk_mfmas(mask, muc=QSCALE[0]), fills, self.budget)
         e(body)
         # everything of tile t-1 must be done before its check
         pend_prev = [f for f in left if f in f_def or f.tag.startswith("dma")]
@@ -995,7 +1059,9 @@ class Gen:
             e([I("v_add_u32", T(36), tile_slot, VKL)])
             e([I("ds_read_b128", K_(kb, ds), T(36), mods=f"offset:{512 * (ds & 1) + 2048 * kb + 8192 * (ds >> 1)}")
                for ds in range(4) for kb in range(4)])
-            e(qk_mfmas())
+            # QSCALE: the checked tile with C = 0 (its exact max), the next one
+            # shifted by the new mu (its later slices exp S in place)
+            e(qk_mfmas(muc=QSCALE[0] and Xs != X))
             if self.causal:
                 if Xs == X:  # tile at position sT - 1
                     e([I("s_sub_u32", sT0, sT, 1)])
@@ -1011,8 +1077,12 @@ class Gen:
                 for qb in range(4):
                     m = T(20 + qb)
                     e(row_max(qb, m, T(30), T(31)))
-                    e([I("v_mul_f32", m, sC, m), I("v_add_f32", m, sT1, m), I("v_max_f32", m, m, MU(qb)),
+                    if not QSCALE[0]:
+                        e([I("v_mul_f32", m, sC, m)])
+                    e([I("v_add_f32", m, sT1, m), I("v_max_f32", m, m, MU(qb)),
                        I("v_sub_f32", T(24), MU(qb), m), I("v_exp_f32", T(24), T(24)), I("v_mov_b32", MU(qb), m)])
+                    if QSCALE[0]:
+                        e([I("v_sub_f32", MUC(qb)[r], 0, m) for r in range(4)])
                     for db in range(8):
                         for r in range(4):
                             e([I("v_accvgpr_read_b32", T(25), O_(db, qb)[r]),
@@ -1022,7 +1092,7 @@ class Gen:
                 e(exps_all(X))
             else:
                 e([I("v_mov_b32", ACC(Xs), 0)])
-                e(exps_all(Xs, also_or=True))
+                e(exps_all(Xs, also_or=True, shifted=QSCALE[0]))
         e([I("v_mov_b32", ACC(X), 0), I("s_nop", 4)])
         for k, blk, ret in self.sites:
             if blk == name:
