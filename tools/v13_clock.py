@@ -58,4 +58,17 @@ for rep in range(3):
             out.update({"clock_GHz": round(float(ghz), 3), "cycles_per_wave_tile": round(float(dt.mean() / tiles), 1),
                         "wave_us_mean": round(float(dr.mean() / 100), 1),
                         "wave_us_min_max": [round(float(dr.min() / 100), 1), round(float(dr.max() / 100), 1)]})
+            # by XCD (workgroup w runs on XCD w % 8): clock, wave time, and the
+            # span from the first wave's start to each XCD's last exit
+            wg = np.arange(len(dt)) // 4
+            start = float(r0.min())
+            xcd = {}
+            for x in range(8):
+                m = wg % 8 == x
+                xcd[x] = {"GHz": round(float(dt[m].sum() / dr[m].sum() * 0.1), 3),
+                          "wave_us_mean": round(float(dr[m].mean() / 100), 1),
+                          "wave_us_max": round(float(dr[m].max() / 100), 1),
+                          "end_us_max": round(float((r1[m].max() - start) / 100), 1)}
+            out["by_xcd"] = xcd
+            out["span_us"] = round(float((r1.max() - start) / 100), 1)
     print(json.dumps(out), flush=True)
