@@ -336,13 +336,19 @@ int pli_attn_decode_dev(const void* q, const void* k, const void* v, void* o,
  *
  * pli_flash_attn_fwd_variant: 21 attn_fwd_v2 (round-1 kernel), 50 / 51
  *   attn_fwd_v7 prescaled / exact, 54 / 55 attn_fwd_v10 prescaled / exact,
- *   60 attn_fwd_v10 exact in 4-wave workgroups (causal default), 70 / 71
- *   attn_fwd_v12 (one wave per SIMD, 64 rows per wave; 71 persistent =
- *   non-causal default for bf16 D = 128, bitwise equal to 55; other inputs
- *   take 55); 72 = 71 with the defer-max threshold at 0 (tests); 73 / 74
- *   attn_fwd_v12 causal, one block per workgroup / persistent pair walk
- *   (74 = causal default).  Prescaled variants round Q * scale * log2(e) to
+ *   60 attn_fwd_v10 exact in 4-wave workgroups, 70 / 71 attn_fwd_v12 (one
+ *   wave per SIMD, 64 rows per wave; 71 persistent, bitwise equal to 55;
+ *   other inputs take 55); 72 = 71 with the defer-max threshold at 0
+ *   (tests); 73 / 74 attn_fwd_v12 causal, one block per workgroup /
+ *   persistent pair walk; 80 / 81 / 82 attn_fwd_v13 (16x16x32 MFMA, one
+ *   generated instruction stream) persistent / one block per workgroup /
+ *   80 with the rescale path at nearly every tile (tests) -- 80 is the
+ *   default for bf16 D = 128, Nk >= 128, Nk % 64 == 0; 83 / 84 / 85 the
+ *   causal forms (83 = causal default where (Nk - Nq) % 64 == 0; other
+ *   shapes take 74 / 60).  Prescaled variants round Q * scale * log2(e) to
  *   the 16-bit input type (2^-9 relative score error in bf16).
+ * pli_gemm_w5 schedule (all gemm_w5 routes): W5_SPLIT, DMA spread over both
+ *   halves of each 64-deep K step (gemm_w5.hip).
  * pli_gemm_variant / pli_gemm_ws_variant: 0 default; 1 128^2 tile; 2 256^2
  *   one-phase; 3 phased SCHED 0; 4 one-phase + setprio; 5-8 phased SCHED
  *   1/3/5/7; 9-11 grouped one-phase (group_m 4/8/16); 12-15 grouped phased
