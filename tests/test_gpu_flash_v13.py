@@ -116,7 +116,9 @@ def test_v13_rescale_stress(name):
 # block per workgroup heaviest first (forward order), 85 = 83 with the
 # rescale path at nearly every tile
 CAUSAL = [(4, 32, 8, 1024, 1024), (2, 32, 32, 2048, 2048), (2, 16, 4, 4096, 4096), (3, 40, 8, 1024, 1024),
-          (2, 8, 2, 256, 512), (1, 4, 4, 128, 128), (1, 8, 8, 704, 768), (2, 4, 2, 320, 320)]
+          (2, 8, 2, 256, 512), (1, 4, 4, 128, 128), (1, 8, 8, 704, 768), (2, 4, 2, 320, 320),
+          # pair walk with reversed second blocks and a diagonal offset (Nk - Nq = 1024 / 512)
+          (4, 32, 8, 1024, 2048), (2, 32, 8, 2048, 2560)]
 
 
 @pytest.mark.parametrize("qmul", (1, 4))
