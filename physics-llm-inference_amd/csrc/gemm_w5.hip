@@ -60,6 +60,12 @@
 #ifndef W5_ABL_DMA
 #define W5_ABL_DMA 0  // timing only: no DMA in the loop (results wrong)
 #endif
+#ifndef W5_ABL_RD
+#define W5_ABL_RD 0  // timing only: no fragment reads in the loop (results wrong)
+#endif
+#ifndef W5_ABL_BAR
+#define W5_ABL_BAR 0  // timing only: no barriers in the loop (races; results wrong)
+#endif
 #ifndef W5_SPLIT
 // 1: the (S, h1) fragments are read in half 0's first 16 gaps, a barrier
 // after gap 24 frees slot S, and 5 of step S+2's DMA pieces go into half 0's
@@ -285,11 +291,11 @@ __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A
             if constexpr (std::is_same_v<T, bf16_t>) w4v::mfma_bf16<J>(bop(fb[P][ni]), fa[P][mi]);
             else w4v::mfma_f16<J>(bop(fb[P][ni]), fa[P][mi]);
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (RD && J % RS == 0 && J / RS < 16)
+            if constexpr (!W5_ABL_RD && RD && J % RS == 0 && J / RS < 16)
                 frag_read(std::integral_constant<int, RH>{}, std::integral_constant<int, J / RS>{}, rsa, rsb);
             if constexpr (J == BAR) {
                 frag_wait(std::integral_constant<int, RH>{});
-                __builtin_amdgcn_s_barrier();
+                if constexpr (!W5_ABL_BAR) __builtin_amdgcn_s_barrier();
                 __builtin_amdgcn_sched_barrier(0);
             }
             constexpr int D = J - DS0;
@@ -341,7 +347,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A
                    s + 2, I{}, std::integral_constant<int, 28>{}, std::integral_constant<int, 7>{},
                    std::integral_constant<int, 24>{});
             asm volatile("s_waitcnt vmcnt(5)" ::: "memory");  // step s+1 landed (5 of s+2's pieces in flight)
-            __builtin_amdgcn_s_barrier();
+            if constexpr (!W5_ABL_BAR) __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
             half_x(O{}, more_tag, Z{}, img_off(s + 1, 0), img_off(s + 1, 1), std::integral_constant<int, 5>{},
                    std::integral_constant<int, 11>{}, s + 2, std::integral_constant<int, W5_RD_STRIDE>{}, N0{},
