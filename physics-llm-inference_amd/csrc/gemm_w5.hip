@@ -73,6 +73,33 @@
 // half-0 ones meet no fragment read
 #define W5_SPLIT 1
 #endif
+// W5_SPLIT placement (A/B knobs): half-0 read stride, barrier gap, DMA
+// pieces in half 0 with their first gap and spacing; half-1 read stride,
+// first DMA gap and spacing (the remaining 16 - W5S_N0 pieces)
+#ifndef W5S_RS0
+#define W5S_RS0 1
+#endif
+#ifndef W5S_BAR
+#define W5S_BAR 24
+#endif
+#ifndef W5S_N0
+#define W5S_N0 5
+#endif
+#ifndef W5S_D0
+#define W5S_D0 28
+#endif
+#ifndef W5S_DS0
+#define W5S_DS0 7
+#endif
+#ifndef W5S_RS1
+#define W5S_RS1 W5_RD_STRIDE
+#endif
+#ifndef W5S_D1
+#define W5S_D1 0
+#endif
+#ifndef W5S_DS1
+#define W5S_DS1 6
+#endif
 
 namespace pli {
 namespace {
@@ -343,15 +370,19 @@ __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A
         // position), its B pieces in half 1 (into A(s)'s); else all 16 in half 1
         if constexpr (W5_SPLIT) {
             using I = std::integral_constant<int, 1>;
-            half_x(Z{}, std::true_type{}, O{}, img_off(s, 0), img_off(s, 1), N0{}, std::integral_constant<int, 5>{},
-                   s + 2, I{}, std::integral_constant<int, 28>{}, std::integral_constant<int, 7>{},
-                   std::integral_constant<int, 24>{});
-            asm volatile("s_waitcnt vmcnt(5)" ::: "memory");  // step s+1 landed (5 of s+2's pieces in flight)
+            (void)I{};
+            half_x(Z{}, std::true_type{}, O{}, img_off(s, 0), img_off(s, 1), N0{},
+                   std::integral_constant<int, W5S_N0>{}, s + 2, std::integral_constant<int, W5S_RS0>{},
+                   std::integral_constant<int, W5S_D0>{}, std::integral_constant<int, W5S_DS0>{},
+                   std::integral_constant<int, W5S_BAR>{});
+            // step s+1 landed (W5S_N0 of s+2's pieces in flight)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(W5S_N0) : "memory");
             if constexpr (!W5_ABL_BAR) __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
-            half_x(O{}, more_tag, Z{}, img_off(s + 1, 0), img_off(s + 1, 1), std::integral_constant<int, 5>{},
-                   std::integral_constant<int, 11>{}, s + 2, std::integral_constant<int, W5_RD_STRIDE>{}, N0{},
-                   std::integral_constant<int, 6>{}, std::integral_constant<int, -1>{});
+            half_x(O{}, more_tag, Z{}, img_off(s + 1, 0), img_off(s + 1, 1), std::integral_constant<int, W5S_N0>{},
+                   std::integral_constant<int, 16 - W5S_N0>{}, s + 2, std::integral_constant<int, W5S_RS1>{},
+                   std::integral_constant<int, W5S_D1>{}, std::integral_constant<int, W5S_DS1>{},
+                   std::integral_constant<int, -1>{});
             if constexpr (MORE) frag_wait(Z{});
             return;
         }

@@ -1,0 +1,8 @@
+# gemm_w5 W5_SPLIT placement sweep (bitwise vs s0 = the product placement)
+cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
+export TMPDIR=/tmp
+O=gpurun_out/r4q
+mkdir -p $O
+L=""; for k in s0 s1 s2 s3 s4 s5 s6 s7; do L="$L tools/ab/libpli_w5$k.so"; done
+LIBS="$L" VARIANTS=0 LAYOUTS=nt,nn SHAPES=8192x8192x8192,8192x8192x4096,4096x4096x4096 ROUNDS=5 timeout -k 10 500 python -u tools/ab_gemm.py > $O/ab.log 2>&1
+rc=$?; exit $rc
