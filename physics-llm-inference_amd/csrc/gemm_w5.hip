@@ -18,7 +18,8 @@
 //           step S+2's 16 DMA pieces go into slot S in gaps 28-56;
 //   s_waitcnt vmcnt(5) + barrier: step S+1's pieces landed everywhere;
 //   half 1: MFMAs on (S, h1); in their gaps the (S+1, h0) fragments are read
-//           from slot S+1 and the other 11 DMA pieces of step S+2 issue.
+//           from slot S+1 (every third gap) and the other 11 DMA pieces of
+//           step S+2 issue (gaps 1, 7, ... 61).
 // (W5_SPLIT 0, round 3: all 16 pieces in half 1 beside the reads, one
 // barrier per step; the split is bitwise the same and 0.5-2 % faster,
 // profiles/r04/gemm/ab_w5_split.log.)  Past the last step the DMA re-loads
@@ -92,10 +93,10 @@
 #define W5S_DS0 7
 #endif
 #ifndef W5S_RS1
-#define W5S_RS1 W5_RD_STRIDE
+#define W5S_RS1 3  // placement sweep: profiles/r04/gemm/ab_w5_split_placement.log (s6)
 #endif
 #ifndef W5S_D1
-#define W5S_D1 0
+#define W5S_D1 1
 #endif
 #ifndef W5S_DS1
 #define W5S_DS1 6
