@@ -108,10 +108,16 @@ class Wave:
         self.pc = 0
         self.done = False
         self.count = 0
+        self.wid = None  # (workgroup, wave), set by the runner
 
 
 class Emu:
-    def __init__(self, prog, heap, lds_bytes=163840, trace=False):
+    def __init__(self, prog, heap, lds_bytes=163840, trace=False, structural=False):
+        # structural: scalar and control flow only -- MFMA, VALU, DS and the
+        # vector memory traffic are skipped, each LDS-DMA records its wave
+        # and scalar source base in dma_log (the stream-order tests)
+        self.structural = structural
+        self.dma_log = []
         self.prog = [i for i in prog]
         self.labels = {ins.ops[0]: k for k, ins in enumerate(self.prog) if ins.op == "label"}
         self.heap = heap
@@ -232,6 +238,10 @@ class Emu:
         if op in ("label", "s_nop", "s_waitcnt"):
             return
         k = ins.kind()
+        if self.structural and not op.startswith("s_"):
+            if op == "global_load_lds_dwordx4":
+                self.dma_log.append((w.wid, self.sc(w, o[1]), self.off(ins), w.m0))
+            return
         if k == "mfma":
             return self.mfma(w, ins)
         if op.startswith("v_"):

@@ -80,7 +80,7 @@ def program(**kw):
     return _PROG[key]
 
 
-def run(q, k, v, scale=None, grid=None, muoff=7.0, layout="bhsd", causal=False, **kw):
+def run(q, k, v, scale=None, grid=None, muoff=7.0, layout="bhsd", causal=False, structural=False, **kw):
     """q [B,H,Nq,128], k / v [B,Hkv,Nk,128] float arrays (rounded to bf16) ->
     O [B,H,Nq,128] float32 from the emulated kernel.  layout 'bshd' stores
     the tensors as [B,S,H,D] (strided heads)."""
@@ -116,15 +116,19 @@ def run(q, k, v, scale=None, grid=None, muoff=7.0, layout="bhsd", causal=False, 
                     causal)
     kaddr = heap.alloc(args.nbytes, args.tobytes())
     prog = program(causal=causal, **kw)
-    em = E.Emu(prog, heap)
+    em = E.Emu(prog, heap, structural=structural)
+    em.kbase = ka
     for wg in range(G):
         waves = []
         for wv in range(4):
             w = E.Wave()
             w.s[0], w.s[1], w.s[2], w.s[3] = kaddr & 0xFFFFFFFF, kaddr >> 32, wg, wv
+            w.wid = (wg, wv)
             waves.append(w)
         em.lds[:] = 0
         em.run_wg(waves)
+    if structural:
+        return None, em
     raw = heap.view(oa)[:B * H * Nq * D * 2].view(np.uint16)
     if layout == "bshd":
         o = E.bf16_to_f32(raw.reshape(B, Nq, H, D).astype(np.uint32)).transpose(0, 2, 1, 3)
