@@ -50,7 +50,7 @@ FLASH_KERNEL = ("attn_fwd_v13 persistent (variant 80; v_mfma_f32_16x16x32_bf16, 
                 "tools/gen_flash_v13.py)")
 JSON_OUT = sys.stdout  # main() points it at the original stdout and sends fd 1 to stderr
 GEMM_KERNEL = ("gemm_w5 (256x256 tile, one wave per SIMD, K staged 64 deep; variant 43, its persistent walk, "
-               "where M, N are multiples of 256 and 128 <= K <= 4096)")
+               "where M, N are multiples of 256 and K >= 128)")
 CAUSAL_KERNEL = "attn_fwd_v13c causal, persistent pair walk (variant 83)"
 
 

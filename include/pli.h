@@ -106,7 +106,7 @@ int pli_gemm(const void* a, const void* b, void* c, const void* bias, int m,
  * torch.float32)).  Shapes with at least 128 tiles of 256 x 256, K % 64 == 0,
  * N % 8 == 0 and 256 rows of A and B addressable by a 32-bit offset take
  * gemm_w5 with an fp32 epilogue (its persistent walk when M, N are multiples
- * of 256 and K <= 4096); other K % 64 == 0, N % 32 == 0 shapes with 16-byte
+ * of 256 and K >= 128); other K % 64 == 0, N % 32 == 0 shapes with 16-byte
  * aligned rows the LDS split-K kernel with one slice; the rest a
  * one-thread-per-output kernel.
  */
@@ -355,8 +355,7 @@ int pli_attn_decode_dev(const void* q, const void* k, const void* v, void* o,
  *   (8/4/2/16); 20 mid-M; 21 small-M; 22/24 direct-load split-K; 25-29 LDS
  *   split-K (256/512/128 targets, 3-deep ring); 40 gemm_w4v (one wave per
  *   SIMD, K 32 deep); 41 gemm_w5 (K 64 deep), 43 gemm_w5 persistent walk
- *   (M, N multiples of 256) -- 43 is the large-shape default for K <= 4096,
- *   41 above.
+ *   (M, N multiples of 256) -- 43 is the large-shape default (K >= 128).
  * pli_gemv_variant: 0-16 (rows per wave x 16-B chunks per lane x waves per
  *   block, gemv.hip), -1 default.
  * pli_attn_decode_variant: mode -1 default, 2/9/11/13 load-layout modes

@@ -2236,13 +2236,15 @@ static int gemm_dispatch(const void* a, const void* b, void* c, const void* bias
     // vs 1344 / 1305, torch 1560 / 1391; profiles/r03/gemm/ab_w5.log).
     // gemm_w4v (variant 40, K 32 deep) sits between them.
     // Its persistent walk (variant 43, K stream continued across tiles) where
-    // M, N are multiples of 256 and 128 <= K <= 4096: the per-tile prologue is a
-    // larger share there (8192^2 x 1024 NT / NN 1260 / 1188 vs 1180 / 1114,
-    // 16384 x 8192 x 1024 1320 / 1245 vs 1187 / 1163, hipBLASLt 1237 / 1083
-    // and 1284 / 1109); at K = 8192 the one-tile form is 0.5-2 % ahead
-    // (profiles/r03/gemm/ab_w5_persistent.log)
+    // M, N are multiples of 256 and K >= 128: the per-tile prologue is a
+    // larger share at short K (8192^2 x 1024 NT / NN 1260 / 1188 vs 1180 /
+    // 1114, 16384 x 8192 x 1024 1320 / 1245 vs 1187 / 1163, hipBLASLt 1237 /
+    // 1083 and 1284 / 1109; profiles/r03/gemm/ab_w5_persistent.log); with the
+    // split DMA schedule it is also level or ahead at K = 8192 / 16384 (NN
+    // 8192^3 1508 vs 1491, 8192^2 x 16384 NT / NN 1520 / 1505 vs 1508 / 1490;
+    // profiles/r04/gemm/ab_w5_persistent_deepK.log)
     if (variant == 0 && big && gemm_w5_ok(m, n, k, lda, ldb, ldc, trans_b)) {
-        const bool persist = m % 256 == 0 && n % 256 == 0 && k >= 128 && k <= 4096;
+        const bool persist = m % 256 == 0 && n % 256 == 0 && k >= 128;
         return launch_gemm_w5(a, b, c, bias, m, n, k, lda, ldb, ldc, trans_b, dtype == PLI_BF16, s, 4, persist);
     }
     if (big || (vec && variant >= 2 && k % G2K == 0 && n >= 8)) {
@@ -2339,11 +2341,11 @@ extern "C" int pli_gemm_f32out(const void* a, const void* b, float* c, int m, in
     const bool lds = k % 64 == 0 && k > 0 && n % 32 == 0 && lda % 8 == 0 && ldb % 8 == 0 && al16(a) &&
                      al16(b) && al16(c);
     // large shapes (128+ tiles of 256^2): gemm_w5 with its fp32 epilogue
-    // (persistent where M, N are multiples of 256 and 128 <= K <= 4096); the
+    // (persistent where M, N are multiples of 256 and K >= 128); the
     // TP-8 shard at M 8192 ran 214 us on the split-K kernel below
     if (lds && m >= 512 && n >= 512 && (int64_t)cdiv(m, 256) * cdiv(n, 256) >= 128 &&
         gemm_w5_ok(m, n, k, lda, ldb, n, 1)) {
-        const bool persist = m % 256 == 0 && n % 256 == 0 && k >= 128 && k <= 4096;
+        const bool persist = m % 256 == 0 && n % 256 == 0 && k >= 128;
         return launch_gemm_w5(a, b, c, nullptr, m, n, k, lda, ldb, n, 1, dtype == PLI_BF16, s, 4, persist, true);
     }
     if (lds) {

@@ -61,7 +61,7 @@ def test_w4v_bias_fp16_and_default_route(tb, variant):
     err = ((o.double() - ref).abs() / (ref.abs() + 1)).max().item()
     assert err <= 4e-3, f"fp16 + bias tb={tb}: max rel err {err:.3e}"
     # the default route takes gemm_w5 (persistent: M, N multiples of 256,
-    # K <= 4096) at this size (128+ tiles of 256^2); every variant here runs
+    # K >= 128) at this size (128+ tiles of 256^2); every variant here runs
     # the same MFMA chains, so all agree bitwise
     a, b = _inputs(4096, 2048, 1024, tb, torch.bfloat16, 6)
     assert torch.equal(pli_hip.gemm(a, b, trans_b=tb), pli_hip.gemm(a, b, trans_b=tb, variant=variant))
@@ -81,7 +81,8 @@ def test_w4v_strided_leading_dims(tb, variant):
 
 
 @pytest.mark.parametrize("tb", [True, False], ids=["nt", "nn"])
-@pytest.mark.parametrize("m,n,k", [(8192, 8192, 1024), (16384, 4096, 64), (16384, 4096, 128), (4608, 4096, 192)])
+@pytest.mark.parametrize("m,n,k", [(8192, 8192, 1024), (16384, 4096, 64), (16384, 4096, 128), (4608, 4096, 192),
+                                   (8192, 4096, 8192)])
 def test_w5_persistent_walks_vs_f64(m, n, k, tb):
     """Variant 43 with more tiles than CUs (every workgroup walks several
     tiles, the K stream crossing tile seams; K = 128 is the two-step
@@ -95,3 +96,20 @@ def test_w5_persistent_walks_vs_f64(m, n, k, tb):
     ref = a[rows].double() @ (b.double().t() if tb else b.double())
     err = ((o[rows].double() - ref).abs() / (ref.abs() + 1)).max().item()
     assert err <= 1e-2, f"{m}x{n}x{k} tb={tb}: max rel err {err:.3e}"
+
+
+def test_w5_f32out_persistent_deep_k():
+    """The fp32-output form (RowParallelLinear(reduce_dtype=torch.float32))
+    on its persistent walk at K = 8192 (two tiles per workgroup): sampled
+    rows against f64 -- unrounded partials: fp32 accumulation error only,
+    well under the 2^-9 of a bf16 output."""
+    import pli_hip
+    a, b = _inputs(8192, 4096, 8192, True, torch.bfloat16, 11)
+    o = pli_hip.gemm_f32out(a, b)
+    assert o.dtype == torch.float32
+    rows = torch.randperm(8192, generator=torch.Generator().manual_seed(2))[:48].to(DEV)
+    ref = a[rows].double() @ b.double().t()
+    err = ((o[rows].double() - ref).abs() / (ref.abs() + 1)).max().item()
+    assert err <= 5e-4, f"f32out K=8192: max rel err {err:.3e}"  # fp32 sums of 8192 products; bf16 output alone is 2^-9
+    # bitwise: the bf16-output default route rounds the same accumulators
+    assert torch.equal(o.to(torch.bfloat16), pli_hip.gemm(a, b, trans_b=True))
