@@ -100,6 +100,9 @@ bool attn_v13_ok(int D, int is_bf16, int causal, int Nq, int Nk, const V7Strides
     if (D != 128 || !is_bf16 || Nk < 128 || Nk % 64 != 0 || Nq < 1) return false;
     // causal: the bottom-right diagonal on 64-key tile boundaries
     if (causal && (Nq > Nk || (Nk - Nq) % 64 != 0)) return false;
+    // causal: the stream's tile count and index carry the block's order in
+    // bit 16 (tools/v13/kernel.py block_params), so counts stay below 2^16
+    if (causal && Nk / 64 > 0xFFFF) return false;
     // 32-bit per-lane offsets: a Q / O head's rows, a K / V tile
     const int64_t q_ext = ((int64_t)Nq - 1) * st.qn * 2 + 256, o_ext = ((int64_t)Nq - 1) * st.on * 2 + 256;
     const int64_t kv_tile = 64 * std::max(st.kn, st.vn) * 2;
