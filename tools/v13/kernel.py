@@ -621,13 +621,16 @@ class Gen:
     bottom-right-masked kernel (attn_fwd_v13c)"""
 
     def __init__(self, ndef=4, budget=8, dma_spacing=6, tag="%=", stamp=False, causal=False, abl=(), dma_cost=8,
-                 rev=True, qscale=False):
+                 rev=True, qscale=False, dma_pv=0, dma_pv_spacing=16):
         global DMA_COST
         QSCALE[0] = bool(qscale)
         # causal: the second block of each pair streams its tiles in the
         # reversed order of tile_of (its 8 workgroups then read every K/V
         # tile at the same time)
         self.rev = causal and rev
+        # dma_pv > 0: the V half of each tile's DMA in the PV phase from gap
+        # dma_pv on, dma_pv_spacing apart (A/B knob; 0 = all in the QK phase)
+        self.dma_pv, self.dma_pv_spacing = dma_pv, dma_pv_spacing
         self.ndef, self.budget, self.dma_spacing, self.tag = ndef, budget, dma_spacing, tag
         ABL.clear()
         ABL.update(abl)
@@ -927,7 +930,17 @@ class Gen:
         if "soft" in ABL:
             f_def = []
         fills += f_def
-        fills += dma_fills(sSP2, earliest0=1, spacing=self.dma_spacing, rev=self.rev)
+        dma = dma_fills(sSP2, earliest0=1, spacing=self.dma_spacing, rev=self.rev)
+        dma_pv = []
+        if self.dma_pv:
+            # the V pieces (4-7, their own M0 write) and the advance go to the
+            # PV phase: tile t+2 only has to land by step t+1's barrier
+            dma, dma_pv = dma[:5], dma[5:]
+            for n, f in enumerate(dma_pv[:4]):
+                f.earliest = 64 + self.dma_pv + self.dma_pv_spacing * n
+                f.deps = [] if n == 0 else [dma_pv[n - 1]]
+            dma_pv[4].deps = [dma_pv[3]]
+        fills += dma
         # V(t-1) d-blocks 0, 1
         for db in (0, 1):
             for ins in v_reads(db):
@@ -976,7 +989,7 @@ class Gen:
             for ins in v_reads(db):
                 vr.append(Fill(ins, 2, earliest=B0 + (pv_first_gap(db - 3) + 9 if db >= 3 else 0),
                                deadline=B0 + pv_first_gap(db) - 6, tag="vread"))
-        fills = [ka] + kr + vr + fills
+        fills = [ka] + kr + vr + fills + dma_pv
         body, left = schedule(pv, fills, self.budget, gap_offset=B0)
         e(body)
         e(drain(left, B0 + 71))
