@@ -5,7 +5,7 @@
 // v_mfma_f32_32x32x2_f32 (exact f32 fma chain, 64 FLOP/clk/SIMD -- the same
 // rate as the fp32 VALU, but one instruction per 4096 FLOPs and no VALU left
 // busy).  128x128 workgroup tile, 4 waves of 64x64 (2x2 MFMA tiles of
-// 32x32), K tiles of 32 register-staged into a double-buffered LDS image
+// 32x32; 8 waves of 64x32 when the grid is under two workgroups per CU), K tiles of 32 register-staged into a double-buffered LDS image
 // ([k][m] / [k][n], rows padded to 129 floats where the transposed stores
 // need it), one barrier per K tile.  Lane l feeds A[i = l&31][k = l>>5] and
 // B[k = l>>5][j = l&31] of each k-pair: consecutive words for every half-wave.
@@ -21,26 +21,32 @@ namespace {
 
 constexpr int FT = 128, FK = 32, FP = FT + 1;
 
-template <bool TRANS_B>
-__global__ __launch_bounds__(256, 2) void gemm_f32_mfma(const float* __restrict__ A, const float* __restrict__ B,
-                                                       float* __restrict__ C, const float* __restrict__ bias,
-                                                       int M, int N, int K, int64_t lda, int64_t ldb,
-                                                       int64_t ldc) {
+// NW = 4: waves of 64x64 (2x2 MFMA tiles); NW = 8 (two waves per SIMD, for
+// grids of fewer than two workgroups per CU, e.g. the ch05 demo's 2048^3):
+// waves of 64x32 (2x1), the same per-output MFMA chains (bitwise equal).
+template <bool TRANS_B, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void gemm_f32_mfma(const float* __restrict__ A,
+                                                               const float* __restrict__ B,
+                                                               float* __restrict__ C,
+                                                               const float* __restrict__ bias, int M, int N,
+                                                               int K, int64_t lda, int64_t ldb, int64_t ldc) {
     // As[buf][k][m] (pad 129), Bs[buf][k][n] (pad 129 when transposed on store)
     constexpr int BS_LD = TRANS_B ? FP : FT;
+    constexpr int NT = 64 * NW, NJ = NW == 4 ? 2 : 1, WNS = 32 * NJ;  // threads, n-tiles per wave, wave width
     __shared__ float As[2][FK][FP];
     __shared__ __attribute__((aligned(16))) float Bs[2][FK][BS_LD];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave >> 1, wn = wave & 1;
+    const int wm = NW == 4 ? wave >> 1 : wave >> 2, wn = NW == 4 ? wave & 1 : wave & 3;
     const int h32 = lane >> 5, l32 = lane & 31;
     const int bm = blockIdx.y * FT, bn = blockIdx.x * FT;
 
-    // staging: 4 float4 of A and of B per thread per K tile
-    f32x4 ra[4], rb[4];
+    // staging: 1024 float4 of A and of B per K tile, 4 (NW 4) or 2 per thread
+    constexpr int NS = 1024 / NT;
+    f32x4 ra[NS], rb[NS];
     auto load = [&](int k0) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int idx = tid + 256 * i;
+        for (int i = 0; i < NS; ++i) {
+            const int idx = tid + NT * i;
             {   // A[m][k0 + 4q .. +3]
                 const int m = idx >> 3, q = idx & 7;
                 const int gm = bm + m, gk = k0 + 4 * q;
@@ -62,8 +68,8 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_mfma(const float* __restrict_
     };
     auto store = [&](int buf) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int idx = tid + 256 * i;
+        for (int i = 0; i < NS; ++i) {
+            const int idx = tid + NT * i;
             {
                 const int m = idx >> 3, q = idx & 7;
 #pragma unroll
@@ -80,11 +86,11 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_mfma(const float* __restrict_
         }
     };
 
-    f32x16 acc[2][2];
+    f32x16 acc[2][NJ];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < NJ; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
@@ -98,15 +104,15 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_mfma(const float* __restrict_
 #pragma unroll
         for (int kp = 0; kp < FK; kp += 2) {
             const int kr = kp + h32;
-            float a[2], b[2];
+            float a[2], b[NJ];
 #pragma unroll
             for (int i = 0; i < 2; ++i) a[i] = As[buf][kr][wm * 64 + 32 * i + l32];
 #pragma unroll
-            for (int j = 0; j < 2; ++j) b[j] = Bs[buf][kr][wn * 64 + 32 * j + l32];
+            for (int j = 0; j < NJ; ++j) b[j] = Bs[buf][kr][wn * WNS + 32 * j + l32];
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int j = 0; j < 2; ++j)
+                for (int j = 0; j < NJ; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
         }
         if (t + 1 < nk) store(buf ^ 1);
@@ -117,8 +123,8 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_mfma(const float* __restrict_
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int n = bn + wn * 64 + 32 * j + l32;
+        for (int j = 0; j < NJ; ++j) {
+            const int n = bn + wn * WNS + 32 * j + l32;
             if (n >= N) continue;
             const float bv = bias ? bias[n] : 0.f;
 #pragma unroll
@@ -150,13 +156,16 @@ bool gemm_f32_mfma_ok(const void* a, const void* b, const void* c, int k, int n,
 
 int launch_gemm_f32_mfma(const void* a, const void* b, void* c, const void* bias, int M, int N, int K,
                          int64_t lda, int64_t ldb, int64_t ldc, int trans_b, hipStream_t s) {
-    const dim3 grid(cdiv(N, FT), cdiv(M, FT)), block(256);
-    if (trans_b)
-        hipLaunchKernelGGL((gemm_f32_mfma<true>), grid, block, 0, s, (const float*)a, (const float*)b, (float*)c,
-                           (const float*)bias, M, N, K, lda, ldb, ldc);
-    else
-        hipLaunchKernelGGL((gemm_f32_mfma<false>), grid, block, 0, s, (const float*)a, (const float*)b, (float*)c,
-                           (const float*)bias, M, N, K, lda, ldb, ldc);
+    const dim3 grid(cdiv(N, FT), cdiv(M, FT));
+    // fewer than two workgroups per CU: eight waves per workgroup (two per
+    // SIMD) so one wave's LDS reads and barrier overlap the other's MFMAs
+    const bool w8 = (int64_t)grid.x * grid.y < 2 * (int64_t)cu_count(s);
+#define F32_LAUNCH(TB, NW) \
+    hipLaunchKernelGGL((gemm_f32_mfma<TB, NW>), grid, dim3(64 * NW), 0, s, (const float*)a, (const float*)b, \
+                       (float*)c, (const float*)bias, M, N, K, lda, ldb, ldc)
+    if (trans_b) { if (w8) F32_LAUNCH(true, 8); else F32_LAUNCH(true, 4); }
+    else { if (w8) F32_LAUNCH(false, 8); else F32_LAUNCH(false, 4); }
+#undef F32_LAUNCH
     return launch_status("gemm_f32_mfma");
 }
 
