@@ -19,12 +19,15 @@
 namespace pli {
 namespace {
 
-constexpr int FT = 128, FK = 32, FP = FT + 1;
+constexpr int FT = 128, FP = FT + 1;
+#ifndef F32_KT8
+#define F32_KT8 32  // K tile of the eight-wave form (A/B knob)
+#endif
 
 // NW = 4: waves of 64x64 (2x2 MFMA tiles); NW = 8 (two waves per SIMD, for
 // grids of fewer than two workgroups per CU, e.g. the ch05 demo's 2048^3):
 // waves of 64x32 (2x1), the same per-output MFMA chains (bitwise equal).
-template <bool TRANS_B, int NW = 4>
+template <bool TRANS_B, int NW = 4, int FK = 32>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void gemm_f32_mfma(const float* __restrict__ A,
                                                                const float* __restrict__ B,
                                                                float* __restrict__ C,
@@ -40,21 +43,21 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gemm_f32_mfma(const float* __
     const int h32 = lane >> 5, l32 = lane & 31;
     const int bm = blockIdx.y * FT, bn = blockIdx.x * FT;
 
-    // staging: 1024 float4 of A and of B per K tile, 4 (NW 4) or 2 per thread
-    constexpr int NS = 1024 / NT;
+    // staging: 32 FK float4 of A and of B per K tile
+    constexpr int NS = 32 * FK / NT, RQ = FK / 4;  // float4 per thread, per A / NT-B row
     f32x4 ra[NS], rb[NS];
     auto load = [&](int k0) {
 #pragma unroll
         for (int i = 0; i < NS; ++i) {
             const int idx = tid + NT * i;
             {   // A[m][k0 + 4q .. +3]
-                const int m = idx >> 3, q = idx & 7;
+                const int m = idx / RQ, q = idx % RQ;
                 const int gm = bm + m, gk = k0 + 4 * q;
                 ra[i] = (gm < M && gk < K) ? *reinterpret_cast<const f32x4*>(A + (int64_t)gm * lda + gk)
                                            : f32x4{0.f, 0.f, 0.f, 0.f};
             }
             if constexpr (TRANS_B) {  // B[n][k0 + 4q .. +3]
-                const int n = idx >> 3, q = idx & 7;
+                const int n = idx / RQ, q = idx % RQ;
                 const int gn = bn + n, gk = k0 + 4 * q;
                 rb[i] = (gn < N && gk < K) ? *reinterpret_cast<const f32x4*>(B + (int64_t)gn * ldb + gk)
                                            : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -71,12 +74,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gemm_f32_mfma(const float* __
         for (int i = 0; i < NS; ++i) {
             const int idx = tid + NT * i;
             {
-                const int m = idx >> 3, q = idx & 7;
+                const int m = idx / RQ, q = idx % RQ;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) As[buf][4 * q + j][m] = ra[i][j];
             }
             if constexpr (TRANS_B) {
-                const int n = idx >> 3, q = idx & 7;
+                const int n = idx / RQ, q = idx % RQ;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) Bs[buf][4 * q + j][n] = rb[i][j];
             } else {
@@ -161,7 +164,8 @@ int launch_gemm_f32_mfma(const void* a, const void* b, void* c, const void* bias
     // SIMD) so one wave's LDS reads and barrier overlap the other's MFMAs
     const bool w8 = (int64_t)grid.x * grid.y < 2 * (int64_t)cu_count(s);
 #define F32_LAUNCH(TB, NW) \
-    hipLaunchKernelGGL((gemm_f32_mfma<TB, NW>), grid, dim3(64 * NW), 0, s, (const float*)a, (const float*)b, \
+    hipLaunchKernelGGL((gemm_f32_mfma<TB, NW, NW == 8 ? F32_KT8 : 32>), grid, dim3(64 * NW), 0, s, (const float*)a, \
+                       (const float*)b, \
                        (float*)c, (const float*)bias, M, N, K, lda, ldb, ldc)
     if (trans_b) { if (w8) F32_LAUNCH(true, 8); else F32_LAUNCH(true, 4); }
     else { if (w8) F32_LAUNCH(false, 8); else F32_LAUNCH(false, 4); }
