@@ -812,8 +812,13 @@ class Gen:
         e(body)
         e(drain(left, 64))
         if self.rev:
+            # only the wave whose diagonal tile this is has masked scores in it
+            # (a first tile is never past a wave's diagonal)
+            skip = Lb(f"nomask{self.new_uid()}")
             e(self.tile_of(sT0, 0))
+            e([I("s_cmp_lt_u32", sT0, sTD), I("s_cbranch_scc1", skip)])
             e(mask_tile(sT0))
+            e([label(skip)])
         elif self.causal:
             e(mask_tile(0))
         # exact row max -> mu = max * c + muoff; P(0) into state 0
