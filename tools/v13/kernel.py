@@ -621,7 +621,7 @@ class Gen:
     bottom-right-masked kernel (attn_fwd_v13c)"""
 
     def __init__(self, ndef=4, budget=8, dma_spacing=6, tag="%=", stamp=False, causal=False, abl=(), dma_cost=8,
-                 rev=True, qscale=False, dma_pv=0, dma_pv_spacing=16):
+                 rev=True, qscale=False, dma_pv=0, dma_pv_spacing=16, budget_pv=None):
         global DMA_COST
         QSCALE[0] = bool(qscale)
         # causal: the second block of each pair streams its tiles in the
@@ -631,6 +631,7 @@ class Gen:
         # dma_pv > 0: the V half of each tile's DMA in the PV phase from gap
         # dma_pv on, dma_pv_spacing apart (A/B knob; 0 = all in the QK phase)
         self.dma_pv, self.dma_pv_spacing = dma_pv, dma_pv_spacing
+        self.budget_pv = budget if budget_pv is None else budget_pv  # the steps' PV-phase issue budget
         self.ndef, self.budget, self.dma_spacing, self.tag = ndef, budget, dma_spacing, tag
         ABL.clear()
         ABL.update(abl)
@@ -995,7 +996,7 @@ class Gen:
                 vr.append(Fill(ins, 2, earliest=B0 + (pv_first_gap(db - 3) + 9 if db >= 3 else 0),
                                deadline=B0 + pv_first_gap(db) - 6, tag="vread"))
         fills = [ka] + kr + vr + fills + dma_pv
-        body, left = schedule(pv, fills, self.budget, gap_offset=B0)
+        body, left = schedule(pv, fills, self.budget_pv, gap_offset=B0)
         e(body)
         e(drain(left, B0 + 71))
 
