@@ -60,7 +60,8 @@ def per_kernel(path_glob: str, counter: str) -> dict:
 
 def per_kernel_with_time(d: str, counter: str) -> dict:
     """{(kernel, grid): [(value, duration_ns)]} from a pass directory holding
-    counter_collection.csv and kernel_trace.csv (joined on Correlation_Id)"""
+    counter_collection.csv and kernel_trace.csv (joined on Correlation_Id;
+    without a trace, the counter row's own dispatch timestamps)"""
     out = defaultdict(list)
     for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         dur = {}
@@ -77,8 +78,11 @@ def per_kernel_with_time(d: str, counter: str) -> dict:
                     continue
                 lab = kernel_label(row["Kernel_Name"])
                 if lab:
-                    out[(lab, int(row["Grid_Size"]))].append(
-                        (float(row["Counter_Value"]), dur.get(row.get("Correlation_Id"))))
+                    t = dur.get(row.get("Correlation_Id"))
+                    if t is None and row.get("End_Timestamp") and row.get("Start_Timestamp"):
+                        # rocprofv3 7.x also stamps the dispatch in the counter rows
+                        t = int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
+                    out[(lab, int(row["Grid_Size"]))].append((float(row["Counter_Value"]), t))
     return out
 
 
@@ -95,7 +99,6 @@ def main():
     res = {}
     mean = lambda v: sum(v) / len(v) if v else 0.0  # noqa: E731
     labels = sorted({kk for (kk, _) in set(fetch) | set(write)})
-    d = sys.argv[1]
     for k in labels:
         grids = sorted({g for (kk, g) in set(fetch) | set(write) if kk == k})
         if not grids:
