@@ -568,7 +568,8 @@ int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int
         const bool bf = std::is_same<T, bf16_t>::value;
         const bool cv = variant >= 83;  // the causal forms
         const V7Strides s7{st.qb, st.qh, st.qn, st.kb, st.kh, st.kn, st.vb, st.vh, st.vn, st.ob, st.oh, st.on};
-        if (cv == (causal != 0) && attn_v13_ok(D, bf ? 1 : 0, causal, Nq, Nk, s7) && c_ok)
+        // v13 scales in fp32 (s * c - mu by v_fma): any c > 0 (scale = 1 etc.)
+        if (cv == (causal != 0) && attn_v13_ok(D, bf ? 1 : 0, causal, Nq, Nk, s7) && c_log2 > 0.f)
             return launch_attn_v13(q, k, v, o, B, H, group, Nq, Nk, s7, scale, stream, variant != 81 && variant != 84,
                                    (variant == 82 || variant == 85) ? -1.f : 7.f, nullptr, causal != 0);
         variant = causal ? 74 : 71;

@@ -163,3 +163,27 @@ def test_v13_causal_unaligned_offset_falls_back():
     q, k, v = inputs((2, 8, 2, 300, 512), 3)
     assert torch.equal(pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=83),
                        pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=74))
+
+
+@pytest.mark.parametrize("scale", (1.0, 0.25, 2.0 ** -0.5 / 8))
+@pytest.mark.parametrize("causal", (False, True))
+def test_v13_explicit_scale(scale, causal):
+    """Non-default softmax scales (ch06/flash_attention.py:18-26 takes any
+    scale): v13 applies c = scale * log2(e) in fp32, so c > 1 (scale 1.0)
+    stays on it; against an f64 attention with the same scale."""
+    import pli_hip
+    q, k, v = inputs((2, 8, 2, 256, 512) if causal else (2, 8, 2, 300, 512), 13)
+    var = 83 if causal else 80
+    out = pli_hip.flash_attn_fwd(q, k, v, scale=scale, causal=causal, variant=var)
+    g = q.shape[1] // k.shape[1]
+    kf, vf = (t.double().repeat_interleave(g, dim=1) for t in (k, v))
+    sc = (q.double() @ kf.transpose(-1, -2)) * scale
+    if causal:
+        nq, nk = q.shape[2], k.shape[2]
+        i = torch.arange(nq, device=q.device)[:, None]
+        j = torch.arange(nk, device=q.device)[None, :]
+        sc = sc.masked_fill(j > i + (nk - nq), float("-inf"))
+    ref = torch.softmax(sc, -1) @ vf
+    err = max_err(out, ref)
+    tol = 1e-2 if scale < 0.5 else 2.0 ** -8 * v.abs().max().item()
+    assert err <= tol, f"scale {scale} causal {causal}: max |err| {err:.4e} > {tol:.4e}"
