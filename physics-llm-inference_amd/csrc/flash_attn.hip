@@ -675,7 +675,13 @@ extern "C" int pli_flash_attn_fwd_variant(const void* q, const void* k, const vo
         vec = vec && (strides[i] % 8 == 0) && (!inner || strides[i] >= head_dim);
     }
     if (vec) {
-        if (variant < 0) variant = causal ? kDefaultCausalVariant : kDefaultVariant;
+        // c = scale * log2(e) > 1 (e.g. scale 1.0 on D = 128): the default is
+        // variant 21; v13 (80-85, any c > 0 when asked for) spreads c * s so far
+        // that its rescale path runs at nearly every key tile -- B8 H32 S4096
+        // N(0,1) inputs, scale 1.0: 3.68 ms on v13 vs 2.28 on 21, causal 2.38
+        // vs 1.38 (profiles/r04/scale/time_v13_at_c_gt_1.jsonl; with the default: time_default.jsonl)
+        if (variant < 0)
+            variant = scale * 1.4426950408889634f > 1.f ? 21 : causal ? kDefaultCausalVariant : kDefaultVariant;
         if (dtype == PLI_BF16)
             return head_dim == 128 ? launch_mfma<bf16_t, 128>(q, k, v, o, batch, heads, group, n_q, n_kv, st, scale, causal, s, variant)
                                    : launch_mfma<bf16_t, 64>(q, k, v, o, batch, heads, group, n_q, n_kv, st, scale, causal, s, variant);
