@@ -543,6 +543,18 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
 // at B8 S4096 H32 D128 in the same process (profiles/r04/flash/ab.log); where
 // v13 does not apply (fp16, D != 128, Nk % 64, Nk < 128) it routes to 71
 constexpr int kDefaultVariant = 80;
+// v13's mu = row max * c + PLI_V13_MUOFF (log2 units): P <= 2^-MUOFF right
+// after a max is taken and a tile takes the rescale path once a row max grows
+// by MUOFF + 1 (some P >= 2).  62 (since round 4; was 7, the THR 8 of v10 /
+// v12): P stays a normal bf16 / fp32 down to 2^-126, so only scores 64+ log2
+// units under the row max flush to 0 (weight < 2^-64), and the rescale path
+// all but vanishes where the scaled scores spread wide -- B8 H32 S4096, N(0,1)
+// inputs, TF/s 7 -> 62: scale 1.0 590 -> 1368 (causal 452 -> 1172), 0.25
+// 1150 -> 1386 (891 -> 1167), 1/sqrt(128) 1377 -> 1390 (1166 -> 1167)
+// (profiles/r04/scale/ab_muoff.jsonl)
+#ifndef PLI_V13_MUOFF
+#define PLI_V13_MUOFF 62.f
+#endif
 // causal: attn_fwd_v12 causal (74; one block per workgroup where the
 // persistent pair walk does not tile the shape), 60 where v12 does not apply
 // (fp16, D != 128, Nq > Nk, Nk % 64): B8 S4096 H32 D128 bf16 1002 (74, the
@@ -571,7 +583,7 @@ int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int
         // v13 scales in fp32 (s * c - mu by v_fma): any c > 0 (scale = 1 etc.)
         if (cv == (causal != 0) && attn_v13_ok(D, bf ? 1 : 0, causal, Nq, Nk, s7) && c_log2 > 0.f)
             return launch_attn_v13(q, k, v, o, B, H, group, Nq, Nk, s7, scale, stream, variant != 81 && variant != 84,
-                                   (variant == 82 || variant == 85) ? -1.f : 7.f, nullptr, causal != 0);
+                                   (variant == 82 || variant == 85) ? -1.f : PLI_V13_MUOFF, nullptr, causal != 0);
         variant = causal ? 74 : 71;
     }
     if (variant == 70 || variant == 71 || variant == 72) {
@@ -675,13 +687,7 @@ extern "C" int pli_flash_attn_fwd_variant(const void* q, const void* k, const vo
         vec = vec && (strides[i] % 8 == 0) && (!inner || strides[i] >= head_dim);
     }
     if (vec) {
-        // c = scale * log2(e) > 1 (e.g. scale 1.0 on D = 128): the default is
-        // variant 21; v13 (80-85, any c > 0 when asked for) spreads c * s so far
-        // that its rescale path runs at nearly every key tile -- B8 H32 S4096
-        // N(0,1) inputs, scale 1.0: 3.68 ms on v13 vs 2.28 on 21, causal 2.38
-        // vs 1.38 (profiles/r04/scale/time_v13_at_c_gt_1.jsonl; with the default: time_default.jsonl)
-        if (variant < 0)
-            variant = scale * 1.4426950408889634f > 1.f ? 21 : causal ? kDefaultCausalVariant : kDefaultVariant;
+        if (variant < 0) variant = causal ? kDefaultCausalVariant : kDefaultVariant;
         if (dtype == PLI_BF16)
             return head_dim == 128 ? launch_mfma<bf16_t, 128>(q, k, v, o, batch, heads, group, n_q, n_kv, st, scale, causal, s, variant)
                                    : launch_mfma<bf16_t, 64>(q, k, v, o, batch, heads, group, n_q, n_kv, st, scale, causal, s, variant);

@@ -208,7 +208,7 @@ extern "C" int pli_diag_v13_clock(const void* q, const void* k, const void* v, v
     using namespace pli;
     const int64_t sn = 128, sh = (int64_t)N * 128, sb = (int64_t)H * N * 128;
     const V7Strides st{sb, sh, sn, sb, sh, sn, sb, sh, sn, sb, sh, sn};
-    const int rc = launch_attn_v13(q, k, v, o, B, H, 1, N, N, st, 1.f / sqrtf(128.f), 0, true, 7.f, stamps, false);
+    const int rc = launch_attn_v13(q, k, v, o, B, H, 1, N, N, st, 1.f / sqrtf(128.f), 0, true, 62.f, stamps, false);
     if (rc != 0 || hipDeviceSynchronize() != hipSuccess) return -1;
     return 0;
 }

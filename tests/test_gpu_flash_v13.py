@@ -187,3 +187,31 @@ def test_v13_explicit_scale(scale, causal):
     err = max_err(out, ref)
     tol = 1e-2 if scale < 0.5 else 2.0 ** -8 * v.abs().max().item()
     assert err <= tol, f"scale {scale} causal {causal}: max |err| {err:.4e} > {tol:.4e}"
+
+
+@pytest.mark.parametrize("causal", (False, True))
+def test_v13_rescale_past_default_offset(causal):
+    """Row maxima that grow by more than the default mu offset + 1 (63 log2
+    units, PLI_V13_MUOFF in csrc/flash_attn.hip) inside one row: key 450
+    aligned with query 500 (~ +100 log2 units in tile 7) and key 200 with
+    query 300 (~ +75 in tile 3; both visible under the causal mask), so the
+    default program takes its rescale path on its own; against the f64
+    reference, and within rounding of 82 / 85 (the rescale path at nearly
+    every tile)."""
+    import numpy as np
+    import pli_hip
+    from oracle.numerics import round_to_bf16, seeded_normal
+    q = seeded_normal((1, 2, 512, 128), 31, "bf16")
+    k = seeded_normal((1, 2, 512, 128), 32, "bf16")
+    v = seeded_normal((1, 2, 512, 128), 33, "bf16")
+    k[:, :, 450] = 8.0 * np.sign(q[:, :, 500])
+    k[:, :, 200] = 6.0 * np.sign(q[:, :, 300])
+    q, k, v = dev(q), dev(round_to_bf16(k)), dev(v)
+    c = 128 ** -0.5 * 1.4426950408889634
+    rise = (q[0, :, 500].double() * k[0, :, 450].double()).sum(-1) * c
+    assert rise.min().item() > 64, "the spike must exceed the default offset"
+    var = 83 if causal else 80
+    out = pli_hip.flash_attn_fwd(q, k, v, causal=causal, variant=var)
+    err = max_err(out, torch_attention(q, k, v, causal=causal))
+    assert err <= 2.0 ** -8 * v.abs().max().item(), f"causal {causal}: {err:.4e}"
+    assert_agree_to_rounding(pli_hip.flash_attn_fwd(q, k, v, causal=causal, variant=var + 2), out, v)

@@ -5,7 +5,8 @@ ctypes side by side; each round times $ITERS back-to-back launches of its
 pli_flash_attn_fwd_variant (variant $VARIANT, default -1 = the default
 kernel) on the bench config (random data), libraries interleaved, after a
 warm-up; prints the median / min TF/s per library and whether its output is
-bitwise equal to the first library's.  $CAUSAL=1 times the causal form."""
+bitwise equal to the first library's.  $CAUSAL=1 times the causal form,
+$SCALE sets the softmax scale (default 1/sqrt(D))."""
 import ctypes
 import json
 import os
@@ -19,6 +20,7 @@ LIBS = os.environ.get("LIBS", "tools/ab/libpli_base.so physics-llm-inference_amd
 ROUNDS, ITERS = int(os.environ.get("ROUNDS", "8")), int(os.environ.get("ITERS", "20"))
 VARIANTS = [int(v) for v in os.environ.get("VARIANTS", os.environ.get("VARIANT", "-1")).split(",")]
 CAUSAL = int(os.environ.get("CAUSAL", "0"))
+SCALE = float(os.environ.get("SCALE", "0"))  # softmax scale (0: 1/sqrt(D))
 SHAPES = [tuple(int(x) for x in sh.split(",")) for sh in os.environ.get("SHAPE", "8,32,4096,128").split(";")]
 libs = []
 for p in LIBS:
@@ -41,7 +43,7 @@ for (B, H, N, D) in SHAPES:
     def call(a):
         li, var = arms[a]
         rc = libs[li](q.data_ptr(), k.data_ptr(), v.data_ptr(), outs[a].data_ptr(), B, H, H, N, N, D, st,
-                      D ** -0.5, CAUSAL, BF16, ctypes.c_void_p(stream.cuda_stream), var)
+                      SCALE or D ** -0.5, CAUSAL, BF16, ctypes.c_void_p(stream.cuda_stream), var)
         assert rc == 0, (LIBS[li], var, rc)
 
     pairs = N * (N + 1) // 2 if CAUSAL else N * N
@@ -62,7 +64,7 @@ for (B, H, N, D) in SHAPES:
             res[a].append(flops / (s.elapsed_time(e) / ITERS * 1e-3) / 1e12)
     ref = outs[0].float()
     for a, (li, var) in enumerate(arms):
-        print(json.dumps({"lib": LIBS[li], "shape": [B, H, N, D], "variant": var, "causal": CAUSAL,
+        print(json.dumps({"lib": LIBS[li], "shape": [B, H, N, D], "variant": var, "causal": CAUSAL, "scale": SCALE or D ** -0.5,
                           "TF/s_median": statistics.median(res[a]), "TF/s_min": min(res[a]),
                           "TF/s_max": max(res[a]), "bitwise_eq_first": bool(torch.equal(outs[a], outs[0])),
                           "max_diff_first": (outs[a].float() - ref).abs().max().item()}), flush=True)

@@ -17,7 +17,8 @@ Layout per wave (lane l: i = l & 15, g = l >> 4):
     permutation by two ds_read_b64_tr_b16 per fragment).
   * O^T = V^T P^T as 8 d-blocks x 4 q-blocks in a[0:127]; the row sum l on
     the matrix core (an all-ones A operand).
-  * Defer-max on P itself: mu = (row max) * c + 7 when a tile's max is
+  * Defer-max on P itself: mu = (row max) * c + muoff (a launch argument:
+    62 in the product since round 4, 7 before; the text below is for 7) when a tile's max is
     taken, so P <= 2^-7 right after; a tile is accepted while every P < 2,
     which is bit 14 of each bf16 half (one v_or3_b32 per two words).  P >= 2
     means the row max grew by 8 in log2 units (the THR 8 rule of v10/v12):
