@@ -592,7 +592,7 @@ int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int
             const V7Strides s7{st.qb, st.qh, st.qn, st.kb, st.kh, st.kn,
                                st.vb, st.vh, st.vn, st.ob, st.oh, st.on};
             return launch_attn_v12(q, k, v, o, B, H, group, Nq, Nk, s7, scale, stream, variant != 70,
-                                   variant == 72 ? 0.f : 8.f);
+                                   variant == 72 ? 0.f : 64.f);
         }
         variant = causal ? 60 : 55;
     }
@@ -601,7 +601,7 @@ int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int
         if (causal && attn_v12_ok(D, bf ? 1 : 0, 0, Nk) && Nq <= Nk && c_ok) {
             const V7Strides s7{st.qb, st.qh, st.qn, st.kb, st.kh, st.kn,
                                st.vb, st.vh, st.vn, st.ob, st.oh, st.on};
-            return launch_attn_v12(q, k, v, o, B, H, group, Nq, Nk, s7, scale, stream, variant == 74, 8.f, true);
+            return launch_attn_v12(q, k, v, o, B, H, group, Nq, Nk, s7, scale, stream, variant == 74, 64.f, true);
         }
         variant = causal ? 60 : 55;
     }

@@ -182,8 +182,10 @@ __device__ __forceinline__ float v12_xor32_sum(float x) {
 typedef __attribute__((ext_vector_type(2))) float v12f2;
 // defer-max threshold THR (log2 units, a template argument so the shipped
 // instantiation's register allocation is not touched): the shipped kernel
-// runs 8; variant 72 (tests only) runs 0, a rescale whenever a tile raises a
-// row's max
+// runs 64 since round 4 (8 before; P <= 2^64 is a normal bf16 / fp32 value,
+// and the rescale path all but vanishes where the scaled scores spread wide,
+// as for v13's offset 62, csrc/flash_attn.hip PLI_V13_MUOFF); variant 72
+// (tests only) runs 0, a rescale whenever a tile raises a row's max
 
 #ifdef PLI_FLASH_STAMPS
 // diagnostic build only (tools/build_diag.sh): per-segment s_memtime sums
@@ -258,7 +260,7 @@ __device__ __forceinline__ void causal_block(int l, int G, int nblocks, int qb, 
 // the wave's first masked one on are masked in place (-inf) right after their
 // QK^T chains, and the persistent walk is causal_block's pair walk (every
 // workgroup the same triangular share).
-template <int STAMP = 0, int THR = 8, bool CAUSAL = false>
+template <int STAMP = 0, int THR = 64, bool CAUSAL = false>
 __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
     uint16_t* __restrict__ o, int H, int group, int Nq, int Nk, V7Strides st, float c, int qblocks,
@@ -710,14 +712,15 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v12(
         // one temporary for the thresholds: the allocation has no room
         float tq;
         uint64_t hit;
-        static_assert(THR == 0 || THR == 8, "threshold literal");
+        static_assert(THR == 0 || THR == 8 || THR == 64, "threshold literal");
 #define V12_SETTLE_ASM(T)                                                                                      \
     asm volatile("v_mul_f32 %0, %0, %4\n\tv_mul_f32 %1, %1, %4\n\tv_add_f32 %2, " T ", %5\n\t"              \
                  "v_cmp_gt_f32_e64 %3, %0, %2\n\tv_add_f32 %2, " T ", %6\n\tv_cmp_gt_f32_e64 vcc, %1, %2\n\t" \
                  "s_or_b64 %3, %3, vcc"                                                                        \
                  : "+v"(mxA), "+v"(mxB), "=&v"(tq), "=&s"(hit)                                                  \
                  : "v"(c), "v"(mA), "v"(mB) : "vcc", "scc")
-        if constexpr (THR == 8) V12_SETTLE_ASM("0x41000000");
+        if constexpr (THR == 64) V12_SETTLE_ASM("0x42800000");
+        else if constexpr (THR == 8) V12_SETTLE_ASM("0x41000000");
         else V12_SETTLE_ASM("0");
 #undef V12_SETTLE_ASM
         if (__builtin_expect(hit != 0, 0)) {
@@ -1016,8 +1019,8 @@ bool attn_v12_ok(int D, int is_bf16, int causal, int Nk) {
 int launch_attn_v12(const void* q, const void* k, const void* v, void* o, int B, int H, int group, int Nq,
                     int Nk, const V7Strides& st, float scale, hipStream_t stream, bool persistent, float thr,
                     bool causal) {
-    PLI_REQUIRE(thr == 0.f || thr == 8.f, "attn_fwd_v12: defer-max threshold %g not built", thr);
-    PLI_REQUIRE(!causal || (thr == 8.f && Nq <= Nk), "attn_fwd_v12: causal needs Nq <= Nk (THR 8)");
+    PLI_REQUIRE(thr == 0.f || thr == 64.f, "attn_fwd_v12: defer-max threshold %g not built", thr);
+    PLI_REQUIRE(!causal || (thr == 64.f && Nq <= Nk), "attn_fwd_v12: causal needs Nq <= Nk (THR 64)");
     const int qblocks = cdiv(Nq, 256);
     const int64_t nb = (int64_t)B * H * qblocks;
     PLI_REQUIRE(nb < (1ll << 31), "pli_flash_attn_fwd: grid too large");
@@ -1054,13 +1057,13 @@ int launch_attn_v12(const void* q, const void* k, const void* v, void* o, int B,
     const auto* vv = (const uint16_t*)v;
     auto* oo = (uint16_t*)o;
     if (causal)
-        hipLaunchKernelGGL((attn_fwd_v12<0, 8, true>), gr, blk, 0, stream, qq, kk, vv, oo, H, group, Nq, Nk, st, c,
+        hipLaunchKernelGGL((attn_fwd_v12<0, 64, true>), gr, blk, 0, stream, qq, kk, vv, oo, H, group, Nq, Nk, st, c,
                            qblocks, (int)nb);
     else if (thr == 0.f)
         hipLaunchKernelGGL((attn_fwd_v12<0, 0>), gr, blk, 0, stream, qq, kk, vv, oo, H, group, Nq, Nk, st, c,
                            qblocks, (int)nb);
     else
-        hipLaunchKernelGGL((attn_fwd_v12<0, 8>), gr, blk, 0, stream, qq, kk, vv, oo, H, group, Nq, Nk, st, c,
+        hipLaunchKernelGGL((attn_fwd_v12<0, 64>), gr, blk, 0, stream, qq, kk, vv, oo, H, group, Nq, Nk, st, c,
                            qblocks, (int)nb);
     return launch_status("attn_fwd_v12");
 }
@@ -1084,10 +1087,10 @@ extern "C" int pli_diag_v12_stamps(const void* q, const void* k, const void* v, 
     const dim3 gr(grid > 0 && grid < nb ? grid : nb);
     // mode 1: per-segment stamps; mode 2: entry / exit clock only (words 0, 1)
     if (mode == 2)
-        hipLaunchKernelGGL((attn_fwd_v12<2, 8>), gr, dim3(256), 0, 0, (const uint16_t*)q, (const uint16_t*)k,
+        hipLaunchKernelGGL((attn_fwd_v12<2, 64>), gr, dim3(256), 0, 0, (const uint16_t*)q, (const uint16_t*)k,
                            (const uint16_t*)v, (uint16_t*)o, H, 1, N, N, st, c, qblocks, nb);
     else
-        hipLaunchKernelGGL((attn_fwd_v12<1, 8>), gr, dim3(256), 0, 0, (const uint16_t*)q, (const uint16_t*)k,
+        hipLaunchKernelGGL((attn_fwd_v12<1, 64>), gr, dim3(256), 0, 0, (const uint16_t*)q, (const uint16_t*)k,
                            (const uint16_t*)v, (uint16_t*)o, H, 1, N, N, st, c, qblocks, nb);
     if (hipDeviceSynchronize() != hipSuccess) return -1;
     hipMemcpyFromSymbol(out, HIP_SYMBOL(g_v12_stamps), 24 * sizeof(unsigned long long));

@@ -37,7 +37,10 @@ typedef __attribute__((ext_vector_type(2))) float f32x2;
 constexpr int V7_KT = 64;       // keys per tile
 constexpr int V7_QW = 32;       // query rows per wave
 constexpr int V7_NW = 8;        // waves per workgroup
-constexpr float V7_THR = 8.f;   // defer-max threshold (log2 units): P <= 2^8
+// defer-max threshold (log2 units): P <= 2^THR.  bf16 64 since round 4 (8
+// before; a normal bf16 / fp32 value, the rescale path all but vanishes where
+// the scaled scores spread wide -- as v12 / v13); fp16 8 (its P stops at 2^15)
+template <typename T> constexpr float v7_thr() { return std::is_same<T, bf16_t>::value ? 64.f : 8.f; }
 
 template <int D> struct V7Layout {
     static constexpr int KS = 2 * D + 16;  // K row stride (bytes): b128 reads conflict-free
@@ -286,7 +289,7 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_v7(
             expo();
             asm volatile("" : "+v"(s[0]), "+v"(s[1]));
             stamp(2);
-            const bool up = PRE != 0 ? mx > V7_THR : mx * c > m_run + V7_THR;
+            const bool up = PRE != 0 ? mx > v7_thr<T>() : mx * c > m_run + v7_thr<T>();
             if (__ballot(up)) {
                 // rare: some row's max rose by more than the threshold.  K(t)
                 // is still in LDS: recompute S and redo the exps.  (O holds
@@ -642,7 +645,7 @@ __global__ __launch_bounds__(NW4 ? 256 : 512, 2) void attn_fwd_v10(
             expo();
             asm volatile("" : "+v"(s[0]), "+v"(s[1]));
             stamp(2);
-            const bool up = PRE != 0 ? mx > V7_THR : mx * c > m_run + V7_THR;
+            const bool up = PRE != 0 ? mx > v7_thr<T>() : mx * c > m_run + v7_thr<T>();
             if (__ballot(up)) {
                 float alpha;
                 if constexpr (PRE != 0) {
