@@ -15,9 +15,10 @@
 // program in a CPU emulator; tests/test_gpu_flash_v13.py on the device.
 //
 // Differences from v12 a caller can see: none in the contract; numerically
-// P = bf16(exp2(s c - mu)) with mu = (row max) c + 7 (P <= 2^-7 when the max
-// is taken, checked < 2 per tile, i.e. the same THR 8 defer-max rule in
-// log2 units), l from the same rounded P on the matrix core, 1/l by v_rcp.
+// P = bf16(exp2(s c - mu)) with mu = (row max) c + muoff (62 from the
+// launcher: P <= 2^-62 when the max is taken, checked < 2 per tile, so a row
+// max may grow by 63 log2 units before the rescale path -- v12's THR 64
+// rule), l from the same rounded P on the matrix core, 1/l by v_rcp.
 #include <cstring>
 
 #include "flash_v7.h"
