@@ -40,11 +40,12 @@ def f64_attention(q, k, v, causal=False):
 
 
 CASES = [  # (B, H, Hkv, Nq, Nk, grid, layout, muoff, causal)
+    # muoff 62: the product's offset (csrc/flash_attn.hip PLI_V13_MUOFF); 7: round 4's first builds
     (1, 1, 1, 256, 128, None, "bhsd", 7.0, False),      # one block, two key tiles
-    (1, 2, 2, 256, 320, 1, "bhsd", 7.0, False),         # persistent: two blocks of five tiles on one workgroup
+    (1, 2, 2, 256, 320, 1, "bhsd", 62.0, False),        # persistent: two blocks of five tiles on one workgroup
     (2, 2, 1, 200, 128, 1, "bshd", 7.0, False),         # GQA, ragged Nq, BSHD strides, nt = 2 across seams
     (1, 1, 1, 256, 256, None, "bhsd", -1.0, False),     # the rescale path at nearly every tile
-    (1, 2, 1, 256, 512, None, "bhsd", 7.0, True),       # causal, Nq < Nk (diagonal offset 4 tiles)
+    (1, 2, 1, 256, 512, None, "bhsd", 62.0, True),      # causal, Nq < Nk (diagonal offset 4 tiles)
     (1, 1, 1, 512, 512, None, "bhsd", -1.0, True),      # causal, two blocks, rescales on masked tiles
 ]
 
@@ -87,3 +88,19 @@ def test_v13_header_is_current():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_flash_v13.py"), "--check"],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_v13_spike_past_product_offset():
+    """at the product's mu offset (62): key 200 aligned with query 230 raises
+    that row's max by ~100 log2 units in tile 3, past the 63 the offset
+    allows, so the rare path runs; P <= 2^-62 elsewhere stays exact"""
+    rng = np.random.default_rng(5)
+    q = rng.standard_normal((1, 1, 256, 128))
+    k = rng.standard_normal((1, 1, 256, 128))
+    v = rng.standard_normal((1, 1, 256, 128))
+    k[0, 0, 200] = 8.0 * np.sign(q[0, 0, 230])
+    assert (q[0, 0, 230] @ k[0, 0, 200]) / np.sqrt(128) * np.log2(np.e) > 64
+    o, em = R.run(q, k, v, muoff=62.0)
+    assert em.counts.get("v_sub_f32", 0) > 0, "the rescale path never ran"
+    err = np.abs(o - f64_attention(q, k, v)).max()
+    assert err <= 2.0 ** -8 * np.abs(v).max(), f"max |err| {err:.3e}"
