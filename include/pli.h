@@ -347,8 +347,9 @@ int pli_attn_decode_dev(const void* q, const void* k, const void* v, void* o,
  *   causal forms (83 = causal default where (Nk - Nq) % 64 == 0; other
  *   shapes take 74 / 60).  Prescaled variants round Q * scale * log2(e) to
  *   the 16-bit input type (2^-9 relative score error in bf16).  The v13
- *   forms take any scale > 0; v7 / v10 / v12 take scale * log2(e) <= 1
- *   and larger scales fall back to 21.
+ *   forms, v12 and the exact v7 / v10 bodies (51 / 55 / 60) take any
+ *   scale > 0; the prescaled 50 / 54 take scale * log2(e) <= 1 (larger
+ *   scales fall back to 21).
  * pli_gemm_w5 schedule (all gemm_w5 routes): W5_SPLIT, DMA spread over both
  *   halves of each 64-deep K step (gemm_w5.hip).
  * pli_gemm_variant / pli_gemm_ws_variant: 0 default; 1 128^2 tile; 2 256^2

@@ -576,6 +576,9 @@ int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int
     // v7 / v10 also prescale Q by c, so c > 1 could overflow fp16 Q.
     const float c_log2 = scale * 1.4426950408889634f;
     const bool c_ok = c_log2 > 0.f && c_log2 <= 1.f;
+    // the exact bodies (v12 70-74, v7 / v10 51 / 55 / 60) apply c by fma to
+    // the fp32 scores: any c > 0; only the prescaled ones (50 / 54) need c <= 1
+    const bool c_pos = c_log2 > 0.f;
     if (variant >= 80 && variant <= 85) {
         const bool bf = std::is_same<T, bf16_t>::value;
         const bool cv = variant >= 83;  // the causal forms
@@ -588,7 +591,7 @@ int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int
     }
     if (variant == 70 || variant == 71 || variant == 72) {
         const bool bf = std::is_same<T, bf16_t>::value;
-        if (attn_v12_ok(D, bf ? 1 : 0, causal, Nk) && c_ok) {
+        if (attn_v12_ok(D, bf ? 1 : 0, causal, Nk) && c_pos) {
             const V7Strides s7{st.qb, st.qh, st.qn, st.kb, st.kh, st.kn,
                                st.vb, st.vh, st.vn, st.ob, st.oh, st.on};
             return launch_attn_v12(q, k, v, o, B, H, group, Nq, Nk, s7, scale, stream, variant != 70,
@@ -598,7 +601,7 @@ int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int
     }
     if (variant == 73 || variant == 74) {
         const bool bf = std::is_same<T, bf16_t>::value;
-        if (causal && attn_v12_ok(D, bf ? 1 : 0, 0, Nk) && Nq <= Nk && c_ok) {
+        if (causal && attn_v12_ok(D, bf ? 1 : 0, 0, Nk) && Nq <= Nk && c_pos) {
             const V7Strides s7{st.qb, st.qh, st.qn, st.kb, st.kh, st.kn,
                                st.vb, st.vh, st.vn, st.ob, st.oh, st.on};
             return launch_attn_v12(q, k, v, o, B, H, group, Nq, Nk, s7, scale, stream, variant == 74, 64.f, true);
@@ -606,7 +609,7 @@ int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int
         variant = causal ? 60 : 55;
     }
     if (variant == 50 || variant == 51 || variant == 54 || variant == 55 || variant == 60) {
-        if (c_ok) {
+        if (variant == 50 || variant == 54 ? c_ok : c_pos) {
             const V7Strides s7{st.qb, st.qh, st.qn, st.kb, st.kh, st.kn,
                                st.vb, st.vh, st.vn, st.ob, st.oh, st.on};
             return launch_attn_v7(q, k, v, o, B, H, group, Nq, Nk, D, s7, scale, causal,

@@ -231,3 +231,39 @@ def test_v12_causal_stress():
         out = pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=74)
         err = max_err(out, torch_attention(q, k, v, causal=True))
         assert err <= 2.0 ** -8 * v.abs().max().item(), f"{name}: {err:.4e}"
+
+
+def _scaled_ref(q, k, v, scale, causal):
+    g = q.shape[1] // k.shape[1]
+    kf, vf = (t.double().repeat_interleave(g, dim=1) for t in (k, v))
+    sc = (q.double() @ kf.transpose(-1, -2)) * scale
+    if causal:
+        nq, nk = q.shape[2], k.shape[2]
+        i = torch.arange(nq, device=q.device)[:, None]
+        j = torch.arange(nk, device=q.device)[None, :]
+        sc = sc.masked_fill(j > i + (nk - nq), float("-inf"))
+    return torch.softmax(sc, -1) @ vf
+
+
+@pytest.mark.parametrize("scale", (1.0, 0.25))
+@pytest.mark.parametrize("case", [(128, "bf16", 71, False), (128, "bf16", 74, True), (128, "bf16", 55, False),
+                                  (128, "bf16", 60, True), (128, "f16", None, False), (64, "bf16", None, False),
+                                  (64, "f16", None, True), (64, "bf16", 51, True)],
+                         ids=lambda c: "d{}-{}-v{}-causal{}".format(*c))
+def test_fallback_bodies_explicit_scale(case, scale):
+    """The exact fallback bodies (v12 71 / 74, v10 55 / 60, v7 51; D = 64 and
+    fp16 by the default route) apply c = scale * log2(e) by fma to fp32
+    scores, so scale 1.0 (c > 1) runs on them instead of variant 21; against
+    an f64 attention with the same scale.  Defer threshold 64 (bf16) / 8
+    (fp16): at scale 1.0 the rescale path runs in most rows."""
+    import pli_hip
+    D, dt, var, causal = case
+    dtype = torch.bfloat16 if dt == "bf16" else torch.float16
+    gen = torch.Generator(device=DEV).manual_seed(D + (var or 0) + int(scale * 8))
+    q = torch.randn(2, 8, 320, D, device=DEV, dtype=dtype, generator=gen)
+    k = torch.randn(2, 2, 384, D, device=DEV, dtype=dtype, generator=gen)
+    v = torch.randn(2, 2, 384, D, device=DEV, dtype=dtype, generator=gen)
+    out = pli_hip.flash_attn_fwd(q, k, v, scale=scale, causal=causal, variant=var)
+    err = max_err(out, _scaled_ref(q, k, v, scale, causal))
+    tol = 2.0 ** -8 * v.abs().max().item()
+    assert err <= tol, f"{case} scale {scale}: max |err| {err:.4e} > {tol:.4e}"
