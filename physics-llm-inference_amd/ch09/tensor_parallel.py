@@ -59,8 +59,10 @@ def _shard_linear_f32(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 
 
 def tp_group_active(world_size: int, group=None) -> bool:
-    """True when a process group of exactly ``world_size`` ranks exists."""
-    return (world_size > 1 and dist.is_available() and dist.is_initialized()
+    """True when a process group of exactly ``world_size`` ranks exists.  A
+    one-rank layer reduces only through a group passed to it explicitly (the
+    reference's single-process behaviour stays the default)."""
+    return ((world_size > 1 or group is not None) and dist.is_available() and dist.is_initialized()
             and dist.get_world_size(group) == world_size)
 
 
@@ -119,13 +121,25 @@ class RowParallelLinear(nn.Module):
 
 
 def row_parallel_forward_overlapped(x: torch.Tensor, weight: torch.Tensor, chunks: int = 4,
-                                    group=None) -> torch.Tensor:
+                                    group=None, world_size: int | None = None,
+                                    reduce_dtype: torch.dtype | None = None) -> torch.Tensor:
     """Chunked RowParallel forward: GEMM of rows-chunk i+1 overlaps the async
-    all-reduce of chunk i (RCCL runs on its own stream).  Same result as
-    ``RowParallelLinear.forward`` up to fp32-accumulate rounding."""
+    all-reduce of chunk i (RCCL runs on its own stream, ordered after the
+    chunk's GEMM on the current stream; ``wait`` orders the caller after all
+    of them).  ``world_size`` is the layer's TP degree (default: the group's
+    size) and gates the all-reduce exactly as ``RowParallelLinear.forward``
+    does (``tp_group_active``); ``reduce_dtype=torch.float32`` keeps the
+    partials in fp32 (``pli_gemm_f32out``) through the all-reduce and rounds
+    the sum once.  Same result as ``RowParallelLinear.forward`` up to the
+    per-chunk GEMM's accumulation order."""
+    assert reduce_dtype in (None, torch.float32), "reduce_dtype: None or torch.float32"
+    if world_size is None:
+        world_size = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    reduce = tp_group_active(world_size, group)
     x2 = x.reshape(-1, x.shape[-1])
     m = x2.shape[0]
-    out = torch.empty(m, weight.shape[0], dtype=x.dtype, device=x.device)
+    f32 = reduce_dtype is not None and x.dtype != reduce_dtype
+    out = torch.empty(m, weight.shape[0], dtype=torch.float32 if f32 else x.dtype, device=x.device)
     bounds = [m * i // chunks for i in range(chunks + 1)]
     handles = []
     for i in range(chunks):
@@ -133,14 +147,20 @@ def row_parallel_forward_overlapped(x: torch.Tensor, weight: torch.Tensor, chunk
         if hi == lo:
             continue
         part = out[lo:hi]
-        if x2.is_cuda:
+        if f32 and x2.is_cuda:
+            pli_hip.gemm_f32out(x2[lo:hi], weight.detach(), out=part)
+        elif f32:
+            part.copy_(F.linear(x2[lo:hi].float(), weight.detach().float()))
+        elif x2.is_cuda:
             pli_hip.gemm(x2[lo:hi], weight.detach(), trans_b=True, out=part)
         else:
             part.copy_(F.linear(x2[lo:hi], weight))
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        if reduce:
             handles.append(dist.all_reduce(part, op=dist.ReduceOp.SUM, group=group, async_op=True))
     for h in handles:
         h.wait()
+    if f32:
+        out = out.to(x.dtype)
     return out.view(*x.shape[:-1], weight.shape[0])
 
 

@@ -471,25 +471,6 @@ def test_row_parallel_shard_full_config(tp):
     assert_lin_close(torch.from_numpy(y[rows]), olin.linear(x[rows], w), "bf16", f"TP{tp} shard")
 
 
-@pytest.mark.skipif(not torch.cuda.is_available() or torch.cuda.device_count() < 2,
-                    reason="needs >= 2 visible GPUs (RCCL all-reduce of the row-parallel partials)")
-def test_row_parallel_rccl_two_ranks():
-    """HIP shard GEMM + dist.all_reduce over RCCL ("nccl" backend), 2 ranks
-    on 2 GPUs: the all-reduced partials equal the full F.linear within the
-    bf16 partial-rounding bound (tests/tp_rccl_worker.py)."""
-    import socket
-    import subprocess
-    import sys
-    with socket.socket() as sk:  # a free port: a stale listener on a fixed one would fail the rendezvous
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
-    worker = os.path.join(os.path.dirname(__file__), "tp_rccl_worker.py")
-    procs = [subprocess.Popen([sys.executable, worker, str(r), "2"], env=env) for r in range(2)]
-    rcs = [p.wait(timeout=110) for p in procs]
-    assert rcs == [0, 0], rcs
-
-
 # ------------------------------------------------------- softmax / stream ---
 @pytest.mark.parametrize("shape,dt", [((4, 8, 64), "fp32"), ((5,), "fp32"), ((33, 1000), "bf16"),
                                       ((7, 4097), "fp16")])

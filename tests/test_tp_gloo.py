@@ -48,6 +48,9 @@ def _worker(rank: int, world: int, port: int, out_dir: str):
             l32 = RowParallelLinear(K, N, world_size=world, rank=rank, reduce_dtype=torch.float32)
             l32.weight.copy_(w[:, sl])
             y3 = l32.to(torch.bfloat16)(x[:, sl].to(torch.bfloat16)).float()
+            # the chunked form with fp32 partials, keyed on the layer's world size
+            y4 = row_parallel_forward_overlapped(x[:, sl].to(torch.bfloat16), l32.weight, chunks=3,
+                                                 world_size=world, reduce_dtype=torch.float32).float()
         # TP MLP: every rank must end with the same full output
         torch.manual_seed(100 + rank)
         mlp = TensorParallelMLP(TensorParallelConfig(world_size=world, rank=rank, hidden_dim=16,
@@ -55,7 +58,7 @@ def _worker(rank: int, world: int, port: int, out_dir: str):
         with torch.no_grad():
             ym = mlp(torch.ones(3, 16))
         np.savez(os.path.join(out_dir, f"rank{rank}.npz"), y=y.numpy(), y2=y2.numpy(), ym=ym.numpy(),
-                 y3=y3.numpy())
+                 y3=y3.numpy(), y4=y4.numpy())
     finally:
         dist.destroy_process_group()
 
@@ -81,3 +84,5 @@ def test_row_parallel_allreduce_gloo_world2(tmp_path):
     full16 = linear(round_to_bf16(x), round_to_bf16(w))
     for ri in r:
         assert np.abs(ri["y3"] - full16).max() <= 2.0 ** -8 * (np.abs(full16).max() + 1)
+        assert np.abs(ri["y4"] - full16).max() <= 2.0 ** -8 * (np.abs(full16).max() + 1)
+        np.testing.assert_allclose(ri["y4"], ri["y3"], rtol=2.0 ** -7, atol=1e-6)

@@ -206,7 +206,7 @@ LDS_GAP = 1024  # LDS bytes per wave per 16-cycle gap (256 B/clk per CU, 4 waves
 
 # timing-only A/B knobs (tools/build_v13_ab.sh; Gen(abl=..., dma_cost=...)):
 # ABL "dma" drops the LDS-DMA loads, "exp" turns v_exp_f32 into v_mov_b32,
-# "check" drops the defer-max branch; in the step loop only: "kread" / "vread"
+# "check" drops the defer-max branch, "or" the v_or3_b32 that gather its bits; in the step loop only: "kread" / "vread"
 # drop the K / V fragment reads, "barrier" the per-step barrier, "soft" the
 # softmax stream -- results wrong, timing only
 ABL = set()
@@ -382,6 +382,8 @@ def softmax_fills(X, slices, earliest_of, deadline_of=None, ytag=0, prev_cv=None
         fills += grp
         groups.append(grp)
         cvs.append((cv, w))
+        if len(cvs) == 2 and "or" in ABL:  # timing-only: no defer-max bits (use with abl "check")
+            cvs = []
         if len(cvs) == 2:
             (c0, w0), (c1, w1) = cvs
             od = [c0, c1] + ([last_or] if last_or else [])
