@@ -534,18 +534,19 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
 //      defer-max on P itself (bf16, D = 128, non-causal, Nk % 64 == 0, Nk >=
 //      128; else 71)
 //  81: variant 80 with one block per workgroup
-//  82: variant 80 with mu = max * c - 1 (a rescale at nearly every tile whose
-//      max reaches the running max): tests only, exercises the rare path
+//  82: variant 80 with mu = max * c (P = 1 at the max, so every row's l >= 1
+//      and the rare path runs at every tile): tests only
 //  83 / 84: attn_fwd_v13c causal (bottom-right, Nq <= Nk, (Nk - Nq) % 64 ==
 //      0): 83 persistent (the pair walk where it tiles the grid), 84 one
-//      block per workgroup heaviest first; 85 = 83 with mu = max * c - 1
+//      block per workgroup heaviest first; 85 = 83 with mu = max * c
 // default since round 4: attn_fwd_v13 (80), 1388 vs 1242 TF/s for v12 (71)
 // at B8 S4096 H32 D128 in the same process (profiles/r04/flash/ab.log); where
 // v13 does not apply (fp16, D != 128, Nk % 64, Nk < 128) it routes to 71
 constexpr int kDefaultVariant = 80;
 // v13's mu = row max * c + PLI_V13_MUOFF (log2 units): P <= 2^-MUOFF right
-// after a max is taken and a tile takes the rescale path once a row max grows
-// by MUOFF + 1 (some P >= 2).  62 (since round 4; was 7, the THR 8 of v10 /
+// after a max is taken and a tile takes the rescale path once some row's sum l
+// reaches 1 (since round 5; a row max grown by about MUOFF - log2 Nk -- the P
+// >= 2 bit test of round 4 fired at MUOFF + 1).  62 (since round 4; was 7, the THR 8 of v10 /
 // v12): P stays a normal bf16 / fp32 down to 2^-126, so only scores 64+ log2
 // units under the row max flush to 0 (weight < 2^-64), and the rescale path
 // all but vanishes where the scaled scores spread wide -- B8 H32 S4096, N(0,1)
@@ -586,7 +587,7 @@ int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int
         // v13 scales in fp32 (s * c - mu by v_fma): any c > 0 (scale = 1 etc.)
         if (cv == (causal != 0) && attn_v13_ok(D, bf ? 1 : 0, causal, Nq, Nk, s7) && c_log2 > 0.f)
             return launch_attn_v13(q, k, v, o, B, H, group, Nq, Nk, s7, scale, stream, variant != 81 && variant != 84,
-                                   (variant == 82 || variant == 85) ? -1.f : PLI_V13_MUOFF, nullptr, causal != 0);
+                                   (variant == 82 || variant == 85) ? 0.f : PLI_V13_MUOFF, nullptr, causal != 0);
         variant = causal ? 74 : 71;
     }
     if (variant == 70 || variant == 71 || variant == 72) {

@@ -19,6 +19,7 @@ Semantics of the less common instructions, as this file implements them:
       offset + 16 * lane
   v_permlane16_swap_b32 a, b  rows (16 lanes) 1, 3 of a <-> rows 0, 2 of b
   v_permlane32_swap_b32 a, b  lanes 32-63 of a <-> lanes 0-31 of b
+  v_exp_f32 ... clamp  VOP3 clamp of the result to [0, 1]
 """
 from __future__ import annotations
 
@@ -332,13 +333,20 @@ class Emu:
             return self.vset(w, o[0], f2u(np.maximum(np.maximum(gf(o[1]), gf(o[2])), gf(o[3]))))
         if op == "v_exp_f32":
             with np.errstate(over="ignore"):
-                return self.vset(w, o[0], f2u(np.exp2(gf(o[1]))))
+                r = np.exp2(gf(o[1]))
+            if "clamp" in ins.mods.split():  # VOP3 clamp: [0, 1] (NaN -> 0)
+                r = np.where(np.isnan(r), np.float32(0), np.clip(r, np.float32(0), np.float32(1)))
+            return self.vset(w, o[0], f2u(r.astype(np.float32)))
         if op == "v_rcp_f32":
             with np.errstate(divide="ignore"):
                 return self.vset(w, o[0], f2u(np.float32(1.0) / gf(o[1])))
         if op == "v_cvt_pk_bf16_f32":
             lo, hi = bf16_rne(gf(o[1])), bf16_rne(gf(o[2]))
             return self.vset(w, o[0], lo | (hi << 16))
+        if op in ("v_cmp_lt_f32_e32", "v_cmp_le_f32_e32"):
+            a, b = gf(o[1]), gf(o[2])
+            w.vcc = np.where(w.exec, a < b if op == "v_cmp_lt_f32_e32" else a <= b, False)
+            return
         if op in ("v_cmp_ne_u32_e32", "v_cmp_gt_u32_e32", "v_cmp_gt_i32_e32", "v_cmp_lt_i32_e32"):
             a, b = g(o[1]), g(o[2])
             if op.endswith("i32_e32"):

@@ -215,6 +215,19 @@ DMA_COST = 8
 # block (bf16, RNE) and -mu enters as the first QK MFMA's C operand, so the
 # softmax stream is exp2(S) in place + cvt: no v_fma_f32 per score
 QSCALE = [False]
+# LCHECK (Gen(lcheck=True), the product since round 5): the defer-max check
+# reads the row sums l instead of OR-ing the bits of every P word.  P =
+# bf16(exp2(s c - mu)) with v_exp_f32's clamp (P <= 1: never inf), the row-sum
+# MFMAs of tile t-1 run at the end of QK(t) (before the check, not in PV(t-1)),
+# and a tile takes the rare path once some row's l >= 1.  In the normal regime
+# l <= Nk 2^(growth - muoff) << 1; l >= 1 needs a row max grown by about muoff
+# - log2(Nk) -- the same event the P >= 2 bit test caught at muoff + 1, a
+# little earlier.  A clamped P (growth > muoff) is caught the same way (it
+# adds 1 to l) and redone by the rare path, which first takes the tile's old
+# sums back out of l.  Saves the 16 v_or3_b32 + v_and + v_cmp per wave-tile
+# (3 VALU instead).
+LCHECK = [True]
+NEGONES = 0xBF80BF80
 
 
 def schedule(mfmas, fills, budget=8, gap_offset=0, lds_gap=LDS_GAP):
@@ -303,19 +316,43 @@ def qk_done_gap(kb, qb):
     return 16 * qb + 12 + kb
 
 
+def rowsum_mfmas(X, ones=None):
+    """l(qb) += 1^T P(X, qb, kp) for the tile in P state X (all-ones A operand)"""
+    ones = ONES if ones is None else ones
+    return [mfma(L_(qb), ones, P_(X, qb, kp), L_(qb)) for qb in range(4) for kp in range(2)]
+
+
+def qk_with_rowsums(mask=None, muc=False, Xr=None):
+    """LCHECK: QK(t) with the row sums of tile t-1 (state Xr) interleaved
+    into its last 8 MFMAs (after every deferred slice of t-1 is due, so the
+    check right after the phase reads complete sums); returns the MFMA list
+    and done(kb, qb) -> the gap after which S(kb, qb) is complete"""
+    qk = qk_mfmas(mask, muc)
+    if Xr is None:
+        return qk, lambda kb, qb: qk_done_gap(kb, qb)
+    rs = rowsum_mfmas(Xr)
+    out, pos = qk[:56], {}
+    for j in range(56, 64):
+        out += [rs[j - 56], qk[j]]
+    for j in range(64):
+        pos[j] = j if j < 56 else 2 * j - 55
+    return out, lambda kb, qb: pos[qk_done_gap(kb, qb)]
+
+
 def pv_mfmas(X):
     out = []
     for db in range(8):
         for kp in range(2):
             for qb in range(4):
                 out.append(mfma(O_(db, qb), VF(db % NVF, kp), P_(X, qb, kp), O_(db, qb)))
-        qb, kp = db % 4, db // 4
-        out.append(mfma(L_(qb), ONES, P_(X, qb, kp), L_(qb)))
+        if not LCHECK[0]:
+            qb, kp = db % 4, db // 4
+            out.append(mfma(L_(qb), ONES, P_(X, qb, kp), L_(qb)))
     return out
 
 
 def pv_first_gap(db):
-    return 9 * db
+    return (8 if LCHECK[0] else 9) * db
 
 
 def k_reads():
@@ -371,8 +408,9 @@ def softmax_fills(X, slices, earliest_of, deadline_of=None, ytag=0, prev_cv=None
                       tag="exp", hard=dl is not None)
             f0 = f1 = None
         else:
-            e0 = Fill(I("v_exp_f32", y0, y0), 8, trans=True, deps=[f0], sep=1, tag="exp")
-            e1 = Fill(I("v_exp_f32", y1, y1), 8, trans=True, deps=[f1], sep=1, tag="exp")
+            xm = "clamp" if LCHECK[0] else ""
+            e0 = Fill(I("v_exp_f32", y0, y0, mods=xm), 8, trans=True, deps=[f0], sep=1, tag="exp")
+            e1 = Fill(I("v_exp_f32", y1, y1, mods=xm), 8, trans=True, deps=[f1], sep=1, tag="exp")
         fm = f1
         w = P_(X, qb, kb >> 1)[2 * (kb & 1) + hh]
         cv = Fill(I("v_cvt_pk_bf16_f32", w, y0, y1), 4, deps=[e0, e1], sep=1, tag="cvt",
@@ -382,7 +420,7 @@ def softmax_fills(X, slices, earliest_of, deadline_of=None, ytag=0, prev_cv=None
         fills += grp
         groups.append(grp)
         cvs.append((cv, w))
-        if len(cvs) == 2 and "or" in ABL:  # timing-only: no defer-max bits (use with abl "check")
+        if len(cvs) == 2 and ("or" in ABL or LCHECK[0]):  # LCHECK / timing-only "or": no defer-max bits
             cvs = []
         if len(cvs) == 2:
             (c0, w0), (c1, w1) = cvs
@@ -592,10 +630,11 @@ def exps_all(X, also_or=False, shifted=False):
             c += [I("v_sub_f32", y0, s[2 * hh], MU(qb)), I("v_sub_f32", y1, s[2 * hh + 1], MU(qb)),
                   I("v_exp_f32", y0, y0), I("v_exp_f32", y1, y1)]
         else:
+            xm = "clamp" if LCHECK[0] else ""
             c += [I("v_fma_f32", y0, s[2 * hh], sC, Neg(MU(qb))), I("v_fma_f32", y1, s[2 * hh + 1], sC, Neg(MU(qb))),
-                  I("v_exp_f32", y0, y0), I("v_exp_f32", y1, y1)]
+                  I("v_exp_f32", y0, y0, mods=xm), I("v_exp_f32", y1, y1, mods=xm)]
         c += [I("v_cvt_pk_bf16_f32", w, y0, y1)]
-        if also_or:
+        if also_or and not LCHECK[0]:
             c.append(I("v_or_b32", ACC(X), ACC(X), w))
     return c
 
@@ -624,9 +663,11 @@ class Gen:
     bottom-right-masked kernel (attn_fwd_v13c)"""
 
     def __init__(self, ndef=4, budget=8, dma_spacing=6, tag="%=", stamp=False, causal=False, abl=(), dma_cost=8,
-                 rev=True, qscale=False, dma_pv=0, dma_pv_spacing=16, budget_pv=None):
+                 rev=True, qscale=False, dma_pv=0, dma_pv_spacing=16, budget_pv=None, lcheck=True):
         global DMA_COST
         QSCALE[0] = bool(qscale)
+        assert not (qscale and lcheck), "QSCALE is built on the P-bit check (lcheck=False)"
+        LCHECK[0] = bool(lcheck)
         # causal: the second block of each pair streams its tiles in the
         # reversed order of tile_of (its 8 workgroups then read every K/V
         # tile at the same time)
@@ -804,7 +845,8 @@ class Gen:
             e([I("s_lshr_b32", sTD, sCQ0, 6), I("s_add_u32", sTD, sTD, sOFFT)])  # the wave's diagonal tile
         e([I("v_accvgpr_write_b32", A(k), 0) for k in range(128)])
         e([I("v_mov_b32", L_(qb)[r], 0) for qb in range(4) for r in range(4)])
-        e([I("v_mov_b32", ACC(0), 0), I("v_mov_b32", ACC(1), 0)])
+        if not LCHECK[0]:
+            e([I("v_mov_b32", ACC(0), 0), I("v_mov_b32", ACC(1), 0)])
         e([I("s_waitcnt", "vmcnt(0)"), I("s_barrier")])
         if QSCALE[0]:
             e(self.q_prescale())
@@ -918,6 +960,11 @@ class Gen:
         if "check" in ABL:
             e([label(ret)])
             return
+        if LCHECK[0]:  # some row's l >= 1 (its row sums ran right before)
+            e([I("v_max3_f32", T(37), L_(0)[0], L_(1)[0], L_(2)[0]), I("v_max_f32", T(37), T(37), L_(3)[0]),
+               I("v_cmp_le_f32_e32", VCC, 1.0, T(37)),  # 1 <= l: a clamped P (= 1) alone trips it
+               I("s_mov_b32", sRET, k), I("s_cbranch_vccnz", Lb(rare_block)), label(ret)])
+            return
         e([I("v_and_b32", T(37), 0x40004000, ACC(Xc)), I("v_cmp_ne_u32_e32", VCC, 0, T(37)),
            I("s_mov_b32", sRET, k), I("s_cbranch_vccnz", Lb(rare_block)), label(ret)])
 
@@ -955,10 +1002,12 @@ class Gen:
             for ins in v_reads(db):
                 if "vread" not in ABL:
                     fills.append(Fill(ins, 2, earliest=40 + 8 * db, tag="vread"))
-        # softmax(t), zero ACC(X) first
+        # softmax(t), zero ACC(X) first (P-bit check)
+        qk, done = qk_with_rowsums(mask, QSCALE[0], Xp if LCHECK[0] else None)
         z = Fill(I("v_mov_b32", ACC(X), 0), 4, tag="zero")
-        fills.append(z)
-        f_now, cvn, last_or = softmax_fills(X, now, lambda qb, kb: qk_done_gap(kb, qb) + 3, ytag=len(dfr),
+        if not LCHECK[0]:
+            fills.append(z)
+        f_now, cvn, last_or = softmax_fills(X, now, lambda qb, kb: done(kb, qb) + 3, ytag=len(dfr),
                                             prev_cv=cvd)
         now_groups = softmax_fills.groups
         if "soft" in ABL:
@@ -969,7 +1018,7 @@ class Gen:
         fills += f_now
         if QSCALE[0] and mask == "diag":
             e([I("v_add_f32", TRIMU(qb)[r], TRI[r], MUC(qb)[r]) for qb in range(4) for r in range(4)])
-        body, left = schedule(qk_mfmas(mask, muc=QSCALE[0]), fills, self.budget)
+        body, left = schedule(qk, fills, self.budget)
         e(body)
         # everything of tile t-1 must be done before its check
         pend_prev = [f for f in left if f in f_def or f.tag.startswith("dma")]
@@ -979,14 +1028,14 @@ class Gen:
         for grp in now_groups:
             if any(f.gap is not None for f in grp):
                 pend_prev += [f for f in grp if f.gap is None]
-        e(drain(pend_prev, 63))
+        e(drain(pend_prev, len(qk) - 1))
         left = [f for f in left if f.gap is None]
         # ---- defer-max check of tile t-1
         self.check(Xp, f"rare_s{Xp}")
         e([I("s_waitcnt", "vmcnt(8)")] + ([] if "barrier" in ABL else [I("s_barrier")]))
-        # ---- PV phase (gaps numbered on from the QK phase's 64, so the
+        # ---- PV phase (gaps numbered on from the QK phase's, so the
         # leftover softmax keeps its dependency distances)
-        B0 = 64
+        B0 = len(qk)
         fills = left
         ka = Fill(I("v_add_u32", VKA, sSP1, VKL), 4, earliest=B0, tag="kaddr")
         kr = [Fill(ins, 2, deps=[ka], sep=1, earliest=B0 + n // 2, deadline=B0 + 40, tag="kread")
@@ -1001,7 +1050,7 @@ class Gen:
         fills = [ka] + kr + vr + fills + dma_pv
         body, left = schedule(pv, fills, self.budget_pv, gap_offset=B0)
         e(body)
-        e(drain(left, B0 + 71))
+        e(drain(left, B0 + len(pv) - 1))
 
     def tail(self, X):
         """last tile T (state X): its deferred slices, its check, PV(T) with
@@ -1012,6 +1061,8 @@ class Gen:
         e([I("v_add_u32", VVA, sSM1, VVL)])
         f_def, _, _ = softmax_fills(X, dfr, lambda qb, kb: 0, ytag=0)
         e(drain(f_def, 0))
+        if LCHECK[0]:
+            e(rowsum_mfmas(X))
         self.check(X, f"rare_t{X}")
         e(v_reads(0) + v_reads(1))
         fills = []
@@ -1021,9 +1072,10 @@ class Gen:
                                   deadline=pv_first_gap(db) - 6, tag="vread"))
         # the next block's Q rows (or this block's again past the last block)
         fills += chain(self.q_offsets(sNQ0, sNQH), earliest=4)
-        body, left = schedule(pv_mfmas(X), fills, self.budget)
+        pv = pv_mfmas(X)
+        body, left = schedule(pv, fills, self.budget)
         e(body)
-        e(drain(left, 71))
+        e(drain(left, len(pv) - 1))
 
     # ---- epilogue ---------------------------------------------------------
     def epilogue(self):
@@ -1075,6 +1127,11 @@ class Gen:
         site whose id is in sRET."""
         e, Lb = self.emit, self.L
         e([label(Lb(name)), I("s_nop", 7), I("s_nop", 7), I("s_load_dword", sT1, sKA, 4 * AI["muoff"])])
+        if LCHECK[0]:
+            # the tile's old P (still in state X) out of l: l -= 1^T P(X)
+            neg = V(T(32).i, 4)
+            e([I("v_mov_b32", neg[r], NEGONES) for r in range(4)])
+            e(rowsum_mfmas(X, neg))
         for tile_slot, Xs, redo in ((sSM1, X, True), (sS0, 1 - X, has_next)):
             if not redo:
                 continue
@@ -1112,10 +1169,15 @@ class Gen:
                                I("v_accvgpr_write_b32", O_(db, qb)[r], T(25))])
                     e([I("v_mul_f32", L_(qb)[r], L_(qb)[r], T(24)) for r in range(4)])
                 e(exps_all(X))
+                if LCHECK[0]:  # its new sums (the step's row sums of this tile already ran)
+                    e(rowsum_mfmas(X))
             else:
-                e([I("v_mov_b32", ACC(Xs), 0)])
+                if not LCHECK[0]:
+                    e([I("v_mov_b32", ACC(Xs), 0)])
                 e(exps_all(Xs, also_or=True, shifted=QSCALE[0]))
-        e([I("v_mov_b32", ACC(X), 0), I("s_nop", 4)])
+        if not LCHECK[0]:
+            e([I("v_mov_b32", ACC(X), 0)])
+        e([I("s_nop", 4)])
         for k, blk, ret in self.sites:
             if blk == name:
                 e([I("s_cmp_eq_u32", sRET, k), I("s_cbranch_scc1", ret)])
