@@ -103,12 +103,14 @@ int pli_gemm(const void* a, const void* b, void* c, const void* bias, int m,
  * fp16 (dtype), C fp32 contiguous (ldc = n), fp32 accumulate -- the
  * row-parallel partial of ch09/tensor_parallel.py:66-68 kept in fp32 so the
  * all-reduce sums unrounded partials (RowParallelLinear(reduce_dtype=
- * torch.float32)).  Shapes with at least 128 tiles of 256 x 256, K % 64 == 0,
- * N % 8 == 0 and 256 rows of A and B addressable by a 32-bit offset take
- * gemm_w5 with an fp32 epilogue (its persistent walk when M, N are multiples
- * of 256 and K >= 128); other K % 64 == 0, N % 32 == 0 shapes with 16-byte
- * aligned rows the LDS split-K kernel with one slice; the rest a
- * one-thread-per-output kernel.
+ * torch.float32)).  Routes, in the order gemm.hip pli_gemm_f32out checks
+ * them: (1) K % 64 == 0, N % 32 == 0, lda % 8 == 0, ldb % 8 == 0, A / B / C
+ * 16-byte aligned, M >= 512, N >= 512, at least 128 tiles of 256 x 256 and
+ * 256 rows of A and B addressable by a 32-bit offset: gemm_w5 with an fp32
+ * epilogue (its persistent walk when M, N are multiples of 256 and K >=
+ * 128); (2) the rest of (1)'s alignment class (K % 64 == 0, N % 32 == 0,
+ * lda / ldb % 8 == 0, 16-byte aligned A / B / C): the LDS split-K kernel
+ * with one slice; (3) everything else: a one-thread-per-output kernel.
  */
 int pli_gemm_f32out(const void* a, const void* b, float* c, int m, int n, int k, int64_t lda,
                     int64_t ldb, int dtype, void* stream);
@@ -342,10 +344,10 @@ int pli_attn_decode_dev(const void* q, const void* k, const void* v, void* o,
  *   (tests); 73 / 74 attn_fwd_v12 causal, one block per workgroup /
  *   persistent pair walk; 80 / 81 / 82 attn_fwd_v13 (16x16x32 MFMA, one
  *   generated instruction stream) persistent / one block per workgroup /
- *   80 with the rescale path at nearly every tile (tests) -- 80 is the
- *   default for bf16 D = 128, Nk >= 128, Nk % 64 == 0; 83 / 84 / 85 the
- *   causal forms (83 = causal default where (Nk - Nq) % 64 == 0; other
- *   shapes take 74 / 60).  Prescaled variants round Q * scale * log2(e) to
+ *   80 with the rescale path at every tile (tests) -- 80 is the default
+ *   for bf16 and fp16 (attn_fwd_v13h, the f16 MFMA) D = 128, Nk >= 128,
+ *   Nk % 64 == 0; 83 / 84 / 85 the causal forms (83 = causal default where
+ *   (Nk - Nq) % 64 == 0; other shapes take 74 / 60).  Prescaled variants round Q * scale * log2(e) to
  *   the 16-bit input type (2^-9 relative score error in bf16).  The v13
  *   forms, v12 and the exact v7 / v10 bodies (51 / 55 / 60) take any
  *   scale > 0; the prescaled 50 / 54 take scale * log2(e) <= 1 (larger

@@ -531,8 +531,9 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
 //  80: attn_fwd_v13 (flash_v13.hip): 4 waves x 64 rows, one wave per SIMD,
 //      v_mfma_f32_16x16x32_bf16 (the shape the chip clocks higher under load),
 //      one generated instruction stream (tools/gen_flash_v13.py), persistent;
-//      defer-max on P itself (bf16, D = 128, non-causal, Nk % 64 == 0, Nk >=
-//      128; else 71)
+//      defer-max on P itself (D = 128, non-causal, Nk % 64 == 0, Nk >= 128;
+//      else 71); fp16 inputs run the same program on the f16 MFMA
+//      (attn_fwd_v13h / v13hc, since round 5; before: 71 -> 55 / 60)
 //  81: variant 80 with one block per workgroup
 //  82: variant 80 with mu = max * c (P = 1 at the max, so every row's l >= 1
 //      and the rare path runs at every tile): tests only
@@ -556,6 +557,21 @@ constexpr int kDefaultVariant = 80;
 #ifndef PLI_V13_MUOFF
 #define PLI_V13_MUOFF 62.f
 #endif
+// Range of V this offset supports (bf16 v13; the v12 / v7 / v10 bf16 bodies'
+// threshold 64 mirrors it): P is about 2^-62 at a row's max, so P * V stays a
+// normal fp32 down to |V| ~ 2^-64 and products below flush gradually
+// (subnormal fp32 keeps 2^-149 absolute); on the other side P <= 1 (v13's
+// clamp) and O <= l max|V|, so any finite bf16 V is safe.  Exercised at |V|
+// scaled by 2^-60 and 2^50 against f64 (tests/test_gpu_flash_v13.py
+// test_v13_v_range, variants 80 / 83 / 71 / 55).
+// fp16 (attn_fwd_v13h / v13hc, since round 5): fp16 P is normal down to 2^-14
+// and zero below 2^-24, so the offset stays small -- P <= 2^-4 when a max is
+// taken, the rescale path once a row max grows by 5 (some P >= 2, the bit-14
+// test), scores 20+ log2 units under the running estimate flush to 0 (weight
+// < 2^-20 of the row's largest: at most Nk * 2^-20 of the sum in total)
+#ifndef PLI_V13_MUOFF_F16
+#define PLI_V13_MUOFF_F16 4.f
+#endif
 // causal: attn_fwd_v12 causal (74; one block per workgroup where the
 // persistent pair walk does not tile the shape), 60 where v12 does not apply
 // (fp16, D != 128, Nq > Nk, Nk % 64): B8 S4096 H32 D128 bf16 1002 (74, the
@@ -574,7 +590,9 @@ int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int
     // scale*log2(e): only for c > 0 is that the row's largest scaled score
     // (c <= 0 would make exp2(s*c - m) >= 1 and overflow); zero or negative
     // scales never get here (the generic kernel's max is of the scaled scores).
-    // v7 / v10 also prescale Q by c, so c > 1 could overflow fp16 Q.
+    // Only the prescaled variants 50 / 54 multiply Q by c in the 16-bit input
+    // type (so c > 1 could overflow fp16 Q): they alone need c <= 1; v13, v12
+    // and the exact 51 / 55 / 60 apply c by fma in fp32 (any c > 0).
     const float c_log2 = scale * 1.4426950408889634f;
     const bool c_ok = c_log2 > 0.f && c_log2 <= 1.f;
     // the exact bodies (v12 70-74, v7 / v10 51 / 55 / 60) apply c by fma to
@@ -585,9 +603,13 @@ int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int
         const bool cv = variant >= 83;  // the causal forms
         const V7Strides s7{st.qb, st.qh, st.qn, st.kb, st.kh, st.kn, st.vb, st.vh, st.vn, st.ob, st.oh, st.on};
         // v13 scales in fp32 (s * c - mu by v_fma): any c > 0 (scale = 1 etc.)
+        // the rare-path sweep (82 / 85): bf16's l check trips at every tile with
+        // mu = max * c (P = 1 at the max), fp16's P-bit check with mu = max * c - 1
+        const float sweep = bf ? 0.f : -1.f;
         if (cv == (causal != 0) && attn_v13_ok(D, bf ? 1 : 0, causal, Nq, Nk, s7) && c_log2 > 0.f)
             return launch_attn_v13(q, k, v, o, B, H, group, Nq, Nk, s7, scale, stream, variant != 81 && variant != 84,
-                                   (variant == 82 || variant == 85) ? 0.f : PLI_V13_MUOFF, nullptr, causal != 0);
+                                   (variant == 82 || variant == 85) ? sweep : bf ? PLI_V13_MUOFF : PLI_V13_MUOFF_F16,
+                                   nullptr, causal != 0, !bf);
         variant = causal ? 74 : 71;
     }
     if (variant == 70 || variant == 71 || variant == 72) {

@@ -66,6 +66,27 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v13c(V13Args args) {
     asm volatile(PLI_V13C_BODY::"s"(kp), "s"(wg), "s"(wave), "s"((unsigned)(uintptr_t)smem) : PLI_V13_CLOBBERS);
 }
 
+// fp16 Q / K / V / O: the same programs on v_mfma_f32_16x16x32_f16, P packed
+// to fp16 (RNE) and checked with the bit-14 test (tools/v13/kernel.py
+// Gen(dtype="f16"); the launcher passes mu offset PLI_V13_MUOFF_F16)
+__global__ __launch_bounds__(256, 1) void attn_fwd_v13h(V13Args args) {
+    __shared__ __attribute__((aligned(1024))) char smem[163840];
+    (void)args;
+    const void* kp = (const void*)__builtin_amdgcn_kernarg_segment_ptr();
+    const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const unsigned wg = blockIdx.x;
+    asm volatile(PLI_V13H_BODY::"s"(kp), "s"(wg), "s"(wave), "s"((unsigned)(uintptr_t)smem) : PLI_V13_CLOBBERS);
+}
+
+__global__ __launch_bounds__(256, 1) void attn_fwd_v13hc(V13Args args) {
+    __shared__ __attribute__((aligned(1024))) char smem[163840];
+    (void)args;
+    const void* kp = (const void*)__builtin_amdgcn_kernarg_segment_ptr();
+    const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const unsigned wg = blockIdx.x;
+    asm volatile(PLI_V13HC_BODY::"s"(kp), "s"(wg), "s"(wave), "s"((unsigned)(uintptr_t)smem) : PLI_V13_CLOBBERS);
+}
+
 // floor(x / d) == ((x * m) >> 31) >> l for 0 <= x < 2^31 (Granlund-Montgomery,
 // N = 31: m = ceil(2^(31+l) / d) < 2^32 with l = ceil(log2 d))
 void magic31(uint32_t d, uint32_t& m, uint32_t& l) {
@@ -98,7 +119,8 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v13_stamp(V13Args args) {
 }  // namespace
 
 bool attn_v13_ok(int D, int is_bf16, int causal, int Nq, int Nk, const V7Strides& st) {
-    if (D != 128 || !is_bf16 || Nk < 128 || Nk % 64 != 0 || Nq < 1) return false;
+    (void)is_bf16;  // bf16 and fp16 programs
+    if (D != 128 || Nk < 128 || Nk % 64 != 0 || Nq < 1) return false;
     // causal: the bottom-right diagonal on 64-key tile boundaries
     if (causal && (Nq > Nk || (Nk - Nq) % 64 != 0)) return false;
     // causal: the stream's tile count and index carry the block's order in
@@ -115,8 +137,9 @@ bool attn_v13_ok(int D, int is_bf16, int causal, int Nq, int Nk, const V7Strides
 
 int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B, int H, int group, int Nq,
                     int Nk, const V7Strides& st, float scale, hipStream_t stream, bool persistent, float muoff,
-                    uint32_t* stamps, bool causal) {
-    PLI_REQUIRE(attn_v13_ok(128, 1, causal, Nq, Nk, st), "attn_fwd_v13: shape not supported");
+                    uint32_t* stamps, bool causal, bool fp16) {
+    PLI_REQUIRE(attn_v13_ok(128, fp16 ? 0 : 1, causal, Nq, Nk, st), "attn_fwd_v13: shape not supported");
+    PLI_REQUIRE(!(fp16 && stamps), "attn_fwd_v13: the stamp build is bf16");
     const int qblocks = cdiv(Nq, 256);
     const int64_t nb = (int64_t)B * H * qblocks;
     PLI_REQUIRE(nb < (1ll << 31) && nb > 0, "attn_fwd_v13: grid too large");
@@ -190,6 +213,14 @@ int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B,
 #else
     (void)stamps;
 #endif
+    if (fp16) {
+        if (causal) {
+            hipLaunchKernelGGL(attn_fwd_v13hc, dim3((unsigned)grid), dim3(256), 0, stream, a);
+            return launch_status("attn_fwd_v13hc");
+        }
+        hipLaunchKernelGGL(attn_fwd_v13h, dim3((unsigned)grid), dim3(256), 0, stream, a);
+        return launch_status("attn_fwd_v13h");
+    }
     if (causal) {
         hipLaunchKernelGGL(attn_fwd_v13c, dim3((unsigned)grid), dim3(256), 0, stream, a);
         return launch_status("attn_fwd_v13c");
@@ -209,7 +240,8 @@ extern "C" int pli_diag_v13_clock(const void* q, const void* k, const void* v, v
     using namespace pli;
     const int64_t sn = 128, sh = (int64_t)N * 128, sb = (int64_t)H * N * 128;
     const V7Strides st{sb, sh, sn, sb, sh, sn, sb, sh, sn, sb, sh, sn};
-    const int rc = launch_attn_v13(q, k, v, o, B, H, 1, N, N, st, 1.f / sqrtf(128.f), 0, true, 62.f, stamps, false);
+    const int rc = launch_attn_v13(q, k, v, o, B, H, 1, N, N, st, 1.f / sqrtf(128.f), 0, true, 62.f, stamps, false,
+                                   false);
     if (rc != 0 || hipDeviceSynchronize() != hipSuccess) return -1;
     return 0;
 }

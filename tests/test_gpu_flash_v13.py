@@ -215,3 +215,21 @@ def test_v13_rescale_past_default_offset(causal):
     err = max_err(out, torch_attention(q, k, v, causal=causal))
     assert err <= 2.0 ** -8 * v.abs().max().item(), f"causal {causal}: {err:.4e}"
     assert_agree_to_rounding(pli_hip.flash_attn_fwd(q, k, v, causal=causal, variant=var + 2), out, v)
+
+
+@pytest.mark.parametrize("vexp", (-60, 50))
+@pytest.mark.parametrize("variant", (80, 83, 71, 55))
+def test_v13_v_range(variant, vexp):
+    """|V| scaled by 2^-60 / 2^50 (exact in bf16): with P ~ 2^-62 at the row
+    max (mu offset 62; the v12 / v10 bf16 threshold 64 likewise), P * V runs
+    near the fp32 subnormal range or far above 1 -- the output, scaled back,
+    against the f64 reference (the range the offset supports)."""
+    import pli_hip
+    causal = variant == 83
+    q, k, v = inputs((2, 4, 2, 256, 512) if causal else (2, 4, 2, 300, 512), 41)
+    vs = v * (2.0 ** vexp)
+    assert torch.isfinite(vs).all() and (vs.abs() > 0).sum() == (v.abs() > 0).sum()
+    out = pli_hip.flash_attn_fwd(q, k, vs, causal=causal, variant=variant)
+    ref = torch_attention(q, k, v, causal=causal)
+    err = max_err(out.double() * 2.0 ** -vexp, ref)
+    assert err <= 1e-2, f"variant {variant} |V| * 2^{vexp}: max |err| {err:.4e}"

@@ -1,0 +1,104 @@
+"""attn_fwd_v13h / v13hc: fp16 Q / K / V / O on the generated v13 program
+(tools/v13/kernel.py Gen(dtype="f16"): v_mfma_f32_16x16x32_f16, P packed to
+fp16 with RNE, the bit-14 defer-max check, mu offset PLI_V13_MUOFF_F16 = 4)
+-- the default route for fp16 D = 128 since round 5 (before: v12 -> v10).
+
+Same references as tests/test_gpu_flash_v13.py (ch06/attention_memory.py:
+19-33 in float64 over the whole output, fp32 per head at the bench config),
+on fp16 inputs; variant 82 / 85 (mu = max * c - 1: the rescale path at
+nearly every tile) within rounding of 80 / 83."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from test_gpu_flash_v12 import DEV, assert_agree_to_rounding, max_err, torch_attention
+from test_gpu_flash_v13 import CAUSAL, SHAPES
+
+pytestmark = pytest.mark.gpu
+
+
+def h(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV).to(torch.float16)
+
+
+def inputs16(shape, seed):
+    from oracle.numerics import seeded_normal
+    B, H, Hkv, Nq, Nk = shape
+    return (h(seeded_normal((B, H, Nq, 128), seed, "fp16")), h(seeded_normal((B, Hkv, Nk, 128), seed + 1, "fp16")),
+            h(seeded_normal((B, Hkv, Nk, 128), seed + 2, "fp16")))
+
+
+@pytest.mark.parametrize("qmul", (1, 4))
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "b{}h{}kv{}q{}k{}".format(*s))
+def test_v13_f16_vs_f64_full_tensor(shape, qmul):
+    import pli_hip
+    q, k, v = inputs16(shape, sum(shape) % 983)
+    q = q * qmul  # exact in fp16
+    ref = torch_attention(q, k, v)
+    tol = 1e-2 if qmul == 1 else 2.0 ** -8 * v.abs().max().item()
+    outs = {}
+    for var in (80, 81, 82):
+        outs[var] = pli_hip.flash_attn_fwd(q, k, v, variant=var)
+        assert outs[var].dtype == torch.float16
+        err = max_err(outs[var], ref)
+        assert err <= tol, f"{shape} q*{qmul} variant {var}: max |err| {err:.4e} > {tol:.4e}"
+    assert torch.equal(outs[80], outs[81]), f"{shape}: 80 != 81"
+    assert_agree_to_rounding(outs[82], outs[80], v)
+
+
+@pytest.mark.parametrize("shape", CAUSAL, ids=lambda s: "b{}h{}kv{}q{}k{}".format(*s))
+def test_v13_f16_causal_vs_f64_full_tensor(shape):
+    import pli_hip
+    q, k, v = inputs16(shape, sum(shape) % 977)
+    ref = torch_attention(q, k, v, causal=True)
+    outs = {}
+    for var in (83, 84, 85):
+        outs[var] = pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=var)
+        err = max_err(outs[var], ref)
+        assert err <= 1e-2, f"{shape} causal variant {var}: max |err| {err:.4e}"
+    assert_agree_to_rounding(outs[83], outs[84], v)
+    assert_agree_to_rounding(outs[85], outs[83], v)
+
+
+@pytest.mark.parametrize("causal", (False, True))
+def test_v13_f16_full_config_all_heads(causal):
+    """B8 S4096 H32 D128 fp16 (the bench shape): all 256 heads against an
+    fp32 torch attention per head; the default route is v13h / v13hc."""
+    import pli_hip
+    B, H, N, D = 8, 32, 4096, 128
+    g = torch.Generator(device=DEV).manual_seed(11)
+    q, k, v = (torch.randn(B, H, N, D, device=DEV, dtype=torch.float16, generator=g) for _ in range(3))
+    out = pli_hip.flash_attn_fwd(q, k, v, causal=causal)
+    assert torch.equal(out, pli_hip.flash_attn_fwd(q, k, v, causal=causal, variant=83 if causal else 80))
+    for b in range(B):
+        ref = torch_attention(q[b:b + 1], k[b:b + 1], v[b:b + 1], dtype=torch.float32, heads_per_chunk=4,
+                              causal=causal)
+        err = max_err(out[b:b + 1], ref)
+        assert err <= 1e-2, f"batch {b} causal {causal}: max |err| {err:.4e} over its 32 heads"
+
+
+@pytest.mark.parametrize("name", ("spike", "first", "late", "all", "seam2", "seam5"))
+def test_v13_f16_rescale_stress(name):
+    import pli_hip
+    from stress_cases import stress_inputs
+    q, k, v = (h(x) for x in stress_inputs(name))
+    if k.shape[2] < 128:
+        pytest.skip("v13 needs Nk >= 128")
+    out = pli_hip.flash_attn_fwd(q, k, v, variant=80)
+    err = max_err(out, torch_attention(q, k, v))
+    assert err <= 2.0 ** -8 * v.abs().max().item(), f"{name}: {err:.4e}"
+    assert_agree_to_rounding(pli_hip.flash_attn_fwd(q, k, v, variant=82), out, v)
+
+
+@pytest.mark.parametrize("scale", (1.0, 0.25))
+def test_v13_f16_explicit_scale(scale):
+    import pli_hip
+    q, k, v = inputs16((2, 8, 2, 300, 512), 17)
+    out = pli_hip.flash_attn_fwd(q, k, v, scale=scale, variant=80)
+    kf, vf = (t.double().repeat_interleave(4, dim=1) for t in (k, v))
+    ref = torch.softmax((q.double() @ kf.transpose(-1, -2)) * scale, -1) @ vf
+    err = max_err(out, ref)
+    tol = 1e-2 if scale < 0.5 else 2.0 ** -8 * v.abs().max().item()
+    assert err <= tol, f"scale {scale}: max |err| {err:.4e} > {tol:.4e}"

@@ -24,8 +24,9 @@ from v13 import run as R  # noqa: E402
 from v13.isa import analyse  # noqa: E402
 
 
-def f64_attention(q, k, v, causal=False):
-    r = lambda x: E.bf16_to_f32(E.bf16_rne(x.astype(np.float32))).astype(np.float64)  # noqa: E731
+def f64_attention(q, k, v, causal=False, dtype="bf16"):
+    enc, dec = (E.f16_rne, E.f16_to_f32) if dtype == "f16" else (E.bf16_rne, E.bf16_to_f32)
+    r = lambda x: dec(enc(x.astype(np.float32))).astype(np.float64)  # noqa: E731
     qf, kf, vf = r(q), r(k), r(v)
     g = q.shape[1] // k.shape[1]
     kf, vf = np.repeat(kf, g, axis=1), np.repeat(vf, g, axis=1)
@@ -79,9 +80,10 @@ def test_v13_spike_rescale():
 
 
 def test_v13_hazard_pass_is_idempotent():
-    """the committed program needs no further padding or waits"""
+    """the committed programs need no further padding or waits"""
     for causal in (False, True):
-        assert analyse(R.program(causal=causal)) == {}
+        for dtype in ("bf16", "f16"):
+            assert analyse(R.program(causal=causal, dtype=dtype)) == {}
 
 
 def test_v13_header_is_current():
@@ -104,3 +106,28 @@ def test_v13_spike_past_product_offset():
     assert em.counts.get("v_sub_f32", 0) > 0, "the rescale path never ran"
     err = np.abs(o - f64_attention(q, k, v)).max()
     assert err <= 2.0 ** -8 * np.abs(v).max(), f"max |err| {err:.3e}"
+
+
+F16_CASES = [  # (B, H, Hkv, Nq, Nk, grid, layout, muoff, causal): the fp16 program (Gen(dtype="f16"))
+    (1, 2, 2, 256, 320, 1, "bhsd", 4.0, False),         # the launcher's fp16 offset, persistent
+    (2, 2, 1, 200, 128, 1, "bshd", 4.0, False),         # GQA, ragged Nq, BSHD
+    (1, 1, 1, 256, 256, None, "bhsd", -1.0, False),     # P-bit check: the rescale path at nearly every tile
+    (1, 2, 1, 256, 512, None, "bhsd", 4.0, True),       # causal, diagonal offset
+]
+
+
+@pytest.mark.parametrize("case", F16_CASES, ids=lambda c: "f16-b{}h{}kv{}q{}k{}g{}-{}-mu{}-causal{}".format(*c))
+def test_v13_f16_program_vs_f64(case):
+    """fp16 Q / K / V / O on v_mfma_f32_16x16x32_f16, P packed to fp16 (RNE)
+    and checked with the bit-14 test, against f64 on fp16-rounded inputs"""
+    B, H, Hkv, Nq, Nk, grid, lay, muoff, causal = case
+    rng = np.random.default_rng(7 + sum(case[:5]))
+    q = rng.standard_normal((B, H, Nq, 128))
+    k = rng.standard_normal((B, Hkv, Nk, 128))
+    v = rng.standard_normal((B, Hkv, Nk, 128))
+    o, em = R.run(q, k, v, grid=grid, layout=lay, muoff=muoff, causal=causal, dtype="f16")
+    assert em.counts.get("v_mfma_f32_16x16x32_f16", 0) > 0 and em.counts.get("v_mfma_f32_16x16x32_bf16", 0) == 0
+    err = np.abs(o - f64_attention(q, k, v, causal, dtype="f16")).max()
+    assert err <= 1e-2, f"max |err| {err:.3e}"
+    if muoff < 0:
+        assert em.counts.get("v_sub_f32", 0) > 0, "the rescale path never ran"

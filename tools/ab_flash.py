@@ -6,7 +6,7 @@ pli_flash_attn_fwd_variant (variant $VARIANT, default -1 = the default
 kernel) on the bench config (random data), libraries interleaved, after a
 warm-up; prints the median / min TF/s per library and whether its output is
 bitwise equal to the first library's.  $CAUSAL=1 times the causal form,
-$SCALE sets the softmax scale (default 1/sqrt(D))."""
+$SCALE sets the softmax scale (default 1/sqrt(D)), $DTYPE bf16 / fp16."""
 import ctypes
 import json
 import os
@@ -33,17 +33,17 @@ for p in LIBS:
 # (library, variant) arms, interleaved round by round
 arms = [(li, var) for li in range(len(LIBS)) for var in VARIANTS]
 stream = torch.cuda.current_stream()
-BF16 = 2  # PLI_BF16
+DT = {"bf16": (2, torch.bfloat16), "fp16": (1, torch.float16)}[os.environ.get("DTYPE", "bf16")]  # PLI_BF16 / PLI_FP16
 for (B, H, N, D) in SHAPES:
     g = torch.Generator(device="cuda").manual_seed(0)
-    q, k, v = (torch.randn(B, H, N, D, device="cuda", dtype=torch.bfloat16, generator=g) for _ in range(3))
+    q, k, v = (torch.randn(B, H, N, D, device="cuda", dtype=DT[1], generator=g) for _ in range(3))
     outs = [torch.empty_like(q) for _ in arms]
     st = (ctypes.c_int64 * 12)(*(int(x) for t in (q, k, v, q) for x in t.stride()[:3]))
 
     def call(a):
         li, var = arms[a]
         rc = libs[li](q.data_ptr(), k.data_ptr(), v.data_ptr(), outs[a].data_ptr(), B, H, H, N, N, D, st,
-                      SCALE or D ** -0.5, CAUSAL, BF16, ctypes.c_void_p(stream.cuda_stream), var)
+                      SCALE or D ** -0.5, CAUSAL, DT[0], ctypes.c_void_p(stream.cuda_stream), var)
         assert rc == 0, (LIBS[li], var, rc)
 
     pairs = N * (N + 1) // 2 if CAUSAL else N * N

@@ -10,7 +10,7 @@ defer-max logic and the epilogue produce the right output.  What it does not:
 timing, wait counts, races between waves inside one barrier interval.
 
 Semantics of the less common instructions, as this file implements them:
-  v_mfma_f32_16x16x32_bf16  A lane l: row l&15, k = 8(l>>4)+j (j-th bf16 of
+  v_mfma_f32_16x16x32_bf16 / _f16  A lane l: row l&15, k = 8(l>>4)+j (j-th bf16 of
       the 4 registers, low half first); B lane l: col l&15, same k; C/D lane
       l: col l&15, rows 4(l>>4)+r (register r)
   ds_read_b64_tr_b16  per 16-lane group, lane 4q+p addresses row q, columns
@@ -53,6 +53,17 @@ def bf16_rne(f32):
 
 def bf16_to_f32(b):
     return u2f((np.asarray(b, dtype=np.uint32) & 0xFFFF) << 16)
+
+
+def f16_rne(f32):
+    """f32 array -> fp16 bit patterns (uint32 holding 16 bits), RNE"""
+    with np.errstate(over="ignore"):
+        h = np.asarray(f32, dtype=np.float32).astype(np.float16)
+    return h.view(np.uint16).astype(np.uint32)
+
+
+def f16_to_f32(b):
+    return (np.asarray(b, dtype=np.uint32) & 0xFFFF).astype(np.uint16).view(np.float16).astype(np.float32)
 
 
 class Heap:
@@ -259,6 +270,7 @@ class Emu:
     def mfma(self, w, ins):
         d, a, b, c = ins.ops
         ra, rb = self.regs(w, a), self.regs(w, b)
+        dec = f16_to_f32 if ins.op.endswith("_f16") else bf16_to_f32
         A = np.zeros((16, 32))
         B = np.zeros((32, 16))
         for l in range(LANES):
@@ -267,8 +279,8 @@ class Emu:
                 wb = int(rb[j // 2, l])
                 ha = (wa >> (16 * (j % 2))) & 0xFFFF
                 hb = (wb >> (16 * (j % 2))) & 0xFFFF
-                A[l % 16, 8 * (l // 16) + j] = float(bf16_to_f32(ha))
-                B[8 * (l // 16) + j, l % 16] = float(bf16_to_f32(hb))
+                A[l % 16, 8 * (l // 16) + j] = float(dec(ha))
+                B[8 * (l // 16) + j, l % 16] = float(dec(hb))
         D = A @ B
         if isinstance(c, int):
             assert c == 0
@@ -342,6 +354,9 @@ class Emu:
                 return self.vset(w, o[0], f2u(np.float32(1.0) / gf(o[1])))
         if op == "v_cvt_pk_bf16_f32":
             lo, hi = bf16_rne(gf(o[1])), bf16_rne(gf(o[2]))
+            return self.vset(w, o[0], lo | (hi << 16))
+        if op == "v_cvt_pk_f16_f32":
+            lo, hi = f16_rne(gf(o[1])), f16_rne(gf(o[2]))
             return self.vset(w, o[0], lo | (hi << 16))
         if op in ("v_cmp_lt_f32_e32", "v_cmp_le_f32_e32"):
             a, b = gf(o[1]), gf(o[2])

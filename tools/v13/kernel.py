@@ -35,6 +35,11 @@ from .isa import A, EXEC, Ins, M0, Neg, S, SCC, V, VCC, label
 
 MFMA = "v_mfma_f32_16x16x32_bf16"
 BF16_ONES = 0x3F803F80
+# the element type of Q / K / V / O and of P (Gen(dtype=...)): the MFMA, the
+# all-ones row-sum operand and the f32 -> 16-bit pack (both RNE)
+DTYPES = {"bf16": {"mfma": "v_mfma_f32_16x16x32_bf16", "ones": BF16_ONES, "cvt": "v_cvt_pk_bf16_f32"},
+          "f16": {"mfma": "v_mfma_f32_16x16x32_f16", "ones": 0x3C003C00, "cvt": "v_cvt_pk_f16_f32"}}
+DT = dict(DTYPES["bf16"])
 
 # ---------------------------------------------------------------- registers
 
@@ -179,7 +184,7 @@ def I(op, *ops, mods="", note=""):
 
 
 def mfma(d, a, b, c):
-    return I(MFMA, d, a, b, c)
+    return I(DT["mfma"], d, a, b, c)
 
 
 # ---------------------------------------------------------------- scheduler
@@ -413,7 +418,7 @@ def softmax_fills(X, slices, earliest_of, deadline_of=None, ytag=0, prev_cv=None
             e1 = Fill(I("v_exp_f32", y1, y1, mods=xm), 8, trans=True, deps=[f1], sep=1, tag="exp")
         fm = f1
         w = P_(X, qb, kb >> 1)[2 * (kb & 1) + hh]
-        cv = Fill(I("v_cvt_pk_bf16_f32", w, y0, y1), 4, deps=[e0, e1], sep=1, tag="cvt",
+        cv = Fill(I(DT["cvt"], w, y0, y1), 4, deps=[e0, e1], sep=1, tag="cvt",
                   deadline=dl if QSCALE[0] else None, hard=QSCALE[0] and dl is not None)
         slot_cv[slot] = cv
         grp = [f for f in (f0, f1, e0, e1, cv) if f is not None]
@@ -633,7 +638,7 @@ def exps_all(X, also_or=False, shifted=False):
             xm = "clamp" if LCHECK[0] else ""
             c += [I("v_fma_f32", y0, s[2 * hh], sC, Neg(MU(qb))), I("v_fma_f32", y1, s[2 * hh + 1], sC, Neg(MU(qb))),
                   I("v_exp_f32", y0, y0, mods=xm), I("v_exp_f32", y1, y1, mods=xm)]
-        c += [I("v_cvt_pk_bf16_f32", w, y0, y1)]
+        c += [I(DT["cvt"], w, y0, y1)]
         if also_or and not LCHECK[0]:
             c.append(I("v_or_b32", ACC(X), ACC(X), w))
     return c
@@ -663,10 +668,19 @@ class Gen:
     bottom-right-masked kernel (attn_fwd_v13c)"""
 
     def __init__(self, ndef=4, budget=8, dma_spacing=6, tag="%=", stamp=False, causal=False, abl=(), dma_cost=8,
-                 rev=True, qscale=False, dma_pv=0, dma_pv_spacing=16, budget_pv=None, lcheck=True):
+                 rev=True, qscale=False, dma_pv=0, dma_pv_spacing=16, budget_pv=None, lcheck=None, dtype="bf16"):
         global DMA_COST
+        # fp16: P keeps the bit check (P < 2: bit 14 of an fp16 half too) --
+        # the l >= 1 test needs muoff >> log2 Nk, which fp16 P (normal down to
+        # 2^-14, zero below 2^-24) cannot give; the launcher passes muoff 4
+        DT.clear()
+        DT.update(DTYPES[dtype])
+        if lcheck is None:
+            lcheck = dtype == "bf16"
+        assert not (dtype == "f16" and lcheck), "fp16 runs the P-bit check"
         QSCALE[0] = bool(qscale)
         assert not (qscale and lcheck), "QSCALE is built on the P-bit check (lcheck=False)"
+        assert not (qscale and dtype != "bf16")
         LCHECK[0] = bool(lcheck)
         # causal: the second block of each pair streams its tiles in the
         # reversed order of tile_of (its 8 workgroups then read every K/V
@@ -747,7 +761,7 @@ class Gen:
             e([I("s_lshl_b32", sT6, sL, 2), I("s_lshr_b32", sT7, sWKOFF, 12), I("s_add_u32", sT6, sT6, sT7),
                I("v_writelane_b32", STAMPV, sT6, 8)])
         # ones selector, ring slots, causal mask operands
-        e([I("v_mov_b32", ONES[k], BF16_ONES) for k in range(4)])
+        e([I("v_mov_b32", ONES[k], DT["ones"]) for k in range(4)])
         e([I("s_mov_b32", sS0, 0), I("s_mov_b32", sSP1, SLOT), I("s_mov_b32", sSP2, 2 * SLOT),
            I("s_mov_b32", sSM1, 4 * SLOT)])
         if self.causal:
@@ -1097,8 +1111,8 @@ class Gen:
                         e([I("v_accvgpr_read_b32", T(28 + r), O_(db, qb)[r])])
                     for r in range(4):
                         e([I("v_mul_f32", T(28 + r), T(28 + r), T(20 + qb))])
-                    e([I("v_cvt_pk_bf16_f32", T(w + 2 * half), T(28), T(29)),
-                       I("v_cvt_pk_bf16_f32", T(w + 2 * half + 1), T(30), T(31))])
+                    e([I(DT["cvt"], T(w + 2 * half), T(28), T(29)),
+                       I(DT["cvt"], T(w + 2 * half + 1), T(30), T(31))])
                 e([I("v_permlane16_swap_b32", T(w), T(w + 2)), I("v_permlane16_swap_b32", T(w + 1), T(w + 3))])
             e([I("v_cmp_gt_u32_e32", VCC, ARG(AI["nq"]), T(24)), I("s_and_saveexec_b64", S(sT2.i, 2), VCC)])
             for dbp in range(4):

@@ -80,10 +80,11 @@ def program(**kw):
     return _PROG[key]
 
 
-def run(q, k, v, scale=None, grid=None, muoff=7.0, layout="bhsd", causal=False, structural=False, **kw):
-    """q [B,H,Nq,128], k / v [B,Hkv,Nk,128] float arrays (rounded to bf16) ->
-    O [B,H,Nq,128] float32 from the emulated kernel.  layout 'bshd' stores
-    the tensors as [B,S,H,D] (strided heads)."""
+def run(q, k, v, scale=None, grid=None, muoff=7.0, layout="bhsd", causal=False, structural=False, dtype="bf16", **kw):
+    """q [B,H,Nq,128], k / v [B,Hkv,Nk,128] float arrays (rounded to bf16, or
+    fp16 with dtype="f16") -> O [B,H,Nq,128] float32 from the emulated kernel.
+    layout 'bshd' stores the tensors as [B,S,H,D] (strided heads)."""
+    enc, dec = (E.f16_rne, E.f16_to_f32) if dtype == "f16" else (E.bf16_rne, E.bf16_to_f32)
     B, H, Nq, D = q.shape
     Hkv, Nk = k.shape[1], k.shape[2]
     assert D == 128 and Nk % 64 == 0 and Nk >= 128
@@ -92,7 +93,7 @@ def run(q, k, v, scale=None, grid=None, muoff=7.0, layout="bhsd", causal=False, 
     heap = E.Heap()
 
     def put(x, lay):
-        b16 = E.bf16_rne(np.asarray(x, dtype=np.float32)).astype(np.uint16)
+        b16 = enc(np.asarray(x, dtype=np.float32)).astype(np.uint16)
         if lay == "bshd":
             b16 = np.ascontiguousarray(b16.transpose(0, 2, 1, 3))
             Bx, Sx, Hx, Dx = b16.shape
@@ -115,7 +116,7 @@ def run(q, k, v, scale=None, grid=None, muoff=7.0, layout="bhsd", causal=False, 
     args = args_for(qa, ka, va, oa, B, H, Hkv, Nq, Nk, list(sq) + list(sk) + list(sv) + list(so), scale, G, muoff,
                     causal)
     kaddr = heap.alloc(args.nbytes, args.tobytes())
-    prog = program(causal=causal, **kw)
+    prog = program(causal=causal, dtype=dtype, **kw)
     em = E.Emu(prog, heap, structural=structural)
     em.kbase = ka
     for wg in range(G):
@@ -131,7 +132,7 @@ def run(q, k, v, scale=None, grid=None, muoff=7.0, layout="bhsd", causal=False, 
         return None, em
     raw = heap.view(oa)[:B * H * Nq * D * 2].view(np.uint16)
     if layout == "bshd":
-        o = E.bf16_to_f32(raw.reshape(B, Nq, H, D).astype(np.uint32)).transpose(0, 2, 1, 3)
+        o = dec(raw.reshape(B, Nq, H, D).astype(np.uint32)).transpose(0, 2, 1, 3)
     else:
-        o = E.bf16_to_f32(raw.reshape(B, H, Nq, D).astype(np.uint32))
+        o = dec(raw.reshape(B, H, Nq, D).astype(np.uint32))
     return np.ascontiguousarray(o), em
