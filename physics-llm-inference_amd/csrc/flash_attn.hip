@@ -606,10 +606,10 @@ int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int
         // the rare-path sweep (82 / 85): bf16's l check trips at every tile with
         // mu = max * c (P = 1 at the max), fp16's P-bit check with mu = max * c - 1
         const float sweep = bf ? 0.f : -1.f;
-        if (cv == (causal != 0) && attn_v13_ok(D, bf ? 1 : 0, causal, Nq, Nk, s7) && c_log2 > 0.f)
+        if (cv == (causal != 0) && attn_v13_ok(D, bf ? 1 : 0, causal, Nq, Nk, s7) && c_log2 > 0.f && H < (1 << 16))
             return launch_attn_v13(q, k, v, o, B, H, group, Nq, Nk, s7, scale, stream, variant != 81 && variant != 84,
                                    (variant == 82 || variant == 85) ? sweep : bf ? PLI_V13_MUOFF : PLI_V13_MUOFF_F16,
-                                   nullptr, causal != 0, !bf);
+                                   nullptr, causal != 0, !bf, D);
         variant = causal ? 74 : 71;
     }
     if (variant == 70 || variant == 71 || variant == 72) {

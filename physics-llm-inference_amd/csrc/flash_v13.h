@@ -1,0 +1,21 @@
+// attn_fwd_v13's kernel argument block, shared by the D = 128 bodies
+// (flash_v13.hip) and the D = 64 ones (flash_v13_d64.hip): 64 dwords in the
+// layout of tools/v13/kernel.py ARG_LAYOUT (the generated body reads it
+// through the kernarg pointer).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace pli {
+
+struct V13Args {
+    uint32_t w[64];
+};
+static_assert(sizeof(V13Args) == 256, "V13Args layout");
+
+// launch one of the head-dim-64 bodies (bf16 / fp16, plain / causal) on
+// `grid` workgroups of 256 threads; returns the launch status
+int launch_v13_d64(bool fp16, bool causal, unsigned grid, const V13Args& a, hipStream_t stream);
+
+}  // namespace pli

@@ -28,23 +28,20 @@
 #include "flash_v13_asm.h"
 #endif
 #include "pli_common.h"
+#include "flash_v13.h"
 
 namespace pli {
 namespace {
 
-// kernel argument block: 64 dwords, the layout of tools/v13/kernel.py
-// ARG_LAYOUT (the body reads it through the kernarg pointer)
-struct V13Args {
-    uint32_t w[64];
-};
-static_assert(sizeof(V13Args) == 256, "V13Args layout");
-
+// (A_SHIFTS packs the three magic-division shifts and the head count:
+// shq | shh << 5 | shg << 10 | H << 16 -- the block-parameter dwords 0..36
+// then fit s56..s92 and the program keeps off s32 / s100 / s101)
 enum : int {
     A_Q = 0, A_K = 2, A_V = 4, A_O = 6, A_QB = 8, A_QH = 10, A_KB = 12, A_KH = 14, A_VB = 16, A_VH = 18,
-    A_OB = 20, A_OH = 22, A_QN = 24, A_ON, A_NQ, A_NT, A_QBLOCKS, A_NBLOCKS, A_MAGQ, A_SHQ, A_MAGH, A_SHH,
-    A_MAGG, A_SHG, A_H, A_CW, A_HX, A_G, A_KN, A_VN, A_C, A_MUOFF, A_TBK, A_TBV, A_STAMP, A_STAMP_HI, A_OFFT
+    A_OB = 20, A_OH = 22, A_QN = 24, A_ON, A_NQ, A_NT, A_QBLOCKS, A_NBLOCKS, A_MAGQ, A_MAGH, A_MAGG, A_SHIFTS,
+    A_CW, A_HX, A_G, A_KN, A_VN, A_C, A_MUOFF, A_TBK, A_TBV, A_STAMP, A_STAMP_HI, A_OFFT
 };
-static_assert(A_G == 39 && A_OFFT == 48, "argument layout (tools/v13/kernel.py ARG_LAYOUT)");
+static_assert(A_G == 36 && A_OFFT == 45, "argument layout (tools/v13/kernel.py ARG_LAYOUT)");
 
 __global__ __launch_bounds__(256, 1) void attn_fwd_v13(V13Args args) {
     __shared__ __attribute__((aligned(1024))) char smem[163840];
@@ -120,14 +117,15 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v13_stamp(V13Args args) {
 
 bool attn_v13_ok(int D, int is_bf16, int causal, int Nq, int Nk, const V7Strides& st) {
     (void)is_bf16;  // bf16 and fp16 programs
-    if (D != 128 || Nk < 128 || Nk % 64 != 0 || Nq < 1) return false;
+    // head dim 128, or 64 (the D = 64 bodies in flash_v13_d64.hip)
+    if ((D != 128 && D != 64) || Nk < 128 || Nk % 64 != 0 || Nq < 1) return false;
     // causal: the bottom-right diagonal on 64-key tile boundaries
     if (causal && (Nq > Nk || (Nk - Nq) % 64 != 0)) return false;
     // causal: the stream's tile count and index carry the block's order in
     // bit 16 (tools/v13/kernel.py block_params), so counts stay below 2^16
     if (causal && Nk / 64 > 0xFFFF) return false;
     // 32-bit per-lane offsets: a Q / O head's rows, a K / V tile
-    const int64_t q_ext = ((int64_t)Nq - 1) * st.qn * 2 + 256, o_ext = ((int64_t)Nq - 1) * st.on * 2 + 256;
+    const int64_t q_ext = ((int64_t)Nq - 1) * st.qn * 2 + 2 * D, o_ext = ((int64_t)Nq - 1) * st.on * 2 + 2 * D;
     const int64_t kv_tile = 64 * std::max(st.kn, st.vn) * 2;
     if (q_ext >= (1ll << 32) || o_ext >= (1ll << 32) || kv_tile >= (1ll << 31)) return false;
     for (int64_t s : {st.qb, st.qh, st.kb, st.kh, st.vb, st.vh, st.ob, st.oh, st.qn, st.kn, st.vn, st.on})
@@ -137,9 +135,10 @@ bool attn_v13_ok(int D, int is_bf16, int causal, int Nq, int Nk, const V7Strides
 
 int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B, int H, int group, int Nq,
                     int Nk, const V7Strides& st, float scale, hipStream_t stream, bool persistent, float muoff,
-                    uint32_t* stamps, bool causal, bool fp16) {
-    PLI_REQUIRE(attn_v13_ok(128, fp16 ? 0 : 1, causal, Nq, Nk, st), "attn_fwd_v13: shape not supported");
-    PLI_REQUIRE(!(fp16 && stamps), "attn_fwd_v13: the stamp build is bf16");
+                    uint32_t* stamps, bool causal, bool fp16, int D) {
+    PLI_REQUIRE(attn_v13_ok(D, fp16 ? 0 : 1, causal, Nq, Nk, st), "attn_fwd_v13: shape not supported");
+    PLI_REQUIRE(H > 0 && H < (1 << 16), "attn_fwd_v13: H = %d past the packed 16-bit head count", H);
+    PLI_REQUIRE(!((fp16 || D != 128) && stamps), "attn_fwd_v13: the stamp build is bf16, D = 128");
     const int qblocks = cdiv(Nq, 256);
     const int64_t nb = (int64_t)B * H * qblocks;
     PLI_REQUIRE(nb < (1ll << 31) && nb > 0, "attn_fwd_v13: grid too large");
@@ -191,10 +190,11 @@ int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B,
     a.w[A_NT] = (uint32_t)(Nk / 64);
     a.w[A_QBLOCKS] = (uint32_t)qblocks;
     a.w[A_NBLOCKS] = (uint32_t)nb;
-    magic31((uint32_t)qblocks, a.w[A_MAGQ], a.w[A_SHQ]);
-    magic31((uint32_t)H, a.w[A_MAGH], a.w[A_SHH]);
-    magic31((uint32_t)group, a.w[A_MAGG], a.w[A_SHG]);
-    a.w[A_H] = (uint32_t)H;
+    uint32_t shq, shh, shg;
+    magic31((uint32_t)qblocks, a.w[A_MAGQ], shq);
+    magic31((uint32_t)H, a.w[A_MAGH], shh);
+    magic31((uint32_t)group, a.w[A_MAGG], shg);
+    a.w[A_SHIFTS] = shq | (shh << 5) | (shg << 10) | ((uint32_t)H << 16);
     a.w[A_CW] = cw;
     a.w[A_HX] = hx;
     a.w[A_OFFT] = causal ? (uint32_t)((Nk - Nq) / 64) : 0u;
@@ -213,6 +213,7 @@ int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B,
 #else
     (void)stamps;
 #endif
+    if (D == 64) return launch_v13_d64(fp16, causal, (unsigned)grid, a, stream);
     if (fp16) {
         if (causal) {
             hipLaunchKernelGGL(attn_fwd_v13hc, dim3((unsigned)grid), dim3(256), 0, stream, a);
@@ -241,7 +242,7 @@ extern "C" int pli_diag_v13_clock(const void* q, const void* k, const void* v, v
     const int64_t sn = 128, sh = (int64_t)N * 128, sb = (int64_t)H * N * 128;
     const V7Strides st{sb, sh, sn, sb, sh, sn, sb, sh, sn, sb, sh, sn};
     const int rc = launch_attn_v13(q, k, v, o, B, H, 1, N, N, st, 1.f / sqrtf(128.f), 0, true, 62.f, stamps, false,
-                                   false);
+                                   false, 128);
     if (rc != 0 || hipDeviceSynchronize() != hipSuccess) return -1;
     return 0;
 }

@@ -21,10 +21,11 @@ int launch_attn_v7(const void* q, const void* k, const void* v, void* o, int B, 
 // (attn_v13_ok: bf16 or fp16 -- is_bf16 only picks the program)
 bool attn_v12_ok(int D, int is_bf16, int causal, int Nk);
 bool attn_v13_ok(int D, int is_bf16, int causal, int Nq, int Nk, const V7Strides& st);
-// attn_fwd_v13 (flash_v13.hip): bf16 or fp16 (fp16 = true), D = 128
+// attn_fwd_v13 (flash_v13.hip, flash_v13_d64.hip): bf16 or fp16 (fp16 =
+// true), head dim D = 128 or 64
 int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B, int H, int group, int Nq,
                     int Nk, const V7Strides& st, float scale, hipStream_t stream, bool persistent, float muoff,
-                    uint32_t* stamps = nullptr, bool causal = false, bool fp16 = false);
+                    uint32_t* stamps = nullptr, bool causal = false, bool fp16 = false, int D = 128);
 // thr: the defer-max threshold (log2 units); 64 and 0 are the built forms
 int launch_attn_v12(const void* q, const void* k, const void* v, void* o, int B, int H, int group, int Nq,
                     int Nk, const V7Strides& st, float scale, hipStream_t stream, bool persistent,

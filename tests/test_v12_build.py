@@ -54,3 +54,38 @@ def test_v12_no_compiler_agpr_use_or_spill(tmp_path, src):
     assert not own, f"hipcc-generated AGPR/scratch/M0 accesses in {src}: {own[:8]}"
     sizes = [int(x) for x in re.findall(r"\.private_segment_fixed_size:\s+(\d+)", text)]
     assert sizes and not any(sizes), f"{src}: a kernel uses scratch ({sizes})"
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+@pytest.mark.parametrize("src", ["flash_v13.hip", "flash_v13_d64.hip"])
+def test_v13_asm_only_kernels_build_clean(tmp_path, src):
+    """attn_fwd_v13's bodies are one inline-asm statement each (tools/
+    gen_flash_v13.py): the clobber list names no register hipcc reserves
+    (no -Winline-asm warning: the program keeps off s32 / s100 / s101 and
+    saves / restores m0 itself), no kernel has a stack frame or scratch, and
+    no instruction hipcc generates outside the asm touches an AGPR, scratch,
+    m0 or s32."""
+    out = tmp_path / "k.s"
+    cmd = [HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "-Winline-asm",
+           "-I" + os.path.join(ROOT, "include"), "-I" + CSRC, "-S", "--cuda-device-only",
+           os.path.join(CSRC, src), "-o", str(out)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "inline asm clobber list contains reserved registers" not in r.stderr, r.stderr[-1500:]
+    text = out.read_text()
+    in_asm = False
+    own = []
+    for line in text.splitlines():
+        if ";;#ASMSTART" in line:
+            in_asm = True
+            continue
+        if ";;#ASMEND" in line:
+            in_asm = False
+            continue
+        code = line.split(";")[0]
+        if not in_asm and (re.search(r"\bv_accvgpr_(read|write)|\bscratch_(load|store)", code)
+                           or re.search(r"\bm0\b|\bs32\b|\bs\[3[0-2]:", code)):
+            own.append(line.strip())
+    assert not own, f"hipcc-generated AGPR / scratch / m0 / s32 accesses in {src}: {own[:8]}"
+    sizes = [int(x) for x in re.findall(r"\.private_segment_fixed_size:\s+(\d+)", text)]
+    assert sizes and not any(sizes), f"{src}: a kernel uses scratch ({sizes})"

@@ -131,3 +131,30 @@ def test_v13_f16_program_vs_f64(case):
     assert err <= 1e-2, f"max |err| {err:.3e}"
     if muoff < 0:
         assert em.counts.get("v_sub_f32", 0) > 0, "the rescale path never ran"
+
+
+D64_CASES = [  # (B, H, Hkv, Nq, Nk, grid, layout, muoff, causal, dtype): head dim 64 (Gen(hd=64))
+    (1, 2, 2, 256, 320, 1, "bhsd", 62.0, False, "bf16"),   # persistent: two blocks of five tiles
+    (2, 2, 1, 200, 128, 1, "bshd", 62.0, False, "bf16"),   # GQA, ragged Nq, BSHD
+    (1, 1, 1, 256, 256, None, "bhsd", 0.0, False, "bf16"),  # the rescale path at every tile
+    (1, 2, 1, 256, 512, None, "bhsd", 62.0, True, "bf16"),  # causal, diagonal offset
+    (1, 2, 2, 256, 320, 1, "bhsd", 4.0, False, "f16"),     # fp16, persistent
+    (1, 1, 1, 256, 256, None, "bhsd", -1.0, True, "f16"),   # fp16 causal, P-bit rescale at nearly every tile
+]
+
+
+@pytest.mark.parametrize("case", D64_CASES, ids=lambda c: "d64-b{}h{}kv{}q{}k{}g{}-{}-mu{}-causal{}-{}".format(*c))
+def test_v13_d64_program_vs_f64(case):
+    """head dim 64: the first halves of the D = 128 tile images, 4 DMA pieces
+    per wave, 32 + 32 MFMAs per tile (reference ch01 MHA d=512 h=8 and the
+    ch06 GPU tests run head_dim 64)"""
+    B, H, Hkv, Nq, Nk, grid, lay, muoff, causal, dtype = case
+    rng = np.random.default_rng(11 + sum(case[:5]))
+    q = rng.standard_normal((B, H, Nq, 64))
+    k = rng.standard_normal((B, Hkv, Nk, 64))
+    v = rng.standard_normal((B, Hkv, Nk, 64))
+    o, em = R.run(q, k, v, grid=grid, layout=lay, muoff=muoff, causal=causal, dtype=dtype)
+    err = np.abs(o - f64_attention(q, k, v, causal, dtype=dtype)).max()
+    assert err <= 1e-2, f"max |err| {err:.3e}"
+    if muoff <= 0:
+        assert em.counts.get("v_sub_f32", 0) > 0, "the rescale path never ran"

@@ -300,6 +300,11 @@ class Emu:
         gf = lambda x: u2f(self.vec(w, x))  # noqa: E731
         if op == "v_mov_b32":
             return self.vset(w, o[0], g(o[1]))
+        if op == "v_writelane_b32":  # vdst[lane] = scalar (EXEC ignored)
+            w.v[o[0].i][int(o[2])] = self.sc(w, o[1]) & M32
+            return
+        if op == "v_readlane_b32":  # sdst = vsrc[lane]
+            return self.sset(w, o[0], int(w.v[o[1].i][int(o[2])]))
         if op == "v_accvgpr_write_b32":
             return self.vset(w, o[0], g(o[1]))
         if op == "v_accvgpr_read_b32":

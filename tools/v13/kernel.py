@@ -40,6 +40,32 @@ BF16_ONES = 0x3F803F80
 DTYPES = {"bf16": {"mfma": "v_mfma_f32_16x16x32_bf16", "ones": BF16_ONES, "cvt": "v_cvt_pk_bf16_f32"},
           "f16": {"mfma": "v_mfma_f32_16x16x32_f16", "ones": 0x3C003C00, "cvt": "v_cvt_pk_f16_f32"}}
 DT = dict(DTYPES["bf16"])
+# head dim (Gen(hd=...)): 128, or 64 -- the D = 64 tile images are the first
+# halves of the D = 128 ones (K: 8 KiB of 64 keys x 128 B rows, V likewise),
+# so the same swizzle, fragment offsets and DMA piece map serve both; per
+# tile 16 pieces instead of 32 (4 per wave), 32 + 32 MFMAs instead of 64 + 64
+GEOM = {"hd": 128}
+
+
+def NDS():
+    """32-wide d slices of Q / K (QK MFMA k steps)"""
+    return GEOM["hd"] // 32
+
+
+def NDB():
+    """16-wide d blocks of O / V (PV MFMA rows)"""
+    return GEOM["hd"] // 16
+
+
+def NPW():
+    """LDS-DMA pieces per wave per tile (K half, then V half)"""
+    return GEOM["hd"] // 16
+
+
+def WSH():
+    """sWKOFF = wave << WSH() = the wave's byte offset in an image (8 pieces of
+    1 KiB per wave at D = 128, 4 at D = 64: 32 hd bytes)"""
+    return 12 if GEOM["hd"] == 128 else 11
 
 # ---------------------------------------------------------------- registers
 
@@ -142,36 +168,45 @@ def K_(kb, ds):
 
 # SGPRs (hipcc keeps its own in s0..s15)
 sKA = S(16, 2)
-sWKOFF, sL, sC, sNT, sTBK, sTBV = S(18), S(19), S(20), S(21), S(22), S(23)  # sWKOFF = 4096 * wave
+sWKOFF, sL, sC, sNT, sTBK, sTBV = S(18), S(19), S(20), S(21), S(22), S(23)  # sWKOFF = 32 hd * wave
 sCOH, sCQ0, sOFFT = S(24, 2), S(26), S(27)
-sNQH, sNOH, sNQ0, sNXNT, sTD, sDNT = S(28, 2), S(30, 2), S(32), S(33), S(34), S(35)
+# (s32 is hipcc's stack pointer and s100 / s101 are reserved too: the
+# program uses s16..s31 and s33..s99 only, so hipcc's -Winline-asm check of
+# the clobber list is clean)
+sNQH, sNOH, sNQ0, sNXNT, sTD, sDNT = S(28, 2), S(30, 2), S(93), S(33), S(34), S(35)
 sNXK, sNXV, sNXIDX, sT = S(36, 2), S(38, 2), S(40), S(41)
 sDK, sDV, sDIDX = S(42, 2), S(44, 2), S(46)
 sSM1, sS0, sSP1, sSP2, sHASN = S(47), S(48), S(49), S(50), S(51)
 sDIR = sHASN  # causal: the current block's stream order (1 = reversed), see block_params
 sT0, sT1, sT8, sRET = S(52), S(53), S(54), S(55)
-ARGS = 56  # block-parameter arguments: s56..s95 (dwords 0..39)
+ARGS = 56  # block-parameter arguments: s56..s92 (dwords 0..36)
 
 
 def ARG(k, n=1):
     return S(ARGS + k, n)
 
 
-sT2, sT3, sT4, sT5, sT6, sT7 = (S(96 + k) for k in range(6))
+sT2, sT3, sT4, sT5, sT6, sT7 = (S(94 + k) for k in range(6))  # sT2 even: sT2:sT3 is a 64-bit pair
 SGPR_FIRST = 16
-SGPR_LAST = 101
+SGPR_LAST = 99
+SGPR_SKIP = (32,)
+M0SAVE = (V(217), 63)  # m0 is saved in lane 63 of v217 (the stamp build's record: lanes 0-8) and restored at exit
 
 # kernel argument dwords (V13Args in csrc/flash_v13.hip)
-# (dwords 0..39 are reloaded into s56..s95 at every block transition; 40..
-# are read at init or by a single s_load where needed)
+# (dwords 0..36 are reloaded into s56..s92 at every block transition; 37..
+# are read at init or by a single s_load where needed).  "shifts" packs the
+# three magic-division shifts and the head count: shq | shh << 5 | shg << 10
+# | H << 16 (SALU shifts read bits 4:0 of their count)
 ARG_LAYOUT = ["q", "q_hi", "k", "k_hi", "v", "v_hi", "o", "o_hi",
               "qb", "qb_hi", "qh", "qh_hi", "kb", "kb_hi", "kh", "kh_hi",
               "vb", "vb_hi", "vh", "vh_hi", "ob", "ob_hi", "oh", "oh_hi",
-              "qn", "on", "nq", "nt", "qblocks", "nblocks", "magq", "shq",
-              "magh", "shh", "magg", "shg", "H", "cw", "hx", "G",
+              "qn", "on", "nq", "nt", "qblocks", "nblocks", "magq", "magh",
+              "magg", "shifts", "cw", "hx", "G",
               "kn", "vn", "c", "muoff", "tbk", "tbv", "stamp", "stamp_hi",
               "offt", "pad1", "pad2", "pad3", "pad4", "pad5", "pad6", "pad7",
-              "pad8", "pad9", "pad10", "pad11", "pad12", "pad13", "pad14", "pad15"]
+              "pad8", "pad9", "pad10", "pad11", "pad12", "pad13", "pad14", "pad15",
+              "pad16", "pad17", "pad18"]
+assert len(ARG_LAYOUT) == 64
 AI = {n: i for i, n in enumerate(ARG_LAYOUT)}
 
 SLOT = 32768  # one ring slot: K image (16 KiB) then V image (16 KiB)
@@ -313,12 +348,17 @@ def qk_mfmas(mask=None, muc=False):
             return TRIMU(qb) if muc else TRI
         return MUC(qb) if muc else 0
     return [mfma(S_(kb, qb), K_(kb, ds), Q_(qb, ds), S_(kb, qb) if ds else c0(kb, qb))
-            for qb in range(4) for ds in range(4) for kb in range(4)]
+            for qb in range(4) for ds in range(NDS()) for kb in range(4)]
 
 
 def qk_done_gap(kb, qb):
     """QK phase gap after which S(kb, qb) is complete"""
-    return 16 * qb + 12 + kb
+    return 4 * NDS() * qb + 4 * (NDS() - 1) + kb
+
+
+def qk_first(kb, qb):
+    """QK phase index of the MFMA that starts S(kb, qb) (it overwrites S)"""
+    return 4 * NDS() * qb + kb
 
 
 def rowsum_mfmas(X, ones=None):
@@ -330,39 +370,54 @@ def rowsum_mfmas(X, ones=None):
 def qk_with_rowsums(mask=None, muc=False, Xr=None):
     """LCHECK: QK(t) with the row sums of tile t-1 (state Xr) interleaved
     into its last 8 MFMAs (after every deferred slice of t-1 is due, so the
-    check right after the phase reads complete sums); returns the MFMA list
-    and done(kb, qb) -> the gap after which S(kb, qb) is complete"""
+    check right after the phase reads complete sums); returns the MFMA list,
+    done(kb, qb) -> the gap after which S(kb, qb) is complete and first(kb,
+    qb) -> the index of the MFMA that starts S(kb, qb)"""
     qk = qk_mfmas(mask, muc)
+    n = len(qk)
     if Xr is None:
-        return qk, lambda kb, qb: qk_done_gap(kb, qb)
+        return qk, lambda kb, qb: qk_done_gap(kb, qb), lambda kb, qb: qk_first(kb, qb)
     rs = rowsum_mfmas(Xr)
-    out, pos = qk[:56], {}
-    for j in range(56, 64):
-        out += [rs[j - 56], qk[j]]
-    for j in range(64):
-        pos[j] = j if j < 56 else 2 * j - 55
-    return out, lambda kb, qb: pos[qk_done_gap(kb, qb)]
+    out, pos = qk[:n - 8], {}
+    for j in range(n - 8, n):
+        out += [rs[j - (n - 8)], qk[j]]
+    for j in range(n):
+        pos[j] = j if j < n - 8 else 2 * j - (n - 9)
+    # the deferred slices of t-1 (q-block 3) are due before their S blocks are
+    # overwritten -- before the row sums of q-block 3 (rs[6], rs[7]) read them
+    assert pos[qk_first(3, 3)] - 1 < out.index(rs[6])
+    return out, lambda kb, qb: pos[qk_done_gap(kb, qb)], lambda kb, qb: pos[qk_first(kb, qb)]
 
 
 def pv_mfmas(X):
     out = []
-    for db in range(8):
+    per = 8 // NDB()  # P-bit check: the 8 row sums spread over the d-blocks
+    for db in range(NDB()):
         for kp in range(2):
             for qb in range(4):
                 out.append(mfma(O_(db, qb), VF(db % NVF, kp), P_(X, qb, kp), O_(db, qb)))
         if not LCHECK[0]:
-            qb, kp = db % 4, db // 4
-            out.append(mfma(L_(qb), ONES, P_(X, qb, kp), L_(qb)))
+            for r in range(per * db, per * db + per):
+                qb, kp = r % 4, r // 4
+                out.append(mfma(L_(qb), ONES, P_(X, qb, kp), L_(qb)))
     return out
 
 
 def pv_first_gap(db):
-    return (8 if LCHECK[0] else 9) * db
+    return (8 if LCHECK[0] else 8 + 8 // NDB()) * db
+
+
+def vbuf_free(db):
+    """earliest PV gap for d-block db's V^T reads: its buffer (db mod 3) is
+    d-block db-3's, free one MFMA after that block's last use"""
+    if GEOM["hd"] == 128:
+        return pv_first_gap(db - 3) + 9  # (the D = 128 schedules as built in round 4)
+    return pv_first_gap(db - 3) + pv_first_gap(1) + 1
 
 
 def k_reads():
     return [I("ds_read_b128", K_(kb, ds), VKA, mods=f"offset:{512 * (ds & 1) + 2048 * kb + 8192 * (ds >> 1)}")
-            for ds in range(4) for kb in range(4)]
+            for ds in range(NDS()) for kb in range(4)]
 
 
 def v_reads(db):
@@ -441,11 +496,17 @@ def softmax_fills(X, slices, earliest_of, deadline_of=None, ytag=0, prev_cv=None
 # ---------------------------------------------------------------- SALU helpers
 
 
-def div_magic(out, x, mag, sh):
-    """out = x / d for x < 2^31 (mag, sh from the host: Granlund-Montgomery
-    with N = 31): ((x * mag) >> 31) >> sh"""
-    return [I("s_mul_hi_u32", sT6, x, mag), I("s_mul_i32", sT7, x, mag), I("s_lshl_b32", sT6, sT6, 1),
-            I("s_lshr_b32", sT7, sT7, 31), I("s_or_b32", sT6, sT6, sT7), I("s_lshr_b32", out, sT6, sh)]
+def div_magic(out, x, mag, shpos):
+    """out = x / d for x < 2^31 (mag and the shift from the host:
+    Granlund-Montgomery with N = 31): ((x * mag) >> 31) >> sh, sh at bit
+    shpos of the packed "shifts" argument"""
+    sh = ARG(AI["shifts"])
+    c = [I("s_mul_hi_u32", sT6, x, mag), I("s_mul_i32", sT7, x, mag), I("s_lshl_b32", sT6, sT6, 1),
+         I("s_lshr_b32", sT7, sT7, 31), I("s_or_b32", sT6, sT6, sT7)]
+    if shpos:
+        c += [I("s_lshr_b32", sT7, sh, shpos)]
+        sh = sT7
+    return c + [I("s_lshr_b32", out, sT6, sh)]
 
 
 def mad64(out, base, x, st, y, st2):
@@ -482,7 +543,7 @@ def block_params(sx, causal=False, uid=0, rev=0):
           I("s_cselect_b32", sT4, 0, sT4), I("s_cselect_b32", sT5, 8, sT5),
           I("s_and_b32", sT2, sx, 7), I("s_lshr_b32", sT3, sx, 3), I("s_mul_i32", sT4, sT2, sT4),
           I("s_min_u32", sT2, sT2, sT5), I("s_add_u32", sT4, sT4, sT2), I("s_add_u32", sT4, sT4, sT3)]
-    c += div_magic(sT5, sT4, ARG(AI["magq"]), ARG(AI["shq"]))
+    c += div_magic(sT5, sT4, ARG(AI["magq"]), 0)
     c += [I("s_mul_i32", sT2, sT5, QB), I("s_sub_u32", sT2, sT4, sT2)]
     if causal:
         # heaviest first: query height QB-1-r
@@ -513,11 +574,11 @@ def block_params(sx, causal=False, uid=0, rev=0):
     else:
         c += [I("s_mov_b32", sT8, ARG(AI["nt"]))]
     # q0 = qblk * 256 + 64 * wave
-    c += [I("s_lshl_b32", sT2, sT2, 8), I("s_lshr_b32", sT3, sWKOFF, 6), I("s_add_u32", sNQ0, sT2, sT3)]
+    c += [I("s_lshl_b32", sT2, sT2, 8), I("s_lshr_b32", sT3, sWKOFF, WSH() - 6), I("s_add_u32", sNQ0, sT2, sT3)]
     # b = bh / H, h = bh - b * H, hk = h / group
-    c += div_magic(sT4, sT5, ARG(AI["magh"]), ARG(AI["shh"]))
-    c += [I("s_mul_i32", sT2, sT4, ARG(AI["H"])), I("s_sub_u32", sT3, sT5, sT2)]
-    c += div_magic(sT5, sT3, ARG(AI["magg"]), ARG(AI["shg"]))
+    c += div_magic(sT4, sT5, ARG(AI["magh"]), 5)
+    c += [I("s_lshr_b32", sT2, ARG(AI["shifts"]), 16), I("s_mul_i32", sT2, sT4, sT2), I("s_sub_u32", sT3, sT5, sT2)]
+    c += div_magic(sT5, sT3, ARG(AI["magg"]), 10)
     # heads: b in sT4, h in sT3, hk in sT5
     c += mad64(sNQH, ARG(AI["q"], 2), sT4, ARG(AI["qb"], 2), sT3, ARG(AI["qh"], 2))
     c += mad64(sNOH, ARG(AI["o"], 2), sT4, ARG(AI["ob"], 2), sT3, ARG(AI["oh"], 2))
@@ -537,32 +598,35 @@ def block_params(sx, causal=False, uid=0, rev=0):
 
 def load_args():
     return [I("s_load_dwordx16", ARG(0, 16), sKA, 0), I("s_load_dwordx16", ARG(16, 16), sKA, 64),
-            I("s_load_dwordx8", ARG(32, 8), sKA, 128), I("s_waitcnt", "lgkmcnt(0)")]
+            I("s_load_dwordx4", ARG(32, 4), sKA, 128), I("s_load_dword", ARG(36), sKA, 144),
+            I("s_waitcnt", "lgkmcnt(0)")]
 
 
 # ---------------------------------------------------------------- DMA
 
 
 def dma_fills(slot_reg, earliest0=2, spacing=6, rev=False):
-    """the 8 LDS-DMA pieces of the stream's next tile into slot slot_reg
-    (K pieces 4w..4w+3 of the K image, V pieces of the V image; one M0 write
-    per four), the stream switch before and the advance after"""
+    """the NPW() LDS-DMA pieces (8 at D = 128, 4 at D = 64) of the stream's
+    next tile into slot slot_reg (K pieces NPW/2 w .. of the K image, V
+    pieces of the V image; one M0 write per half), the stream switch before
+    and the advance after"""
     sw = Fill([I("s_cmp_eq_u32", sDIDX, sDNT), I("s_cselect_b64", sDK, sNXK, sDK),
                I("s_cselect_b64", sDV, sNXV, sDV), I("s_cselect_b32", sDIDX, sNXIDX, sDIDX),
                I("s_cselect_b32", sDNT, sNXNT, sDNT)],
               2, earliest=earliest0 - 1, tag="dmasw")
     fills = [sw]
     prev = sw
-    for j in range(8):
+    half = NPW() // 2
+    for j in range(NPW()):
         ins = []
         if j == 0:
             ins.append(I("s_add_u32", M0, slot_reg, sWKOFF))
-        if j == 4:
+        if j == half:
             ins += [I("s_add_u32", M0, slot_reg, sWKOFF), I("s_add_u32", M0, M0, VIMG)]
-        src = sDK if j < 4 else sDV
-        off = DMAK(j) if j < 4 else DMAV(j - 4)
+        src = sDK if j < half else sDV
+        off = DMAK(j) if j < half else DMAV(j - half)
         if "dma" not in ABL:
-            ins.append(I("global_load_lds_dwordx4", off, src, mods=f"offset:{1024 * (j % 4)}"))
+            ins.append(I("global_load_lds_dwordx4", off, src, mods=f"offset:{1024 * (j % half)}"))
         f = Fill(ins, DMA_COST, deps=[prev], sep=1 if j else 0, earliest=earliest0 + spacing * j, tag="dma")
         fills.append(f)
         prev = f
@@ -668,8 +732,12 @@ class Gen:
     bottom-right-masked kernel (attn_fwd_v13c)"""
 
     def __init__(self, ndef=4, budget=8, dma_spacing=6, tag="%=", stamp=False, causal=False, abl=(), dma_cost=8,
-                 rev=True, qscale=False, dma_pv=0, dma_pv_spacing=16, budget_pv=None, lcheck=None, dtype="bf16"):
+                 rev=True, qscale=False, dma_pv=0, dma_pv_spacing=16, budget_pv=None, lcheck=None, dtype="bf16",
+                 hd=128):
         global DMA_COST
+        assert hd in (64, 128)
+        GEOM["hd"] = hd
+        assert not (qscale and hd != 128)
         # fp16: P keeps the bit check (P < 2: bit 14 of an fp16 half too) --
         # the l >= 1 test needs muoff >> log2 Nk, which fp16 P (normal down to
         # 2^-14, zero below 2^-24) cannot give; the launcher passes muoff 4
@@ -690,6 +758,7 @@ class Gen:
         # dma_pv on, dma_pv_spacing apart (A/B knob; 0 = all in the QK phase)
         self.dma_pv, self.dma_pv_spacing = dma_pv, dma_pv_spacing
         self.budget_pv = budget if budget_pv is None else budget_pv  # the steps' PV-phase issue budget
+        assert not (dma_pv and GEOM["hd"] != 128), "dma_pv: D = 128 only"
         self.ndef, self.budget, self.dma_spacing, self.tag = ndef, budget, dma_spacing, tag
         ABL.clear()
         ABL.update(abl)
@@ -713,8 +782,9 @@ class Gen:
     # ---- init ------------------------------------------------------------
     def init(self, in_kernarg, in_wg, in_wave):
         e = self.emit
-        e([I("s_mov_b64", sKA, in_kernarg), I("s_mov_b32", sL, in_wg), I("s_lshl_b32", sWKOFF, in_wave, 12)])
-        # dwords 40..47 (kn, vn, c, muoff, tbk, tbv, stamp) into s88..s95 first
+        e([I("v_writelane_b32", M0SAVE[0], M0, M0SAVE[1])])  # m0 is not on the clobber list
+        e([I("s_mov_b64", sKA, in_kernarg), I("s_mov_b32", sL, in_wg), I("s_lshl_b32", sWKOFF, in_wave, WSH())])
+        # dwords 37..44 (kn, vn, c, muoff, tbk, tbv, stamp) into s88..s95 first
         e([I("s_load_dwordx8", S(88, 8), sKA, 4 * AI["kn"])])
         if self.causal:
             e([I("s_load_dword", sOFFT, sKA, 4 * AI["offt"])])
@@ -740,10 +810,10 @@ class Gen:
            I("v_lshrrev_b32", t[4], 4, LANE), I("v_and_b32", t[4], 1, t[4]), I("v_lshlrev_b32", t[4], 1, t[4]),
            I("v_add_u32", t[3], t[3], t[4]), I("v_and_b32", t[4], 1, LANE), I("v_add_u32", t[3], t[3], t[4]),
            I("v_lshlrev_b32", t[3], 4, t[3])])                                          # 16 * laneCh
-        for j in range(4):
-            # K piece pc = 4w + j: rowbase 16((pc>>1)&3) + 8(pc&1), chbase 8(pc>>3)
-            # V piece: rowbase 8(pc&7), chbase 8(pc>>3)
-            e([I("s_lshr_b32", sT2, sWKOFF, 10), I("s_add_u32", sT2, sT2, j),           # pc = 4 wave + j
+        for j in range(NPW() // 2):
+            # K piece pc = (NPW/2) w + j: rowbase 16((pc>>1)&3) + 8(pc&1), chbase 8(pc>>3)
+            # V piece: rowbase 8(pc&7), chbase 8(pc>>3) (D = 64: pc < 8, chbase 0)
+            e([I("s_lshr_b32", sT2, sWKOFF, 10), I("s_add_u32", sT2, sT2, j),           # pc = (NPW/2) wave + j
                I("s_lshr_b32", sT3, sT2, 1), I("s_and_b32", sT3, sT3, 3), I("s_lshl_b32", sT3, sT3, 4),
                I("s_and_b32", sT4, sT2, 1), I("s_lshl_b32", sT4, sT4, 3), I("s_add_u32", sT3, sT3, sT4),  # K rowbase
                I("s_and_b32", sT4, sT2, 7), I("s_lshl_b32", sT4, sT4, 3),               # V rowbase
@@ -758,7 +828,7 @@ class Gen:
             # = this wave's record index (workgroup x 4 + wave)
             e([I("s_memtime", S(96, 2)), I("s_memrealtime", S(98, 2)), I("s_waitcnt", "lgkmcnt(0)")])
             e([I("v_writelane_b32", STAMPV, S(96 + k), k) for k in range(4)])
-            e([I("s_lshl_b32", sT6, sL, 2), I("s_lshr_b32", sT7, sWKOFF, 12), I("s_add_u32", sT6, sT6, sT7),
+            e([I("s_lshl_b32", sT6, sL, 2), I("s_lshr_b32", sT7, sWKOFF, WSH()), I("s_add_u32", sT6, sT6, sT7),
                I("v_writelane_b32", STAMPV, sT6, 8)])
         # ones selector, ring slots, causal mask operands
         e([I("v_mov_b32", ONES[k], DT["ones"]) for k in range(4)])
@@ -781,7 +851,7 @@ class Gen:
                   I("v_min_u32", T(0), sT0, T(0)), I("v_mul_lo_u32", T(0), T(0), ARG(AI["qn"])),
                   I("v_lshlrev_b32", T(1), 4, VG), I("v_add_u32", QOFF(qb), T(0), T(1))]
         for qb in range(4):
-            for ds in range(4):
+            for ds in range(NDS()):
                 c.append(I("global_load_dwordx4", Q_(qb, ds), QOFF(qb), qh, mods=f"offset:{64 * ds}"))
         return c
 
@@ -857,7 +927,7 @@ class Gen:
         e([I("s_load_dword", sT8, sKA, 4 * AI["muoff"])])
         if self.causal:
             e([I("s_lshr_b32", sTD, sCQ0, 6), I("s_add_u32", sTD, sTD, sOFFT)])  # the wave's diagonal tile
-        e([I("v_accvgpr_write_b32", A(k), 0) for k in range(128)])
+        e([I("v_accvgpr_write_b32", A(k), 0) for k in range(16 * NDB())])  # O
         e([I("v_mov_b32", L_(qb)[r], 0) for qb in range(4) for r in range(4)])
         if not LCHECK[0]:
             e([I("v_mov_b32", ACC(0), 0), I("v_mov_b32", ACC(1), 0)])
@@ -868,9 +938,10 @@ class Gen:
         e([I("v_add_u32", VKA, sS0, VKL)])
         e(k_reads())
         fills = dma_fills(sSP2, earliest0=1, spacing=4, rev=self.rev)
-        body, left = schedule(qk_mfmas(), fills, self.budget)
+        qk0 = qk_mfmas()
+        body, left = schedule(qk0, fills, self.budget)
         e(body)
-        e(drain(left, 64))
+        e(drain(left, len(qk0)))
         if self.rev:
             # only the wave whose diagonal tile this is has masked scores in it
             # (a first tile is never past a wave's diagonal)
@@ -891,7 +962,7 @@ class Gen:
                 e([I("v_mul_f32", T(20 + qb), sC, T(20 + qb)), I("v_add_f32", MU(qb), sT8, T(20 + qb))])
         e(exps_all(0))
         # tile 1 landed (tile 2 in flight): K(1) fragments
-        e([I("s_waitcnt", "vmcnt(8)"), I("s_barrier"), I("v_add_u32", VKA, sSP1, VKL)])
+        e([I("s_waitcnt", f"vmcnt({NPW()})"), I("s_barrier"), I("v_add_u32", VKA, sSP1, VKL)])
         e(k_reads())
         e([I("s_mov_b32", sT, 1)])
         # steps t = 1 .. nt-1, two per iteration (P states 1 / 0)
@@ -995,7 +1066,8 @@ class Gen:
         # ---- QK phase
         fills = []
         # deferred slices of tile t-1 (they read S(., 3): before QK(t) overwrites it)
-        dl = lambda qb, kb: 16 * qb + kb - 1  # noqa: E731
+        qk, done, first = qk_with_rowsums(mask, QSCALE[0], Xp if LCHECK[0] else None)
+        dl = lambda qb, kb: first(kb, qb) - 1  # noqa: E731
         f_def, cvd, last_or_prev = softmax_fills(Xp, dfr, lambda qb, kb: 0, dl, ytag=0)
         if "soft" in ABL:
             f_def = []
@@ -1011,13 +1083,13 @@ class Gen:
                 f.deps = [] if n == 0 else [dma_pv[n - 1]]
             dma_pv[4].deps = [dma_pv[3]]
         fills += dma
-        # V(t-1) d-blocks 0, 1
+        # V(t-1) d-blocks 0, 1 (from 32 MFMAs before the phase ends)
         for db in (0, 1):
             for ins in v_reads(db):
                 if "vread" not in ABL:
-                    fills.append(Fill(ins, 2, earliest=40 + 8 * db, tag="vread"))
+                    fills.append(Fill(ins, 2, earliest=(40 if GEOM["hd"] == 128 else len(qk) - 32) + 8 * db,
+                                      tag="vread"))
         # softmax(t), zero ACC(X) first (P-bit check)
-        qk, done = qk_with_rowsums(mask, QSCALE[0], Xp if LCHECK[0] else None)
         z = Fill(I("v_mov_b32", ACC(X), 0), 4, tag="zero")
         if not LCHECK[0]:
             fills.append(z)
@@ -1046,20 +1118,20 @@ class Gen:
         left = [f for f in left if f.gap is None]
         # ---- defer-max check of tile t-1
         self.check(Xp, f"rare_s{Xp}")
-        e([I("s_waitcnt", "vmcnt(8)")] + ([] if "barrier" in ABL else [I("s_barrier")]))
+        e([I("s_waitcnt", f"vmcnt({NPW()})")] + ([] if "barrier" in ABL else [I("s_barrier")]))
         # ---- PV phase (gaps numbered on from the QK phase's, so the
         # leftover softmax keeps its dependency distances)
         B0 = len(qk)
         fills = left
         ka = Fill(I("v_add_u32", VKA, sSP1, VKL), 4, earliest=B0, tag="kaddr")
-        kr = [Fill(ins, 2, deps=[ka], sep=1, earliest=B0 + n // 2, deadline=B0 + 40, tag="kread")
-              for n, ins in enumerate(k_reads())] if "kread" not in ABL else []
         pv = pv_mfmas(Xp)
-        # V d-block db (2..7) reads: after d-block db-3's MFMAs (same buffer), well before db's
+        kr = [Fill(ins, 2, deps=[ka], sep=1, earliest=B0 + n // 2, deadline=B0 + min(40, len(pv) - 8), tag="kread")
+              for n, ins in enumerate(k_reads())] if "kread" not in ABL else []
+        # V d-block db (2..) reads: after d-block db-3's MFMAs (same buffer), well before db's
         vr = []
-        for db in range(2 if "vread" not in ABL else 8, 8):
+        for db in range(2 if "vread" not in ABL else NDB(), NDB()):
             for ins in v_reads(db):
-                vr.append(Fill(ins, 2, earliest=B0 + (pv_first_gap(db - 3) + 9 if db >= 3 else 0),
+                vr.append(Fill(ins, 2, earliest=B0 + (vbuf_free(db) if db >= 3 else 0),
                                deadline=B0 + pv_first_gap(db) - 6, tag="vread"))
         fills = [ka] + kr + vr + fills + dma_pv
         body, left = schedule(pv, fills, self.budget_pv, gap_offset=B0)
@@ -1080,9 +1152,9 @@ class Gen:
         self.check(X, f"rare_t{X}")
         e(v_reads(0) + v_reads(1))
         fills = []
-        for db in range(2, 8):
+        for db in range(2, NDB()):
             for ins in v_reads(db):
-                fills.append(Fill(ins, 2, earliest=pv_first_gap(db - 3) + 9 if db >= 3 else 0,
+                fills.append(Fill(ins, 2, earliest=vbuf_free(db) if db >= 3 else 0,
                                   deadline=pv_first_gap(db) - 6, tag="vread"))
         # the next block's Q rows (or this block's again past the last block)
         fills += chain(self.q_offsets(sNQ0, sNQH), earliest=4)
@@ -1104,7 +1176,7 @@ class Gen:
                I("v_and_b32", T(26), 1, VG), I("v_lshlrev_b32", T(26), 5, T(26)),
                I("v_lshrrev_b32", T(27), 1, VG), I("v_lshlrev_b32", T(27), 4, T(27)),
                I("v_add3_u32", OOFF(qb), T(25), T(26), T(27))])
-            for dbp in range(4):
+            for dbp in range(NDB() // 2):
                 w = 4 * dbp  # words T(w) .. T(w+3)
                 for half, db in enumerate((2 * dbp, 2 * dbp + 1)):
                     for r in range(4):
@@ -1115,7 +1187,7 @@ class Gen:
                        I(DT["cvt"], T(w + 2 * half + 1), T(30), T(31))])
                 e([I("v_permlane16_swap_b32", T(w), T(w + 2)), I("v_permlane16_swap_b32", T(w + 1), T(w + 3))])
             e([I("v_cmp_gt_u32_e32", VCC, ARG(AI["nq"]), T(24)), I("s_and_saveexec_b64", S(sT2.i, 2), VCC)])
-            for dbp in range(4):
+            for dbp in range(NDB() // 2):
                 e([I("global_store_dwordx4", OOFF(qb), V(T(4 * dbp).i, 4), sCOH, mods=f"offset:{64 * dbp}")])
             e([I("s_mov_b64", EXEC, S(sT2.i, 2))])
         # next block
@@ -1151,7 +1223,7 @@ class Gen:
                 continue
             e([I("v_add_u32", T(36), tile_slot, VKL)])
             e([I("ds_read_b128", K_(kb, ds), T(36), mods=f"offset:{512 * (ds & 1) + 2048 * kb + 8192 * (ds >> 1)}")
-               for ds in range(4) for kb in range(4)])
+               for ds in range(NDS()) for kb in range(4)])
             # QSCALE: the checked tile with C = 0 (its exact max), the next one
             # shifted by the new mu (its later slices exp S in place)
             e(qk_mfmas(muc=QSCALE[0] and Xs != X))
@@ -1176,7 +1248,7 @@ class Gen:
                        I("v_sub_f32", T(24), MU(qb), m), I("v_exp_f32", T(24), T(24)), I("v_mov_b32", MU(qb), m)])
                     if QSCALE[0]:
                         e([I("v_sub_f32", MUC(qb)[r], 0, m) for r in range(4)])
-                    for db in range(8):
+                    for db in range(NDB()):
                         for r in range(4):
                             e([I("v_accvgpr_read_b32", T(25), O_(db, qb)[r]),
                                I("v_mul_f32", T(25), T(25), T(24)),
@@ -1208,14 +1280,14 @@ class Gen:
             # exit stamps into lanes 4-7; lanes 0-7 stored at stamp + 32 * record
             e([I("s_memtime", S(96, 2)), I("s_memrealtime", S(98, 2)), I("s_waitcnt", "lgkmcnt(0)")])
             e([I("v_writelane_b32", STAMPV, S(96 + k), 4 + k) for k in range(4)])
-            e([I("v_readlane_b32", sT6, STAMPV, 8), I("s_load_dwordx2", S(96, 2), sKA, 4 * AI["stamp"]),
+            e([I("v_readlane_b32", sT6, STAMPV, 8), I("s_load_dwordx2", S(88, 2), sKA, 4 * AI["stamp"]),
                I("s_waitcnt", "lgkmcnt(0)"), I("s_lshl_b32", sT6, sT6, 5),
                I("v_lshlrev_b32", T(0), 2, LANE), I("v_add_u32", T(0), sT6, T(0)),
-               I("s_mov_b64", EXEC, 0xFF), I("global_store_dword", T(0), STAMPV, S(96, 2)),
+               I("s_mov_b64", EXEC, 0xFF), I("global_store_dword", T(0), STAMPV, S(88, 2)),
                I("s_mov_b64", EXEC, -1), I("s_waitcnt", "vmcnt(0)")])
         e([I("s_branch", Lb("exit"))])
         for X in (0, 1):
             self.rare(f"rare_s{X}", X, True)
             self.rare(f"rare_t{X}", X, False)
-        e([label(Lb("exit"))])
+        e([label(Lb("exit")), I("v_readlane_b32", sT7, M0SAVE[0], M0SAVE[1]), I("s_mov_b32", M0, sT7)])
         return self.prog

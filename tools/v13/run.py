@@ -51,10 +51,11 @@ def args_for(qa, ka, va, oa, B, H, Hkv, Nq, Nk, strides_el, scale, G, muoff=7.0,
         d[name], d[name + "_hi"] = val & 0xFFFFFFFF, val >> 32
     d["qn"], d["kn"], d["vn"], d["on"] = st[2], st[5], st[8], st[11]
     d["nq"], d["nt"], d["qblocks"], d["nblocks"] = Nq, Nk // 64, qblocks, nblocks
-    d["magq"], d["shq"] = magic(qblocks)
-    d["magh"], d["shh"] = magic(H)
-    d["magg"], d["shg"] = magic(group)
-    d["H"] = H
+    d["magq"], shq = magic(qblocks)
+    d["magh"], shh = magic(H)
+    d["magg"], shg = magic(group)
+    assert H < (1 << 16)
+    d["shifts"] = shq | (shh << 5) | (shg << 10) | (H << 16)
     if causal:
         walk, lg8, lghq, per, hx = pair_walk(nblocks, qblocks, G)
         d["cw"] = walk | (lg8 << 8) | (lghq << 16) | (per << 24)
@@ -81,13 +82,13 @@ def program(**kw):
 
 
 def run(q, k, v, scale=None, grid=None, muoff=7.0, layout="bhsd", causal=False, structural=False, dtype="bf16", **kw):
-    """q [B,H,Nq,128], k / v [B,Hkv,Nk,128] float arrays (rounded to bf16, or
+    """q [B,H,Nq,D], k / v [B,Hkv,Nk,D] (D = 128 or 64) float arrays (rounded to bf16, or
     fp16 with dtype="f16") -> O [B,H,Nq,128] float32 from the emulated kernel.
     layout 'bshd' stores the tensors as [B,S,H,D] (strided heads)."""
     enc, dec = (E.f16_rne, E.f16_to_f32) if dtype == "f16" else (E.bf16_rne, E.bf16_to_f32)
     B, H, Nq, D = q.shape
     Hkv, Nk = k.shape[1], k.shape[2]
-    assert D == 128 and Nk % 64 == 0 and Nk >= 128
+    assert D in (64, 128) and Nk % 64 == 0 and Nk >= 128
     assert not causal or (Nk - Nq >= 0 and (Nk - Nq) % 64 == 0)
     scale = 1.0 / math.sqrt(D) if scale is None else scale
     heap = E.Heap()
@@ -116,7 +117,7 @@ def run(q, k, v, scale=None, grid=None, muoff=7.0, layout="bhsd", causal=False, 
     args = args_for(qa, ka, va, oa, B, H, Hkv, Nq, Nk, list(sq) + list(sk) + list(sv) + list(so), scale, G, muoff,
                     causal)
     kaddr = heap.alloc(args.nbytes, args.tobytes())
-    prog = program(causal=causal, dtype=dtype, **kw)
+    prog = program(causal=causal, dtype=dtype, **(dict(kw, hd=64) if D == 64 else kw))
     em = E.Emu(prog, heap, structural=structural)
     em.kbase = ka
     for wg in range(G):
