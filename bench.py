@@ -223,6 +223,34 @@ def bench_torch_sdpa(q, k, v, o, stream) -> dict:
     return out
 
 
+def bench_flash_dtypes(stream) -> dict:
+    """The default flash route at the bench shape (B8 H32 S4096) for the other
+    element types / head dims the reference runs (ch06/test_ch06.py:158-189
+    is fp16 head_dim 64; ch01 MHA d=512 h=8 is head_dim 64): fp16 D=128,
+    bf16 D=64, fp16 D=64, non-causal and causal; events over 20 launches
+    after 10 warm-up.  Reported only (value is the bf16 D=128 headline)."""
+    import pli_hip
+    out = {}
+    for dt, D_ in (("fp16", 128), ("bf16", 64), ("fp16", 64)):
+        tdt = torch.float16 if dt == "fp16" else torch.bfloat16
+        g = torch.Generator(device="cuda").manual_seed(77)
+        q, k, v = (torch.randn(B, H, S, D_, device="cuda", dtype=tdt, generator=g) for _ in range(3))
+        o = torch.empty_like(q)
+        r = {}
+        for causal in (False, True):
+            fn = lambda: pli_hip.flash_attn_fwd(q, k, v, causal=causal, out=o)  # noqa: E731
+            for _ in range(10):
+                fn()
+            ms = event_time_ms(fn, 20, stream)
+            pairs = S * (S + 1) // 2 if causal else S * S
+            r["causal" if causal else "non_causal"] = {"ms": ms,
+                                                       "TFLOP/s": 4 * B * H * D_ * pairs / (ms * 1e-3) / 1e12}
+        out[f"{dt}_d{D_}"] = r
+        del q, k, v, o
+    out["kernels"] = "attn_fwd_v13h (fp16 D128), attn_fwd_v13_d64 / v13h_d64 (D64) and their causal forms"
+    return out
+
+
 def headline_summary(r: dict) -> dict:
     """the numbers the round's verdict reads, in one short record (the last
     key of the JSON line, so it survives any tail truncation)"""
@@ -248,6 +276,10 @@ def headline_summary(r: dict) -> dict:
             out[f"{tp}_shard_TFLOP/s"] = [sh["TFLOP/s"], sh["torch_F.linear_TFLOP/s"]]
     if "decode_attn" in r:
         out["decode_attn_GB/s"] = r["decode_attn"]["GB/s"]
+    if "flash_dtypes" in r:
+        for key, val in r["flash_dtypes"].items():
+            if isinstance(val, dict):
+                out[f"flash_{key}_TFLOP/s"] = [val["non_causal"]["TFLOP/s"], val["causal"]["TFLOP/s"]]
     return out
 
 
@@ -823,6 +855,11 @@ def main():
     if not args.flash_only:
         log("[bench] torch sdpa comparison")
         extra["flash_torch_sdpa"] = bench_torch_sdpa(q, k, v, o, stream)
+        log("[bench] flash fp16 / head dim 64")
+        extra["flash_dtypes"] = bench_flash_dtypes(stream)
+        fd = extra["flash_dtypes"]
+        log("[bench] flash " + ", ".join(f"{key} {val['non_causal']['TFLOP/s']:.0f}/{val['causal']['TFLOP/s']:.0f}"
+                                          for key, val in fd.items() if isinstance(val, dict)) + " TF/s (plain/causal)")
     if args.flash_only:
         pass
     elif not args.quick:
@@ -909,7 +946,7 @@ def main():
     # the bulky records first, the sub-results a reader checks last: the
     # driver keeps only the tail of stdout (~8 KB), so flash_causal, gemv,
     # gemm, tp_gemm and the one-line summary must sit at the end of the line
-    late = ("flash_causal", "decode_attn", "gemv", "gemm", "tp_gemm")
+    late = ("flash_causal", "flash_dtypes", "decode_attn", "gemv", "gemm", "tp_gemm")
     for key, val in extra.items():
         if key not in late:
             result[key] = val

@@ -1,7 +1,7 @@
-# round-4 validation: smoke, the whole GPU suite, bench.py, and its rocprofv3 kernel summary
+# round validation (round 4, 5): smoke, the whole GPU suite, bench.py, and its rocprofv3 kernel summary
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 export TMPDIR=/tmp
-O=$GRAFT_REPO_ROOT/gpurun_out/${FINAL_TAG:-final8}
+O=$GRAFT_REPO_ROOT/gpurun_out/${FINAL_TAG:-r05_final}
 mkdir -p $O
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
 rc=$?; tail -3 $O/smoke.log; [ $rc -eq 0 ] || exit $rc
