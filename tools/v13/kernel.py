@@ -268,6 +268,12 @@ QSCALE = [False]
 # (3 VALU instead).
 LCHECK = [True]
 NEGONES = 0xBF80BF80
+# SHORTFIRST (Gen(causal=True, short_first=True), A/B knob): the pair walk
+# runs each workgroup's short block (height a) first and its long block
+# (QB-1-a) second, both streamed forward, so a tile's second read comes at
+# most 4a+4 tile-times after its first (the round-4 order reads it again up
+# to 64 later, the reversed second block about 67-2u later)
+SHORTFIRST = [False]
 
 
 def schedule(mfmas, fills, budget=8, gap_offset=0, lds_gap=LDS_GAP):
@@ -564,7 +570,7 @@ def block_params(sx, causal=False, uid=0, rev=0):
               I("s_add_u32", sT2, sT2, sT7),
               I("s_sub_u32", sT6, QB, 1), I("s_sub_u32", sT6, sT6, sT5),
               I("s_and_b32", sT4, sT4, 1)] + ([I("s_cselect_b32", sRET, 1, 0)] if rev else []) + [
-              I("s_cselect_b32", sT4, sT5, sT6),
+              I("s_cselect_b32", sT4, sT6, sT5) if SHORTFIRST[0] else I("s_cselect_b32", sT4, sT5, sT6),
               I("s_mov_b32", sT5, sT2), I("s_mov_b32", sT2, sT4), label(done)]
         # key tiles the block's last row sees: min(nt, 4 qblk + 4 + off / 64)
         c += [I("s_lshl_b32", sT8, sT2, 2), I("s_add_u32", sT8, sT8, 4), I("s_add_u32", sT8, sT8, sOFFT),
@@ -733,8 +739,10 @@ class Gen:
 
     def __init__(self, ndef=4, budget=8, dma_spacing=6, tag="%=", stamp=False, causal=False, abl=(), dma_cost=8,
                  rev=True, qscale=False, dma_pv=0, dma_pv_spacing=16, budget_pv=None, lcheck=None, dtype="bf16",
-                 hd=128):
+                 hd=128, short_first=False):
         global DMA_COST
+        SHORTFIRST[0] = bool(short_first)
+        assert not (short_first and rev and causal), "short_first streams both blocks forward (rev=False)"
         assert hd in (64, 128)
         GEOM["hd"] = hd
         assert not (qscale and hd != 128)
