@@ -3,7 +3,8 @@
 of each shipped hot-path kernel at its bench shape, nothing else, so each
 kernel's counters come from dispatches of one known grid.
 
-  flash    attn_fwd_v13 (default) and attn_fwd_v13c (causal default), B8 S4096 H32 D128
+  flash    attn_fwd_v13 (default) and attn_fwd_v13c (causal default), B8 S4096 H32 D128;
+           attn_fwd_v13h (fp16), attn_fwd_v13_d64 / v13h_d64 (head dim 64) at B8 S4096 H32
   flash12  attn_fwd_v12 (variant 71) and v12 causal (74), the round-3 kernels
   gemm     gemm_w5 4096^3 NN and NT (pli_gemm default routes)
   gemv     gemv_vec 4096^2 (W rotated over 24 copies)
@@ -54,6 +55,15 @@ for _ in range(N_LAUNCH):
     pli_hip.flash_attn_fwd(q, k, v, out=o, causal=True, variant=74)
 torch.cuda.synchronize()
 del q, k, v, o
+# fp16 D = 128 and head dim 64 (bf16 / fp16) on their default routes
+# (attn_fwd_v13h, attn_fwd_v13_d64, attn_fwd_v13h_d64 since round 5)
+for dt, hd in ((torch.float16, 128), (torch.bfloat16, 64), (torch.float16, 64)):
+    q, k, v = (torch.randn(B, H, S, hd, device="cuda", dtype=dt, generator=g) for _ in range(3))
+    o = torch.empty_like(q)
+    for _ in range(N_LAUNCH):
+        pli_hip.flash_attn_fwd(q, k, v, out=o)
+    torch.cuda.synchronize()
+    del q, k, v, o
 n = 4096
 a = torch.randn(n, n, device="cuda", dtype=torch.bfloat16, generator=g)
 b = torch.randn(n, n, device="cuda", dtype=torch.bfloat16, generator=g)

@@ -20,7 +20,8 @@ import re
 import sys
 from collections import defaultdict
 
-KERNELS = ("gemm_w5", "attn_fwd_v13c", "attn_fwd_v13", "attn_fwd_v12", "attn_fwd_v10", "attn_fwd_v7", "gemm_f32_mfma", "gemm_naive_f32", "hbm_read_probe", "attn_fwd_v2", "attn_decode_chunk", "attn_decode_combine", "gemv_vec", "gemm_mfma",
+KERNELS = ("gemm_w5", "attn_fwd_v13hc_d64", "attn_fwd_v13h_d64", "attn_fwd_v13c_d64", "attn_fwd_v13_d64",
+           "attn_fwd_v13hc", "attn_fwd_v13h", "attn_fwd_v13c", "attn_fwd_v13", "attn_fwd_v12", "attn_fwd_v10", "attn_fwd_v7", "gemm_f32_mfma", "gemm_naive_f32", "hbm_read_probe", "attn_fwd_v2", "attn_decode_chunk", "attn_decode_combine", "gemv_vec", "gemm_mfma",
            "gemm_smallm_nt", "scale_copy_vec", "Cijk_")
 
 
