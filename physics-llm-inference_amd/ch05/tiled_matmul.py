@@ -5,9 +5,12 @@ standalone CUDA ``main``) and the dropped ``ch05/triton_matmul.py``
 (``triton_matmul(a, b, block_m, block_n, block_k)``, ``:67-96``): one
 signature, one C ABI entry point, two kernels behind it --
 
-* bf16/fp16: 128x128x64 LDS-staged tile on ``v_mfma_f32_32x32x16`` (fp32
-  accumulate, output in the input dtype; the Triton kernel stored fp16,
-  ``:61``);
+* bf16/fp16: ``pli_gemm``'s routes (csrc/gemm.hip) -- large shapes (at least
+  128 tiles of 256 x 256, K % 64 == 0) run ``gemm_w5``: a 256 x 256 tile, one
+  wave per SIMD owning 128 x 128 of C^T in the accumulator file, K staged 64
+  deep by LDS-DMA, ``v_mfma_f32_16x16x32`` (persistent walk for K >= 128);
+  smaller shapes the 128 x 128 / 256 x 256 LDS tiles; fp32 accumulate,
+  output in the input dtype (the Triton kernel stored fp16, ``:61``);
 * fp32: 128x128x32 LDS-staged tile on ``v_mfma_f32_32x32x2_f32`` (exact
   fp32 fma chain); unaligned / K % 4 != 0 shapes take a 64x64 LDS-tiled VALU
   kernel.

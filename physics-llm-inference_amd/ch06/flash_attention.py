@@ -142,8 +142,11 @@ def flash_attention_memory_bytes(
 
 def explain_flash_attention() -> str:
     return (
-        "FlashAttention on MI355X: per 32-row query slice a wave keeps Q in registers,\n"
-        "streams 64-key K/V tiles through LDS, computes S^T = K Q^T and O^T += V^T P^T on\n"
-        "v_mfma_f32_32x32x16 and keeps the online-softmax (m, l) per lane in fp32.\n"
-        "HBM traffic is O(N d): Q, K, V read once per head, O written once."
+        "FlashAttention on MI355X (attn_fwd_v13): one wave per SIMD keeps 64 query rows\n"
+        "(Q^T and O^T in the accumulator file), K/V arrive by LDS-DMA in 64-key tiles two\n"
+        "tiles ahead, S^T = K Q^T and O^T += V^T P^T run on v_mfma_f32_16x16x32 (bf16 or\n"
+        "f16; head dim 128 or 64), P = exp2(s c - mu) goes from the scores straight into\n"
+        "the PV operand, the row sums l run on the matrix core and a tile takes the\n"
+        "rescale path only when some row's l reaches 1 (defer-max).  HBM traffic is\n"
+        "O(N d): Q, K, V read once per head, O written once."
     )
