@@ -6,7 +6,11 @@
 // wave-tile.  bf16 and fp16, plain and causal; flash_v13.hip's launcher
 // fills the arguments and calls launch_v13_d64.
 #include "flash_v13.h"
+#ifdef PLI_V13D64_AB_HEADER  // timing-only A/B builds (tools/build_v13_ab.sh)
+#include PLI_V13D64_AB_HEADER
+#else
 #include "flash_v13_d64_asm.h"
+#endif
 #include "pli_common.h"
 
 namespace pli {
