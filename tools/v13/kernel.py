@@ -383,6 +383,8 @@ def qk_with_rowsums(mask=None, muc=False, Xr=None):
     n = len(qk)
     if Xr is None:
         return qk, lambda kb, qb: qk_done_gap(kb, qb), lambda kb, qb: qk_first(kb, qb)
+    if "rsum" in ABL:  # timing only: no row-sum MFMAs
+        return qk, lambda kb, qb: qk_done_gap(kb, qb), lambda kb, qb: qk_first(kb, qb)
     rs = rowsum_mfmas(Xr)
     out, pos = qk[:n - 8], {}
     for j in range(n - 8, n):
@@ -479,10 +481,16 @@ def softmax_fills(X, slices, earliest_of, deadline_of=None, ytag=0, prev_cv=None
             e1 = Fill(I("v_exp_f32", y1, y1, mods=xm), 8, trans=True, deps=[f1], sep=1, tag="exp")
         fm = f1
         w = P_(X, qb, kb >> 1)[2 * (kb & 1) + hh]
-        cv = Fill(I(DT["cvt"], w, y0, y1), 4, deps=[e0, e1], sep=1, tag="cvt",
+        cdeps = [e0, e1]
+        rsv = []
+        if "rsumv" in ABL:  # timing only: the row sums as VALU adds of the fp32 P (no row-sum MFMAs)
+            a0 = Fill(I("v_add_f32", L_(qb)[0], L_(qb)[0], y0), 4, deps=[e0], sep=1, tag="rsumv")
+            a1 = Fill(I("v_add_f32", L_(qb)[0], L_(qb)[0], y1), 4, deps=[a0, e1], sep=1, tag="rsumv")
+            rsv, cdeps = [a0, a1], [e0, e1, a1]
+        cv = Fill(I(DT["cvt"], w, y0, y1), 4, deps=cdeps, sep=1, tag="cvt",
                   deadline=dl if QSCALE[0] else None, hard=QSCALE[0] and dl is not None)
         slot_cv[slot] = cv
-        grp = [f for f in (f0, f1, e0, e1, cv) if f is not None]
+        grp = [f for f in (f0, f1, e0, e1, *rsv, cv) if f is not None]
         fills += grp
         groups.append(grp)
         cvs.append((cv, w))
