@@ -40,3 +40,28 @@ def test_bench_gpus2_launches_two_ranks():
 def test_bench_world_size_mismatch_fails():
     r = _run(["--gpus", "2", "--selftest"], env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode == 3 and "WORLD_SIZE 1 != --gpus 2" in r.stderr
+
+
+def test_headline_summary_and_tail_order():
+    """The JSON line ends with the sub-results and `summary` (the driver
+    keeps only ~8 KB of stdout's tail): summary carries the flash, causal,
+    dtype-leg, GEMV, GEMM and TP numbers from their records."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", BENCH)
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    r = {"roofline": {"achieved": 1390.0, "frac": 0.552, "kernel_ms": 1.58},
+         "unramped": {"TFLOP/s": 1350.0},
+         "flash_causal": {"TFLOP/s": 1150.0, "ms": 0.96},
+         "gemv": {"us_per_launch": 7.3, "GB/s": 4600.0,
+                  "roofline": {"frac": 0.575, "measured_peak": 4510.0}},
+         "gemm": {"TFLOP/s": 1258.0, "torch_mm_TFLOP/s": 1223.0},
+         "tp_gemm": {"gemm_TFLOP/s": 1488.0, "torch_F.linear_TFLOP/s": 1576.0,
+                     "shard_gemm_per_rank": {"tp2": {"TFLOP/s": 1437.0, "torch_F.linear_TFLOP/s": 1511.0}}},
+         "flash_dtypes": {"fp16_d128": {"non_causal": {"TFLOP/s": 1300.0}, "causal": {"TFLOP/s": 1108.0}},
+                          "kernels": "..."}}
+    s = bench.headline_summary(r)
+    assert s["flash_TFLOP/s"] == 1390.0 and s["flash_unramped_TFLOP/s"] == 1350.0
+    assert s["causal_TFLOP/s"] == 1150.0 and s["gemv_us"] == 7.3 and s["gemv_size_matched_probe_GB/s"] == 4510.0
+    assert s["tp2_shard_TFLOP/s"] == [1437.0, 1511.0] and s["flash_fp16_d128_TFLOP/s"] == [1300.0, 1108.0]
+    assert len(json.dumps(s)) < 2048  # fits the tail with room to spare
