@@ -68,9 +68,12 @@ const char* pli_last_error(void);
  * elements, {q_b, q_h, q_n, k_b, k_h, k_n, v_b, v_h, v_n, o_b, o_h, o_n}.
  * causal != 0 masks key j for query i when j > i + (n_kv - n_q)
  * (bottom-right aligned, = torch.triu(ones, diagonal=1) when n_q == n_kv).
- * dtype: PLI_BF16 / PLI_F16 run the MFMA kernel (head_dim 64 or 128),
- * PLI_F32 (and any other head_dim <= 256) the generic fp32-accumulate kernel.
- * Softmax statistics are fp32 regardless of dtype.
+ * dtype: PLI_BF16 / PLI_F16 with head_dim 64 or 128 run the MFMA kernels --
+ * attn_fwd_v13 (one generated program per dtype x head_dim x causal form)
+ * where n_kv >= 128 and n_kv % 64 == 0 (causal: (n_kv - n_q) % 64 == 0),
+ * else attn_fwd_v12 / v10; PLI_F32 (and any other head_dim <= 256) the
+ * generic fp32-accumulate kernel.  Softmax statistics are fp32 regardless
+ * of dtype.
  */
 int pli_flash_attn_fwd(const void* q, const void* k, const void* v, void* o,
                        int batch, int heads, int kv_heads, int n_q, int n_kv,
