@@ -233,3 +233,31 @@ def test_v13_v_range(variant, vexp):
     ref = torch_attention(q, k, v, causal=causal)
     err = max_err(out.double() * 2.0 ** -vexp, ref)
     assert err <= 1e-2, f"variant {variant} |V| * 2^{vexp}: max |err| {err:.4e}"
+
+
+@pytest.mark.parametrize("dt,hd", (("bf16", 128), ("fp16", 128), ("bf16", 64), ("fp16", 64)))
+@pytest.mark.parametrize("causal", (False, True))
+def test_v13_gradual_max_growth(dt, hd, causal):
+    """Scores that rise steadily with the key position (about 100 log2 units
+    over the 1024 keys, ~6 per tile): the row max keeps growing, so the
+    defer-max rescale runs many times, triggered by the accumulated row sum
+    l (round 5's check; fp16: the P-bit check) rather than by one spike;
+    against the f64 reference."""
+    import pli_hip
+    tdt = torch.bfloat16 if dt == "bf16" else torch.float16
+    g = torch.Generator(device=DEV).manual_seed(61 + hd)
+    B, H, N = 1, 4, 1024
+    u = torch.randn(hd, device=DEV, generator=g, dtype=torch.float64)
+    u = u / u.norm()
+    c = hd ** -0.5 * 1.4426950408889634
+    amp = 100.0 / c  # score rise (raw units) over the sequence: 100 log2 units after scaling
+    q = (u * amp ** 0.5 + 0.3 * torch.randn(B, H, N, hd, device=DEV, generator=g, dtype=torch.float64))
+    pos = torch.arange(N, device=DEV, dtype=torch.float64)[:, None] / N
+    k = (pos * u * amp ** 0.5 + 0.3 * torch.randn(B, H, N, hd, device=DEV, generator=g, dtype=torch.float64))
+    v = torch.randn(B, H, N, hd, device=DEV, generator=g, dtype=torch.float64)
+    q, k, v = (t.to(tdt) for t in (q, k, v))
+    assert torch.isfinite(q).all() and torch.isfinite(k).all()
+    out = pli_hip.flash_attn_fwd(q, k, v, causal=causal)
+    ref = torch_attention(q, k, v, causal=causal)
+    err = max_err(out, ref)
+    assert err <= 2.0 ** -8 * v.abs().max().item() + 1e-2, f"{dt} D{hd} causal {causal}: max |err| {err:.4e}"
