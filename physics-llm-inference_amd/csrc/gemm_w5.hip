@@ -102,8 +102,116 @@
 #define W5S_DS1 6
 #endif
 
+#ifndef W5_Q4
+// 1: four meeting points per step (A / B images freed and landed apart, each
+// by its own wait + barrier); see w5q below
+#define W5_Q4 0
+#endif
+#ifndef W5Q_RA0
+#define W5Q_RA0 0
+#endif
+#ifndef W5Q_RAS
+#define W5Q_RAS 2
+#endif
+#ifndef W5Q_BA
+#define W5Q_BA 20
+#endif
+#ifndef W5Q_DA0
+#define W5Q_DA0 21
+#endif
+#ifndef W5Q_DAS
+#define W5Q_DAS 4
+#endif
+#ifndef W5Q_RB0
+#define W5Q_RB0 23
+#endif
+#ifndef W5Q_RBS
+#define W5Q_RBS 4
+#endif
+#ifndef W5Q_BB
+#define W5Q_BB 54
+#endif
+#ifndef W5Q_DB0
+#define W5Q_DB0 55
+#endif
+#ifndef W5Q_DBS
+#define W5Q_DBS 4
+#endif
+#ifndef W5Q_VA
+#define W5Q_VA 66
+#endif
+#ifndef W5Q_RC0
+#define W5Q_RC0 68
+#endif
+#ifndef W5Q_RCS
+#define W5Q_RCS 2
+#endif
+#ifndef W5Q_VB
+#define W5Q_VB 96
+#endif
+#ifndef W5Q_RD0
+#define W5Q_RD0 97
+#endif
+#ifndef W5Q_RDS
+#define W5Q_RDS 2
+#endif
+
 namespace pli {
 namespace {
+
+
+// W5_Q4 schedule of one K step (gap g follows MFMA g of 128; MFMAs 0-63 on
+// the (S, h0) fragments, 64-127 on (S, h1)):
+//   A(S, h1) reads at RA0 + RAS i; at BA they are waited for and the
+//   workgroup meets: slot S's A image is free, and step S+2's A pieces go in
+//   at DA0 + DAS i (between them the B(S, h1) reads, RB0 + RBS i); at BB the
+//   B reads are waited for, the workgroup meets, and S+2's B pieces go in at
+//   DB0 + DBS i.  At VA this wave's A(S+1) pieces have landed (vmcnt: the 8
+//   B(S+1) pieces and the S+2 pieces issued so far may be in flight), the
+//   workgroup meets, and A(S+1, h0) is read at RC0 + RCS i; at VB the same
+//   for B(S+1), read at RD0 + RDS i.  Each image gets its own free / landed
+//   point, so a piece has >= 140 gaps from issue to use.
+namespace w5q {
+constexpr int RA0 = W5Q_RA0, RAS = W5Q_RAS, BA = W5Q_BA, DA0 = W5Q_DA0, DAS = W5Q_DAS, RB0 = W5Q_RB0,
+              RBS = W5Q_RBS, BB = W5Q_BB, DB0 = W5Q_DB0, DBS = W5Q_DBS, VA = W5Q_VA, RC0 = W5Q_RC0,
+              RCS = W5Q_RCS, VB = W5Q_VB, RD0 = W5Q_RD0, RDS = W5Q_RDS;
+constexpr int dma_gap(int j) { return j < 8 ? DA0 + DAS * j : DB0 + DBS * (j - 8); }
+constexpr int dma_at(int g) {
+    for (int j = 0; j < 16; ++j)
+        if (dma_gap(j) == g) return j;
+    return -1;
+}
+constexpr int issued_before(int g) {
+    int n = 0;
+    for (int j = 0; j < 16; ++j) n += dma_gap(j) < g;
+    return n;
+}
+// read at gap g: 0-7 A(S, h1), 8-15 B(S, h1), 16-23 A(S+1, h0), 24-31 B(S+1, h0)
+constexpr int read_gap(int r) {
+    return r < 8 ? RA0 + RAS * r : r < 16 ? RB0 + RBS * (r - 8) : r < 24 ? RC0 + RCS * (r - 16) : RD0 + RDS * (r - 24);
+}
+constexpr int read_at(int g) {
+    for (int r = 0; r < 32; ++r)
+        if (read_gap(r) == g) return r;
+    return -1;
+}
+constexpr bool valid() {
+    for (int g = 0; g < 128; ++g) {
+        int nr = 0, nd = 0;
+        for (int r = 0; r < 32; ++r) nr += read_gap(r) == g;
+        for (int j = 0; j < 16; ++j) nd += dma_gap(j) == g;
+        if (nr > 1 || nd > 1) return false;
+    }
+    for (int r = 0; r < 8; ++r)
+        if (read_gap(r) >= BA || read_gap(8 + r) >= BB || read_gap(16 + r) <= VA || read_gap(16 + r) < 64 ||
+            read_gap(24 + r) <= VB || read_gap(24 + r) > 127)
+            return false;
+    for (int j = 0; j < 8; ++j)
+        if (dma_gap(j) <= BA || dma_gap(8 + j) <= BB || dma_gap(8 + j) > 127) return false;
+    return BA < BB && BB < 64 && VA < VB && issued_before(VB) == 16 && issued_before(VA) >= 8;
+}
+static_assert(!W5_Q4 || valid(), "W5_Q4 schedule: overlapping or misordered events");
+}  // namespace w5q
 
 template <int... I, class Fn>
 __device__ __forceinline__ void w5_for(std::integer_sequence<int, I...>, Fn&& fn) {
@@ -237,8 +345,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A
                 sc = min(s - ks, ks - 1);
             }
         }
-        const uint16_t* src = j < 8 ? ab + sc * 64 : (TRANS_B ? bb + sc * 64 : bb + (int64_t)sc * 64 * ldb);
         const uint32_t off = j < 8 ? aoff[i] : boff[i];
+        const uint16_t* src = j < 8 ? ab + sc * 64 : (TRANS_B ? bb + sc * 64 : bb + (int64_t)sc * 64 * ldb);
         if constexpr (W5_DMA_IMM && i % 4 > 0) dma_next(std::integral_constant<int, i % 4>{}, src, off);
         else dma1(src, off, slot);
     };
@@ -362,8 +470,64 @@ __global__ __launch_bounds__(256, 1) void gemm_w5(const uint16_t* __restrict__ A
 
     using Z = std::integral_constant<int, 0>;
     using O = std::integral_constant<int, 1>;
+    auto frag_wait_x = [&](auto p_tag, auto b_tag) __attribute__((always_inline)) {
+        constexpr int P = decltype(p_tag)::value;
+        constexpr bool Bop = decltype(b_tag)::value;
+        if constexpr (!Bop) {
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(fa[P][0]), "+v"(fa[P][1]), "+v"(fa[P][2]), "+v"(fa[P][3]), "+v"(fa[P][4]),
+                           "+v"(fa[P][5]), "+v"(fa[P][6]), "+v"(fa[P][7])::"memory");
+        } else if constexpr (TRANS_B) {
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(fb[P][0]), "+v"(fb[P][1]), "+v"(fb[P][2]), "+v"(fb[P][3]), "+v"(fb[P][4]),
+                           "+v"(fb[P][5]), "+v"(fb[P][6]), "+v"(fb[P][7])::"memory");
+        } else {
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(fb[P][0].lo), "+v"(fb[P][0].hi), "+v"(fb[P][1].lo), "+v"(fb[P][1].hi),
+                           "+v"(fb[P][2].lo), "+v"(fb[P][2].hi), "+v"(fb[P][3].lo), "+v"(fb[P][3].hi),
+                           "+v"(fb[P][4].lo), "+v"(fb[P][4].hi), "+v"(fb[P][5].lo), "+v"(fb[P][5].hi),
+                           "+v"(fb[P][6].lo), "+v"(fb[P][6].hi), "+v"(fb[P][7].lo), "+v"(fb[P][7].hi)::"memory");
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // W5_Q4: one K step, 128 MFMAs with the w5q events in their gaps
+    auto step_q4 = [&](int s, auto more_tag) __attribute__((always_inline)) {
+        constexpr bool MORE = decltype(more_tag)::value;
+        const uint32_t sa0 = img_off(s, 0), sb0 = img_off(s, 1), sa1 = img_off(s + 1, 0), sb1 = img_off(s + 1, 1);
+        w5_sfor<128>([&](auto JJ) {
+            constexpr int J = JJ, P = J / 64, JL = J % 64, ni = JL / 8, mi = JL % 8;
+            if constexpr (std::is_same_v<T, bf16_t>) w4v::mfma_bf16<JL>(bop(fb[P][ni]), fa[P][mi]);
+            else w4v::mfma_f16<JL>(bop(fb[P][ni]), fa[P][mi]);
+            __builtin_amdgcn_sched_barrier(0);
+            constexpr int r = w5q::read_at(J);
+            if constexpr (!W5_ABL_RD && r >= 0 && r < 16)
+                frag_read(std::integral_constant<int, 1>{}, std::integral_constant<int, r>{}, sa0, sb0);
+            if constexpr (!W5_ABL_RD && r >= 16 && MORE)
+                frag_read(std::integral_constant<int, 0>{}, std::integral_constant<int, r - 16>{}, sa1, sb1);
+            if constexpr (J == w5q::BA || J == w5q::BB) {
+                frag_wait_x(std::integral_constant<int, 1>{}, std::bool_constant<J == w5q::BB>{});
+                if constexpr (!W5_ABL_BAR) __builtin_amdgcn_s_barrier();
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            if constexpr (J == w5q::VA || J == w5q::VB) {
+                // this wave's A (VA) / B (VB) pieces of step s+1 landed
+                constexpr int n = (J == w5q::VA ? 8 : 0) + w5q::issued_before(J);
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n) : "memory");
+                if constexpr (!W5_ABL_BAR) __builtin_amdgcn_s_barrier();
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            constexpr int d = w5q::dma_at(J);
+            if constexpr (!W5_ABL_DMA && d >= 0) dma_piece(std::integral_constant<int, d>{}, s + 2);
+            __builtin_amdgcn_sched_barrier(0);
+        });
+        if constexpr (MORE) frag_wait(Z{});
+    };
     auto step = [&](int s, auto more_tag) __attribute__((always_inline)) {
         constexpr bool MORE = decltype(more_tag)::value;  // a step s+1 follows
+        if constexpr (W5_Q4) {
+            step_q4(s, more_tag);
+            return;
+        }
         using N0 = std::integral_constant<int, 0>;
         using N8 = std::integral_constant<int, 8>;
         using N16 = std::integral_constant<int, 16>;
