@@ -271,26 +271,23 @@ class Emu:
         d, a, b, c = ins.ops
         ra, rb = self.regs(w, a), self.regs(w, b)
         dec = f16_to_f32 if ins.op.endswith("_f16") else bf16_to_f32
+        # halves j = 0..7 of lane l: word j // 2, bits 16 (j % 2) (vectorised;
+        # the same A, B and A @ B as the per-element form)
+        lane = np.arange(LANES)
+        jj = np.arange(8)[:, None]
+        ha = (np.asarray(ra, dtype=np.uint32)[jj // 2, lane] >> (16 * (jj % 2)).astype(np.uint32)) & 0xFFFF
+        hb = (np.asarray(rb, dtype=np.uint32)[jj // 2, lane] >> (16 * (jj % 2)).astype(np.uint32)) & 0xFFFF
         A = np.zeros((16, 32))
         B = np.zeros((32, 16))
-        for l in range(LANES):
-            for j in range(8):
-                wa = int(ra[j // 2, l])
-                wb = int(rb[j // 2, l])
-                ha = (wa >> (16 * (j % 2))) & 0xFFFF
-                hb = (wb >> (16 * (j % 2))) & 0xFFFF
-                A[l % 16, 8 * (l // 16) + j] = float(dec(ha))
-                B[8 * (l // 16) + j, l % 16] = float(dec(hb))
+        A[lane % 16, 8 * (lane // 16) + jj] = dec(ha).astype(np.float64)
+        B[8 * (lane // 16) + jj, lane % 16] = dec(hb).astype(np.float64)
         D = A @ B
         if isinstance(c, int):
             assert c == 0
             C = np.zeros((4, LANES))
         else:
             C = u2f(self.regs(w, c)).astype(np.float64)
-        out = np.zeros((4, LANES))
-        for l in range(LANES):
-            for r in range(4):
-                out[r, l] = C[r, l] + D[4 * (l // 16) + r, l % 16]
+        out = C + D[4 * (lane // 16) + np.arange(4)[:, None], lane % 16]
         self.regs(w, d)[:] = f2u(out.astype(np.float32))
 
     # ---- VALU -------------------------------------------------------------
