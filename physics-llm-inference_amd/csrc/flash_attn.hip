@@ -531,8 +531,9 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
 //  80: attn_fwd_v13 (flash_v13.hip): 4 waves x 64 rows, one wave per SIMD,
 //      v_mfma_f32_16x16x32_bf16 (the shape the chip clocks higher under load),
 //      one generated instruction stream (tools/gen_flash_v13.py), persistent;
-//      defer-max on P itself (D = 128, non-causal, Nk % 64 == 0, Nk >= 128;
-//      else 71); fp16 inputs run the same program on the f16 MFMA
+//      defer-max on P itself (D = 128 / 64, non-causal, Nk % 64 == 0 and Nk
+//      >= 128, or any Nk > 64 on the ragged bodies attn_fwd_v13r / v13hr --
+//      round 5; else 71); fp16 inputs run the same program on the f16 MFMA
 //      (attn_fwd_v13h / v13hc, since round 5; before: 71 -> 55 / 60)
 //  81: variant 80 with one block per workgroup
 //  82: variant 80 with mu = max * c (P = 1 at the max, so every row's l >= 1
@@ -542,7 +543,8 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
 //      block per workgroup heaviest first; 85 = 83 with mu = max * c
 // default since round 4: attn_fwd_v13 (80), 1388 vs 1242 TF/s for v12 (71)
 // at B8 S4096 H32 D128 in the same process (profiles/r04/flash/ab.log); where
-// v13 does not apply (fp16, D != 128, Nk % 64, Nk < 128) it routes to 71
+// v13 does not apply (D not 64 / 128, Nk <= 64, causal with Nk % 64 or
+// (Nk - Nq) % 64) it routes to 71 / 74
 constexpr int kDefaultVariant = 80;
 // v13's mu = row max * c + PLI_V13_MUOFF (log2 units): P <= 2^-MUOFF right
 // after a max is taken and a tile takes the rescale path once some row's sum l

@@ -14,8 +14,9 @@ struct V13Args {
 };
 static_assert(sizeof(V13Args) == 256, "V13Args layout");
 
-// launch one of the head-dim-64 bodies (bf16 / fp16, plain / causal) on
-// `grid` workgroups of 256 threads; returns the launch status
-int launch_v13_d64(bool fp16, bool causal, unsigned grid, const V13Args& a, hipStream_t stream);
+// launch one of the head-dim-64 bodies (bf16 / fp16, plain / causal /
+// ragged -- Nk % 64 != 0, non-causal) on `grid` workgroups of 256 threads;
+// returns the launch status
+int launch_v13_d64(bool fp16, bool causal, bool ragged, unsigned grid, const V13Args& a, hipStream_t stream);
 
 }  // namespace pli

@@ -1,7 +1,8 @@
 // attn_fwd_v13: flash-attention forward on v_mfma_f32_16x16x32_bf16
-// (reference ch06/flash_attention.py:14-74; gfx950, bf16, D = 128, Nk a
-// multiple of 64 and >= 128; causal -- bottom-right, (Nk - Nq) % 64 == 0 --
-// as the second program attn_fwd_v13c; other cases take v12 / v10).
+// (reference ch06/flash_attention.py:14-74; gfx950, bf16 / fp16, D = 128 /
+// 64, Nk a multiple of 64 and >= 128 or -- attn_fwd_v13r -- any Nk > 64;
+// causal -- bottom-right, (Nk - Nq) % 64 == 0 -- as the second program
+// attn_fwd_v13c; other cases take v12 / v10).
 //
 // One wave per SIMD, 64 query rows per wave (4 q-blocks of 16), persistent
 // workgroups of 4 waves walking 256-row blocks.  The body is ONE generated
@@ -84,6 +85,27 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v13hc(V13Args args) {
     asm volatile(PLI_V13HC_BODY::"s"(kp), "s"(wg), "s"(wave), "s"((unsigned)(uintptr_t)smem) : PLI_V13_CLOBBERS);
 }
 
+// Nk % 64 != 0 (non-causal): the last key tile is streamed from key Nk - 64,
+// inside the head, and the keys it shares with the tile before get P = 0
+// (tools/v13/kernel.py RAGGED; P0 = 64 - Nk % 64 in the cw argument)
+__global__ __launch_bounds__(256, 1) void attn_fwd_v13r(V13Args args) {
+    __shared__ __attribute__((aligned(1024))) char smem[163840];
+    (void)args;
+    const void* kp = (const void*)__builtin_amdgcn_kernarg_segment_ptr();
+    const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const unsigned wg = blockIdx.x;
+    asm volatile(PLI_V13R_BODY::"s"(kp), "s"(wg), "s"(wave), "s"((unsigned)(uintptr_t)smem) : PLI_V13_CLOBBERS);
+}
+
+__global__ __launch_bounds__(256, 1) void attn_fwd_v13hr(V13Args args) {
+    __shared__ __attribute__((aligned(1024))) char smem[163840];
+    (void)args;
+    const void* kp = (const void*)__builtin_amdgcn_kernarg_segment_ptr();
+    const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const unsigned wg = blockIdx.x;
+    asm volatile(PLI_V13HR_BODY::"s"(kp), "s"(wg), "s"(wave), "s"((unsigned)(uintptr_t)smem) : PLI_V13_CLOBBERS);
+}
+
 // floor(x / d) == ((x * m) >> 31) >> l for 0 <= x < 2^31 (Granlund-Montgomery,
 // N = 31: m = ceil(2^(31+l) / d) < 2^32 with l = ceil(log2 d))
 void magic31(uint32_t d, uint32_t& m, uint32_t& l) {
@@ -117,8 +139,10 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v13_stamp(V13Args args) {
 
 bool attn_v13_ok(int D, int is_bf16, int causal, int Nq, int Nk, const V7Strides& st) {
     (void)is_bf16;  // bf16 and fp16 programs
-    // head dim 128, or 64 (the D = 64 bodies in flash_v13_d64.hip)
-    if ((D != 128 && D != 64) || Nk < 128 || Nk % 64 != 0 || Nq < 1) return false;
+    // head dim 128, or 64 (the D = 64 bodies in flash_v13_d64.hip); Nk a
+    // multiple of 64 from 128, or (non-causal) any Nk > 64: the ragged bodies
+    if ((D != 128 && D != 64) || Nq < 1) return false;
+    if (Nk % 64 == 0 ? Nk < 128 : (causal || Nk <= 64)) return false;
     // causal: the bottom-right diagonal on 64-key tile boundaries
     if (causal && (Nq > Nk || (Nk - Nq) % 64 != 0)) return false;
     // causal: the stream's tile count and index carry the block's order in
@@ -187,7 +211,7 @@ int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B,
     a.w[A_VN] = (uint32_t)(st.vn * 2);
     a.w[A_ON] = (uint32_t)(st.on * 2);
     a.w[A_NQ] = (uint32_t)Nq;
-    a.w[A_NT] = (uint32_t)(Nk / 64);
+    a.w[A_NT] = (uint32_t)cdiv(Nk, 64);
     a.w[A_QBLOCKS] = (uint32_t)qblocks;
     a.w[A_NBLOCKS] = (uint32_t)nb;
     uint32_t shq, shh, shg;
@@ -195,7 +219,8 @@ int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B,
     magic31((uint32_t)H, a.w[A_MAGH], shh);
     magic31((uint32_t)group, a.w[A_MAGG], shg);
     a.w[A_SHIFTS] = shq | (shh << 5) | (shg << 10) | ((uint32_t)H << 16);
-    a.w[A_CW] = cw;
+    const bool ragged = Nk % 64 != 0;  // (non-causal: the walk word is free for P0)
+    a.w[A_CW] = ragged ? (uint32_t)(64 - Nk % 64) : cw;
     a.w[A_HX] = hx;
     a.w[A_OFFT] = causal ? (uint32_t)((Nk - Nq) / 64) : 0u;
     const float c = scale * 1.4426950408889634f;
@@ -213,7 +238,15 @@ int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B,
 #else
     (void)stamps;
 #endif
-    if (D == 64) return launch_v13_d64(fp16, causal, (unsigned)grid, a, stream);
+    if (D == 64) return launch_v13_d64(fp16, causal, ragged, (unsigned)grid, a, stream);
+    if (ragged) {
+        if (fp16) {
+            hipLaunchKernelGGL(attn_fwd_v13hr, dim3((unsigned)grid), dim3(256), 0, stream, a);
+            return launch_status("attn_fwd_v13hr");
+        }
+        hipLaunchKernelGGL(attn_fwd_v13r, dim3((unsigned)grid), dim3(256), 0, stream, a);
+        return launch_status("attn_fwd_v13r");
+    }
     if (fp16) {
         if (causal) {
             hipLaunchKernelGGL(attn_fwd_v13hc, dim3((unsigned)grid), dim3(256), 0, stream, a);

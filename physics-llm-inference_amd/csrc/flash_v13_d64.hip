@@ -3,7 +3,7 @@
 // tools/v13/kernel.py with Gen(hd=64) -- the D = 64 K / V tile images are the
 // first halves of the D = 128 ones (same swizzle, fragment offsets and DMA
 // piece map), 4 LDS-DMA pieces per wave and 32 + 32 MFMAs per 64 x 64
-// wave-tile.  bf16 and fp16, plain and causal; flash_v13.hip's launcher
+// wave-tile.  bf16 and fp16, plain, causal and ragged (Nk % 64 != 0); flash_v13.hip's launcher
 // fills the arguments and calls launch_v13_d64.
 #include "flash_v13.h"
 #ifdef PLI_V13D64_AB_HEADER  // timing-only A/B builds (tools/build_v13_ab.sh)
@@ -31,10 +31,20 @@ PLI_V13_D64_KERNEL(attn_fwd_v13_d64, PLI_V13_D64_BODY)
 PLI_V13_D64_KERNEL(attn_fwd_v13c_d64, PLI_V13C_D64_BODY)
 PLI_V13_D64_KERNEL(attn_fwd_v13h_d64, PLI_V13H_D64_BODY)
 PLI_V13_D64_KERNEL(attn_fwd_v13hc_d64, PLI_V13HC_D64_BODY)
+PLI_V13_D64_KERNEL(attn_fwd_v13r_d64, PLI_V13R_D64_BODY)
+PLI_V13_D64_KERNEL(attn_fwd_v13hr_d64, PLI_V13HR_D64_BODY)
 
 }  // namespace
 
-int launch_v13_d64(bool fp16, bool causal, unsigned grid, const V13Args& a, hipStream_t stream) {
+int launch_v13_d64(bool fp16, bool causal, bool ragged, unsigned grid, const V13Args& a, hipStream_t stream) {
+    if (ragged) {  // (non-causal only: attn_v13_ok)
+        if (fp16) {
+            hipLaunchKernelGGL(attn_fwd_v13hr_d64, dim3(grid), dim3(256), 0, stream, a);
+            return launch_status("attn_fwd_v13hr_d64");
+        }
+        hipLaunchKernelGGL(attn_fwd_v13r_d64, dim3(grid), dim3(256), 0, stream, a);
+        return launch_status("attn_fwd_v13r_d64");
+    }
     if (fp16 && causal) {
         hipLaunchKernelGGL(attn_fwd_v13hc_d64, dim3(grid), dim3(256), 0, stream, a);
         return launch_status("attn_fwd_v13hc_d64");

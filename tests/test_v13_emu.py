@@ -158,3 +158,56 @@ def test_v13_d64_program_vs_f64(case):
     assert err <= 1e-2, f"max |err| {err:.3e}"
     if muoff <= 0:
         assert em.counts.get("v_sub_f32", 0) > 0, "the rescale path never ran"
+
+
+RAGGED_CASES = [  # (B, H, Hkv, Nq, Nk, grid, layout, muoff, D, dtype): Nk % 64 != 0 (Gen(ragged=True))
+    (1, 2, 2, 256, 200, 1, "bhsd", 62.0, 128, "bf16"),   # persistent: the stream shifts and parks on a ragged tile
+    (2, 2, 1, 200, 330, 1, "bshd", 62.0, 128, "bf16"),   # GQA, ragged Nq, BSHD strides
+    (1, 1, 1, 256, 190, None, "bhsd", 0.0, 128, "bf16"),  # the rescale path at every tile, the last one too
+    (1, 1, 1, 130, 65, None, "bhsd", 62.0, 128, "bf16"),  # Nk = 65: the last tile overlaps the first by 63 keys
+    (1, 2, 2, 256, 200, 1, "bhsd", 4.0, 128, "f16"),     # fp16, persistent
+    (1, 1, 1, 256, 190, None, "bhsd", -1.0, 128, "f16"),  # fp16 P-bit check: rescales at nearly every tile
+    (1, 2, 2, 256, 330, 1, "bhsd", 62.0, 64, "bf16"),    # head dim 64, persistent
+    (1, 1, 1, 256, 190, None, "bhsd", -1.0, 64, "f16"),   # head dim 64, fp16, rescales
+]
+
+
+@pytest.mark.parametrize("case", RAGGED_CASES,
+                         ids=lambda c: "ragged-b{}h{}kv{}q{}k{}g{}-{}-mu{}-d{}-{}".format(*c))
+def test_v13_ragged_program_vs_f64(case):
+    """Nk not a multiple of 64 (non-causal): the last key tile streams from key
+    Nk - 64 and the keys it shares with the tile before get P = 0; the heap
+    is bounds-checked, so a read past the last head's rows would fail"""
+    B, H, Hkv, Nq, Nk, grid, lay, muoff, D, dtype = case
+    rng = np.random.default_rng(13 + sum(case[:5]))
+    q = rng.standard_normal((B, H, Nq, D))
+    k = rng.standard_normal((B, Hkv, Nk, D))
+    v = rng.standard_normal((B, Hkv, Nk, D))
+    o, em = R.run(q, k, v, grid=grid, layout=lay, muoff=muoff, dtype=dtype)
+    err = np.abs(o - f64_attention(q, k, v, dtype=dtype)).max()
+    assert err <= 1e-2, f"max |err| {err:.3e}"
+    if muoff <= 0:
+        assert em.counts.get("v_sub_f32", 0) > 0, "the rescale path never ran"
+
+
+def test_v13_ragged_spikes():
+    """a key in the overlap (counted once, in the tile before) and a key in
+    the last tile's own part, each raising its row's max past the product's
+    offset: the rare paths of the step and of the tail, with the overlap
+    masked after the redo"""
+    rng = np.random.default_rng(17)
+    q = rng.standard_normal((1, 1, 256, 128))
+    k = rng.standard_normal((1, 1, 200, 128))
+    v = rng.standard_normal((1, 1, 200, 128))
+    k[0, 0, 150] = 8.0 * np.sign(q[0, 0, 10])   # overlap: keys 136..191 are the last tile's first 56
+    k[0, 0, 195] = 8.0 * np.sign(q[0, 0, 99])   # the last tile's own keys 192..199
+    o, em = R.run(q, k, v, muoff=62.0)
+    assert em.counts.get("v_sub_f32", 0) > 0, "the rescale path never ran"
+    err = np.abs(o - f64_attention(q, k, v)).max()
+    assert err <= 2.0 ** -8 * np.abs(v).max(), f"max |err| {err:.3e}"
+
+
+def test_v13_ragged_hazard_pass_is_idempotent():
+    for dtype in ("bf16", "f16"):
+        for hd in (128, 64):
+            assert analyse(R.program(causal=False, dtype=dtype, ragged=True, hd=hd)) == {}

@@ -364,12 +364,13 @@ class Emu:
             a, b = gf(o[1]), gf(o[2])
             w.vcc = np.where(w.exec, a < b if op == "v_cmp_lt_f32_e32" else a <= b, False)
             return
-        if op in ("v_cmp_ne_u32_e32", "v_cmp_gt_u32_e32", "v_cmp_gt_i32_e32", "v_cmp_lt_i32_e32"):
+        if op in ("v_cmp_ne_u32_e32", "v_cmp_gt_u32_e32", "v_cmp_gt_i32_e32", "v_cmp_lt_i32_e32",
+                  "v_cmp_le_u32_e32"):
             a, b = g(o[1]), g(o[2])
             if op.endswith("i32_e32"):
                 a, b = a.view(np.int32), b.view(np.int32)
             r = {"v_cmp_ne_u32_e32": a != b, "v_cmp_gt_u32_e32": a > b, "v_cmp_gt_i32_e32": a > b,
-                 "v_cmp_lt_i32_e32": a < b}[op]
+                 "v_cmp_lt_i32_e32": a < b, "v_cmp_le_u32_e32": a <= b}[op]
             w.vcc = np.where(w.exec, r, False)
             return
         if op == "v_cndmask_b32_e32":
@@ -469,6 +470,12 @@ class Emu:
             return
         if op == "s_cmp_le_u32":
             w.scc = int(g(o[0]) <= g(o[1]))
+            return
+        if op == "s_cmp_gt_i32":
+            a, b = g(o[0]), g(o[1])
+            a = a - (1 << 32) if a >= 1 << 31 else a
+            b = b - (1 << 32) if b >= 1 << 31 else b
+            w.scc = int(a > b)
             return
         if op in ("s_cselect_b32", "s_cselect_b64"):
             return self.sset(w, o[0], g(o[1]) if w.scc else g(o[2]))

@@ -145,6 +145,13 @@ TRI = V(206, 4)   # causal: the 16 x 16 diagonal block's C operand (0 / -inf)
 NINF = V(210, 4)  # causal: -inf (C operand of fully masked chains, cndmask source)
 
 
+def PM(kb, hh):
+    """RAGGED (non-causal, so TRI / NINF's registers are free): the AND mask
+    of P word (kb, hh) of the last key tile -- its halves hold keys 16 kb +
+    4 g + 2 hh (+1), kept iff the key is >= P0"""
+    return V(206 + 2 * kb + hh)
+
+
 LANE, VI, VG = V(214), V(215), V(216)
 STAMPV = V(217)  # diagnostic build only
 
@@ -274,6 +281,14 @@ NEGONES = 0xBF80BF80
 # most 4a+4 tile-times after its first (the round-4 order reads it again up
 # to 64 later, the reversed second block about 67-2u later)
 SHORTFIRST = [False]
+# RAGGED (Gen(ragged=True), non-causal, Nk % 64 != 0): the last key tile is
+# streamed from key Nk - 64 (it overlaps the one before by P0 = 64 - Nk % 64
+# keys, so every K / V read stays inside the head); its first P0 keys were
+# already counted, so their P is ANDed to 0 before the row sums and PV read
+# it.  Their scores are real scores of keys the row max has already seen, so
+# mu and the check are unaffected.  P0 rides in the cw argument (unused by the
+# non-causal walk).
+RAGGED = [False]
 
 
 def schedule(mfmas, fills, budget=8, gap_offset=0, lds_gap=LDS_GAP):
@@ -658,11 +673,33 @@ def dma_fills(slot_reg, earliest0=2, spacing=6, rev=False):
                     I("s_add_u32", sDV[0], sDV[0], sT2), I("s_addc_u32", sDV[1], sDV[1], sT4)],
                    8, deps=[prev], sep=0, tag="dmaadv")
     else:
-        adv = Fill([I("s_add_u32", sDK[0], sDK[0], sTBK), I("s_addc_u32", sDK[1], sDK[1], 0),
-                    I("s_add_u32", sDV[0], sDV[0], sTBV), I("s_addc_u32", sDV[1], sDV[1], 0),
-                    I("s_add_u32", sDIDX, sDIDX, 1)], 2, deps=[prev], sep=0, tag="dmaadv")
+        ains = [I("s_add_u32", sDK[0], sDK[0], sTBK), I("s_addc_u32", sDK[1], sDK[1], 0),
+                I("s_add_u32", sDV[0], sDV[0], sTBV), I("s_addc_u32", sDV[1], sDV[1], 0),
+                I("s_add_u32", sDIDX, sDIDX, 1)]
+        cost = 2
+        if RAGGED[0]:
+            # the stream's next tile is the last one: P0 keys back
+            ains += [I("s_sub_u32", sT2, sDNT, 1), I("s_cmp_eq_u32", sDIDX, sT2)] + rag_back(sDK, sDV)
+            cost = 6
+        adv = Fill(ains, cost, deps=[prev], sep=0, tag="dmaadv")
     fills.append(adv)
     return fills
+
+
+def rag_back(k, v):
+    """RAGGED: with SCC set, the K / V stream pointers k, v move back by P0
+    keys (P0 tbk / 64 and P0 tbv / 64 bytes); uses sT2, sT3"""
+    c = [I("s_cselect_b32", sT3, ARG(AI["cw"]), 0)]
+    for (ptr, tb) in ((k, sTBK), (v, sTBV)):
+        c += [I("s_mul_i32", sT2, sT3, tb), I("s_lshr_b32", sT2, sT2, 6),
+              I("s_sub_u32", ptr[0], ptr[0], sT2), I("s_subb_u32", ptr[1], ptr[1], 0)]
+    return c
+
+
+def p_mask(X):
+    """RAGGED: the last tile's P (state X) with its first P0 keys zeroed"""
+    return [I("v_and_b32", P_(X, qb, kb >> 1)[2 * (kb & 1) + hh], P_(X, qb, kb >> 1)[2 * (kb & 1) + hh], PM(kb, hh))
+            for qb in range(4) for kb in range(4) for hh in range(2)]
 
 
 def dma_now(slot_reg, rev=False):
@@ -747,8 +784,10 @@ class Gen:
 
     def __init__(self, ndef=4, budget=8, dma_spacing=6, tag="%=", stamp=False, causal=False, abl=(), dma_cost=8,
                  rev=True, qscale=False, dma_pv=0, dma_pv_spacing=16, budget_pv=None, lcheck=None, dtype="bf16",
-                 hd=128, short_first=False):
+                 hd=128, short_first=False, ragged=False):
         global DMA_COST
+        assert not (ragged and causal), "ragged key counts: the non-causal program only"
+        RAGGED[0] = bool(ragged)
         SHORTFIRST[0] = bool(short_first)
         assert not (short_first and rev and causal), "short_first streams both blocks forward (rev=False)"
         assert hd in (64, 128)
@@ -839,6 +878,18 @@ class Gen:
                 e([I("v_add_u32", t[5], rb, t[2]), I("v_mul_lo_u32", t[5], t[5], st),
                    I("v_add_u32", t[5], t[5], t[3]), I("v_add_u32", dst, sT5, t[5])])
         e(load_args())
+        if RAGGED[0]:
+            # PM(kb, hh): keep the half whose key 16 kb + 4 g + 2 hh (+1) >= P0
+            e([I("v_lshlrev_b32", T(0), 2, VG), I("v_mov_b32", T(4), 0xFFFF), I("v_mov_b32", T(5), 0xFFFF0000)])
+            for kb in range(4):
+                for hh in range(2):
+                    e([I("v_add_u32", T(1), 16 * kb + 2 * hh, T(0)),
+                       I("v_cmp_le_u32_e32", VCC, ARG(AI["cw"]), T(1)),
+                       I("v_cndmask_b32_e32", T(2), 0, T(4), VCC),
+                       I("v_add_u32", T(1), 1, T(1)),
+                       I("v_cmp_le_u32_e32", VCC, ARG(AI["cw"]), T(1)),
+                       I("v_cndmask_b32_e32", T(3), 0, T(5), VCC),
+                       I("v_or_b32", PM(kb, hh), T(2), T(3))])
         if self.stamp:
             # STAMP: lanes 0-3 of v217 = entry s_memtime / s_memrealtime, lane 8
             # = this wave's record index (workgroup x 4 + wave)
@@ -924,6 +975,11 @@ class Gen:
         for (dst, src, tb) in ((sNXK, sDK, sTBK), (sNXV, sDV, sTBV)):
             c += [I("s_mul_i32", sT5, sT4, tb), I("s_ashr_i32", sT3, sT5, 31),
                   I("s_add_u32", dst[0], src[0], sT5), I("s_addc_u32", dst[1], src[1], sT3)]
+        if RAGGED[0]:
+            # (sDK already points P0 keys back once the stream is at or past
+            # the last tile)
+            c += [I("s_sub_u32", sT4, sNT, 1), I("s_sub_u32", sT4, sT4, sDIDX), I("s_cmp_gt_i32", sT4, 0)]
+            c += rag_back(sNXK, sNXV)
         c += [I("s_sub_u32", sNXIDX, sNT, 1), I("s_mov_b32", sNXNT, sNT)]
         c += [I("s_cmp_eq_u32", sHASN, 0), I("s_cbranch_scc1", skip)]
         # the next block's index in s101 (block_params reads it first)
@@ -1163,6 +1219,8 @@ class Gen:
         e([I("v_add_u32", VVA, sSM1, VVL)])
         f_def, _, _ = softmax_fills(X, dfr, lambda qb, kb: 0, ytag=0)
         e(drain(f_def, 0))
+        if RAGGED[0]:
+            e(p_mask(X))
         if LCHECK[0]:
             e(rowsum_mfmas(X))
         self.check(X, f"rare_t{X}")
@@ -1271,6 +1329,8 @@ class Gen:
                                I("v_accvgpr_write_b32", O_(db, qb)[r], T(25))])
                     e([I("v_mul_f32", L_(qb)[r], L_(qb)[r], T(24)) for r in range(4)])
                 e(exps_all(X))
+                if RAGGED[0] and name.startswith("rare_t"):  # the last tile
+                    e(p_mask(X))
                 if LCHECK[0]:  # its new sums (the step's row sums of this tile already ran)
                     e(rowsum_mfmas(X))
             else:

@@ -50,7 +50,7 @@ def args_for(qa, ka, va, oa, B, H, Hkv, Nq, Nk, strides_el, scale, G, muoff=7.0,
                       ("vh", st[7]), ("ob", st[9]), ("oh", st[10])):
         d[name], d[name + "_hi"] = val & 0xFFFFFFFF, val >> 32
     d["qn"], d["kn"], d["vn"], d["on"] = st[2], st[5], st[8], st[11]
-    d["nq"], d["nt"], d["qblocks"], d["nblocks"] = Nq, Nk // 64, qblocks, nblocks
+    d["nq"], d["nt"], d["qblocks"], d["nblocks"] = Nq, -(-Nk // 64), qblocks, nblocks
     d["magq"], shq = magic(qblocks)
     d["magh"], shh = magic(H)
     d["magg"], shg = magic(group)
@@ -61,6 +61,8 @@ def args_for(qa, ka, va, oa, B, H, Hkv, Nq, Nk, strides_el, scale, G, muoff=7.0,
         d["cw"] = walk | (lg8 << 8) | (lghq << 16) | (per << 24)
         d["hx"] = hx
         d["offt"] = (Nk - Nq) // 64
+    elif Nk % 64:
+        d["cw"] = 64 - Nk % 64  # ragged: keys of the last (shifted) tile already counted
     d["c"] = struct.unpack("<I", struct.pack("<f", scale * 1.4426950408889634))[0]
     d["muoff"] = struct.unpack("<I", struct.pack("<f", muoff))[0]
     d["G"] = G
@@ -88,8 +90,11 @@ def run(q, k, v, scale=None, grid=None, muoff=7.0, layout="bhsd", causal=False, 
     enc, dec = (E.f16_rne, E.f16_to_f32) if dtype == "f16" else (E.bf16_rne, E.bf16_to_f32)
     B, H, Nq, D = q.shape
     Hkv, Nk = k.shape[1], k.shape[2]
-    assert D in (64, 128) and Nk % 64 == 0 and Nk >= 128
+    ragged = Nk % 64 != 0
+    assert D in (64, 128) and (Nk >= 128 if not ragged else Nk > 64 and not causal)
     assert not causal or (Nk - Nq >= 0 and (Nk - Nq) % 64 == 0)
+    if ragged:
+        kw = dict(kw, ragged=True)
     scale = 1.0 / math.sqrt(D) if scale is None else scale
     heap = E.Heap()
 
