@@ -18,8 +18,10 @@ returns the mapping): ``block_q`` -> 256 query rows per workgroup (4 waves x
 64 rows, one wave per SIMD, four 16-row q-blocks per wave on the 16x16x32
 MFMA), ``block_k`` -> 64-key K/V tiles, ``num_warps`` -> 4 wave64s per
 workgroup, ``num_stages`` -> a 5-slot LDS ring with K/V DMA'd two tiles
-ahead (causal bf16 D = 128 runs the same program with the mask,
-attn_fwd_v13c; fp16, D = 64 and Nk < 128 take attn_fwd_v12 / v10 / v7).  The GPU path ignores the requested values (results do not
+ahead (causal runs the same program with the mask, attn_fwd_v13c; fp16 on
+the f16 MFMA; D = 64 on half-width images; key counts that are not a multiple
+of 64 on the ragged form, attn_fwd_v13r; Nk <= 64 and other head dims take
+attn_fwd_v12 / v10 / v7).  The GPU path ignores the requested values (results do not
 depend on the blocking; the kernel's tiles are set by the MFMA / LDS
 mapping); the CPU recurrence uses ``block_q``/``block_k`` as the reference
 does.  Non-positive or non-integer fields are rejected on both paths.  Softmax statistics are fp32 on both paths (the reference keeps
