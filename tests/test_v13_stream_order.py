@@ -83,3 +83,44 @@ def test_causal_stream_order(shape):
         # past its last block the stream parks on one tile (at most two extra loads)
         assert got[L][:len(seq)] == seq, f"workgroup {L}: {got[L][:len(seq)]} != {seq}"
         assert len(got[L]) - len(seq) <= 2
+
+
+def ragged_stream(B, H, Hkv, Nq, Nk, grid):
+    """non-causal, Nk % 64 != 0: (kv head, first key row) of every tile each
+    workgroup streams (wave 0's first K piece)"""
+    z = np.zeros
+    _, em = R.run(z((B, H, Nq, 128)), z((B, Hkv, Nk, 128)), z((B, Hkv, Nk, 128)), grid=grid, structural=True)
+    row_b, head_b = 128 * 2, Nk * 128 * 2
+    seq = {}
+    for (wg, wv), base, off, _m0 in em.dma_log:
+        rel = base - em.kbase
+        if wv == 0 and off == 0 and 0 <= rel < B * Hkv * head_b:
+            assert (rel % head_b) % row_b == 0
+            seq.setdefault(wg, []).append((rel // head_b, (rel % head_b) // row_b))
+    return seq
+
+
+@pytest.mark.parametrize("shape", [(1, 8, 8, 512, 200, 16), (2, 4, 2, 300, 130, 8), (1, 16, 4, 256, 65, None)],
+                         ids=lambda s: "b{}h{}kv{}q{}k{}g{}".format(*s))
+def test_ragged_stream_stays_in_head(shape):
+    """Gen(ragged=True): every block streams key rows 0, 64, ..., 64 (nt - 2)
+    and then Nk - 64 (the last tile overlapping the one before), so no K / V
+    read leaves its head; the persistent walk's seams and park included"""
+    B, H, Hkv, Nq, Nk, grid = shape
+    QB, nt = -(-Nq // 256), -(-Nk // 64)
+    nb = B * H * QB
+    G = grid or nb
+    rows = [64 * t for t in range(nt - 1)] + [Nk - 64]
+    got = ragged_stream(B, H, Hkv, Nq, Nk, grid)
+    for L in range(G):
+        seq = []
+        for l in range(L, nb, G):
+            n8, r8 = (0, 8) if nb < 8 else (nb >> 3, nb & 7)
+            x, i = l & 7, l >> 3
+            lb = x * n8 + min(x, r8) + i
+            bh = lb // QB
+            b, h = divmod(bh, H)
+            seq += [(b * Hkv + h // (H // Hkv), r) for r in rows]
+        assert got[L][:len(seq)] == seq, f"workgroup {L}: {got[L][:len(seq)]} != {seq}"
+        # past its last block the stream parks on its last (shifted) tile
+        assert all(t == seq[-1] for t in got[L][len(seq):]) and len(got[L]) - len(seq) <= 2
