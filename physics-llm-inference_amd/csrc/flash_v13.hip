@@ -162,7 +162,8 @@ int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B,
                     uint32_t* stamps, bool causal, bool fp16, int D) {
     PLI_REQUIRE(attn_v13_ok(D, fp16 ? 0 : 1, causal, Nq, Nk, st), "attn_fwd_v13: shape not supported");
     PLI_REQUIRE(H > 0 && H < (1 << 16), "attn_fwd_v13: H = %d past the packed 16-bit head count", H);
-    PLI_REQUIRE(!((fp16 || D != 128) && stamps), "attn_fwd_v13: the stamp build is bf16, D = 128");
+    PLI_REQUIRE(!((fp16 || D != 128 || Nk % 64 != 0 || causal) && stamps),
+                "attn_fwd_v13: the stamp build is bf16, D = 128, non-causal, Nk % 64 == 0");
     const int qblocks = cdiv(Nq, 256);
     const int64_t nb = (int64_t)B * H * qblocks;
     PLI_REQUIRE(nb < (1ll << 31) && nb > 0, "attn_fwd_v13: grid too large");
