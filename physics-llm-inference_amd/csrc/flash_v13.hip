@@ -1,8 +1,8 @@
 // attn_fwd_v13: flash-attention forward on v_mfma_f32_16x16x32_bf16
 // (reference ch06/flash_attention.py:14-74; gfx950, bf16 / fp16, D = 128 /
 // 64, Nk a multiple of 64 and >= 128 or -- attn_fwd_v13r -- any Nk > 64;
-// causal -- bottom-right, (Nk - Nq) % 64 == 0 -- as the second program
-// attn_fwd_v13c; other cases take v12 / v10).
+// causal -- bottom-right, Nk % 64 == 0, any Nq <= Nk -- as the second
+// program attn_fwd_v13c; other cases take v12 / v10).
 //
 // One wave per SIMD, 64 query rows per wave (4 q-blocks of 16), persistent
 // workgroups of 4 waves walking 256-row blocks.  The body is ONE generated
@@ -143,8 +143,11 @@ bool attn_v13_ok(int D, int is_bf16, int causal, int Nq, int Nk, const V7Strides
     // multiple of 64 from 128, or (non-causal) any Nk > 64: the ragged bodies
     if ((D != 128 && D != 64) || Nq < 1) return false;
     if (Nk % 64 == 0 ? Nk < 128 : (causal || Nk <= 64)) return false;
-    // causal: the bottom-right diagonal on 64-key tile boundaries
-    if (causal && (Nq > Nk || (Nk - Nq) % 64 != 0)) return false;
+    // causal: Nq <= Nk and whole key tiles; any diagonal offset -- rows are
+    // processed as Nq + s virtual rows, s = (-Nq) & 63, which puts the
+    // bottom-right diagonal on 64-key tile boundaries (tools/v13/kernel.py
+    // qshift; rows below s are neither loaded nor stored)
+    if (causal && (Nq > Nk || Nk % 64 != 0)) return false;
     // causal: the stream's tile count and index carry the block's order in
     // bit 16 (tools/v13/kernel.py block_params), so counts stay below 2^16
     if (causal && Nk / 64 > 0xFFFF) return false;
@@ -164,7 +167,8 @@ int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B,
     PLI_REQUIRE(H > 0 && H < (1 << 16), "attn_fwd_v13: H = %d past the packed 16-bit head count", H);
     PLI_REQUIRE(!((fp16 || D != 128 || Nk % 64 != 0 || causal) && stamps),
                 "attn_fwd_v13: the stamp build is bf16, D = 128, non-causal, Nk % 64 == 0");
-    const int qblocks = cdiv(Nq, 256);
+    const int nqv = causal ? Nq + ((-Nq) & 63) : Nq;  // causal: virtual rows (Nk - nqv) % 64 == 0
+    const int qblocks = cdiv(nqv, 256);
     const int64_t nb = (int64_t)B * H * qblocks;
     PLI_REQUIRE(nb < (1ll << 31) && nb > 0, "attn_fwd_v13: grid too large");
     int grid = (int)nb;
@@ -223,7 +227,7 @@ int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B,
     const bool ragged = Nk % 64 != 0;  // (non-causal: the walk word is free for P0)
     a.w[A_CW] = ragged ? (uint32_t)(64 - Nk % 64) : cw;
     a.w[A_HX] = hx;
-    a.w[A_OFFT] = causal ? (uint32_t)((Nk - Nq) / 64) : 0u;
+    a.w[A_OFFT] = causal ? (uint32_t)((Nk - nqv) / 64) : 0u;
     const float c = scale * 1.4426950408889634f;
     std::memcpy(&a.w[A_C], &c, 4);
     std::memcpy(&a.w[A_MUOFF], &muoff, 4);

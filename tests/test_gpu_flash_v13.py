@@ -110,7 +110,8 @@ def test_v13_rescale_stress(name):
     assert_agree_to_rounding(pli_hip.flash_attn_fwd(q, k, v, variant=82), out, v)
 
 
-# causal (bottom-right mask, (Nk - Nq) % 64 == 0): 83 persistent (pair walk
+# causal (bottom-right mask, Nk % 64 == 0; any diagonal offset -- rows run as
+# Nq + ((-Nq) & 63) virtual rows since round 5): 83 persistent (pair walk
 # where it tiles the grid; the second block of each pair streams its key
 # tiles in the reversed order of tools/v13/kernel.py Gen.tile_of), 84 one
 # block per workgroup heaviest first (forward order), 85 = 83 with the
@@ -118,7 +119,11 @@ def test_v13_rescale_stress(name):
 CAUSAL = [(4, 32, 8, 1024, 1024), (2, 32, 32, 2048, 2048), (2, 16, 4, 4096, 4096), (3, 40, 8, 1024, 1024),
           (2, 8, 2, 256, 512), (1, 4, 4, 128, 128), (1, 8, 8, 704, 768), (2, 4, 2, 320, 320),
           # pair walk with reversed second blocks and a diagonal offset (Nk - Nq = 1024 / 512)
-          (4, 32, 8, 1024, 2048), (2, 32, 8, 2048, 2560)]
+          (4, 32, 8, 1024, 2048), (2, 32, 8, 2048, 2560),
+          # offsets that are not a multiple of 64 (virtual rows): 212, 24 (pair walk over 1024 virtual
+          # rows), 96, 28, 255 (one query row), 1
+          (2, 8, 2, 300, 512), (4, 32, 8, 1000, 1024), (2, 16, 4, 4000, 4096), (1, 4, 4, 100, 128),
+          (2, 8, 8, 1, 256), (1, 8, 2, 703, 704)]
 
 
 @pytest.mark.parametrize("qmul", (1, 4))
@@ -157,12 +162,15 @@ def test_v13_causal_full_config_all_heads():
     assert_agree_to_rounding(pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=85), out, v)
 
 
-def test_v13_causal_unaligned_offset_falls_back():
-    """Nk - Nq not a multiple of 64: the causal v13 variants route to v12."""
+def test_v13_causal_unaligned_offset_runs_v13():
+    """Nk - Nq not a multiple of 64 (chunked prefill: 300 new rows over 512
+    keys) runs attn_fwd_v13c on virtual rows, not v12: the default route
+    equals 83 bitwise and differs from 74 in rounding only."""
     import pli_hip
     q, k, v = inputs((2, 8, 2, 300, 512), 3)
-    assert torch.equal(pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=83),
-                       pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=74))
+    out = pli_hip.flash_attn_fwd(q, k, v, causal=True)
+    assert torch.equal(out, pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=83))
+    assert_agree_to_rounding(out, pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=74), v)
 
 
 @pytest.mark.parametrize("scale", (1.0, 0.25, 2.0 ** -0.5 / 8))

@@ -48,6 +48,9 @@ CASES = [  # (B, H, Hkv, Nq, Nk, grid, layout, muoff, causal)
     (1, 1, 1, 256, 256, None, "bhsd", 0.0, False),      # the rescale path at every tile (l >= 1 from the start)
     (1, 2, 1, 256, 512, None, "bhsd", 62.0, True),      # causal, Nq < Nk (diagonal offset 4 tiles)
     (1, 1, 1, 512, 512, None, "bhsd", 0.0, True),       # causal, two blocks, rescales on masked tiles
+    (1, 2, 1, 200, 512, None, "bhsd", 62.0, True),      # causal, diagonal offset 312 (virtual rows: + 56)
+    (1, 8, 8, 1000, 1024, 16, "bhsd", 62.0, True),      # causal pair walk over 1024 virtual rows (offset 24)
+    (1, 1, 1, 100, 256, None, "bhsd", 0.0, True),       # causal, offset 156, rescales at every tile
 ]
 
 

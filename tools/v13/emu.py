@@ -326,6 +326,10 @@ class Emu:
             return self.vset(w, o[0], (g(o[1]).astype(np.uint64) * g(o[2])) & M32)
         if op == "v_min_u32":
             return self.vset(w, o[0], np.minimum(g(o[1]), g(o[2])))
+        if op == "v_max_u32":
+            return self.vset(w, o[0], np.maximum(g(o[1]), g(o[2])))
+        if op == "v_subrev_u32":
+            return self.vset(w, o[0], (g(o[2]).astype(np.int64) - g(o[1])) & M32)
         if op == "v_mbcnt_lo_u32_b32":
             lane = np.arange(LANES)
             return self.vset(w, o[0], (np.minimum(lane, 32) + g(o[2])).astype(np.uint32))

@@ -759,6 +759,14 @@ def exps_all(X, also_or=False, shifted=False):
     return c
 
 
+def qshift(dst):
+    """causal: dst = s = (-Nq) & 63, the virtual-row shift that puts the
+    bottom-right diagonal on 64-key tile boundaries when (Nk - Nq) % 64 != 0
+    (Nk % 64 == 0): row q is processed as q + s of Nq + s rows (the launcher
+    sizes the blocks and the diagonal tile offset for Nq + s)"""
+    return [I("s_sub_u32", dst, 0, ARG(AI["nq"])), I("s_and_b32", dst, dst, 63)]
+
+
 def mask_tile(tile):
     """causal, straight line (prologue and rare path): scores of the tile
     whose index is in SGPR `tile` with key > row + off set to -inf.  Lane
@@ -911,11 +919,17 @@ class Gen:
 
     # ---- per-block scalar setup -----------------------------------------
     def q_offsets(self, q0, qh):
-        """QOFF(qb) = min(q0 + 16 qb + i, Nq - 1) * qn + 16 g; Q loads"""
+        """QOFF(qb) = min(q0 + 16 qb + i, Nq - 1) * qn + 16 g; Q loads.
+        Causal: rows are virtual, q' = q + s with s = (-Nq) & 63 (QSHIFT),
+        so the load row is min(max(q', s) - s, Nq - 1)"""
         c = [I("s_sub_u32", sT0, ARG(AI["nq"]), 1)]
+        if self.causal:
+            c += qshift(sT1)
         for qb in range(4):
-            c += [I("v_add_u32", T(0), q0, VI), I("v_add_u32", T(0), 16 * qb, T(0)),
-                  I("v_min_u32", T(0), sT0, T(0)), I("v_mul_lo_u32", T(0), T(0), ARG(AI["qn"])),
+            c += [I("v_add_u32", T(0), q0, VI), I("v_add_u32", T(0), 16 * qb, T(0))]
+            if self.causal:
+                c += [I("v_max_u32", T(0), sT1, T(0)), I("v_subrev_u32", T(0), sT1, T(0))]
+            c += [I("v_min_u32", T(0), sT0, T(0)), I("v_mul_lo_u32", T(0), T(0), ARG(AI["qn"])),
                   I("v_lshlrev_b32", T(1), 4, VG), I("v_add_u32", QOFF(qb), T(0), T(1))]
         for qb in range(4):
             for ds in range(NDS()):
@@ -1243,10 +1257,15 @@ class Gen:
         e([I("s_nop", 7), I("s_nop", 7)])
         for qb in range(4):
             e([I("v_rcp_f32", T(20 + qb), L_(qb)[0])])
+        if self.causal:
+            e(qshift(sT1))
         for qb in range(4):
-            # O offsets and the row mask of this q-block
-            e([I("v_add_u32", T(24), sCQ0, VI), I("v_add_u32", T(24), 16 * qb, T(24)),
-               I("v_mul_lo_u32", T(25), T(24), ARG(AI["on"])),
+            # O offsets and the row mask of this q-block (causal: the real
+            # row q' - s; a virtual row below s wraps and is not stored)
+            e([I("v_add_u32", T(24), sCQ0, VI), I("v_add_u32", T(24), 16 * qb, T(24))])
+            if self.causal:
+                e([I("v_subrev_u32", T(24), sT1, T(24))])
+            e([I("v_mul_lo_u32", T(25), T(24), ARG(AI["on"])),
                I("v_and_b32", T(26), 1, VG), I("v_lshlrev_b32", T(26), 5, T(26)),
                I("v_lshrrev_b32", T(27), 1, VG), I("v_lshlrev_b32", T(27), 4, T(27)),
                I("v_add3_u32", OOFF(qb), T(25), T(26), T(27))])
