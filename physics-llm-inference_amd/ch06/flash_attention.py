@@ -18,7 +18,8 @@ returns the mapping): ``block_q`` -> 256 query rows per workgroup (4 waves x
 64 rows, one wave per SIMD, four 16-row q-blocks per wave on the 16x16x32
 MFMA), ``block_k`` -> 64-key K/V tiles, ``num_warps`` -> 4 wave64s per
 workgroup, ``num_stages`` -> a 5-slot LDS ring with K/V DMA'd two tiles
-ahead (causal runs the same program with the mask, attn_fwd_v13c; fp16 on
+ahead (causal runs the same program with the mask, attn_fwd_v13c, at any
+diagonal offset; fp16 on
 the f16 MFMA; D = 64 on half-width images; key counts that are not a multiple
 of 64 on the ragged form, attn_fwd_v13r; Nk <= 64 and other head dims take
 attn_fwd_v12 / v10 / v7).  The GPU path ignores the requested values (results do not
