@@ -106,6 +106,26 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_v13hr(V13Args args) {
     asm volatile(PLI_V13HR_BODY::"s"(kp), "s"(wg), "s"(wave), "s"((unsigned)(uintptr_t)smem) : PLI_V13_CLOBBERS);
 }
 
+// causal with Nk % 64 != 0: the shifted last key tile, masked by VALU on its
+// shifted keys (tools/v13/kernel.py rag step; P0 in the top byte of hx)
+__global__ __launch_bounds__(256, 1) void attn_fwd_v13rc(V13Args args) {
+    __shared__ __attribute__((aligned(1024))) char smem[163840];
+    (void)args;
+    const void* kp = (const void*)__builtin_amdgcn_kernarg_segment_ptr();
+    const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const unsigned wg = blockIdx.x;
+    asm volatile(PLI_V13RC_BODY::"s"(kp), "s"(wg), "s"(wave), "s"((unsigned)(uintptr_t)smem) : PLI_V13_CLOBBERS);
+}
+
+__global__ __launch_bounds__(256, 1) void attn_fwd_v13hrc(V13Args args) {
+    __shared__ __attribute__((aligned(1024))) char smem[163840];
+    (void)args;
+    const void* kp = (const void*)__builtin_amdgcn_kernarg_segment_ptr();
+    const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const unsigned wg = blockIdx.x;
+    asm volatile(PLI_V13HRC_BODY::"s"(kp), "s"(wg), "s"(wave), "s"((unsigned)(uintptr_t)smem) : PLI_V13_CLOBBERS);
+}
+
 // floor(x / d) == ((x * m) >> 31) >> l for 0 <= x < 2^31 (Granlund-Montgomery,
 // N = 31: m = ceil(2^(31+l) / d) < 2^32 with l = ceil(log2 d))
 void magic31(uint32_t d, uint32_t& m, uint32_t& l) {
@@ -142,15 +162,15 @@ bool attn_v13_ok(int D, int is_bf16, int causal, int Nq, int Nk, const V7Strides
     // head dim 128, or 64 (the D = 64 bodies in flash_v13_d64.hip); Nk a
     // multiple of 64 from 128, or (non-causal) any Nk > 64: the ragged bodies
     if ((D != 128 && D != 64) || Nq < 1) return false;
-    if (Nk % 64 == 0 ? Nk < 128 : (causal || Nk <= 64)) return false;
-    // causal: Nq <= Nk and whole key tiles; any diagonal offset -- rows are
-    // processed as Nq + s virtual rows, s = (-Nq) & 63, which puts the
-    // bottom-right diagonal on 64-key tile boundaries (tools/v13/kernel.py
-    // qshift; rows below s are neither loaded nor stored)
-    if (causal && (Nq > Nk || Nk % 64 != 0)) return false;
+    if (Nk % 64 == 0 ? Nk < 128 : Nk <= 64) return false;
+    // causal: Nq <= Nk, any diagonal offset -- rows are processed as Nq + s
+    // virtual rows, s = (Nk - Nq) & 63, which puts the bottom-right diagonal
+    // on 64-key tile boundaries (tools/v13/kernel.py qshift; rows below s are
+    // neither loaded nor stored); Nk % 64 != 0 on the ragged causal bodies
+    if (causal && Nq > Nk) return false;
     // causal: the stream's tile count and index carry the block's order in
     // bit 16 (tools/v13/kernel.py block_params), so counts stay below 2^16
-    if (causal && Nk / 64 > 0xFFFF) return false;
+    if (causal && cdiv(Nk, 64) > 0xFFFF) return false;
     // 32-bit per-lane offsets: a Q / O head's rows, a K / V tile
     const int64_t q_ext = ((int64_t)Nq - 1) * st.qn * 2 + 2 * D, o_ext = ((int64_t)Nq - 1) * st.on * 2 + 2 * D;
     const int64_t kv_tile = 64 * std::max(st.kn, st.vn) * 2;
@@ -167,7 +187,7 @@ int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B,
     PLI_REQUIRE(H > 0 && H < (1 << 16), "attn_fwd_v13: H = %d past the packed 16-bit head count", H);
     PLI_REQUIRE(!((fp16 || D != 128 || Nk % 64 != 0 || causal) && stamps),
                 "attn_fwd_v13: the stamp build is bf16, D = 128, non-causal, Nk % 64 == 0");
-    const int nqv = causal ? Nq + ((-Nq) & 63) : Nq;  // causal: virtual rows (Nk - nqv) % 64 == 0
+    const int nqv = causal ? Nq + ((Nk - Nq) & 63) : Nq;  // causal: virtual rows, (Nk - nqv) % 64 == 0
     const int qblocks = cdiv(nqv, 256);
     const int64_t nb = (int64_t)B * H * qblocks;
     PLI_REQUIRE(nb < (1ll << 31) && nb > 0, "attn_fwd_v13: grid too large");
@@ -224,9 +244,13 @@ int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B,
     magic31((uint32_t)H, a.w[A_MAGH], shh);
     magic31((uint32_t)group, a.w[A_MAGG], shg);
     a.w[A_SHIFTS] = shq | (shh << 5) | (shg << 10) | ((uint32_t)H << 16);
-    const bool ragged = Nk % 64 != 0;  // (non-causal: the walk word is free for P0)
-    a.w[A_CW] = ragged ? (uint32_t)(64 - Nk % 64) : cw;
-    a.w[A_HX] = hx;
+    // ragged Nk: P0 = 64 - Nk % 64 in cw (non-causal: the walk word is free)
+    // or in the top byte of hx (causal: the pair walk uses cw, hx < 2^24)
+    const bool ragged = Nk % 64 != 0;
+    const uint32_t p0 = ragged ? (uint32_t)(64 - Nk % 64) : 0u;
+    PLI_REQUIRE(hx < (1u << 24), "attn_fwd_v13: %u heads per XCD past the 24-bit walk field", hx);
+    a.w[A_CW] = ragged && !causal ? p0 : cw;
+    a.w[A_HX] = causal ? hx | (p0 << 24) : hx;
     a.w[A_OFFT] = causal ? (uint32_t)((Nk - nqv) / 64) : 0u;
     const float c = scale * 1.4426950408889634f;
     std::memcpy(&a.w[A_C], &c, 4);
@@ -244,6 +268,14 @@ int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B,
     (void)stamps;
 #endif
     if (D == 64) return launch_v13_d64(fp16, causal, ragged, (unsigned)grid, a, stream);
+    if (ragged && causal) {
+        if (fp16) {
+            hipLaunchKernelGGL(attn_fwd_v13hrc, dim3((unsigned)grid), dim3(256), 0, stream, a);
+            return launch_status("attn_fwd_v13hrc");
+        }
+        hipLaunchKernelGGL(attn_fwd_v13rc, dim3((unsigned)grid), dim3(256), 0, stream, a);
+        return launch_status("attn_fwd_v13rc");
+    }
     if (ragged) {
         if (fp16) {
             hipLaunchKernelGGL(attn_fwd_v13hr, dim3((unsigned)grid), dim3(256), 0, stream, a);

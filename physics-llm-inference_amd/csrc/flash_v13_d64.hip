@@ -33,11 +33,21 @@ PLI_V13_D64_KERNEL(attn_fwd_v13h_d64, PLI_V13H_D64_BODY)
 PLI_V13_D64_KERNEL(attn_fwd_v13hc_d64, PLI_V13HC_D64_BODY)
 PLI_V13_D64_KERNEL(attn_fwd_v13r_d64, PLI_V13R_D64_BODY)
 PLI_V13_D64_KERNEL(attn_fwd_v13hr_d64, PLI_V13HR_D64_BODY)
+PLI_V13_D64_KERNEL(attn_fwd_v13rc_d64, PLI_V13RC_D64_BODY)
+PLI_V13_D64_KERNEL(attn_fwd_v13hrc_d64, PLI_V13HRC_D64_BODY)
 
 }  // namespace
 
 int launch_v13_d64(bool fp16, bool causal, bool ragged, unsigned grid, const V13Args& a, hipStream_t stream) {
-    if (ragged) {  // (non-causal only: attn_v13_ok)
+    if (ragged && causal) {
+        if (fp16) {
+            hipLaunchKernelGGL(attn_fwd_v13hrc_d64, dim3(grid), dim3(256), 0, stream, a);
+            return launch_status("attn_fwd_v13hrc_d64");
+        }
+        hipLaunchKernelGGL(attn_fwd_v13rc_d64, dim3(grid), dim3(256), 0, stream, a);
+        return launch_status("attn_fwd_v13rc_d64");
+    }
+    if (ragged) {
         if (fp16) {
             hipLaunchKernelGGL(attn_fwd_v13hr_d64, dim3(grid), dim3(256), 0, stream, a);
             return launch_status("attn_fwd_v13hr_d64");

@@ -1,6 +1,7 @@
-"""attn_fwd_v13r / v13hr (and the head-dim-64 forms): Nk not a multiple of 64
-on the generated v13 program (tools/v13/kernel.py Gen(ragged=True), round 5;
-before, these shapes ran v12 / v10).  The last key tile is streamed from key
+"""attn_fwd_v13r / v13hr / v13rc / v13hrc (and the head-dim-64 forms): Nk not
+a multiple of 64 on the generated v13 program, plain and causal
+(tools/v13/kernel.py Gen(ragged=True), round 5; before, these shapes ran v12 /
+v10).  The last key tile is streamed from key
 Nk - 64 -- inside the head, so no K / V read leaves it -- and the keys it
 shares with the tile before get P = 0 before the row sums and PV read them.
 
@@ -72,12 +73,32 @@ def test_v13_ragged_overlap_spikes():
     assert err <= 2.0 ** -8 * v.abs().max().item(), f"max |err| {err:.4e}"
 
 
-def test_v13_ragged_causal_still_falls_back():
-    """causal with Nk % 64 != 0 stays on v12 (74): 83 equals it bitwise"""
+# causal with Nk % 64 != 0 (attn_fwd_v13rc / v13hrc and the D64 pair): the
+# shifted last tile masked by VALU on its shifted keys; prefill of N tokens
+# (Nq = Nk), chunked prefill (Nq < Nk, any offset), the pair walk's reversed
+# blocks, one query row, Nk = 65
+CAUSAL_SHAPES = [(4, 32, 8, 1000, 1000, 128), (2, 16, 4, 4000, 4000, 128), (1, 4, 4, 200, 200, 128),
+                 (2, 8, 2, 300, 430, 128), (1, 2, 2, 65, 65, 128), (2, 8, 8, 1, 77, 128),
+                 (4, 32, 8, 1000, 1000, 64), (2, 8, 2, 300, 430, 64)]
+
+
+@pytest.mark.parametrize("dtype", (torch.bfloat16, torch.float16), ids=("bf16", "fp16"))
+@pytest.mark.parametrize("qmul", (1, 4))
+@pytest.mark.parametrize("shape", CAUSAL_SHAPES, ids=lambda s: "b{}h{}kv{}q{}k{}d{}".format(*s))
+def test_v13_ragged_causal_vs_f64_full_tensor(shape, qmul, dtype):
     import pli_hip
-    q, k, v = inputs((1, 4, 4, 200, 200, 128), 31, torch.bfloat16)
-    assert torch.equal(pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=83),
-                       pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=74))
+    q, k, v = inputs(shape, sum(shape) % 977, dtype)
+    q = q * qmul
+    ref = torch_attention(q, k, v, causal=True)
+    tol = 1e-2 if qmul == 1 else 2.0 ** -8 * v.abs().max().item()
+    outs = {}
+    for var in (83, 84, 85):
+        outs[var] = pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=var)
+        err = max_err(outs[var], ref)
+        assert err <= tol, f"{shape} q*{qmul} causal variant {var}: max |err| {err:.4e} > {tol:.4e}"
+    assert torch.equal(outs[83], pli_hip.flash_attn_fwd(q, k, v, causal=True)), f"{shape}: default route is not 83"
+    if qmul == 1:
+        assert_agree_to_rounding(outs[83], outs[84], v)
 
 
 def test_v13_ragged_bench_scale():

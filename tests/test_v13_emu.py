@@ -213,4 +213,34 @@ def test_v13_ragged_spikes():
 def test_v13_ragged_hazard_pass_is_idempotent():
     for dtype in ("bf16", "f16"):
         for hd in (128, 64):
-            assert analyse(R.program(causal=False, dtype=dtype, ragged=True, hd=hd)) == {}
+            for causal in (False, True):
+                assert analyse(R.program(causal=causal, dtype=dtype, ragged=True, hd=hd)) == {}
+
+
+RAGGED_CAUSAL_CASES = [  # (B, H, Hkv, Nq, Nk, grid, muoff, D, dtype): causal, Nk % 64 != 0
+    (1, 2, 1, 200, 200, None, 62.0, 128, "bf16"),     # causal prefill of 200 tokens (one block)
+    (1, 8, 8, 1000, 1000, 16, 62.0, 128, "bf16"),     # the pair walk: reversed blocks meet the shifted tile at position 3
+    (1, 8, 8, 1000, 1000, 16, 0.0, 128, "bf16"),      # ... with the rescale path at every tile
+    (2, 8, 2, 700, 770, 16, 62.0, 128, "bf16"),       # GQA, offset 70 (virtual rows + 6), remap walk
+    (1, 2, 1, 65, 65, None, 62.0, 128, "bf16"),       # NT = 2: the last tile overlaps the first by 63 keys
+    (1, 2, 2, 77, 300, None, 4.0, 128, "f16"),        # fp16, short query block
+    (1, 8, 8, 990, 990, 16, 4.0, 64, "f16"),          # head dim 64, fp16, pair walk
+]
+
+
+@pytest.mark.parametrize("case", RAGGED_CAUSAL_CASES,
+                         ids=lambda c: "ragged-causal-b{}h{}kv{}q{}k{}g{}-mu{}-d{}-{}".format(*c))
+def test_v13_ragged_causal_program_vs_f64(case):
+    """causal with Nk % 64 != 0: key tile NT - 1 streams from key Nk - 64 and
+    its step masks the shifted keys by VALU (already-counted keys and keys
+    past each row's diagonal), in both stream orders of the pair walk"""
+    B, H, Hkv, Nq, Nk, grid, muoff, D, dtype = case
+    rng = np.random.default_rng(19 + sum(case[:5]))
+    q = rng.standard_normal((B, H, Nq, D))
+    k = rng.standard_normal((B, Hkv, Nk, D))
+    v = rng.standard_normal((B, Hkv, Nk, D))
+    o, em = R.run(q, k, v, grid=grid, muoff=muoff, causal=True, dtype=dtype)
+    err = np.abs(o - f64_attention(q, k, v, True, dtype=dtype)).max()
+    assert err <= 1e-2, f"max |err| {err:.3e}"
+    if muoff <= 0:
+        assert em.counts.get("v_sub_f32", 0) > 0, "the rescale path never ran"

@@ -31,18 +31,19 @@ def stream(B, H, Hkv, Nq, Nk, grid):
     z = np.zeros
     _, em = R.run(z((B, H, Nq, 128)), z((B, Hkv, Nk, 128)), z((B, Hkv, Nk, 128)), grid=grid, causal=True,
                   structural=True)
-    tile_b, head_b = 64 * 128 * 2, Nk * 128 * 2
+    row_b, head_b = 128 * 2, Nk * 128 * 2
     seq = {}
     for (wg, wv), base, off, _m0 in em.dma_log:
         rel = base - em.kbase
         if wv == 0 and off == 0 and 0 <= rel < B * Hkv * head_b:  # wave 0's first K piece of each tile
-            seq.setdefault(wg, []).append((rel // head_b, (rel % head_b) // tile_b))
+            seq.setdefault(wg, []).append((rel // head_b, (rel % head_b) // row_b))  # (kv head, first key row)
     return seq
 
 
 def expected(B, H, Hkv, Nq, Nk, G):
-    Nqv = Nq + ((-Nq) & 63)  # virtual rows (launch_attn_v13): the diagonal on tile boundaries
-    QB, nt, offt = -(-Nqv // 256), Nk // 64, (Nk - Nqv) // 64
+    Nqv = Nq + ((Nk - Nq) & 63)  # virtual rows (launch_attn_v13): the diagonal on tile boundaries
+    QB, nt, offt = -(-Nqv // 256), -(-Nk // 64), (Nk - Nqv) // 64
+    row = lambda t: Nk - 64 if t == nt - 1 else 64 * t  # noqa: E731  (ragged Nk: the last tile shifted back)
     nb = B * H * QB
     walk, lg8, lghq, per, hx = R.pair_walk(nb, QB, G)
     out = {}
@@ -65,18 +66,20 @@ def expected(B, H, Hkv, Nq, Nk, G):
             rev = rev and T >= 4
             order = list(range(T - 4, T)) + list(range(T - 5, -1, -1)) if rev else list(range(T))
             b, h = divmod(bh, H)
-            seq += [(b * Hkv + h // (H // Hkv), t) for t in order]
+            seq += [(b * Hkv + h // (H // Hkv), row(t)) for t in order]
         out[L] = seq
     return walk, out
 
 
 @pytest.mark.parametrize("shape", [(1, 8, 8, 1024, 1024, 16), (1, 8, 4, 1024, 1280, 16), (2, 8, 2, 512, 512, 16),
                                    (1, 8, 8, 1024, 1024, None), (1, 8, 8, 1000, 1024, 16), (1, 8, 4, 990, 1280, 16),
-                                   (1, 8, 4, 700, 1280, None)],
+                                   (1, 8, 4, 700, 1280, None),
+                                   # ragged Nk: the shifted last tile in both orders, the park on tile 0
+                                   (1, 8, 8, 1000, 1000, 16), (1, 8, 4, 900, 1250, 16), (2, 8, 2, 700, 770, None)],
                          ids=lambda s: "b{}h{}kv{}q{}k{}g{}".format(*s))
 def test_causal_stream_order(shape):
     B, H, Hkv, Nq, Nk, grid = shape
-    QB = -(-(Nq + ((-Nq) & 63)) // 256)
+    QB = -(-(Nq + ((Nk - Nq) & 63)) // 256)
     G = grid or B * H * QB
     walk, want = expected(B, H, Hkv, Nq, Nk, G)
     assert walk == (1 if grid else 2)

@@ -455,7 +455,7 @@ def slice_list():
     return [(qb, kb, hh) for qb in range(4) for kb in range(4) for hh in range(2)]
 
 
-def softmax_fills(X, slices, earliest_of, deadline_of=None, ytag=0, prev_cv=None):
+def softmax_fills(X, slices, earliest_of, deadline_of=None, ytag=0, prev_cv=None, extra_deps=None):
     """fills for the given slices of the tile in P state X: per slice two
     v_fma_f32 (s * c - mu), two v_exp_f32, one v_cvt_pk_bf16_f32; one
     v_or3_b32 per two slices into ACC(X).  Temporaries Y rotate over 8 slots
@@ -468,6 +468,8 @@ def softmax_fills(X, slices, earliest_of, deadline_of=None, ytag=0, prev_cv=None
         y0, y1 = Y(2 * slot), Y(2 * slot + 1)
         s = S_(kb, qb)
         deps = [slot_cv[slot]] if slot in slot_cv else []
+        if extra_deps is not None:  # (the ragged causal mask of S(kb, qb))
+            deps = deps + extra_deps(qb, kb)
         ea, dl = earliest_of(qb, kb), deadline_of(qb, kb) if deadline_of else None
         f0 = Fill(I("v_fma_f32", y0, s[2 * hh], sC, Neg(MU(qb))), 4, deps=deps, sep=0, earliest=ea, deadline=dl,
                   tag="fma", hard=dl is not None)
@@ -585,7 +587,8 @@ def block_params(sx, causal=False, uid=0, rev=0):
               I("s_and_b32", sT2, sx, 7), I("s_lshr_b32", sT3, sx, 3),
               I("s_lshr_b32", sT6, CW, 8), I("s_and_b32", sT6, sT6, 0xFF),
               I("s_lshr_b32", sT4, sT3, sT6), I("s_lshl_b32", sT5, sT4, sT6), I("s_sub_u32", sT5, sT3, sT5),
-              I("s_mul_i32", sT2, sT2, ARG(AI["hx"])),
+              *([I("s_and_b32", sT6, ARG(AI["hx"]), 0xFFFFFF), I("s_mul_i32", sT2, sT2, sT6)] if RAGGED[0] else
+                [I("s_mul_i32", sT2, sT2, ARG(AI["hx"]))]),
               I("s_lshr_b32", sT6, CW, 16), I("s_and_b32", sT6, sT6, 0xFF),
               I("s_lshr_b32", sT3, sT5, sT6), I("s_lshl_b32", sT7, sT3, sT6), I("s_sub_u32", sT5, sT5, sT7),
               I("s_add_u32", sT2, sT2, sT3),
@@ -639,10 +642,16 @@ def dma_fills(slot_reg, earliest0=2, spacing=6, rev=False):
     next tile into slot slot_reg (K pieces NPW/2 w .. of the K image, V
     pieces of the V image; one M0 write per half), the stream switch before
     and the advance after"""
-    sw = Fill([I("s_cmp_eq_u32", sDIDX, sDNT), I("s_cselect_b64", sDK, sNXK, sDK),
-               I("s_cselect_b64", sDV, sNXV, sDV), I("s_cselect_b32", sDIDX, sNXIDX, sDIDX),
-               I("s_cselect_b32", sDNT, sNXNT, sDNT)],
-              2, earliest=earliest0 - 1, tag="dmasw")
+    swi = [I("s_cmp_eq_u32", sDIDX, sDNT), I("s_cselect_b64", sDK, sNXK, sDK),
+           I("s_cselect_b64", sDV, sNXV, sDV), I("s_cselect_b32", sDIDX, sNXIDX, sDIDX),
+           I("s_cselect_b32", sDNT, sNXNT, sDNT)]
+    cost = 2
+    if RAGGED[0] and rev:
+        # causal: the last key tile streams from key Nk - 64 (P0 keys back);
+        # sT3 keeps the shift until the advance undoes it
+        swi += p0_to(sT3, True) + is_last_tile() + [I("s_cselect_b32", sT3, sT3, 0)] + rag_shift(sDK, sDV, True)
+        cost = 8
+    sw = Fill(swi, cost, earliest=earliest0 - 1, tag="dmasw")
     fills = [sw]
     prev = sw
     half = NPW() // 2
@@ -663,7 +672,8 @@ def dma_fills(slot_reg, earliest0=2, spacing=6, rev=False):
         # causal: sDIDX bit 16 = the streamed block's order.  Reversed, the
         # positions 0..3 are tiles nt-4 .. nt-1 and position p >= 4 is tile
         # nt-1-p: the step into position p is +1, -4 (p = 4) or -1 tiles
-        adv = Fill([I("s_add_u32", sDIDX, sDIDX, 1), I("s_and_b32", sT2, sDIDX, 0xFFFF),
+        undo = rag_shift(sDK, sDV, False) if RAGGED[0] else []
+        adv = Fill(undo + [I("s_add_u32", sDIDX, sDIDX, 1), I("s_and_b32", sT2, sDIDX, 0xFFFF),
                     I("s_cmp_eq_u32", sT2, 4), I("s_cselect_b32", sT3, -4, -1),
                     I("s_cmp_lt_u32", sT2, 4), I("s_cselect_b32", sT3, 1, sT3),
                     I("s_bitcmp1_b32", sDIDX, 16), I("s_cselect_b32", sT3, sT3, 1),
@@ -759,12 +769,45 @@ def exps_all(X, also_or=False, shifted=False):
     return c
 
 
-def qshift(dst):
-    """causal: dst = s = (-Nq) & 63, the virtual-row shift that puts the
-    bottom-right diagonal on 64-key tile boundaries when (Nk - Nq) % 64 != 0
-    (Nk % 64 == 0): row q is processed as q + s of Nq + s rows (the launcher
-    sizes the blocks and the diagonal tile offset for Nq + s)"""
-    return [I("s_sub_u32", dst, 0, ARG(AI["nq"])), I("s_and_b32", dst, dst, 63)]
+def p0_to(dst, causal):
+    """RAGGED: dst = P0 = 64 - Nk % 64 (the non-causal program has it in
+    the cw argument, the causal one -- whose walk uses cw -- in the top byte
+    of hx)"""
+    if causal:
+        return [I("s_lshr_b32", dst, ARG(AI["hx"]), 24)]
+    return [I("s_mov_b32", dst, ARG(AI["cw"]))]
+
+
+def qshift(dst, tmp):
+    """causal: dst = s = (Nk - Nq) & 63 = (-(Nq + P0)) & 63, the virtual-row
+    shift that puts the bottom-right diagonal on 64-key tile boundaries: row q
+    is processed as q + s of Nq + s rows (the launcher sizes the blocks and
+    the diagonal tile offset for Nq + s)"""
+    c = [I("s_sub_u32", dst, 0, ARG(AI["nq"]))]
+    if RAGGED[0]:
+        c += p0_to(tmp, True) + [I("s_sub_u32", dst, dst, tmp)]
+    return c + [I("s_and_b32", dst, dst, 63)]
+
+
+def is_last_tile():
+    """RAGGED causal: SCC = the stream's current position is key tile NT - 1
+    (forward: position NT - 1; reversed: position 3 of a block whose tile
+    count is NT); uses sT4 .. sT7"""
+    return [I("s_and_b32", sT4, sDIDX, 0xFFFF), I("s_and_b32", sT5, sDNT, 0xFFFF),
+            I("s_cmp_eq_u32", sT5, ARG(AI["nt"])), I("s_cselect_b32", sT7, 3, 0xFFFF),
+            I("s_sub_u32", sT6, ARG(AI["nt"]), 1), I("s_bitcmp1_b32", sDIDX, 16),
+            I("s_cselect_b32", sT6, sT7, sT6), I("s_cmp_eq_u32", sT4, sT6)]
+
+
+def rag_shift(k, v, sub):
+    """RAGGED causal: K / V stream pointers k, v moved back (sub) or forward
+    by sT3 keys (sT3 = P0 or 0); uses sT2"""
+    c = []
+    for (ptr, tb) in ((k, sTBK), (v, sTBV)):
+        c += [I("s_mul_i32", sT2, sT3, tb), I("s_lshr_b32", sT2, sT2, 6)]
+        c += ([I("s_sub_u32", ptr[0], ptr[0], sT2), I("s_subb_u32", ptr[1], ptr[1], 0)] if sub else
+              [I("s_add_u32", ptr[0], ptr[0], sT2), I("s_addc_u32", ptr[1], ptr[1], 0)])
+    return c
 
 
 def mask_tile(tile):
@@ -783,6 +826,27 @@ def mask_tile(tile):
     return c
 
 
+def rag_setup():
+    """RAGGED causal, key tile NT - 1 (keys Nk - 64 + p at position p):
+    T(26) = 4 g - P0, T(27) = i + 64 (sTD - NT + 1) (sTD >= NT - 1 here);
+    uses sT0, sT1"""
+    return p0_to(sT1, True) + [
+        I("s_sub_u32", sT0, sTD, ARG(AI["nt"])), I("s_add_u32", sT0, sT0, 1), I("s_lshl_b32", sT0, sT0, 6),
+        I("v_lshlrev_b32", T(26), 2, VG), I("v_subrev_u32", T(26), sT1, T(26)), I("v_add_u32", T(27), sT0, VI)]
+
+
+def rag_block(kb, qb):
+    """RAGGED causal: S(kb, qb) of key tile NT - 1 masked to -inf where the
+    key is already counted (p < P0) or past the row's diagonal: with x =
+    p - P0 and y = (row's last visible key) - (Nk - 64) - P0, masked iff x >u
+    y (x wraps for p < P0)"""
+    c = [I("v_add_u32", T(29), 16 * qb, T(27))]
+    for r in range(4):
+        c += [I("v_add_u32", T(28), 16 * kb + r, T(26)), I("v_cmp_gt_u32_e32", VCC, T(28), T(29)),
+              I("v_cndmask_b32_e32", S_(kb, qb)[r], S_(kb, qb)[r], NINF[0], VCC)]
+    return c
+
+
 # ---------------------------------------------------------------- program
 
 
@@ -794,7 +858,7 @@ class Gen:
                  rev=True, qscale=False, dma_pv=0, dma_pv_spacing=16, budget_pv=None, lcheck=None, dtype="bf16",
                  hd=128, short_first=False, ragged=False):
         global DMA_COST
-        assert not (ragged and causal), "ragged key counts: the non-causal program only"
+        assert not (ragged and causal and not rev), "ragged causal: the pair-walk program (rev=True)"
         RAGGED[0] = bool(ragged)
         SHORTFIRST[0] = bool(short_first)
         assert not (short_first and rev and causal), "short_first streams both blocks forward (rev=False)"
@@ -886,7 +950,7 @@ class Gen:
                 e([I("v_add_u32", t[5], rb, t[2]), I("v_mul_lo_u32", t[5], t[5], st),
                    I("v_add_u32", t[5], t[5], t[3]), I("v_add_u32", dst, sT5, t[5])])
         e(load_args())
-        if RAGGED[0]:
+        if RAGGED[0] and not self.causal:
             # PM(kb, hh): keep the half whose key 16 kb + 4 g + 2 hh (+1) >= P0
             e([I("v_lshlrev_b32", T(0), 2, VG), I("v_mov_b32", T(4), 0xFFFF), I("v_mov_b32", T(5), 0xFFFF0000)])
             for kb in range(4):
@@ -924,7 +988,7 @@ class Gen:
         so the load row is min(max(q', s) - s, Nq - 1)"""
         c = [I("s_sub_u32", sT0, ARG(AI["nq"]), 1)]
         if self.causal:
-            c += qshift(sT1)
+            c += qshift(sT1, sT2)
         for qb in range(4):
             c += [I("v_add_u32", T(0), q0, VI), I("v_add_u32", T(0), 16 * qb, T(0))]
             if self.causal:
@@ -971,8 +1035,15 @@ class Gen:
             # block (the stream is at position 2: one tile back in either
             # order), a one-tile stream that repeats
             c = [I("s_sub_u32", sNXK[0], sDK[0], sTBK), I("s_subb_u32", sNXK[1], sDK[1], 0),
-                 I("s_sub_u32", sNXV[0], sDV[0], sTBV), I("s_subb_u32", sNXV[1], sDV[1], 0),
-                 I("s_mov_b32", sNXIDX, 0), I("s_mov_b32", sNXNT, 1),
+                 I("s_sub_u32", sNXV[0], sDV[0], sTBV), I("s_subb_u32", sNXV[1], sDV[1], 0)]
+            if RAGGED[0]:
+                # a forward block's position 1 may be key tile NT - 1, whose
+                # unshifted rows run past the head: park on tile 0 instead
+                c += [I("s_cmp_eq_u32", sDIR, 0), I("s_cselect_b32", sT2, sTBK, 0),
+                      I("s_sub_u32", sNXK[0], sNXK[0], sT2), I("s_subb_u32", sNXK[1], sNXK[1], 0),
+                      I("s_cmp_eq_u32", sDIR, 0), I("s_cselect_b32", sT2, sTBV, 0),
+                      I("s_sub_u32", sNXV[0], sNXV[0], sT2), I("s_subb_u32", sNXV[1], sNXV[1], 0)]
+            c += [I("s_mov_b32", sNXIDX, 0), I("s_mov_b32", sNXNT, 1),
                  I("s_add_u32", sT2, sL, ARG(AI["G"])), I("s_cmp_ge_u32", sT2, ARG(AI["nblocks"])),
                  I("s_cbranch_scc1", skip),
                  I("s_add_u32", sT7, sL, ARG(AI["G"]))]
@@ -1034,10 +1105,10 @@ class Gen:
             skip = Lb(f"nomask{self.new_uid()}")
             e(self.tile_of(sT0, 0))
             e([I("s_cmp_lt_u32", sT0, sTD), I("s_cbranch_scc1", skip)])
-            e(mask_tile(sT0))
+            e(self.mask_rt(sT0))
             e([label(skip)])
         elif self.causal:
-            e(mask_tile(0))
+            e(self.mask_rt(0))
         # exact row max -> mu = max * c + muoff; P(0) into state 0
         for qb in range(4):
             e(row_max(qb, T(20 + qb), T(30), T(31)))
@@ -1085,6 +1156,26 @@ class Gen:
                     n += 1
         return c
 
+    def mask_rt(self, tile):
+        """causal, straight line (prologue and rare path): the mask of the
+        tile whose index is in `tile` (SGPR or 0); RAGGED: key tile NT - 1
+        holds shifted keys and takes the rag mask (or all -inf when the
+        wave's diagonal is before it)"""
+        if not RAGGED[0]:
+            return mask_tile(tile)
+        u = self.new_uid()
+        normal, allinf, done = self.L(f"mnorm{u}"), self.L(f"minf{u}"), self.L(f"mdone{u}")
+        c = [I("s_sub_u32", sT6, ARG(AI["nt"]), 1), I("s_cmp_eq_u32", tile, sT6), I("s_cbranch_scc0", normal),
+             I("s_cmp_lt_u32", sTD, sT6), I("s_cbranch_scc1", allinf)]
+        c += rag_setup()
+        for qb in range(4):
+            for kb in range(4):
+                c += rag_block(kb, qb)
+        c += [I("s_branch", done), label(allinf)]
+        c += [I("v_mov_b32", S_(kb, qb)[r], NINF[0]) for qb in range(4) for kb in range(4) for r in range(4)]
+        c += [I("s_branch", done), label(normal)] + mask_tile(tile) + [label(done)]
+        return c
+
     def tile_of(self, dst, pos):
         """causal: the key tile at stream position pos (SGPR or 0) of the
         current block: pos, or reversed (sDIR) nt-4+pos for pos < 4 and
@@ -1112,13 +1203,22 @@ class Gen:
         if self.rev:
             e(self.tile_of(sT0, sT))
             tl = sT0
+        rg, by = Lb(f"rag{u}"), Lb(f"beyond{u}")
+        if RAGGED[0]:
+            # key tile NT - 1 holds keys Nk - 64 .. Nk - 1: the rag step (a
+            # VALU mask on the shifted keys) unless the wave's diagonal is
+            # before it (then every score is masked: the beyond step)
+            e([I("s_sub_u32", sT2, ARG(AI["nt"]), 1), I("s_cmp_eq_u32", tl, sT2), I("s_cbranch_scc1", rg)])
         e([I("s_cmp_lt_u32", tl, sTD), I("s_cbranch_scc1", n), I("s_cmp_eq_u32", tl, sTD),
-           I("s_cbranch_scc1", d)])
+           I("s_cbranch_scc1", d)] + ([label(by)] if RAGGED[0] else []))
         self.step(X, "beyond")
         e([I("s_branch", cont), label(n)])
         self.step(X, None)
         e([I("s_branch", cont), label(d)])
         self.step(X, "diag")
+        if RAGGED[0]:
+            e([I("s_branch", cont), label(rg), I("s_cmp_lt_u32", sTD, sT2), I("s_cbranch_scc1", by)])
+            self.step(X, "rag")
         e([label(cont)])
 
     def check(self, Xc, rare_block):
@@ -1179,8 +1279,20 @@ class Gen:
         z = Fill(I("v_mov_b32", ACC(X), 0), 4, tag="zero")
         if not LCHECK[0]:
             fills.append(z)
+        rag = {}
+        if mask == "rag":
+            # key tile NT - 1 (shifted keys): S(kb, qb) masked by VALU as it
+            # completes, before its softmax slices read it
+            rsetup = Fill(rag_setup(), 8, earliest=0, tag="ragsetup")
+            fills.append(rsetup)
+            for qb in range(4):
+                for kb in range(4):
+                    rag[(kb, qb)] = Fill(rag_block(kb, qb), 16, deps=[rsetup], sep=1, earliest=done(kb, qb) + 3,
+                                         tag="ragmask")
+                    fills.append(rag[(kb, qb)])
         f_now, cvn, last_or = softmax_fills(X, now, lambda qb, kb: done(kb, qb) + 3, ytag=len(dfr),
-                                            prev_cv=cvd)
+                                            prev_cv=cvd,
+                                            extra_deps=(lambda qb, kb: [rag[(kb, qb)]]) if rag else None)
         now_groups = softmax_fills.groups
         if "soft" in ABL:
             f_now, now_groups = [], []
@@ -1193,7 +1305,7 @@ class Gen:
         body, left = schedule(qk, fills, self.budget)
         e(body)
         # everything of tile t-1 must be done before its check
-        pend_prev = [f for f in left if f in f_def or f.tag.startswith("dma")]
+        pend_prev = [f for f in left if f in f_def or f.tag.startswith("dma") or f.tag.startswith("rag")]
         # a slice of tile t that has started finishes before the check: the
         # rare path redoes every P of t from S, and a slice whose fma ran
         # with the old mu must not write its P after that
@@ -1233,7 +1345,7 @@ class Gen:
         e([I("v_add_u32", VVA, sSM1, VVL)])
         f_def, _, _ = softmax_fills(X, dfr, lambda qb, kb: 0, ytag=0)
         e(drain(f_def, 0))
-        if RAGGED[0]:
+        if RAGGED[0] and not self.causal:
             e(p_mask(X))
         if LCHECK[0]:
             e(rowsum_mfmas(X))
@@ -1258,7 +1370,7 @@ class Gen:
         for qb in range(4):
             e([I("v_rcp_f32", T(20 + qb), L_(qb)[0])])
         if self.causal:
-            e(qshift(sT1))
+            e(qshift(sT1, sT2))
         for qb in range(4):
             # O offsets and the row mask of this q-block (causal: the real
             # row q' - s; a virtual row below s wraps and is not stored)
@@ -1325,12 +1437,12 @@ class Gen:
                     e([I("s_sub_u32", sT0, sT, 1)])
                     if self.rev:
                         e(self.tile_of(sT0, sT0))
-                    e(mask_tile(sT0))
+                    e(self.mask_rt(sT0))
                 elif self.rev:
                     e(self.tile_of(sT0, sT))
-                    e(mask_tile(sT0))
+                    e(self.mask_rt(sT0))
                 else:
-                    e(mask_tile(sT))
+                    e(self.mask_rt(sT))
             if Xs == X:
                 for qb in range(4):
                     m = T(20 + qb)
@@ -1348,7 +1460,7 @@ class Gen:
                                I("v_accvgpr_write_b32", O_(db, qb)[r], T(25))])
                     e([I("v_mul_f32", L_(qb)[r], L_(qb)[r], T(24)) for r in range(4)])
                 e(exps_all(X))
-                if RAGGED[0] and name.startswith("rare_t"):  # the last tile
+                if RAGGED[0] and not self.causal and name.startswith("rare_t"):  # the last tile
                     e(p_mask(X))
                 if LCHECK[0]:  # its new sums (the step's row sums of this tile already ran)
                     e(rowsum_mfmas(X))

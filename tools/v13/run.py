@@ -42,7 +42,7 @@ def args_for(qa, ka, va, oa, B, H, Hkv, Nq, Nk, strides_el, scale, G, muoff=7.0,
     st = [2 * s for s in strides_el]
     # causal: rows are virtual, shifted by s = (-Nq) & 63 so the diagonal sits
     # on 64-key tile boundaries (launch_attn_v13)
-    Nqv = Nq + ((-Nq) & 63) if causal else Nq
+    Nqv = Nq + ((Nk - Nq) & 63) if causal else Nq
     qblocks = -(-Nqv // 256)
     nblocks = B * H * qblocks
     group = H // Hkv
@@ -64,6 +64,9 @@ def args_for(qa, ka, va, oa, B, H, Hkv, Nq, Nk, strides_el, scale, G, muoff=7.0,
         d["cw"] = walk | (lg8 << 8) | (lghq << 16) | (per << 24)
         d["hx"] = hx
         d["offt"] = (Nk - Nqv) // 64
+        if Nk % 64:  # ragged causal: P0 in the top byte of hx
+            assert d["hx"] < (1 << 24)
+            d["hx"] |= (64 - Nk % 64) << 24
     elif Nk % 64:
         d["cw"] = 64 - Nk % 64  # ragged: keys of the last (shifted) tile already counted
     d["c"] = struct.unpack("<I", struct.pack("<f", scale * 1.4426950408889634))[0]
@@ -94,8 +97,8 @@ def run(q, k, v, scale=None, grid=None, muoff=7.0, layout="bhsd", causal=False, 
     B, H, Nq, D = q.shape
     Hkv, Nk = k.shape[1], k.shape[2]
     ragged = Nk % 64 != 0
-    assert D in (64, 128) and (Nk >= 128 if not ragged else Nk > 64 and not causal)
-    assert not causal or (Nk - Nq >= 0 and Nk % 64 == 0)
+    assert D in (64, 128) and (Nk >= 128 if not ragged else Nk > 64)
+    assert not causal or Nk - Nq >= 0
     if ragged:
         kw = dict(kw, ragged=True)
     scale = 1.0 / math.sqrt(D) if scale is None else scale
@@ -117,7 +120,7 @@ def run(q, k, v, scale=None, grid=None, muoff=7.0, layout="bhsd", causal=False, 
     va, sv = put(v, layout)
     oa = heap.alloc(B * H * Nq * D * 2 + 256)
     so = (Nq * H * D, D, H * D) if layout == "bshd" else (H * Nq * D, Nq * D, D)
-    qblocks = -(-(Nq + ((-Nq) & 63 if causal else 0)) // 256)
+    qblocks = -(-(Nq + ((Nk - Nq) & 63 if causal else 0)) // 256)
     nb = B * H * qblocks
     G = nb if grid is None else grid
     if causal and pair_walk(nb, qblocks, G)[0] != 1:
