@@ -351,8 +351,8 @@ int pli_attn_decode_dev(const void* q, const void* k, const void* v, void* o,
  *   for bf16 and fp16 (attn_fwd_v13h, the f16 MFMA) D = 128 / 64 with Nk a
  *   multiple of 64 from 128, or any Nk > 64 (attn_fwd_v13r / v13hr: the last
  *   key tile fetched from key Nk - 64, its overlap masked in P); 83 / 84 /
- *   85 the causal forms (83 = causal default where Nk % 64 == 0, any
- *   Nq <= Nk; other shapes take 74 / 60).  Prescaled variants round Q * scale * log2(e) to
+ *   85 the causal forms (83 = causal default for any Nq <= Nk and Nk > 64,
+ *   ragged Nk on attn_fwd_v13rc / v13hrc; other shapes take 74 / 60).  Prescaled variants round Q * scale * log2(e) to
  *   the 16-bit input type (2^-9 relative score error in bf16).  The v13
  *   forms, v12 and the exact v7 / v10 bodies (51 / 55 / 60) take any
  *   scale > 0; the prescaled 50 / 54 take scale * log2(e) <= 1 (larger

@@ -538,13 +538,13 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
 //  81: variant 80 with one block per workgroup
 //  82: variant 80 with mu = max * c (P = 1 at the max, so every row's l >= 1
 //      and the rare path runs at every tile): tests only
-//  83 / 84: attn_fwd_v13c causal (bottom-right, Nq <= Nk, Nk % 64 == 0;
-//      any diagonal offset since round 5 -- virtual rows): 83 persistent (the pair walk where it tiles the grid), 84 one
+//  83 / 84: attn_fwd_v13c causal (bottom-right, Nq <= Nk; any diagonal
+//      offset -- virtual rows -- and ragged Nk -- attn_fwd_v13rc -- since
+//      round 5): 83 persistent (the pair walk where it tiles the grid), 84 one
 //      block per workgroup heaviest first; 85 = 83 with mu = max * c
 // default since round 4: attn_fwd_v13 (80), 1388 vs 1242 TF/s for v12 (71)
 // at B8 S4096 H32 D128 in the same process (profiles/r04/flash/ab.log); where
-// v13 does not apply (D not 64 / 128, Nk <= 64, causal with Nk % 64) it
-// routes to 71 / 74
+// v13 does not apply (D not 64 / 128, Nk <= 64) it routes to 71 / 74
 constexpr int kDefaultVariant = 80;
 // v13's mu = row max * c + PLI_V13_MUOFF (log2 units): P <= 2^-MUOFF right
 // after a max is taken and a tile takes the rescale path once some row's sum l
@@ -581,7 +581,7 @@ constexpr int kDefaultVariant = 80;
 // vs 830 (profiles/r03/flash/ab_causal.log); the pair walk: 1049 at B8 S4096,
 // 1154 at B2 S8192, 1223 at B1 H64 S16384 (ab_causal_pair.log)
 // causal default since round 4: attn_fwd_v13c (83), 1210 vs 1058 TF/s for
-// 74 (profiles/r04/flash/ab_causal.log); Nk % 64 != 0 etc. -> 74
+// 74 (profiles/r04/flash/ab_causal.log); Nk <= 64 etc. -> 74
 constexpr int kDefaultCausalVariant = 83;
 
 template <typename T, int D>

@@ -1,8 +1,8 @@
 // attn_fwd_v13: flash-attention forward on v_mfma_f32_16x16x32_bf16
 // (reference ch06/flash_attention.py:14-74; gfx950, bf16 / fp16, D = 128 /
 // 64, Nk a multiple of 64 and >= 128 or -- attn_fwd_v13r -- any Nk > 64;
-// causal -- bottom-right, Nk % 64 == 0, any Nq <= Nk -- as the second
-// program attn_fwd_v13c; other cases take v12 / v10).
+// causal -- bottom-right, any Nq <= Nk -- as attn_fwd_v13c / v13rc; other
+// cases take v12 / v10).
 //
 // One wave per SIMD, 64 query rows per wave (4 q-blocks of 16), persistent
 // workgroups of 4 waves walking 256-row blocks.  The body is ONE generated
