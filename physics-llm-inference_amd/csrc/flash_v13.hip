@@ -143,7 +143,8 @@ void put64(V13Args& a, int at, uint64_t v) {
 #ifdef PLI_FLASH_STAMPS
 // diagnostic build only (tools/build_diag.sh): the same program with
 // s_memtime / s_memrealtime at each wave's entry and exit (8 dwords per wave
-// at args.stamp + 32 * (workgroup * 4 + wave))
+// at args.stamp + 128 * (workgroup * 4 + wave); lanes 15-21: the seam sums of
+// tools/v13/kernel.py Gen.seam_stamp)
 #include "flash_v13_stamp_asm.h"
 __global__ __launch_bounds__(256, 1) void attn_fwd_v13_stamp(V13Args args) {
     __shared__ __attribute__((aligned(1024))) char smem[163840];

@@ -200,7 +200,8 @@ SGPR_SKIP = (32,)
 M0SAVE = (V(217), 63)  # m0 is saved in lane 63 of v217 (the stamp build's record: lanes 0-8) and restored at exit
 
 # kernel argument dwords (V13Args in csrc/flash_v13.hip)
-# (dwords 0..36 are reloaded into s56..s92 at every block transition; 37..
+# (dwords 0..36 are reloaded into s56..s92 at every block transition -- no
+# instruction writes them, and dropping the reload was measured level; 37..
 # are read at init or by a single s_load where needed).  "shifts" packs the
 # three magic-division shifts and the head count: shq | shh << 5 | shg << 10
 # | H << 16 (SALU shifts read bits 4:0 of their count)
@@ -969,6 +970,9 @@ class Gen:
             e([I("v_writelane_b32", STAMPV, S(96 + k), k) for k in range(4)])
             e([I("s_lshl_b32", sT6, sL, 2), I("s_lshr_b32", sT7, sWKOFF, WSH()), I("s_add_u32", sT6, sT6, sT7),
                I("v_writelane_b32", STAMPV, sT6, 8)])
+            # seam sums (lanes 16-21) from 0, the last point (lane 15) = entry
+            e([I("v_writelane_b32", STAMPV, 0, 16 + k) for k in range(6)] +
+              [I("v_writelane_b32", STAMPV, S(96), 15)])
         # ones selector, ring slots, causal mask operands
         e([I("v_mov_b32", ONES[k], DT["ones"]) for k in range(4)])
         e([I("s_mov_b32", sS0, 0), I("s_mov_b32", sSP1, SLOT), I("s_mov_b32", sSP2, 2 * SLOT),
@@ -1081,14 +1085,18 @@ class Gen:
         epilogue; the walk to the next block"""
         e, Lb = self.emit, self.L
         e([label(Lb("common"))])
+        e(self.seam_stamp(3))
         e([I("s_load_dword", sT8, sKA, 4 * AI["muoff"])])
         if self.causal:
             e([I("s_lshr_b32", sTD, sCQ0, 6), I("s_add_u32", sTD, sTD, sOFFT)])  # the wave's diagonal tile
+        # (zeroing O and l in QK(0)'s gaps instead: level -- the gaps it frees
+        # here it takes from QK(0); profiles/r05/flash/seam/)
         e([I("v_accvgpr_write_b32", A(k), 0) for k in range(16 * NDB())])  # O
         e([I("v_mov_b32", L_(qb)[r], 0) for qb in range(4) for r in range(4)])
         if not LCHECK[0]:
             e([I("v_mov_b32", ACC(0), 0), I("v_mov_b32", ACC(1), 0)])
         e([I("s_waitcnt", "vmcnt(0)"), I("s_barrier")])
+        e(self.seam_stamp(4))
         if QSCALE[0]:
             e(self.q_prescale())
         # tile 0: K(0) fragments, QK(0) with tile 2's DMA beside it
@@ -1122,6 +1130,7 @@ class Gen:
         e([I("s_waitcnt", f"vmcnt({NPW()})"), I("s_barrier"), I("v_add_u32", VKA, sSP1, VKL)])
         e(k_reads())
         e([I("s_mov_b32", sT, 1)])
+        e(self.seam_stamp(5))
         # steps t = 1 .. nt-1, two per iteration (P states 1 / 0)
         e([label(Lb("loop"))])
         self.step_dispatch(1)
@@ -1155,6 +1164,19 @@ class Gen:
                           I("v_cvt_pk_bf16_f32", t0, t1, t2), I("v_accvgpr_write_b32", a, t0)]
                     n += 1
         return c
+
+    def seam_stamp(self, k):
+        """STAMP build: s_memtime now; lane 16 + k of STAMPV += now - (lane
+        15), lane 15 = now (cycles since the previous seam point; points: 0
+        tail start, 1 epilogue, 2 after the O stores, 3 the next block's
+        common code, 4 after its first barrier, 5 the tile loop).  Uses
+        s96..s99 (free at every point)"""
+        if not self.stamp:
+            return []
+        return [I("s_memtime", S(96, 2)), I("s_waitcnt", "lgkmcnt(0)"),
+                I("v_readlane_b32", S(98), STAMPV, 15), I("s_sub_u32", S(99), S(96), S(98)),
+                I("v_readlane_b32", S(98), STAMPV, 16 + k), I("s_add_u32", S(98), S(98), S(99)),
+                I("v_writelane_b32", STAMPV, S(98), 16 + k), I("v_writelane_b32", STAMPV, S(96), 15)]
 
     def mask_rt(self, tile):
         """causal, straight line (prologue and rare path): the mask of the
@@ -1340,6 +1362,7 @@ class Gen:
         """last tile T (state X): its deferred slices, its check, PV(T) with
         the next block's Q loads beside it"""
         e = self.emit
+        e(self.seam_stamp(0))
         dfr, _ = self.deferred()
         e(rotate_slots())
         e([I("v_add_u32", VVA, sSM1, VVL)])
@@ -1366,6 +1389,7 @@ class Gen:
     # ---- epilogue ---------------------------------------------------------
     def epilogue(self):
         e, Lb = self.emit, self.L
+        e(self.seam_stamp(1))
         e([I("s_nop", 7), I("s_nop", 7)])
         for qb in range(4):
             e([I("v_rcp_f32", T(20 + qb), L_(qb)[0])])
@@ -1381,20 +1405,36 @@ class Gen:
                I("v_and_b32", T(26), 1, VG), I("v_lshlrev_b32", T(26), 5, T(26)),
                I("v_lshrrev_b32", T(27), 1, VG), I("v_lshlrev_b32", T(27), 4, T(27)),
                I("v_add3_u32", OOFF(qb), T(25), T(26), T(27))])
+            # packed words of the q-block (W = Y for odd q-blocks, so the next
+            # q-block's packing leaves the data of stores in flight alone, was
+            # measured level: profiles/r05/flash/seam/)
+            W = T
             for dbp in range(NDB() // 2):
-                w = 4 * dbp  # words T(w) .. T(w+3)
+                w = 4 * dbp  # words W(w) .. W(w+3)
                 for half, db in enumerate((2 * dbp, 2 * dbp + 1)):
-                    for r in range(4):
-                        e([I("v_accvgpr_read_b32", T(28 + r), O_(db, qb)[r])])
+                    if "epi_read" not in ABL:  # (timing-only A/B knobs: epi_read / epi_perm / epi_store)
+                        for r in range(4):
+                            e([I("v_accvgpr_read_b32", T(28 + r), O_(db, qb)[r])])
                     for r in range(4):
                         e([I("v_mul_f32", T(28 + r), T(28 + r), T(20 + qb))])
-                    e([I(DT["cvt"], T(w + 2 * half), T(28), T(29)),
-                       I(DT["cvt"], T(w + 2 * half + 1), T(30), T(31))])
-                e([I("v_permlane16_swap_b32", T(w), T(w + 2)), I("v_permlane16_swap_b32", T(w + 1), T(w + 3))])
+                    e([I(DT["cvt"], W(w + 2 * half), T(28), T(29)),
+                       I(DT["cvt"], W(w + 2 * half + 1), T(30), T(31))])
+                if "epi_perm" not in ABL:
+                    e([I("v_permlane16_swap_b32", W(w), W(w + 2)), I("v_permlane16_swap_b32", W(w + 1), W(w + 3))])
             e([I("v_cmp_gt_u32_e32", VCC, ARG(AI["nq"]), T(24)), I("s_and_saveexec_b64", S(sT2.i, 2), VCC)])
+            if "epi_fullline" in ABL:
+                # timing only (wrong layout): each store covers 4 rows x 256 B
+                # (whole 128-B lines), lane l -> row 4 dbp + l / 16, chunk l % 16
+                e([I("v_lshrrev_b32", T(25), 4, LANE), I("v_add_u32", T(25), sCQ0, T(25)),
+                   I("v_add_u32", T(25), 16 * qb, T(25)), I("v_mul_lo_u32", T(25), T(25), ARG(AI["on"])),
+                   I("v_and_b32", T(26), 15, LANE), I("v_lshlrev_b32", T(26), 4, T(26)),
+                   I("v_add_u32", OOFF(qb), T(25), T(26))])
             for dbp in range(NDB() // 2):
-                e([I("global_store_dwordx4", OOFF(qb), V(T(4 * dbp).i, 4), sCOH, mods=f"offset:{64 * dbp}")])
+                if "epi_store" not in ABL:
+                    off = 64 * dbp if "epi_fullline" not in ABL else 0
+                    e([I("global_store_dwordx4", OOFF(qb), V(W(4 * dbp).i, 4), sCOH, mods=f"offset:{off}")])
             e([I("s_mov_b64", EXEC, S(sT2.i, 2))])
+        e(self.seam_stamp(2))
         # next block
         if self.rev:
             e([I("s_add_u32", sT2, sL, ARG(AI["G"])), I("s_cmp_ge_u32", sT2, ARG(AI["nblocks"])),
@@ -1488,9 +1528,9 @@ class Gen:
             e([I("s_memtime", S(96, 2)), I("s_memrealtime", S(98, 2)), I("s_waitcnt", "lgkmcnt(0)")])
             e([I("v_writelane_b32", STAMPV, S(96 + k), 4 + k) for k in range(4)])
             e([I("v_readlane_b32", sT6, STAMPV, 8), I("s_load_dwordx2", S(88, 2), sKA, 4 * AI["stamp"]),
-               I("s_waitcnt", "lgkmcnt(0)"), I("s_lshl_b32", sT6, sT6, 5),
+               I("s_waitcnt", "lgkmcnt(0)"), I("s_lshl_b32", sT6, sT6, 7),
                I("v_lshlrev_b32", T(0), 2, LANE), I("v_add_u32", T(0), sT6, T(0)),
-               I("s_mov_b64", EXEC, 0xFF), I("global_store_dword", T(0), STAMPV, S(88, 2)),
+               I("s_mov_b64", EXEC, 0xFFFFFFFF), I("global_store_dword", T(0), STAMPV, S(88, 2)),
                I("s_mov_b64", EXEC, -1), I("s_waitcnt", "vmcnt(0)")])
         e([I("s_branch", Lb("exit"))])
         for X in (0, 1):

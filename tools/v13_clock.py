@@ -44,10 +44,10 @@ for rep in range(3):
         ms = s.elapsed_time(e) / 20
         out[f"v{var}_TFLOP/s"] = round(flops / ms / 1e9, 1)
         if var == 80:
-            stamps = torch.zeros(256 * 4 * 8, dtype=torch.int32, device="cuda")
+            stamps = torch.zeros(256 * 4 * 32, dtype=torch.int32, device="cuda")
             assert lib.pli_diag_v13_clock(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), B, H, N,
                                           stamps.data_ptr()) == 0
-            st = stamps.cpu().numpy().view(np.uint32).reshape(-1, 8).astype(np.uint64)
+            st = stamps.cpu().numpy().view(np.uint32).reshape(-1, 32)[:, :8].astype(np.uint64)
             t0 = st[:, 0] | (st[:, 1] << 32)
             r0 = st[:, 2] | (st[:, 3] << 32)
             t1 = st[:, 4] | (st[:, 5] << 32)
