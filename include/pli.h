@@ -10,6 +10,11 @@
  *   - device pointers must be 16-byte aligned for the vectorised kernels;
  *     misaligned / oddly strided operands are routed to the generic kernels.
  *   - strides are in ELEMENTS; the innermost (head_dim / K) stride is 1.
+ *   - empty operands: a pointer to an operand with zero elements may be NULL
+ *     (torch hands out a NULL data_ptr for empty tensors).  A call whose
+ *     output is empty does nothing and returns PLI_OK; an empty reduction
+ *     (no keys, K == 0) writes what torch gives for it (O = 0, C = bias or
+ *     0, y = 0).
  *   - return value: PLI_OK (0), a hipError_t code (1..999) from the launch,
  *     or one of the PLI_E* codes below.  pli_last_error() returns a
  *     thread-local message for the last failing call on this thread.
@@ -69,11 +74,11 @@ const char* pli_last_error(void);
  * causal != 0 masks key j for query i when j > i + (n_kv - n_q)
  * (bottom-right aligned, = torch.triu(ones, diagonal=1) when n_q == n_kv).
  * dtype: PLI_BF16 / PLI_F16 with head_dim 64 or 128 run the MFMA kernels --
- * attn_fwd_v13 (one generated program per dtype x head_dim x causal form)
- * where n_kv >= 128 and n_kv % 64 == 0 (causal: (n_kv - n_q) % 64 == 0),
- * else attn_fwd_v12 / v10; PLI_F32 (and any other head_dim <= 256) the
- * generic fp32-accumulate kernel.  Softmax statistics are fp32 regardless
- * of dtype.
+ * attn_fwd_v13 (one generated program per dtype x head_dim x causal x
+ * whole / ragged key tiles) where n_kv > 64 (causal: n_q <= n_kv, any
+ * diagonal offset), else attn_fwd_v12 / v10; PLI_F32 (and any other
+ * head_dim <= 256) the generic fp32-accumulate kernel.  Softmax statistics
+ * are fp32 regardless of dtype.  n_kv == 0 gives O = 0.
  */
 int pli_flash_attn_fwd(const void* q, const void* k, const void* v, void* o,
                        int batch, int heads, int kv_heads, int n_q, int n_kv,

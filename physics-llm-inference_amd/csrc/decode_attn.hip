@@ -451,11 +451,13 @@ extern "C" int pli_kv_append(const void* k_new, const void* v_new, void* k_cache
                              void* stream) {
     using namespace pli;
     clear_error();
-    PLI_REQUIRE(k_new && v_new && k_cache && v_cache && strides && pos_dev,
-                "pli_kv_append: null pointer");
     PLI_REQUIRE(batch >= 0 && n_new >= 0 && kv_heads > 0 && head_dim > 0 && capacity >= 0,
                 "pli_kv_append: bad shape B=%d T=%d Hkv=%d D=%d cap=%d", batch, n_new, kv_heads,
                 head_dim, capacity);
+    // nothing to append: the (possibly NULL, pli.h) operands are not read
+    if (batch == 0 || n_new == 0) return PLI_OK;
+    PLI_REQUIRE(k_new && v_new && k_cache && v_cache && strides && pos_dev,
+                "pli_kv_append: null pointer");
     PLI_REQUIRE(dtype == PLI_F16 || dtype == PLI_BF16, "pli_kv_append: dtype %d (16-bit caches only)",
                 dtype);
     PLI_REQUIRE(head_dim % 8 == 0 && aligned16(k_new) && aligned16(v_new) && aligned16(k_cache) &&
@@ -502,7 +504,6 @@ extern "C" int pli_attn_decode_variant(const void* q, const void* k, const void*
                                        int dtype, void* stream, int mode, int target_wgs) {
     using namespace pli;
     clear_error();
-    PLI_REQUIRE(q && k && v && o && strides, "pli_attn_decode: null pointer");
     PLI_REQUIRE(batch >= 0 && heads > 0 && kv_heads > 0 && n_q >= 0 && n_kv >= 0 && head_dim > 0,
                 "pli_attn_decode: bad shape B=%d H=%d Hkv=%d Nq=%d Nk=%d D=%d", batch, heads,
                 kv_heads, n_q, n_kv, head_dim);
@@ -513,7 +514,13 @@ extern "C" int pli_attn_decode_variant(const void* q, const void* k, const void*
     PLI_REQUIRE(std::isfinite(scale), "pli_attn_decode: non-finite scale");
     PLI_REQUIRE(!causal || n_q <= n_kv || n_kv == 0,
                 "pli_attn_decode: causal needs n_q (%d) <= n_kv (%d)", n_q, n_kv);
+    // empty operands may be NULL (pli.h); an empty cache gives O = 0, written
+    // by the prefill path's generic kernel (it reads no K / V)
     if (batch == 0 || n_q == 0) return PLI_OK;
+    PLI_REQUIRE(q && o && strides && (n_kv == 0 || (k && v)), "pli_attn_decode: null pointer");
+    if (n_kv == 0)
+        return pli_flash_attn_fwd(q, k, v, o, batch, heads, kv_heads, n_q, n_kv, head_dim, strides,
+                                  scale, causal, dtype, stream);
     const bool fast = decode_fast_path(heads, kv_heads, n_q, n_kv, head_dim, dtype, strides) &&
                       aligned16(q) && aligned16(k) && aligned16(v) && aligned16(o);
     // many query rows per kv head (or shapes the decode tile does not take):
@@ -555,13 +562,13 @@ extern "C" int pli_attn_decode_dev(const void* q, const void* k, const void* v, 
                                    size_t workspace_bytes, int dtype, void* stream) {
     using namespace pli;
     clear_error();
-    PLI_REQUIRE(q && k && v && o && strides && n_kv_dev, "pli_attn_decode_dev: null pointer");
     PLI_REQUIRE(batch >= 0 && heads > 0 && kv_heads > 0 && n_q >= 0 && n_kv_max >= 0 &&
                     head_dim > 0 && heads % kv_heads == 0,
                 "pli_attn_decode_dev: bad shape B=%d H=%d Hkv=%d Nq=%d Nmax=%d D=%d", batch, heads,
                 kv_heads, n_q, n_kv_max, head_dim);
     PLI_REQUIRE(std::isfinite(scale), "pli_attn_decode_dev: non-finite scale");
     if (batch == 0 || n_q == 0) return PLI_OK;
+    PLI_REQUIRE(q && k && v && o && strides && n_kv_dev, "pli_attn_decode_dev: null pointer");
     if (!(decode_fast_path(heads, kv_heads, n_q, n_kv_max, head_dim, dtype, strides) &&
           aligned16(q) && aligned16(k) && aligned16(v) && aligned16(o))) {
         set_error("pli_attn_decode_dev: needs bf16/fp16, head_dim 64/128, <= 16 rows per kv "

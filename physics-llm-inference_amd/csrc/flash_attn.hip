@@ -692,7 +692,6 @@ extern "C" int pli_flash_attn_fwd_variant(const void* q, const void* k, const vo
                                           int causal, int dtype, void* stream, int variant) {
     using namespace pli;
     clear_error();
-    PLI_REQUIRE(q && k && v && o && strides, "pli_flash_attn_fwd: null pointer");
     PLI_REQUIRE(batch >= 0 && heads > 0 && kv_heads > 0 && n_q >= 0 && n_kv >= 0 && head_dim > 0,
                 "pli_flash_attn_fwd: bad shape B=%d H=%d Hkv=%d Nq=%d Nk=%d D=%d", batch, heads,
                 kv_heads, n_q, n_kv, head_dim);
@@ -701,7 +700,10 @@ extern "C" int pli_flash_attn_fwd_variant(const void* q, const void* k, const vo
     PLI_REQUIRE(dtype == PLI_F32 || dtype == PLI_F16 || dtype == PLI_BF16,
                 "pli_flash_attn_fwd: bad dtype %d", dtype);
     PLI_REQUIRE(std::isfinite(scale), "pli_flash_attn_fwd: non-finite scale");
+    // empty operands may be NULL (pli.h): no output rows -> nothing to do; no
+    // keys -> O = 0 (the generic kernel reads no K / V)
     if (batch == 0 || n_q == 0) return PLI_OK;
+    PLI_REQUIRE(q && o && strides && (n_kv == 0 || (k && v)), "pli_flash_attn_fwd: null pointer");
     const AttnStrides st{strides[0], strides[1], strides[2], strides[3], strides[4], strides[5],
                          strides[6], strides[7], strides[8], strides[9], strides[10], strides[11]};
     const int group = heads / kv_heads;

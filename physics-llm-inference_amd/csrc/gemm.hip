@@ -2050,11 +2050,11 @@ static int swiglu_dispatch(const void* x, const void* wg, const void* wu, void* 
                            void* stream, void* ws, size_t ws_bytes, int variant) {
     using namespace pli;
     clear_error();
-    PLI_REQUIRE(x && wg && wu && h, "pli_gemm_swiglu: null pointer");
     PLI_REQUIRE(m >= 0 && n >= 0 && k >= 0, "pli_gemm_swiglu: bad shape m=%d n=%d k=%d", m, n, k);
     PLI_REQUIRE(dtype == PLI_F32 || dtype == PLI_F16 || dtype == PLI_BF16,
                 "pli_gemm_swiglu: bad dtype %d", dtype);
-    if (m == 0 || n == 0) return PLI_OK;
+    if (m == 0 || n == 0) return PLI_OK;  // (empty operands may be NULL, pli.h)
+    PLI_REQUIRE(h && (k == 0 || (x && wg && wu)), "pli_gemm_swiglu: null pointer");
     PLI_REQUIRE(ldx >= k && ldwg >= k && ldwu >= k && ldh >= n,
                 "pli_gemm_swiglu: leading dimension too small (ldx=%lld ldwg=%lld ldwu=%lld ldh=%lld)",
                 (long long)ldx, (long long)ldwg, (long long)ldwu, (long long)ldh);
@@ -2137,9 +2137,11 @@ static int gemm_dispatch(const void* a, const void* b, void* c, const void* bias
                          void* stream, int variant, void* ws, size_t ws_bytes) {
     using namespace pli;
     clear_error();
-    PLI_REQUIRE(a && b && c, "pli_gemm: null pointer");
     PLI_REQUIRE(m >= 0 && n >= 0 && k >= 0, "pli_gemm: bad shape m=%d n=%d k=%d", m, n, k);
+    // empty operands may be NULL (pli.h): no output -> nothing to do; K == 0
+    // -> C = bias (or 0), A and B not read
     if (m == 0 || n == 0) return PLI_OK;
+    PLI_REQUIRE(c && (k == 0 || (a && b)), "pli_gemm: null pointer");
     PLI_REQUIRE(lda >= k && ldc >= n && ldb >= (trans_b ? k : n),
                 "pli_gemm: leading dimension too small (lda=%lld ldb=%lld ldc=%lld)",
                 (long long)lda, (long long)ldb, (long long)ldc);
@@ -2331,12 +2333,12 @@ extern "C" int pli_gemm_f32out(const void* a, const void* b, float* c, int m, in
                                int64_t ldb, int dtype, void* stream) {
     using namespace pli;
     clear_error();
-    PLI_REQUIRE(a && b && c, "pli_gemm_f32out: null pointer");
     PLI_REQUIRE(m >= 0 && n >= 0 && k >= 0 && lda >= k && ldb >= k,
                 "pli_gemm_f32out: bad shape m=%d n=%d k=%d lda=%lld ldb=%lld", m, n, k, (long long)lda,
                 (long long)ldb);
     PLI_REQUIRE(dtype == PLI_BF16 || dtype == PLI_F16, "pli_gemm_f32out: bf16 / fp16 inputs only (%d)", dtype);
-    if (m == 0 || n == 0) return PLI_OK;
+    if (m == 0 || n == 0) return PLI_OK;  // (empty operands may be NULL, pli.h)
+    PLI_REQUIRE(c && (k == 0 || (a && b)), "pli_gemm_f32out: null pointer");
     hipStream_t s = (hipStream_t)stream;
     const bool lds = k % 64 == 0 && k > 0 && n % 32 == 0 && lda % 8 == 0 && ldb % 8 == 0 && al16(a) &&
                      al16(b) && al16(c);
@@ -2400,9 +2402,10 @@ static int grouped_dispatch(const void* x, const int32_t* gather, const void* co
                             int64_t ldc, int dtype, void* stream, int variant) {
     using namespace pli;
     clear_error();
-    PLI_REQUIRE(x && w_ptrs && c && offsets, "pli_gemm_grouped: null pointer");
     PLI_REQUIRE(experts > 0 && rows_bound >= 0 && n > 0 && k > 0,
                 "pli_gemm_grouped: bad shape E=%d rows=%d n=%d k=%d", experts, rows_bound, n, k);
+    if (rows_bound == 0) return PLI_OK;  // (empty operands may be NULL, pli.h)
+    PLI_REQUIRE(x && w_ptrs && c && offsets, "pli_gemm_grouped: null pointer");
     PLI_REQUIRE(dtype == PLI_BF16 || dtype == PLI_F16, "pli_gemm_grouped: bf16/fp16 only");
     PLI_REQUIRE(k % 128 == 0 && n % 16 == 0 && ldx % 8 == 0 && ldw % 8 == 0 && ldc % 8 == 0 &&
                     al16(x) && al16(c),

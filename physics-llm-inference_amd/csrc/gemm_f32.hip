@@ -179,10 +179,10 @@ extern "C" int pli_gemm_naive(const float* a, const float* b, float* c, int m, i
                               int64_t ldb, int64_t ldc, void* stream) {
     using namespace pli;
     clear_error();
-    PLI_REQUIRE(a && b && c, "pli_gemm_naive: null pointer");
     PLI_REQUIRE(m >= 0 && n >= 0 && k >= 0 && lda >= k && ldb >= n && ldc >= n,
                 "pli_gemm_naive: bad shape / leading dimensions");
-    if (m == 0 || n == 0) return PLI_OK;
+    if (m == 0 || n == 0) return PLI_OK;  // (empty operands may be NULL, pli.h)
+    PLI_REQUIRE(c && (k == 0 || (a && b)), "pli_gemm_naive: null pointer");
     hipLaunchKernelGGL(gemm_naive_f32, dim3(cdiv(n, 16), cdiv(m, 16)), dim3(256), 0, (hipStream_t)stream, a, b,
                        c, m, n, k, lda, ldb, ldc);
     return launch_status("gemm_naive_f32");

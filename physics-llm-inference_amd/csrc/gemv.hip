@@ -188,12 +188,22 @@ extern "C" int pli_gemv_variant(const void* w, const void* x, void* y, int m, in
                                 int dtype, void* stream, int variant) {
     using namespace pli;
     clear_error();
-    PLI_REQUIRE(w && x && y, "pli_gemv: null pointer");
     PLI_REQUIRE(m >= 0 && k >= 0 && ldw >= k, "pli_gemv: bad shape m=%d k=%d ldw=%lld", m, k,
                 (long long)ldw);
+    PLI_REQUIRE(dtype == PLI_F32 || dtype == PLI_F16 || dtype == PLI_BF16, "pli_gemv: bad dtype %d", dtype);
+    // empty operands may be NULL (pli.h): no rows -> nothing to do; K == 0 ->
+    // y = 0 (torch.mv of an m x 0 matrix), W and x not read
     if (m == 0) return PLI_OK;
-    PLI_REQUIRE(k > 0, "pli_gemv: k must be positive");
+    PLI_REQUIRE(y && (k == 0 || (w && x)), "pli_gemv: null pointer");
     hipStream_t s = (hipStream_t)stream;
+    if (k == 0) {
+        const hipError_t e = hipMemsetAsync(y, 0, (size_t)m * (dtype == PLI_F32 ? 4 : 2), s);
+        if (e != hipSuccess) {
+            set_error("pli_gemv: hipMemsetAsync: %s", hipGetErrorString(e));
+            return (int)e;
+        }
+        return PLI_OK;
+    }
     switch (dtype) {
         case PLI_F32: return launch<float>(w, x, y, m, k, ldw, s, variant);
         case PLI_F16: return launch<f16_t>(w, x, y, m, k, ldw, s, variant);

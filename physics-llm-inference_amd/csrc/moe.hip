@@ -130,7 +130,9 @@ extern "C" int pli_moe_route(const void* logits, int64_t ld_logits, int tokens, 
                              int32_t* workspace, void* stream) {
     using namespace pli;
     clear_error();
-    PLI_REQUIRE(logits && weights && expert_idx && pos && gather && offsets && workspace,
+    // (per-token operands are empty, and may be NULL (pli.h), when tokens == 0;
+    // offsets are still written: all zero)
+    PLI_REQUIRE(offsets && workspace && (tokens == 0 || (logits && weights && expert_idx && pos && gather)),
                 "pli_moe_route: null pointer");
     PLI_REQUIRE(tokens >= 0 && experts > 0 && experts <= 64 && top_k > 0 && top_k <= 8 &&
                     top_k <= experts && ld_logits >= experts,
@@ -175,12 +177,12 @@ extern "C" int pli_moe_combine(const void* y, int64_t ldy, const int32_t* pos, c
                                void* stream) {
     using namespace pli;
     clear_error();
-    PLI_REQUIRE(y && pos && weights && out, "pli_moe_combine: null pointer");
     PLI_REQUIRE(tokens >= 0 && top_k > 0 && hidden > 0 && hidden % 8 == 0 && ldy % 8 == 0 &&
                     ldo % 8 == 0 && ldy >= hidden && ldo >= hidden && aligned16(y) && aligned16(out),
                 "pli_moe_combine: bad shape / alignment (hidden %% 8 == 0, 16-byte rows)");
     PLI_REQUIRE(dtype == PLI_F16 || dtype == PLI_BF16, "pli_moe_combine: bf16/fp16 only");
-    if (tokens == 0) return PLI_OK;
+    if (tokens == 0) return PLI_OK;  // (empty operands may be NULL, pli.h)
+    PLI_REQUIRE(y && pos && weights && out, "pli_moe_combine: null pointer");
     hipStream_t s = (hipStream_t)stream;
     if (dtype == PLI_BF16)
         hipLaunchKernelGGL(moe_combine_kernel<bf16_t>, dim3((unsigned)tokens), dim3(256), 0, s,

@@ -148,13 +148,13 @@ extern "C" int pli_rmsnorm(const void* x, const void* residual, const void* weig
                            int64_t ldh, float eps, int dtype, void* stream) {
     using namespace pli;
     clear_error();
-    PLI_REQUIRE(x && weight && y, "pli_rmsnorm: null pointer");
     PLI_REQUIRE(rows >= 0 && n > 0 && rows < (1ll << 31), "pli_rmsnorm: bad shape rows=%lld n=%d",
                 (long long)rows, n);
     PLI_REQUIRE(ldx >= n && ldy >= n && (!residual || ldr >= n) && (!h_out || ldh >= n),
                 "pli_rmsnorm: leading dimension too small");
     PLI_REQUIRE(eps >= 0.f, "pli_rmsnorm: negative eps");
-    if (rows == 0) return PLI_OK;
+    if (rows == 0) return PLI_OK;  // (empty operands may be NULL, pli.h)
+    PLI_REQUIRE(x && weight && y, "pli_rmsnorm: null pointer");
     hipStream_t s = (hipStream_t)stream;
     switch (dtype) {
         case PLI_BF16: return launch_rmsnorm<bf16_t>(x, residual, weight, y, h_out, rows, n, ldx, ldr, ldy, ldh, eps, s);

@@ -93,10 +93,10 @@ extern "C" int pli_scale_copy(const float* in, float* out, int64_t n_out, int st
                               void* stream) {
     using namespace pli;
     clear_error();
-    PLI_REQUIRE(in && out, "pli_scale_copy: null pointer");
     PLI_REQUIRE(n_out >= 0 && stride >= 1, "pli_scale_copy: bad n=%lld stride=%d",
                 (long long)n_out, stride);
-    if (n_out == 0) return PLI_OK;
+    if (n_out == 0) return PLI_OK;  // (empty operands may be NULL, pli.h)
+    PLI_REQUIRE(in && out, "pli_scale_copy: null pointer");
     hipStream_t s = (hipStream_t)stream;
     const bool vec = stride == 1 && n_out % 4 == 0 &&
                      (((uintptr_t)in | (uintptr_t)out) & 15) == 0;
@@ -119,10 +119,10 @@ extern "C" int pli_softmax_rows(const void* x, void* y, int64_t rows, int n, int
                                 void* stream) {
     using namespace pli;
     clear_error();
-    PLI_REQUIRE(x && y, "pli_softmax_rows: null pointer");
-    PLI_REQUIRE(rows >= 0 && n > 0, "pli_softmax_rows: bad shape rows=%lld n=%d",
+    PLI_REQUIRE(rows >= 0 && n >= 0, "pli_softmax_rows: bad shape rows=%lld n=%d",
                 (long long)rows, n);
-    if (rows == 0) return PLI_OK;
+    if (rows == 0 || n == 0) return PLI_OK;  // (empty operands may be NULL, pli.h)
+    PLI_REQUIRE(x && y, "pli_softmax_rows: null pointer");
     const int64_t grid = (rows + 3) / 4;
     PLI_REQUIRE(grid < (1ll << 31), "pli_softmax_rows: too many rows");
     hipStream_t s = (hipStream_t)stream;
@@ -149,9 +149,9 @@ extern "C" int pli_online_softmax_with_output(const void* x, const void* v, void
                                               void* stream) {
     using namespace pli;
     clear_error();
-    PLI_REQUIRE(x && v && o && d, "pli_online_softmax_with_output: null pointer");
     PLI_REQUIRE(rows >= 0 && n > 0 && dv > 0, "pli_online_softmax_with_output: bad shape");
-    if (rows == 0) return PLI_OK;
+    if (rows == 0) return PLI_OK;  // (empty operands may be NULL, pli.h)
+    PLI_REQUIRE(x && v && o && d, "pli_online_softmax_with_output: null pointer");
     const int64_t grid = (rows + 3) / 4;
     PLI_REQUIRE(grid < (1ll << 31), "pli_online_softmax_with_output: too many rows");
     hipStream_t s = (hipStream_t)stream;

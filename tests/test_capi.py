@@ -71,7 +71,7 @@ def test_argument_validation_without_gpu(built_lib):
     assert b"multiple of kv_heads" in L.pli_last_error()
     assert L.pli_flash_attn_fwd(p, p, p, p, 1, 4, 4, 8, 8, 64, st, float("nan"), 0, 2, None) == EINVAL
     assert L.pli_scale_copy(p, p, 16, 0, None) == EINVAL
-    assert L.pli_softmax_rows(p, p, 4, 0, 0, None) == EINVAL
+    assert L.pli_softmax_rows(p, p, 4, -1, 0, None) == EINVAL
     dec = lambda *shape, causal=0, ws=0: L.pli_attn_decode(p, p, p, p, *shape, st, 0.1, causal,
                                                            None, ws, 2, None)
     assert dec(1, 6, 4, 1, 64, 64) == EINVAL and b"multiple of kv_heads" in L.pli_last_error()
@@ -97,6 +97,37 @@ def test_argument_validation_without_gpu(built_lib):
                                          n3, ld3, ld3, ld3, P3(None, None, None), I3(9, 9, 9), 3, 2, None)
     assert rms(5, 64) == EINVAL and b"m <= 4" in L.pli_last_error()
     assert rms(1, 16384) == EINVAL and b"k <= 8192" in L.pli_last_error()
+
+
+def test_empty_operands_without_gpu(built_lib):
+    """pli.h: an operand with zero elements may be NULL (torch's data_ptr of
+    an empty tensor) and a call whose output is empty returns PLI_OK before
+    any HIP call; a non-empty output still needs its pointer"""
+    import pli_hip
+    L = pli_hip.lib()
+    EINVAL = 1000
+    st = (ctypes.c_int64 * 12)(*([8] * 12))
+    for B, Nq in ((0, 8), (2, 0)):  # no output rows
+        assert L.pli_flash_attn_fwd(None, None, None, None, B, 4, 4, Nq, 8, 64, None, 0.1, 0, 2, None) == 0
+        assert L.pli_attn_decode(None, None, None, None, B, 4, 4, Nq, 8, 64, None, 0.1, 0, None, 0, 2, None) == 0
+    assert L.pli_flash_attn_fwd(None, None, None, None, 1, 4, 4, 8, 0, 64, st, 0.1, 0, 2, None) == EINVAL
+    assert b"null" in L.pli_last_error()  # no keys, but 8 output rows: O is needed
+    for m, n, k in ((0, 8, 8), (8, 0, 8), (0, 0, 0)):
+        assert L.pli_gemm(None, None, None, None, m, n, k, 8, 8, 8, 1, 2, None) == 0
+        assert L.pli_gemm_f32out(None, None, None, m, n, k, 8, 8, 2, None) == 0
+        assert L.pli_gemm_swiglu(None, None, None, None, m, n, k, 8, 8, 8, 8, 2, None) == 0
+        assert L.pli_gemm_naive(None, None, None, m, n, k, 8, 8, 8, None) == 0
+    assert L.pli_gemm(None, None, None, None, 8, 8, 0, 8, 8, 8, 1, 2, None) == EINVAL  # C = bias / 0: C needed
+    assert L.pli_gemv(None, None, None, 0, 16, 16, 2, None) == 0
+    assert L.pli_gemv(None, None, None, 16, 0, 16, 2, None) == EINVAL  # y = 0 has 16 rows
+    assert L.pli_rmsnorm(None, None, None, None, None, 0, 64, 64, 64, 64, 64, 1e-6, 2, None) == 0
+    assert L.pli_softmax_rows(None, None, 0, 64, 2, None) == 0
+    assert L.pli_softmax_rows(None, None, 4, 0, 2, None) == 0
+    assert L.pli_online_softmax_with_output(None, None, None, None, 0, 64, 64, 2, None) == 0
+    assert L.pli_scale_copy(None, None, 0, 1, None) == 0
+    assert L.pli_kv_append(None, None, None, None, 2, 0, 4, 64, 128, None, None, 2, None) == 0
+    assert L.pli_moe_combine(None, 64, None, None, None, 64, 0, 2, 64, 2, None) == 0
+    assert L.pli_gemm_grouped(None, None, None, None, None, None, 4, 0, 64, 128, 128, 128, 64, 2, None) == 0
 
 
 def test_decode_workspace_plan(built_lib):
