@@ -126,3 +126,57 @@ def test_decode_cache_batches_past_2g():
     ref = attn_ref(q.permute(0, 2, 1, 3), kk, vv, False).permute(0, 2, 1, 3)
     err = (out.float() - ref).abs().max().item()
     assert err <= 1e-2, f"max |err| {err:.3e}"
+
+
+def sampled_ref(q, k, v, rows, causal):
+    """fp32 attention of the given query rows only (each row over all keys)"""
+    G = q.shape[1] // k.shape[1]
+    nq, nk = q.shape[2], k.shape[2]
+    qs = q[:, :, rows].float()
+    kf = k.float().repeat_interleave(G, 1)
+    s = (qs @ kf.transpose(-1, -2)) * q.shape[-1] ** -0.5
+    if causal:
+        lim = rows.to(DEV)[:, None] + (nk - nq)
+        s = s.masked_fill(torch.arange(nk, device=DEV)[None, :] > lim, float("-inf"))
+    return torch.softmax(s, -1) @ v.float().repeat_interleave(G, 1)
+
+
+# long prefill on the v13 programs (whole and ragged key tiles, causal, fp16 D64)
+@pytest.mark.parametrize("shape,dtype,causal", [
+    ((1, 4, 1, 32768, 32768, 128), torch.bfloat16, False),
+    ((1, 4, 1, 32768, 32768, 128), torch.bfloat16, True),
+    ((1, 4, 2, 32813, 32813, 128), torch.bfloat16, True),
+    ((1, 2, 2, 65536, 65536, 64), torch.float16, False),
+    ((1, 2, 1, 65536 + 7, 65536 + 7, 64), torch.float16, True),
+], ids=lambda p: str(p) if not isinstance(p, tuple) else "b{}h{}kv{}q{}k{}d{}".format(*p))
+def test_flash_long_sequences(shape, dtype, causal):
+    import pli_hip
+    B, H, Hkv, Nq, Nk, D = shape
+    g = torch.Generator(device=DEV).manual_seed(sum(shape))
+    q = torch.randn(B, H, Nq, D, device=DEV, generator=g).to(dtype)
+    k = torch.randn(B, Hkv, Nk, D, device=DEV, generator=g).to(dtype)
+    v = torch.randn(B, Hkv, Nk, D, device=DEV, generator=g).to(dtype)
+    out = pli_hip.flash_attn_fwd(q, k, v, causal=causal)
+    rows = torch.cat([torch.arange(0, 70), torch.randint(70, Nq - 70, (300,), generator=torch.Generator().manual_seed(1)),
+                      torch.arange(Nq - 70, Nq)])
+    ref = sampled_ref(q, k, v, rows, causal)
+    err = (out[:, :, rows.to(DEV)].float() - ref).abs().max().item()
+    assert err <= 1e-2, f"{shape} causal {causal}: max |err| {err:.3e}"
+
+
+# a chunk of new rows over a cache-long key stream: the causal walk packs the
+# key-tile count into 16 bits (flash_v13.hip attn_v13_ok: cdiv(Nk, 64) <=
+# 0xFFFF), so 65535 tiles run v13 and one tile more the fallback
+@pytest.mark.parametrize("causal", (False, True))
+@pytest.mark.parametrize("nk", (65535 * 64, 65535 * 64 + 64, 65535 * 64 - 13))
+def test_flash_four_million_keys(nk, causal):
+    import pli_hip
+    g = torch.Generator(device=DEV).manual_seed(nk % 1000)
+    q = torch.randn(1, 2, 128, 128, device=DEV, generator=g).to(torch.bfloat16)
+    k = torch.randn(1, 1, nk, 128, device=DEV, generator=g).to(torch.bfloat16)
+    v = torch.randn(1, 1, nk, 128, device=DEV, generator=g).to(torch.bfloat16)
+    out = pli_hip.flash_attn_fwd(q, k, v, causal=causal)
+    rows = torch.arange(128)
+    ref = sampled_ref(q, k, v, rows, causal)
+    err = (out.float() - ref).abs().max().item()
+    assert err <= 1e-2, f"Nk {nk} causal {causal}: max |err| {err:.3e}"
