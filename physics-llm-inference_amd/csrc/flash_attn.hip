@@ -582,7 +582,8 @@ constexpr int kDefaultVariant = 80;
 // 1154 at B2 S8192, 1223 at B1 H64 S16384 (ab_causal_pair.log)
 // causal default since round 4: attn_fwd_v13c (83), 1210 vs 1058 TF/s for
 // 74 (profiles/r04/flash/ab_causal.log); since round 5 83 takes any diagonal
-// offset, ragged Nk, fp16 and D 64 too; Nk <= 64 -> 74, other D / Nq > Nk -> 60
+// offset, ragged Nk, fp16 and D 64 too; Nk <= 64 -> 74 where v12 applies (bf16,
+// D 128, Nk = 64), else 60 (so also other D and Nq > Nk)
 constexpr int kDefaultCausalVariant = 83;
 
 template <typename T, int D>
