@@ -244,3 +244,25 @@ def test_v13_ragged_causal_program_vs_f64(case):
     assert err <= 1e-2, f"max |err| {err:.3e}"
     if muoff <= 0:
         assert em.counts.get("v_sub_f32", 0) > 0, "the rescale path never ran"
+
+
+OLINE_CASES = [  # (B, H, Hkv, Nq, Nk, grid, muoff, D, dtype, causal): Gen(oline=True), the whole-line O stores
+    (2, 2, 1, 200, 128, 1, 62.0, 128, "bf16", False),   # ragged Nq (row masks on both 8-row halves), seams
+    (1, 8, 8, 1000, 1000, 16, 62.0, 128, "bf16", True),  # causal pair walk, virtual rows, ragged Nk
+    (1, 2, 1, 77, 300, None, 4.0, 64, "f16", False),     # head dim 64: one 128-B line per row
+]
+
+
+@pytest.mark.parametrize("case", OLINE_CASES, ids=lambda c: "oline-b{}h{}kv{}q{}k{}g{}-mu{}-d{}-{}-causal{}".format(*c))
+def test_v13_whole_line_stores_vs_f64(case):
+    """the A/B epilogue that stores O as 8 rows x 128 B per instruction (DPP
+    row_ror:8 exchange of the 64-B halves between lanes j and j + 8)"""
+    B, H, Hkv, Nq, Nk, grid, muoff, D, dtype, causal = case
+    rng = np.random.default_rng(23 + sum(case[:5]))
+    q = rng.standard_normal((B, H, Nq, D))
+    k = rng.standard_normal((B, Hkv, Nk, D))
+    v = rng.standard_normal((B, Hkv, Nk, D))
+    o, em = R.run(q, k, v, grid=grid, muoff=muoff, causal=causal, dtype=dtype, oline=True)
+    assert em.counts.get("v_mov_b32_dpp", 0) > 0
+    err = np.abs(o - f64_attention(q, k, v, causal, dtype=dtype)).max()
+    assert err <= 1e-2, f"max |err| {err:.3e}"

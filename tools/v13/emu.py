@@ -20,6 +20,9 @@ Semantics of the less common instructions, as this file implements them:
   v_permlane16_swap_b32 a, b  rows (16 lanes) 1, 3 of a <-> rows 0, 2 of b
   v_permlane32_swap_b32 a, b  lanes 32-63 of a <-> lanes 0-31 of b
   v_exp_f32 ... clamp  VOP3 clamp of the result to [0, 1]
+  v_mov_b32_dpp d, s row_ror:N ... bank_mask:M  lane i of each 16-lane row
+      reads s from lane (i - N) mod 16 of that row; only lanes whose bank
+      (i & 15) >> 2 is set in M (and in exec) are written
 """
 from __future__ import annotations
 
@@ -391,6 +394,16 @@ class Emu:
             self.vset(w, A_, na, full)
             self.vset(w, B_, nb, full)
             return
+        if op == "v_mov_b32_dpp":
+            kv = dict(m.split(":") for m in ins.mods.split())
+            assert set(kv) <= {"row_ror", "row_mask", "bank_mask", "bound_ctrl"}, ins.mods
+            n = int(kv["row_ror"], 0)
+            assert int(kv.get("row_mask", "0xf"), 0) == 0xF
+            bank = int(kv.get("bank_mask", "0xf"), 0)
+            lane = np.arange(LANES)
+            src = g(o[1])[(lane & ~15) | ((lane - n) & 15)]
+            mask = w.exec & (((bank >> ((lane & 15) >> 2)) & 1) == 1)
+            return self.vset(w, o[0], src, mask)
         if op == "v_permlane32_swap_b32":
             A_, B_ = o[0], o[1]
             va, vb = g(A_), g(B_)

@@ -234,15 +234,16 @@ def is_waitcnt_text(s):
 # ---- hazard rules (wait states between a writer and a reader) ------------
 # writer class -> reader class -> wait states (LLVM gfx950 numbers from the
 # probes: XDL 16x16x32 result -> VALU / VMEM read 8; VALU -> MFMA A/B 2;
-# trans -> VALU 1; VALU -> permlane 2; M0 -> LDS-DMA 1)
+# trans -> VALU 1; VALU -> permlane 2; M0 -> LDS-DMA 1; VALU -> DPP source 2,
+# LLVM's DppVgprWaitStates)
 def need_ws(wcls, rcls):
     if wcls == "mfma":
-        return {"valu": 8, "trans": 8, "ds": 8, "vm": 8, "accr": 10, "perm": 8, "mfmaAB": 10,
+        return {"valu": 8, "trans": 8, "ds": 8, "vm": 8, "accr": 10, "perm": 8, "dpp": 8, "mfmaAB": 10,
                 "mfmaC": 0, "salu": 8, "dma": 8}.get(rcls, 0)
     if wcls == "valu":
-        return {"mfmaAB": 2, "mfmaC": 3, "perm": 2}.get(rcls, 0)
+        return {"mfmaAB": 2, "mfmaC": 3, "perm": 2, "dpp": 2}.get(rcls, 0)
     if wcls == "trans":
-        return {"valu": 1, "trans": 1, "ds": 1, "vm": 1, "perm": 2, "mfmaAB": 2, "mfmaC": 3, "accr": 1,
+        return {"valu": 1, "trans": 1, "ds": 1, "vm": 1, "perm": 2, "dpp": 2, "mfmaAB": 2, "mfmaC": 3, "accr": 1,
                 "dma": 1}.get(rcls, 0)
     if wcls == "accw":
         return {"mfmaAB": 3, "mfmaC": 3, "accr": 1}.get(rcls, 0)
@@ -267,6 +268,8 @@ def reader_classes(ins):
         cls = "accr"
     if op.startswith("v_permlane"):
         cls = "perm"
+    if op.endswith("_dpp"):
+        cls = "dpp"
     return [(r, cls) for r in ins.reads()]
 
 

@@ -141,6 +141,10 @@ def OOFF(qb):
     return V(234 + qb)  # = T(16 + qb): epilogue only
 
 
+def OOFFY(qb):
+    return V(250 + qb)  # = T(32 + qb) = QOFF(qb): epilogue only (OLINE's second 8 rows)
+
+
 TRI = V(206, 4)   # causal: the 16 x 16 diagonal block's C operand (0 / -inf)
 NINF = V(210, 4)  # causal: -inf (C operand of fully masked chains, cndmask source)
 
@@ -290,6 +294,13 @@ SHORTFIRST = [False]
 # mu and the check are unaffected.  P0 rides in the cw argument (unused by the
 # non-causal walk).
 RAGGED = [False]
+# OLINE (Gen(oline=True), A/B knob): the epilogue stores O as whole 128-B
+# lines -- 8 rows x 128 B per global_store_dwordx4 instead of the 16 rows x 64
+# B the MFMA output layout gives, the halves exchanged between lanes j and j +
+# 8 by DPP (3 VALU per word pair).  Bitwise equal and level in throughput
+# (profiles/r05/flash/ab_oline.jsonl: the stores drain behind the next
+# block), so the product keeps the half-line stores
+OLINE = [False]
 
 
 def schedule(mfmas, fills, budget=8, gap_offset=0, lds_gap=LDS_GAP):
@@ -857,8 +868,9 @@ class Gen:
 
     def __init__(self, ndef=4, budget=8, dma_spacing=6, tag="%=", stamp=False, causal=False, abl=(), dma_cost=8,
                  rev=True, qscale=False, dma_pv=0, dma_pv_spacing=16, budget_pv=None, lcheck=None, dtype="bf16",
-                 hd=128, short_first=False, ragged=False):
+                 hd=128, short_first=False, ragged=False, oline=False):
         global DMA_COST
+        OLINE[0] = bool(oline)
         assert not (ragged and causal and not rev), "ragged causal: the pair-walk program (rev=True)"
         RAGGED[0] = bool(ragged)
         SHORTFIRST[0] = bool(short_first)
@@ -1395,16 +1407,27 @@ class Gen:
             e([I("v_rcp_f32", T(20 + qb), L_(qb)[0])])
         if self.causal:
             e(qshift(sT1, sT2))
+        if OLINE[0]:
+            e([I("s_lshl_b32", sT5, ARG(AI["on"]), 3)])  # 8 rows of O
         for qb in range(4):
             # O offsets and the row mask of this q-block (causal: the real
-            # row q' - s; a virtual row below s wraps and is not stored)
-            e([I("v_add_u32", T(24), sCQ0, VI), I("v_add_u32", T(24), 16 * qb, T(24))])
+            # row q' - s; a virtual row below s wraps and is not stored).
+            # OLINE: the X stores hold rows j & 7 (lanes j < 8: the first 64 B
+            # of a 128-B line, j >= 8: the second), the Y stores rows 8 + (j & 7)
+            if OLINE[0]:
+                e([I("v_and_b32", T(24), 7, VI), I("v_add_u32", T(24), sCQ0, T(24)),
+                   I("v_add_u32", T(24), 16 * qb, T(24))])
+            else:
+                e([I("v_add_u32", T(24), sCQ0, VI), I("v_add_u32", T(24), 16 * qb, T(24))])
             if self.causal:
                 e([I("v_subrev_u32", T(24), sT1, T(24))])
             e([I("v_mul_lo_u32", T(25), T(24), ARG(AI["on"])),
                I("v_and_b32", T(26), 1, VG), I("v_lshlrev_b32", T(26), 5, T(26)),
                I("v_lshrrev_b32", T(27), 1, VG), I("v_lshlrev_b32", T(27), 4, T(27)),
                I("v_add3_u32", OOFF(qb), T(25), T(26), T(27))])
+            if OLINE[0]:
+                e([I("v_lshrrev_b32", T(26), 3, VI), I("v_lshlrev_b32", T(26), 6, T(26)),
+                   I("v_add_u32", OOFF(qb), OOFF(qb), T(26)), I("v_add_u32", OOFFY(qb), sT5, OOFF(qb))])
             # packed words of the q-block (W = Y for odd q-blocks, so the next
             # q-block's packing leaves the data of stores in flight alone, was
             # measured level: profiles/r05/flash/seam/)
@@ -1421,6 +1444,29 @@ class Gen:
                        I(DT["cvt"], W(w + 2 * half + 1), T(30), T(31))])
                 if "epi_perm" not in ABL:
                     e([I("v_permlane16_swap_b32", W(w), W(w + 2)), I("v_permlane16_swap_b32", W(w + 1), W(w + 3))])
+            if OLINE[0]:
+                # whole 128-B lines: per pair of 64-B halves (Wa: bytes 128 p ..,
+                # Wb: 128 p + 64 ..), lanes j >= 8 of Wa take Wb of lane j - 8
+                # (X: rows j & 7, whole lines) and lanes j < 8 of Wb take Wa of
+                # lane j + 8 (Y: rows 8 + (j & 7)), by DPP row_ror:8 + bank masks
+                for pr in range(NDB() // 4):
+                    Wa, Wb = [W(8 * pr + r) for r in range(4)], [W(8 * pr + 4 + r) for r in range(4)]
+                    e([I("v_mov_b32", T(28 + r), Wb[r]) for r in range(4)])
+                    e([I("v_mov_b32_dpp", Wb[r], Wa[r], mods="row_ror:8 row_mask:0xf bank_mask:0x3")
+                       for r in range(4)])
+                    e([I("v_mov_b32_dpp", Wa[r], T(28 + r), mods="row_ror:8 row_mask:0xf bank_mask:0xc")
+                       for r in range(4)])
+                for y in (0, 1):
+                    if y:
+                        e([I("v_add_u32", T(25), 8, T(24))])
+                    e([I("v_cmp_gt_u32_e32", VCC, ARG(AI["nq"]), T(25) if y else T(24)),
+                       I("s_and_saveexec_b64", S(sT2.i, 2), VCC)])
+                    for pr in range(NDB() // 4):
+                        if "epi_store" not in ABL:
+                            e([I("global_store_dwordx4", OOFFY(qb) if y else OOFF(qb), V(W(8 * pr + 4 * y).i, 4),
+                                 sCOH, mods=f"offset:{128 * pr}")])
+                    e([I("s_mov_b64", EXEC, S(sT2.i, 2))])
+                continue
             e([I("v_cmp_gt_u32_e32", VCC, ARG(AI["nq"]), T(24)), I("s_and_saveexec_b64", S(sT2.i, 2), VCC)])
             if "epi_fullline" in ABL:
                 # timing only (wrong layout): each store covers 4 rows x 256 B
