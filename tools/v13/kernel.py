@@ -301,6 +301,16 @@ RAGGED = [False]
 # (profiles/r05/flash/ab_oline.jsonl: the stores drain behind the next
 # block), so the product keeps the half-line stores
 OLINE = [False]
+# SEAMWAIT (Gen(seam_wait=True), A/B knob): the wait before the block's
+# first barrier retires only key tile 0's DMA pieces (vmcnt(NPW + 4 NDS))
+# instead of every vector-memory operation in flight (vmcnt(0)), so neither
+# the last block's O stores nor the Q loads are waited for there (the Q loads
+# get the hazard pass's counted wait before the first MFMA that reads them).
+# Bitwise equal and level (profiles/r05/flash/ab_seam_wait.jsonl): the seam's
+# stores and Q loads cost time (dropping either is +2 % at S 4096, +6 % at
+# S 1024: ab_seam_ablation.jsonl), but not through this wait or the stores'
+# line count (OLINE) -- so the product keeps vmcnt(0)
+SEAMWAIT = [False]
 
 
 def schedule(mfmas, fills, budget=8, gap_offset=0, lds_gap=LDS_GAP):
@@ -868,9 +878,10 @@ class Gen:
 
     def __init__(self, ndef=4, budget=8, dma_spacing=6, tag="%=", stamp=False, causal=False, abl=(), dma_cost=8,
                  rev=True, qscale=False, dma_pv=0, dma_pv_spacing=16, budget_pv=None, lcheck=None, dtype="bf16",
-                 hd=128, short_first=False, ragged=False, oline=False):
+                 hd=128, short_first=False, ragged=False, oline=False, seam_wait=False):
         global DMA_COST
         OLINE[0] = bool(oline)
+        SEAMWAIT[0] = bool(seam_wait)
         assert not (ragged and causal and not rev), "ragged causal: the pair-walk program (rev=True)"
         RAGGED[0] = bool(ragged)
         SHORTFIRST[0] = bool(short_first)
@@ -998,7 +1009,7 @@ class Gen:
                    I("v_cndmask_b32_e32", TRI[r], 0, NINF[0], VCC)])
 
     # ---- per-block scalar setup -----------------------------------------
-    def q_offsets(self, q0, qh):
+    def q_offsets(self, q0, qh, loads=True):
         """QOFF(qb) = min(q0 + 16 qb + i, Nq - 1) * qn + 16 g; Q loads.
         Causal: rows are virtual, q' = q + s with s = (-Nq) & 63 (QSHIFT),
         so the load row is min(max(q', s) - s, Nq - 1)"""
@@ -1013,7 +1024,8 @@ class Gen:
                   I("v_lshlrev_b32", T(1), 4, VG), I("v_add_u32", QOFF(qb), T(0), T(1))]
         for qb in range(4):
             for ds in range(NDS()):
-                c.append(I("global_load_dwordx4", Q_(qb, ds), QOFF(qb), qh, mods=f"offset:{64 * ds}"))
+                if loads:
+                    c.append(I("global_load_dwordx4", Q_(qb, ds), QOFF(qb), qh, mods=f"offset:{64 * ds}"))
         return c
 
     def block_setup_first(self):
@@ -1030,6 +1042,7 @@ class Gen:
             e(dma_now(sS0, rev=True))
             e(dma_now(sSP1, rev=True))
             e(self._next_params())
+            e(self.first_wait())
             return
         e([I("s_mov_b64", sCOH, sNOH), I("s_mov_b32", sCQ0, sNQ0), I("s_mov_b32", sNT, sT8),
            I("s_mov_b64", sDK, S(sT0.i, 2)), I("s_mov_b64", sDV, S(sT2.i, 2)), I("s_mov_b32", sDIDX, 0),
@@ -1038,6 +1051,15 @@ class Gen:
         e(self._next_params())
         e(dma_now(sS0))
         e(dma_now(sSP1))
+        e(self.first_wait())
+
+    def first_wait(self):
+        """SEAMWAIT: the first block issues its Q loads before key tiles 0 and
+        1, so tile 0 is retired here (vmcnt(NPW): only tile 1 may stay in
+        flight) and the block's first barrier's vmcnt(NPW + 4 NDS), counted
+        for the seam's order (tile 0, tile 1, Q loads, O stores), waits for
+        nothing more on this path"""
+        return [I("s_waitcnt", f"vmcnt({NPW()})")] if SEAMWAIT[0] else []
 
     def _next_params(self):
         """sHASN = L + G < nblocks; if so the next block's params into sNQH,
@@ -1107,7 +1129,13 @@ class Gen:
         e([I("v_mov_b32", L_(qb)[r], 0) for qb in range(4) for r in range(4)])
         if not LCHECK[0]:
             e([I("v_mov_b32", ACC(0), 0), I("v_mov_b32", ACC(1), 0)])
-        e([I("s_waitcnt", "vmcnt(0)"), I("s_barrier")])
+        # this wave's pieces of the block's key tile 0 have landed: on both
+        # paths here the VMEM operations after them are tile 1's NPW pieces and
+        # the NDS x 4 Q loads (and, at a seam, the last block's O stores after
+        # those).  SEAMWAIT 0 waited for everything, the O stores' write-back
+        # and all the Q loads included (timing: profiles/r05/flash/)
+        n_after = NPW() + 4 * NDS()
+        e([I("s_waitcnt", f"vmcnt({n_after})" if SEAMWAIT[0] else "vmcnt(0)"), I("s_barrier")])
         e(self.seam_stamp(4))
         if QSCALE[0]:
             e(self.q_prescale())
@@ -1392,7 +1420,9 @@ class Gen:
                 fills.append(Fill(ins, 2, earliest=vbuf_free(db) if db >= 3 else 0,
                                   deadline=pv_first_gap(db) - 6, tag="vread"))
         # the next block's Q rows (or this block's again past the last block)
-        fills += chain(self.q_offsets(sNQ0, sNQH), earliest=4)
+        # (ABL "qload", timing only: no Q loads here -- every block reuses the
+        # first block's Q)
+        fills += chain(self.q_offsets(sNQ0, sNQH, loads="qload" not in ABL), earliest=4)
         pv = pv_mfmas(X)
         body, left = schedule(pv, fills, self.budget)
         e(body)
