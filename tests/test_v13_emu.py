@@ -266,3 +266,18 @@ def test_v13_whole_line_stores_vs_f64(case):
     assert em.counts.get("v_mov_b32_dpp", 0) > 0
     err = np.abs(o - f64_attention(q, k, v, causal, dtype=dtype)).max()
     assert err <= 1e-2, f"max |err| {err:.3e}"
+
+
+def test_v13_seam_wait_knob():
+    """Gen(seam_wait=True) (A/B knob): the block's first barrier waits for key
+    tile 0 only -- vmcnt(NPW + 4 NDS) there, vmcnt(NPW) after the first
+    block's setup -- and its program is hazard-clean; run on the emulator"""
+    for hd, npw, nds in ((128, 8, 4), (64, 4, 2)):
+        prog = R.program(causal=False, dtype="bf16", hd=hd, seam_wait=True)
+        waits = [i.ops[0] for i in prog if i.op == "s_waitcnt"]
+        assert f"vmcnt({npw + 4 * nds})" in waits and f"vmcnt({npw})" in waits
+        assert analyse(prog) == {}
+    rng = np.random.default_rng(5)
+    q, k, v = (rng.standard_normal(s) for s in ((1, 2, 256, 128), (1, 2, 320, 128), (1, 2, 320, 128)))
+    o, _ = R.run(q, k, v, grid=1, muoff=62.0, seam_wait=True)
+    assert np.abs(o - f64_attention(q, k, v)).max() <= 1e-2
