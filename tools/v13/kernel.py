@@ -311,6 +311,9 @@ OLINE = [False]
 # S 1024: ab_seam_ablation.jsonl), but not through this wait or the stores'
 # line count (OLINE) -- so the product keeps vmcnt(0)
 SEAMWAIT = [False]
+# cache-policy bits of the seam's memory operations (A/B: Gen(o_bits=...,
+# q_bits=...), e.g. "nt" / "sc1" / "sc0 sc1"); the product issues them plain
+CACHEBITS = {"o": "", "q": ""}
 
 
 def schedule(mfmas, fills, budget=8, gap_offset=0, lds_gap=LDS_GAP):
@@ -878,9 +881,11 @@ class Gen:
 
     def __init__(self, ndef=4, budget=8, dma_spacing=6, tag="%=", stamp=False, causal=False, abl=(), dma_cost=8,
                  rev=True, qscale=False, dma_pv=0, dma_pv_spacing=16, budget_pv=None, lcheck=None, dtype="bf16",
-                 hd=128, short_first=False, ragged=False, oline=False, seam_wait=False):
+                 hd=128, short_first=False, ragged=False, oline=False, seam_wait=False, o_bits=0, q_bits=0):
         global DMA_COST
         OLINE[0] = bool(oline)
+        bits = {0: "", 1: "nt", 2: "sc1", 3: "sc0 sc1", 4: "sc0 sc1 nt"}
+        CACHEBITS["o"], CACHEBITS["q"] = bits[o_bits], bits[q_bits]
         SEAMWAIT[0] = bool(seam_wait)
         assert not (ragged and causal and not rev), "ragged causal: the pair-walk program (rev=True)"
         RAGGED[0] = bool(ragged)
@@ -1025,7 +1030,8 @@ class Gen:
         for qb in range(4):
             for ds in range(NDS()):
                 if loads:
-                    c.append(I("global_load_dwordx4", Q_(qb, ds), QOFF(qb), qh, mods=f"offset:{64 * ds}"))
+                    c.append(I("global_load_dwordx4", Q_(qb, ds), QOFF(qb), qh,
+                               mods=f"offset:{64 * ds} {CACHEBITS['q']}".rstrip()))
         return c
 
     def block_setup_first(self):
@@ -1508,7 +1514,8 @@ class Gen:
             for dbp in range(NDB() // 2):
                 if "epi_store" not in ABL:
                     off = 64 * dbp if "epi_fullline" not in ABL else 0
-                    e([I("global_store_dwordx4", OOFF(qb), V(W(4 * dbp).i, 4), sCOH, mods=f"offset:{off}")])
+                    e([I("global_store_dwordx4", OOFF(qb), V(W(4 * dbp).i, 4), sCOH,
+                         mods=f"offset:{off} {CACHEBITS['o']}".rstrip())])
             e([I("s_mov_b64", EXEC, S(sT2.i, 2))])
         e(self.seam_stamp(2))
         # next block
