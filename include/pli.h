@@ -59,6 +59,12 @@ const char* pli_version(void);
 /* Message for the last non-zero return on the calling thread ("" if none). */
 const char* pli_last_error(void);
 
+/* The kernels the calling thread's last entry-point call launched, in launch
+ * order, '+'-separated (e.g. "attn_fwd_v13c", "gemm_splitk_lds_nt+
+ * gemm_splitk_reduce"); "" when it launched none (an empty output).  For
+ * tests and tuning: which route the dispatch took. */
+const char* pli_last_route(void);
+
 /*
  * Fused attention forward:  O = softmax(Q K^T * scale [+ causal mask]) V.
  *

@@ -4,12 +4,16 @@
 #include <atomic>
 #include <cstdarg>
 #include <cstdio>
+#include <cstring>
 
 #include "pli_common.h"
 
 namespace pli {
 
 static thread_local char g_err[512] = {0};
+// kernels launched by the calling thread's current entry-point call, in order
+// ('+'-separated; reset with the error message when a call starts)
+static thread_local char g_route[512] = {0};
 
 void set_error(const char* fmt, ...) {
     va_list ap;
@@ -18,7 +22,10 @@ void set_error(const char* fmt, ...) {
     va_end(ap);
 }
 
-void clear_error() { g_err[0] = 0; }
+void clear_error() {
+    g_err[0] = 0;
+    g_route[0] = 0;
+}
 
 int launch_status(const char* what) {
     hipError_t e = hipGetLastError();
@@ -26,6 +33,8 @@ int launch_status(const char* what) {
         set_error("%s: launch failed: %s", what, hipGetErrorString(e));
         return int(e);
     }
+    const size_t n = strlen(g_route);
+    snprintf(g_route + n, sizeof(g_route) - n, "%s%s", n ? "+" : "", what);
     return PLI_OK;
 }
 
@@ -55,5 +64,7 @@ extern "C" {
 const char* pli_version(void) { return "pli_hip 0.1.0 gfx950"; }
 
 const char* pli_last_error(void) { return pli::g_err; }
+
+const char* pli_last_route(void) { return pli::g_route; }
 
 }  // extern "C"

@@ -413,7 +413,7 @@ int launch_decode(const void* q, const void* k, const void* v, void* o, int B, i
     if (p.splits > 1)
         hipLaunchKernelGGL((attn_decode_combine<T, D>), dim3((unsigned)(bh * M)), dim3(256), 0,
                            stream, part_o, part_ml, (uint16_t*)o, Hkv, G, M, st, p.splits);
-    return launch_status("pli_attn_decode");
+    return launch_status(p.splits > 1 ? "attn_decode_chunk+attn_decode_combine" : "attn_decode_chunk");
 }
 
 // Append n_new tokens of K and V to the caches at the device-resident

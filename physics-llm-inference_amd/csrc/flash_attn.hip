@@ -663,7 +663,7 @@ int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int
             set_error("pli_flash_attn_fwd: unknown variant %d", variant);
             return PLI_EINVAL;
     }
-    return launch_status("attn_fwd");
+    return launch_status("attn_fwd_v2");
 }
 
 template <typename T>

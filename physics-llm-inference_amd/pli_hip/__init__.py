@@ -32,6 +32,7 @@ _c_int, _c_i64, _c_f32, _vp = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctyp
 _SIGS = {
     "pli_version": [],
     "pli_last_error": [],
+    "pli_last_route": [],
     "pli_flash_attn_fwd": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
                            ctypes.POINTER(_c_i64), _c_f32, _c_int, _c_int, _vp],
     "pli_gemv": [_vp, _vp, _vp, _c_int, _c_int, _c_i64, _c_int, _vp],
@@ -110,7 +111,7 @@ def lib() -> ctypes.CDLL:
         for name, argtypes in _SIGS.items():
             fn = getattr(L, name)
             fn.argtypes = argtypes
-            fn.restype = (ctypes.c_char_p if name in ("pli_version", "pli_last_error") else
+            fn.restype = (ctypes.c_char_p if name in ("pli_version", "pli_last_error", "pli_last_route") else
                           ctypes.c_size_t if name.endswith("_workspace_size") else _c_int)
         _lib = L
     return _lib
@@ -123,6 +124,12 @@ def available() -> bool:
     except (PliError, OSError):
         return False
     return torch.cuda.is_available()
+
+
+def last_route() -> str:
+    """the kernels this thread's last library call launched ('+'-separated;
+    pli_last_route)"""
+    return lib().pli_last_route().decode()
 
 
 def _check(rc: int, what: str) -> None:

@@ -48,6 +48,10 @@ def test_flash_rows_past_2g(nq, d, dtype, causal):
     v = torch.randn(1, 1, nk, d, device=DEV, generator=g).to(dtype)
     out = pli_hip.flash_attn_fwd(q, k, v, causal=causal, out=o)
     assert out.data_ptr() == o.data_ptr()
+    # Nk = Nq + 37 (ragged): the v13 ragged bodies inside the 2^32 bound, v7 / v10 past it
+    want = ("attn_fwd_v13" + ("h" if dtype == torch.float16 else "") + ("rc" if causal else "r") +
+            ("_d64" if d == 64 else "")) if nq < 2048 else "attn_fwd_v7"
+    assert pli_hip.last_route() == want
     ref = attn_ref(q.contiguous(), k, v, causal)
     err = (out.float() - ref).abs().max().item()
     assert err <= 1e-2, f"Nq {nq} D {d} causal {causal}: max |err| {err:.3e}"
@@ -60,16 +64,17 @@ def gemm_check(c, ref):
     assert err <= 2.0 ** -7, f"max rel err {err:.3e}"
 
 
-# A [256, 128] at row stride lda: 256 rows x lda x 2 B against gemm_w5's 2^31
+# A [512, 128] at row stride lda: a tile's 256 rows x lda x 2 B against
+# gemm_w5's 2^31 (M 512 x N 16384: the 128 tiles of 256^2 its default route needs)
 @pytest.mark.parametrize("lda", ((1 << 22) - 64, (1 << 22) + 64))
 @pytest.mark.parametrize("trans_b", (False, True))
 def test_gemm_a_rows_past_2g(lda, trans_b):
     import pli_hip
     g = torch.Generator(device=DEV).manual_seed(5)
-    s = torch.empty(256, lda, device=DEV, dtype=torch.bfloat16)
-    s[:, :128] = torch.randn(256, 128, device=DEV, generator=g).to(torch.bfloat16)
+    s = torch.empty(512, lda, device=DEV, dtype=torch.bfloat16)
+    s[:, :128] = torch.randn(512, 128, device=DEV, generator=g).to(torch.bfloat16)
     a = s[:, :128]
-    n = 32768  # 128 tiles of 256^2: gemm_w5 when the offsets fit
+    n = 16384
     b = torch.randn(n, 128, device=DEV, generator=g).to(torch.bfloat16)
     if trans_b:
         c = pli_hip.gemm(a, b, trans_b=True)
@@ -78,10 +83,11 @@ def test_gemm_a_rows_past_2g(lda, trans_b):
         bt = b.t().contiguous()
         c = pli_hip.gemm(a, bt)
         ref = a.float() @ bt.float()
+    assert (pli_hip.last_route() == "gemm_w5") == (lda < (1 << 22)), pli_hip.last_route()
     gemm_check(c, ref)
 
 
-# NN B [128, 32768] at row stride ldb: 64 k-rows x ldb x 2 B against 2^31
+# NN B [128, 32768] at row stride ldb: 64 k-rows x ldb x 2 B against 2^31 (M 512)
 @pytest.mark.parametrize("ldb", ((1 << 24) - 64, (1 << 24) + 64))
 def test_gemm_nn_b_rows_past_2g(ldb):
     import pli_hip
@@ -90,8 +96,10 @@ def test_gemm_nn_b_rows_past_2g(ldb):
     s = torch.empty(128, ldb, device=DEV, dtype=torch.bfloat16)
     s[:, :n] = torch.randn(128, n, device=DEV, generator=g).to(torch.bfloat16)
     b = s[:, :n]
-    a = torch.randn(256, 128, device=DEV, generator=g).to(torch.bfloat16)
-    gemm_check(pli_hip.gemm(a, b), a.float() @ b.float())
+    a = torch.randn(512, 128, device=DEV, generator=g).to(torch.bfloat16)
+    c = pli_hip.gemm(a, b)
+    assert (pli_hip.last_route() == "gemm_w5") == (ldb < (1 << 24)), pli_hip.last_route()
+    gemm_check(c, a.float() @ b.float())
 
 
 def test_gemv_rows_past_4g():
@@ -176,6 +184,11 @@ def test_flash_four_million_keys(nk, causal):
     k = torch.randn(1, 1, nk, 128, device=DEV, generator=g).to(torch.bfloat16)
     v = torch.randn(1, 1, nk, 128, device=DEV, generator=g).to(torch.bfloat16)
     out = pli_hip.flash_attn_fwd(q, k, v, causal=causal)
+    tiles = -(-nk // 64)
+    want = "attn_fwd_v13" + ("rc" if causal and nk % 64 else "r" if nk % 64 else "c" if causal else "")
+    if causal and tiles > 0xFFFF:
+        want = "attn_fwd_v12"  # the causal v12 body (Nk % 64 == 0, bf16 D 128)
+    assert pli_hip.last_route() == want
     rows = torch.arange(128)
     ref = sampled_ref(q, k, v, rows, causal)
     err = (out.float() - ref).abs().max().item()
