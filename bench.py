@@ -787,6 +787,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    route = pli_hip.last_route()  # the kernel the timed step launches (pli_last_route)
     if world > 1:
         dist.barrier()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -958,7 +959,7 @@ def main():
                      **pmc_fields("attn_fwd_v13", kernel_ms),
                      "traffic_source": "profiles/traffic.json: rocprofv3 FETCH_SIZE x2 (gfx950) + WRITE_SIZE "
                                        "per launch, separate --pmc passes (tools/pmc_summary.py), not this run",
-                     "kernel": FLASH_KERNEL, "algorithmic_flops": flops_step,
+                     "kernel": FLASH_KERNEL, "route": route, "algorithmic_flops": flops_step,
                      "kernel_ms": kernel_ms, **measured_roof},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.quick:
