@@ -1794,9 +1794,10 @@ int launch_splitk(const void* a, const void* b, void* c, const void* bias, int M
         PLI_SK_MC(true, false);
         return launch_status("gemm_splitk_lds_nt");
     }
+    const char* name = lds ? "gemm_splitk_lds_nt" : "gemm_splitk_nt";
     if (ks > 1) {
         PLI_SK_MC(true, false);
-        const int rc = launch_status("gemm_splitk_nt");
+        const int rc = launch_status(name);
         if (rc) return rc;
         const int64_t groups = ((int64_t)M * N) / 8;
         const dim3 rgrid((unsigned)cdiv((int)((groups + 255) / 256 * 256), 256));
@@ -1812,7 +1813,7 @@ int launch_splitk(const void* a, const void* b, void* c, const void* bias, int M
     else PLI_SK_MC(false, false);
 #undef PLI_SK_MC
 #undef PLI_SK
-    return launch_status("gemm_splitk_nt");
+    return launch_status(name);
 }
 
 template <typename T>

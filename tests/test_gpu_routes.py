@@ -84,3 +84,33 @@ def test_gemm_and_decode_routes():
     assert pli_hip.last_route() == "attn_decode_chunk+attn_decode_combine"
     pli_hip.attn_decode(q, kc, kc, 0)
     assert pli_hip.last_route() == "attn_fwd_generic"             # empty cache: O = 0
+
+
+# (M, N, K, trans_b, bias, expected route or prefix): csrc/gemm.hip gemm_dispatch
+# through the Python wrapper (which passes a split-K workspace when one is needed)
+GEMM = [
+    (1, 4096, 4096, True, True, "gemm_skinny_nt"),                          # M = 1 with a bias
+    (16, 2048, 2048, True, False, "gemm_smallm_nt"),                        # short K, M <= 32
+    (64, 8192, 1024, True, False, "gemm_midm_nt"),                          # the TP-8 row shard at M 64
+    (128, 8192, 8192, True, False, "gemm_splitk_lds_nt+gemm_splitk_reduce"),  # decode batch, deep K
+    (1024, 4096, 4096, True, False, "gemm_splitk_lds_nt"),                  # few tiles: 128-row slabs
+    (384, 384, 256, False, False, "gemm_mfma"),                             # below the 2 x 2 grid of 256^2
+    (8192, 8192, 1024, True, False, "gemm_w5"),                             # 1024 tiles
+    (4096, 4096, 4096, False, True, "gemm_w5"),                             # NN with a bias
+]
+
+
+@pytest.mark.parametrize("case", GEMM, ids=lambda c: "m{}n{}k{}-nt{}-bias{}".format(*c[:5]))
+def test_gemm_route(case):
+    import pli_hip
+    M, N, K, nt, bias, want = case
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    a = torch.randn(M, K, device=DEV, generator=g).to(BF)
+    b = torch.randn(N, K, device=DEV, generator=g).to(BF) if nt else torch.randn(K, N, device=DEV, generator=g).to(BF)
+    bi = torch.randn(N, device=DEV, generator=g).to(BF) if bias else None
+    c = pli_hip.gemm(a, b, trans_b=nt, bias=bi)
+    route = pli_hip.last_route()
+    assert route == want or (want.endswith("_nt") and route.startswith(want + "+")), route
+    ref = a.float() @ (b.float().t() if nt else b.float()) + (bi.float() if bias else 0)
+    scale = ref.abs().amax(dim=1, keepdim=True).clamp_min(1e-3)
+    assert ((c.float() - ref).abs() / scale).max().item() <= 2.0 ** -7
