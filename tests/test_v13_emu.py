@@ -281,3 +281,26 @@ def test_v13_seam_wait_knob():
     q, k, v = (rng.standard_normal(s) for s in ((1, 2, 256, 128), (1, 2, 320, 128), (1, 2, 320, 128)))
     o, _ = R.run(q, k, v, grid=1, muoff=62.0, seam_wait=True)
     assert np.abs(o - f64_attention(q, k, v)).max() <= 1e-2
+
+
+BEYOND_CASES = [  # (B, H, Hkv, Nq, Nk, grid, muoff, D, dtype): causal, Gen(beyond=True)
+    (1, 1, 1, 512, 512, None, 0.0, 128, "bf16"),    # rescales at every tile, beside the skipped tiles
+    (1, 8, 8, 1000, 1024, 16, 62.0, 128, "bf16"),   # pair walk, virtual rows
+    (1, 8, 8, 990, 990, 16, 4.0, 64, "f16"),        # ragged, fp16 P-bit check, head dim 64
+]
+
+
+@pytest.mark.parametrize("case", BEYOND_CASES, ids=lambda c: "beyond-b{}h{}kv{}q{}k{}g{}-mu{}-d{}-{}".format(*c))
+def test_v13_beyond_light_steps_vs_f64(case):
+    """the A/B form whose tiles past a wave's diagonal skip QK and the
+    softmax (P = 0, the deferred slices' S words = -inf) instead of running
+    them on -inf C operands"""
+    B, H, Hkv, Nq, Nk, grid, muoff, D, dtype = case
+    rng = np.random.default_rng(29 + sum(case[:5]))
+    q = rng.standard_normal((B, H, Nq, D))
+    k = rng.standard_normal((B, Hkv, Nk, D))
+    v = rng.standard_normal((B, Hkv, Nk, D))
+    o, em = R.run(q, k, v, grid=grid, muoff=muoff, causal=True, dtype=dtype, beyond=True)
+    err = np.abs(o - f64_attention(q, k, v, True, dtype=dtype)).max()
+    assert err <= 1e-2, f"max |err| {err:.3e}"
+    assert analyse(R.program(causal=True, dtype=dtype, hd=D, ragged=Nk % 64 != 0, beyond=True)) == {}

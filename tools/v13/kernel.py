@@ -311,6 +311,13 @@ OLINE = [False]
 # S 1024: ab_seam_ablation.jsonl), but not through this wait or the stores'
 # line count (OLINE) -- so the product keeps vmcnt(0)
 SEAMWAIT = [False]
+# BEYOND (Gen(beyond=...), the product since round 5): causal, a key tile
+# past the wave's diagonal (every score masked) skips QK(t) and the softmax
+# of t -- P(t) is set to 0 and the S words its deferred slices read next step
+# to -inf -- instead of running them on -inf C operands; PV(t) next step
+# still runs on the zeros.  Bitwise equal; causal +0.8-1.4 % at S 4096, +2.3
+# % at S 1024 (profiles/r05/flash/ab_beyond.jsonl)
+BEYOND = [True]
 # cache-policy bits of the seam's memory operations (A/B: Gen(o_bits=...,
 # q_bits=...), e.g. "nt" / "sc1" / "sc0 sc1"); the product issues them plain
 CACHEBITS = {"o": "", "q": ""}
@@ -881,9 +888,11 @@ class Gen:
 
     def __init__(self, ndef=4, budget=8, dma_spacing=6, tag="%=", stamp=False, causal=False, abl=(), dma_cost=8,
                  rev=True, qscale=False, dma_pv=0, dma_pv_spacing=16, budget_pv=None, lcheck=None, dtype="bf16",
-                 hd=128, short_first=False, ragged=False, oline=False, seam_wait=False, o_bits=0, q_bits=0):
+                 hd=128, short_first=False, ragged=False, oline=False, seam_wait=False, o_bits=0, q_bits=0,
+                 beyond=True):
         global DMA_COST
         OLINE[0] = bool(oline)
+        BEYOND[0] = bool(beyond)
         bits = {0: "", 1: "nt", 2: "sc1", 3: "sc0 sc1", 4: "sc0 sc1 nt"}
         CACHEBITS["o"], CACHEBITS["q"] = bits[o_bits], bits[q_bits]
         SEAMWAIT[0] = bool(seam_wait)
@@ -1322,6 +1331,13 @@ class Gen:
         # deferred slices of tile t-1 (they read S(., 3): before QK(t) overwrites it)
         qk, done, first = qk_with_rowsums(mask, QSCALE[0], Xp if LCHECK[0] else None)
         dl = lambda qb, kb: first(kb, qb) - 1  # noqa: E731
+        # BEYOND: a tile past this wave's diagonal has every score masked --
+        # no QK(t) and no softmax(t): P(t) = 0 and the S words its deferred
+        # slices read next step = -inf, written after t-1's deferred slices
+        light = mask == "beyond" and BEYOND[0]
+        if light:
+            qk = []  # (t-1's row sums run below, after its deferred slices)
+            dl = None
         f_def, cvd, last_or_prev = softmax_fills(Xp, dfr, lambda qb, kb: 0, dl, ytag=0)
         if "soft" in ABL:
             f_def = []
@@ -1340,7 +1356,9 @@ class Gen:
         # V(t-1) d-blocks 0, 1 (from 32 MFMAs before the phase ends)
         for db in (0, 1):
             for ins in v_reads(db):
-                if "vread" not in ABL:
+                if "vread" not in ABL and light:
+                    fills.append(Fill(ins, 2, earliest=0, tag="vread0"))
+                elif "vread" not in ABL:
                     fills.append(Fill(ins, 2, earliest=(40 if GEOM["hd"] == 128 else len(qk) - 32) + 8 * db,
                                       tag="vread"))
         # softmax(t), zero ACC(X) first (P-bit check)
@@ -1362,7 +1380,7 @@ class Gen:
                                             prev_cv=cvd,
                                             extra_deps=(lambda qb, kb: [rag[(kb, qb)]]) if rag else None)
         now_groups = softmax_fills.groups
-        if "soft" in ABL:
+        if "soft" in ABL or light:
             f_now, now_groups = [], []
         for f in f_now:
             if f.tag == "or" and not any(d.tag == "or" for d in f.deps):
@@ -1373,7 +1391,8 @@ class Gen:
         body, left = schedule(qk, fills, self.budget)
         e(body)
         # everything of tile t-1 must be done before its check
-        pend_prev = [f for f in left if f in f_def or f.tag.startswith("dma") or f.tag.startswith("rag")]
+        pend_prev = [f for f in left if f in f_def or f.tag.startswith("dma") or f.tag.startswith("rag") or
+                     f.tag == "vread0"]
         # a slice of tile t that has started finishes before the check: the
         # rare path redoes every P of t from S, and a slice whose fma ran
         # with the old mu must not write its P after that
@@ -1382,6 +1401,13 @@ class Gen:
                 pend_prev += [f for f in grp if f.gap is None]
         e(drain(pend_prev, len(qk) - 1))
         left = [f for f in left if f.gap is None]
+        if light:
+            if LCHECK[0]:
+                e(rowsum_mfmas(Xp))
+            e([I("v_mov_b32", P_(X, qb, kp)[r], 0) for qb in range(4) for kp in range(2) for r in range(4)])
+            e([I("v_mov_b32", S_(kb, qb)[2 * hh + j], NINF[0]) for (qb, kb, hh) in dfr for j in range(2)])
+            if not LCHECK[0]:
+                e([I("v_mov_b32", ACC(X), 0)])
         # ---- defer-max check of tile t-1
         self.check(Xp, f"rare_s{Xp}")
         e([I("s_waitcnt", f"vmcnt({NPW()})")] + ([] if "barrier" in ABL else [I("s_barrier")]))
