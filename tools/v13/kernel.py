@@ -316,8 +316,11 @@ SEAMWAIT = [False]
 # of t -- P(t) is set to 0 and the S words its deferred slices read next step
 # to -inf -- instead of running them on -inf C operands; PV(t) next step
 # still runs on the zeros.  Bitwise equal; causal +0.8-1.4 % at S 4096, +2.3
-# % at S 1024 (profiles/r05/flash/ab_beyond.jsonl)
-BEYOND = [True]
+# % at S 1024 (profiles/r05/flash/ab_beyond.jsonl).  BEYOND 2 also skips
+# PV(t-1) when tile t-1 was past the diagonal too (step_idle: only the K/V
+# stream and the barrier) and the tail's PV when the last tile is
+# (tail_dispatch)
+BEYOND = [2]
 # cache-policy bits of the seam's memory operations (A/B: Gen(o_bits=...,
 # q_bits=...), e.g. "nt" / "sc1" / "sc0 sc1"); the product issues them plain
 CACHEBITS = {"o": "", "q": ""}
@@ -889,10 +892,10 @@ class Gen:
     def __init__(self, ndef=4, budget=8, dma_spacing=6, tag="%=", stamp=False, causal=False, abl=(), dma_cost=8,
                  rev=True, qscale=False, dma_pv=0, dma_pv_spacing=16, budget_pv=None, lcheck=None, dtype="bf16",
                  hd=128, short_first=False, ragged=False, oline=False, seam_wait=False, o_bits=0, q_bits=0,
-                 beyond=True):
+                 beyond=2):
         global DMA_COST
         OLINE[0] = bool(oline)
-        BEYOND[0] = bool(beyond)
+        BEYOND[0] = int(beyond)
         bits = {0: "", 1: "nt", 2: "sc1", 3: "sc0 sc1", 4: "sc0 sc1 nt"}
         CACHEBITS["o"], CACHEBITS["q"] = bits[o_bits], bits[q_bits]
         SEAMWAIT[0] = bool(seam_wait)
@@ -1193,10 +1196,10 @@ class Gen:
         self.step_dispatch(0)
         e([I("s_add_u32", sT, sT, 1), I("s_cmp_lt_u32", sT, sNT), I("s_cbranch_scc1", Lb("loop"))])
         # tails: the last tile T = nt - 1 is in state (T & 1)
-        self.tail(0)
+        self.tail_dispatch(0)
         e([I("s_branch", Lb("epi"))])
         e([label(Lb("tail1"))])
-        self.tail(1)
+        self.tail_dispatch(1)
         e([label(Lb("epi"))])
         self.epilogue()
 
@@ -1288,6 +1291,14 @@ class Gen:
             e([I("s_sub_u32", sT2, ARG(AI["nt"]), 1), I("s_cmp_eq_u32", tl, sT2), I("s_cbranch_scc1", rg)])
         e([I("s_cmp_lt_u32", tl, sTD), I("s_cbranch_scc1", n), I("s_cmp_eq_u32", tl, sTD),
            I("s_cbranch_scc1", d)] + ([label(by)] if RAGGED[0] else []))
+        b2 = Lb(f"beyond2{u}")
+        if BEYOND[0] >= 2:
+            # the tile before (position t - 1) past the diagonal too: its P is
+            # 0, so PV(t-1) is skipped as well -- the idle step
+            e([I("s_sub_u32", sT1, sT, 1)])
+            if self.rev:
+                e(self.tile_of(sT1, sT1))
+            e([I("s_cmp_gt_u32", sT1, sTD), I("s_cbranch_scc1", b2)])
         self.step(X, "beyond")
         e([I("s_branch", cont), label(n)])
         self.step(X, None)
@@ -1296,7 +1307,50 @@ class Gen:
         if RAGGED[0]:
             e([I("s_branch", cont), label(rg), I("s_cmp_lt_u32", sTD, sT2), I("s_cbranch_scc1", by)])
             self.step(X, "rag")
+        if BEYOND[0] >= 2:
+            e([I("s_branch", cont), label(b2)])
+            self.step_idle(X)
         e([label(cont)])
+
+    def step_idle(self, X):
+        """causal, tiles t and t-1 both past this wave's diagonal (BEYOND):
+        nothing of either reaches O or l (P = 0), so only the stream moves --
+        tile t+2's DMA, the barrier, K(t+1)'s fragments -- and P(t) = 0, the S
+        words its deferred slices would read = -inf (for a light step or the
+        tail after this one)"""
+        e = self.emit
+        dfr, _ = self.deferred()
+        e(rotate_slots())
+        for f in dma_fills(sSP2, earliest0=1, spacing=self.dma_spacing, rev=self.rev):
+            e(f.ins)
+        e([I("v_mov_b32", P_(X, qb, kp)[r], 0) for qb in range(4) for kp in range(2) for r in range(4)])
+        e([I("v_mov_b32", S_(kb, qb)[2 * hh + j], NINF[0]) for (qb, kb, hh) in dfr for j in range(2)])
+        if not LCHECK[0]:
+            e([I("v_mov_b32", ACC(X), 0)])
+        e([I("s_waitcnt", f"vmcnt({NPW()})")] + ([] if "barrier" in ABL else [I("s_barrier")]))
+        e([I("v_add_u32", VKA, sSP1, VKL)])
+        e(k_reads())
+
+    def tail_dispatch(self, X):
+        """causal (BEYOND): the last tile past this wave's diagonal (forward
+        blocks of waves 0-2) adds nothing to O or l -- only the next block's
+        Q loads run"""
+        if not (self.causal and BEYOND[0] >= 2):
+            self.tail(X)
+            return
+        e, Lb = self.emit, self.L
+        u = self.new_uid()
+        light, done = Lb(f"taillight{u}"), Lb(f"tailed{u}")
+        e([I("s_sub_u32", sT1, sNT, 1)])
+        if self.rev:
+            e(self.tile_of(sT1, sT1))
+        e([I("s_cmp_gt_u32", sT1, sTD), I("s_cbranch_scc1", light)])
+        self.tail(X)
+        e([I("s_branch", done), label(light)])
+        e(self.seam_stamp(0))
+        e(rotate_slots())
+        e(self.q_offsets(sNQ0, sNQH, loads="qload" not in ABL))
+        e([label(done)])
 
     def check(self, Xc, rare_block):
         """the defer-max check of the tile in P state Xc (some P >= 2: bit 14
