@@ -1328,8 +1328,19 @@ class Gen:
         if not LCHECK[0]:
             e([I("v_mov_b32", ACC(X), 0)])
         e([I("s_waitcnt", f"vmcnt({NPW()})")] + ([] if "barrier" in ABL else [I("s_barrier")]))
+        skip = None
+        if BEYOND[0] >= 3:
+            # K(t+1) is read only if tile t+1 is not past the diagonal too
+            # (forward blocks: never; reversed: position 4 after the group)
+            skip = self.L(f"nokread{self.new_uid()}")
+            e([I("s_add_u32", sT1, sT, 1)])
+            if self.rev:
+                e(self.tile_of(sT1, sT1))
+            e([I("s_cmp_gt_u32", sT1, sTD), I("s_cbranch_scc1", skip)])
         e([I("v_add_u32", VKA, sSP1, VKL)])
         e(k_reads())
+        if skip:
+            e([label(skip)])
 
     def tail_dispatch(self, X):
         """causal (BEYOND): the last tile past this wave's diagonal (forward
