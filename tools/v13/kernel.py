@@ -319,8 +319,12 @@ SEAMWAIT = [False]
 # % at S 1024 (profiles/r05/flash/ab_beyond.jsonl).  BEYOND 2 also skips
 # PV(t-1) when tile t-1 was past the diagonal too (step_idle: only the K/V
 # stream and the barrier) and the tail's PV when the last tile is
-# (tail_dispatch)
-BEYOND = [2]
+# (tail_dispatch); 3 adds skipping an idle step's K reads when tile t+1 is
+# past the diagonal too (level alone); 4 (the product) adds dropping the
+# diagonal tile's all -inf blocks (kb > qb: 24 QK MFMAs) and, in the light
+# step after it, its all-zero P(qb 0-1, kp 1) from PV and the row sums (18
+# MFMAs): bitwise equal, +0.2-1.3 % (profiles/r05/flash/ab_beyond_diag.jsonl)
+BEYOND = [4]
 # cache-policy bits of the seam's memory operations (A/B: Gen(o_bits=...,
 # q_bits=...), e.g. "nt" / "sc1" / "sc0 sc1"); the product issues them plain
 CACHEBITS = {"o": "", "q": ""}
@@ -892,7 +896,7 @@ class Gen:
     def __init__(self, ndef=4, budget=8, dma_spacing=6, tag="%=", stamp=False, causal=False, abl=(), dma_cost=8,
                  rev=True, qscale=False, dma_pv=0, dma_pv_spacing=16, budget_pv=None, lcheck=None, dtype="bf16",
                  hd=128, short_first=False, ragged=False, oline=False, seam_wait=False, o_bits=0, q_bits=0,
-                 beyond=2):
+                 beyond=4):
         global DMA_COST
         OLINE[0] = bool(oline)
         BEYOND[0] = int(beyond)
@@ -1403,6 +1407,21 @@ class Gen:
         if light:
             qk = []  # (t-1's row sums run below, after its deferred slices)
             dl = None
+        diag_skip = mask == "diag" and BEYOND[0] >= 4
+        if diag_skip:
+            # the diagonal tile's blocks kb > qb are -inf whole: S = -inf by
+            # v_mov instead of their 4 chained MFMAs (qb 3 is never among
+            # them, so t-1's deferred slices, which read S(., 3), are unaffected)
+            dead = {S_(kb, qb).i for qb in range(4) for kb in range(4) if kb > qb}
+            keep = [j for j, m in enumerate(qk) if not (m.op == DT["mfma"] and m.ops[0].i in dead)]
+            newpos = {j: n for n, j in enumerate(keep)}
+            qk = [qk[j] for j in keep]
+            done0, first0 = done, first
+            done = lambda kb, qb: newpos[done0(kb, qb)] if kb <= qb else -3  # noqa: E731
+            first = lambda kb, qb: newpos[first0(kb, qb)]  # noqa: E731
+            dl = lambda qb, kb: first(kb, qb) - 1  # noqa: E731
+            e([I("v_mov_b32", S_(kb, qb)[r], NINF[0]) for qb in range(4) for kb in range(4) if kb > qb
+               for r in range(4)])
         f_def, cvd, last_or_prev = softmax_fills(Xp, dfr, lambda qb, kb: 0, dl, ytag=0)
         if "soft" in ABL:
             f_def = []
@@ -1424,8 +1443,8 @@ class Gen:
                 if "vread" not in ABL and light:
                     fills.append(Fill(ins, 2, earliest=0, tag="vread0"))
                 elif "vread" not in ABL:
-                    fills.append(Fill(ins, 2, earliest=(40 if GEOM["hd"] == 128 else len(qk) - 32) + 8 * db,
-                                      tag="vread"))
+                    fills.append(Fill(ins, 2, earliest=(40 if GEOM["hd"] == 128 and not diag_skip else len(qk) - 32) +
+                                      8 * db, tag="vread"))
         # softmax(t), zero ACC(X) first (P-bit check)
         z = Fill(I("v_mov_b32", ACC(X), 0), 4, tag="zero")
         if not LCHECK[0]:
@@ -1466,9 +1485,13 @@ class Gen:
                 pend_prev += [f for f in grp if f.gap is None]
         e(drain(pend_prev, len(qk) - 1))
         left = [f for f in left if f.gap is None]
+        # light (BEYOND >= 4): tile t-1 is the diagonal one, whose P(qb, kp = 1)
+        # for qb 0, 1 (rows 0-31 x keys 32-63) is all zero: no row sums or PV
+        # MFMAs on them
+        pdead = {P_(Xp, qb, 1).i for qb in (0, 1)} if light and BEYOND[0] >= 4 else set()
         if light:
             if LCHECK[0]:
-                e(rowsum_mfmas(Xp))
+                e([m for m in rowsum_mfmas(Xp) if m.ops[2].i not in pdead])
             e([I("v_mov_b32", P_(X, qb, kp)[r], 0) for qb in range(4) for kp in range(2) for r in range(4)])
             e([I("v_mov_b32", S_(kb, qb)[2 * hh + j], NINF[0]) for (qb, kb, hh) in dfr for j in range(2)])
             if not LCHECK[0]:
@@ -1482,14 +1505,25 @@ class Gen:
         fills = left
         ka = Fill(I("v_add_u32", VKA, sSP1, VKL), 4, earliest=B0, tag="kaddr")
         pv = pv_mfmas(Xp)
+        if pdead:
+            pv = [m for m in pv if m.ops[2].i not in pdead]
         kr = [Fill(ins, 2, deps=[ka], sep=1, earliest=B0 + n // 2, deadline=B0 + min(40, len(pv) - 8), tag="kread")
               for n, ins in enumerate(k_reads())] if "kread" not in ABL else []
         # V d-block db (2..) reads: after d-block db-3's MFMAs (same buffer), well before db's
         vr = []
+        if pdead:  # (positions from the shortened list; a missed deadline is an error)
+            use = {}
+            for j, m in enumerate(pv):
+                if m.ops[0].f == "a":
+                    use.setdefault(m.ops[0].i // 16, []).append(j)
         for db in range(2 if "vread" not in ABL else NDB(), NDB()):
             for ins in v_reads(db):
-                vr.append(Fill(ins, 2, earliest=B0 + (vbuf_free(db) if db >= 3 else 0),
-                               deadline=B0 + pv_first_gap(db) - 6, tag="vread"))
+                if pdead:
+                    vr.append(Fill(ins, 2, earliest=B0 + (use[db - 3][-1] + 2 if db >= 3 else 0),
+                                   deadline=B0 + use[db][0] - 6, tag="vread", hard=True))
+                else:
+                    vr.append(Fill(ins, 2, earliest=B0 + (vbuf_free(db) if db >= 3 else 0),
+                                   deadline=B0 + pv_first_gap(db) - 6, tag="vread"))
         fills = [ka] + kr + vr + fills + dma_pv
         body, left = schedule(pv, fills, self.budget_pv, gap_offset=B0)
         e(body)
