@@ -80,3 +80,17 @@ def max_blocks_by_shared_memory(shared_per_block: int, shared_per_sm: int = MI35
     if shared_per_block == 0:
         return float("inf")
     return shared_per_sm // shared_per_block
+
+
+if __name__ == "__main__":
+    # the chapter's demo (ch05/shared_memory.py)
+    print(explain_shared_memory())
+    print("\nBank Conflict Info:")
+    for key, val in demonstrate_bank_conflicts().items():
+        print(f"  {key}: {val}")
+    cfg = compute_tile_config(n=1024, tile_size=32)
+    print(f"\nTile Configuration Example:\n  Tiles: {cfg.num_tiles}\n  Shared memory: {cfg.shared_memory_bytes} bytes")
+    print("\nShared Memory Occupancy Impact:")
+    for kib in (0, 16, 32, 48):
+        blocks = max_blocks_by_shared_memory(kib * 1024)
+        print(f"  {kib:3d} KB -> " + ("unlimited blocks" if blocks == float("inf") else f"{blocks} blocks/CU"))

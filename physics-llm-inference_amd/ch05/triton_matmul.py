@@ -59,3 +59,31 @@ def benchmark_triton_matmul(m: int = 1024, n: int = 1024, k: int = 1024, warmup:
     torch_us = timed(lambda: torch.matmul(a, b))
     hip_us = timed(lambda: triton_matmul(a, b))
     return MatmulBenchmark(m=m, n=n, k=k, triton_us=hip_us, torch_us=torch_us, speedup=torch_us / hip_us)
+
+
+def triton_matmul_explained() -> str:
+    """The reference's description of its Triton kernel (ch05/triton_matmul.py),
+    and what stands in for it here."""
+    return (
+        "\nThe chapter's Triton matmul: each program instance computes one\n"
+        "BLOCK_M x BLOCK_N output tile, walking K in BLOCK_K steps -- load an A and\n"
+        "a B tile, tl.dot them into an fp32 accumulator, store the tile once.\n\n"
+        "This build has no Triton (TRITON_AVAILABLE is False): triton_matmul runs the\n"
+        "hand-written HIP GEMM -- the same tiling idea written for CDNA4: 256 x 256\n"
+        "output tiles, one wave per SIMD with a 128 x 128 accumulator block in its\n"
+        "AGPRs, A / B staged 64 k deep into LDS by direct-to-LDS DMA two steps ahead,\n"
+        "and v_mfma_f32_16x16x32 on the fragments.  benchmark_triton_matmul reports\n"
+        "that kernel as `triton_us` next to torch.matmul (hipBLASLt).\n"
+    )
+
+
+if __name__ == "__main__":
+    # the chapter's demo (ch05/triton_matmul.py:145-161)
+    print(triton_matmul_explained())
+    if not torch.cuda.is_available():
+        print("no ROCm device")
+    else:
+        print("\nBenchmark Results:\n" + "=" * 60 + f"\nTriton available: {TRITON_AVAILABLE}")
+        for n in (512, 1024, 2048, 4096):
+            r = benchmark_triton_matmul(m=n, n=n, k=n)
+            print(f"{n}x{n}: HIP GEMM {r.triton_us:.1f} us, Torch {r.torch_us:.1f} us, Speedup {r.speedup:.2f}x")

@@ -88,3 +88,19 @@ def benchmark_attention_memory(seq_lens=None, head_dim=64, num_heads=32, batch_s
             results[n] = {"oom": True}
             torch.cuda.empty_cache()
     return results
+
+
+if __name__ == "__main__":
+    # the chapter's demo (ch06/attention_memory.py:127-156): the score matrix's
+    # bytes and arithmetic intensity by sequence length, then (on a device)
+    # measured allocations of the materialised attention
+    print(explain_attention_bottleneck())
+    print("\n" + "=" * 60 + "\nMemory Scaling by Sequence Length\n" + "-" * 60)
+    for n in (512, 1024, 2048, 4096, 8192, 16384, 32768):
+        st = attention_memory_bytes(batch_size=1, num_heads=32, seq_len=n, head_dim=64, dtype_bytes=2)
+        print(f"Seq {n:6d}: {st.total_mb:8.1f} MB, AI={attention_arithmetic_intensity(n, 64):.2f} FLOP/byte")
+    if torch.cuda.is_available():
+        print("\n" + "=" * 60 + "\nActual Memory Usage (GPU)\n" + "-" * 60)
+        for n, d in benchmark_attention_memory().items():
+            print(f"Seq {n}: OOM" if "oom" in d else
+                  f"Seq {n}: theoretical={d['theoretical_mb']:.1f} MB, actual={d['actual_mb']:.1f} MB")

@@ -153,3 +153,32 @@ def explain_flash_attention() -> str:
         "rescale path only when some row's l reaches 1 (defer-max).  HBM traffic is\n"
         "O(N d): Q, K, V read once per head, O written once."
     )
+
+
+def _demo() -> None:
+    """`python -m ch06.flash_attention`: the chapter's demo on this build --
+    the explanation, a check of the fused kernel against the materialised
+    attention on the chapter's fp16 head-dim-64 shape, and the HBM byte model
+    over sequence lengths (the reference module's __main__, ch06/
+    flash_attention.py:143-177)"""
+    from .attention_memory import naive_attention
+
+    print(explain_flash_attention())
+    if not torch.cuda.is_available():
+        print("\nno ROCm device: the kernel check is skipped")
+    else:
+        print("\n" + "=" * 60 + "\nCorrectness Verification\n" + "-" * 60)
+        shape = (2, 8, 256, 64)
+        q, k, v = (torch.randn(*shape, device="cuda", dtype=torch.float16) for _ in range(3))
+        diff = (naive_attention(q, k, v) - flash_attention_forward(q, k, v)).abs().max().item()
+        print(f"Max difference: {diff:.6f} (kernel {pli_hip.last_route()})")
+        print(f"Correctness: {'PASS' if diff < 0.01 else 'FAIL'}")
+    print("\n" + "=" * 60 + "\nMemory Analysis\n" + "-" * 60)
+    for n in (512, 1024, 2048, 4096, 8192):
+        m = flash_attention_memory_bytes(batch_size=1, num_heads=32, seq_len=n, head_dim=64)
+        print(f"Seq {n:5d}: Flash HBM={m['hbm_mb']:.1f} MB, Naive HBM={m['naive_hbm_bytes'] / 2**20:.1f} MB, "
+              f"Savings={m['memory_savings']}")
+
+
+if __name__ == "__main__":
+    _demo()

@@ -50,3 +50,12 @@ def explain_online_softmax() -> str:
 def demonstrate_online_softmax():
     x = torch.tensor([1.0, 2.0, 3.0, 4.0, 5.0])
     return standard_softmax(x), online_softmax(x)
+
+
+if __name__ == "__main__":
+    # the chapter's demo (ch06/online_softmax.py:101-115)
+    print(explain_online_softmax())
+    print("\n" + "=" * 60 + "\nVerification\n" + "-" * 60)
+    demonstrate_online_softmax()
+    xs = torch.randn(4, 8, 64)
+    print(f"\nBatch verification:\nMax difference: {(standard_softmax(xs) - online_softmax(xs)).abs().max().item():.2e}")

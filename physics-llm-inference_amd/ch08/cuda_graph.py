@@ -161,3 +161,56 @@ Solution: capture the step once, replay it with one launch.
     pli_attn_decode_dev), so one capture serves every token position;
   - new tokens are copied into the static input buffer before each replay.
 """
+
+
+def benchmark_graph_vs_eager(model_fn: Callable, input_shape: tuple, batch_size: int = 1,
+                             iterations: int = 100, warmup: int = 10, device: str = "cuda") -> dict | None:
+    """Per-call time of ``model_fn`` launched eagerly vs captured once and
+    replayed as a HIP graph (``ch08/cuda_graph.py:128-182``): wall clock with a
+    sync on both sides of the loop, microseconds per call."""
+    import time
+
+    if not torch.cuda.is_available():
+        return None
+    x = torch.randn(batch_size, *input_shape, device=device)
+
+    def per_call(fn):
+        for _ in range(warmup):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(iterations):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / iterations * 1e6
+
+    eager_us = per_call(lambda: model_fn(x))
+    static_in = torch.zeros_like(x)
+    for _ in range(warmup):  # (allocations made before the capture)
+        model_fn(static_in)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        static_out = model_fn(static_in)
+
+    def replay():
+        static_in.copy_(x)
+        graph.replay()
+
+    graph_us = per_call(replay)
+    torch.testing.assert_close(static_out, model_fn(x))
+    return {"batch_size": batch_size, "eager_us": eager_us, "graph_us": graph_us, "speedup": eager_us / graph_us}
+
+
+if __name__ == "__main__":
+    # the chapter's demo (ch08/cuda_graph.py:185-214): a three-op elementwise
+    # model, eager vs one graph launch
+    print(explain_cuda_graphs())
+    if torch.cuda.is_available():
+        print("\n" + "=" * 60 + "\nHIP Graph Benchmark\n" + "-" * 60)
+        for b in (1, 4, 16):
+            r = benchmark_graph_vs_eager(lambda t: torch.sigmoid(torch.relu(t) * 2.0), (1024,), batch_size=b,
+                                         iterations=1000)
+            print(f"Batch {b:3d}: Eager={r['eager_us']:.1f}us, Graph={r['graph_us']:.1f}us, Speedup={r['speedup']:.2f}x")
+    else:
+        print("\nno ROCm device")

@@ -173,3 +173,20 @@ Experts: two grouped launches over all experts (pli_gemm_grouped): fused
 SwiGLU (W1, W3) then W2, each expert's weights streamed once; tokens are
 read through the gather table.  Combine: one deterministic weighted sum.
 """
+
+
+if __name__ == "__main__":
+    # the chapter's demo (ch09/moe_layer.py)
+    print(explain_moe())
+    print("\n" + "=" * 60 + "\nMoE Layer Demo\n" + "-" * 60)
+    cfg = MoEConfig(hidden_dim=256, expert_dim=512, num_experts=8, num_experts_per_tok=2)
+    moe = MoELayer(cfg)
+    x = torch.randn(2, 16, 256)
+    if torch.cuda.is_available():
+        moe, x = moe.cuda(), x.cuda()
+    y = moe(x)
+    print(f"Input shape:  {x.shape}\nOutput shape: {y.shape}")
+    total = sum(p.numel() for p in moe.parameters())
+    per_expert = sum(p.numel() for p in moe.experts[0].parameters())
+    print(f"\nTotal params:        {total:,}\nParams per expert:   {per_expert:,}\n"
+          f"Active params/token: {per_expert * cfg.num_experts_per_tok:,}")

@@ -92,3 +92,51 @@ def xgmi_all_reduce_bounds(payload_bytes: float, world_size: int,
     mesh = 2 * (n - 1) / n * payload_bytes / (min(n - 1, links) * link_gbps * 1e3)
     return {"ring_us": ring, "mesh_us": mesh,
             "bus_factor": 2 * (n - 1) / n}
+
+
+def explain_nccl() -> str:
+    """The reference's collective-communication primer
+    (ch09/nccl_primitives.py:110-147), written for this build: on ROCm the
+    "nccl" backend of torch.distributed is RCCL, and MI355X GPUs talk over
+    point-to-point xGMI links instead of a switch."""
+    return (
+        "\nRCCL (the ROCm collectives behind torch.distributed's \"nccl\" backend)\n\n"
+        "Collectives a tensor-parallel / expert-parallel model uses:\n"
+        "  all-reduce      every rank ends with the sum of all ranks' buffers\n"
+        "                  (the row-parallel layer's partial products); ring cost\n"
+        "                  2 (N-1)/N x bytes per rank on the slowest link\n"
+        "  all-gather      every rank ends with every rank's shard, (N-1)/N x the\n"
+        "                  gathered bytes per rank\n"
+        "  reduce-scatter  the sum, with rank r keeping its 1/N slice (half an\n"
+        "                  all-reduce)\n"
+        "  all-to-all      rank r sends a different slice to every rank (MoE token\n"
+        "                  routing)\n\n"
+        "Ring all-reduce: the buffer is cut into N chunks; N-1 reduce steps pass\n"
+        "partial sums around the ring, N-1 gather steps pass the finished chunks.\n\n"
+        "MI355X fabric: each GPU has 7 xGMI links (~153 GB/s each) to the other 7\n"
+        "GPUs of the node -- a full mesh, not a switch -- so a single ring runs at\n"
+        "one link's rate, while a collective that uses all links at once is bounded\n"
+        "by 2 x bytes / (N x 153 GB/s) (xgmi_all_reduce_bounds).  Tensor-parallel\n"
+        "layers therefore chunk the all-reduce and overlap it with the next GEMM\n"
+        "(tensor_parallel.row_parallel_forward_overlapped).\n"
+    )
+
+
+if __name__ == "__main__":
+    # the chapter's demo (ch09/nccl_primitives.py:149-181): ring all-reduce
+    # model at the reference's 600 GB/s link, then compute / comm overlap
+    print(explain_nccl())
+    print("\n" + "=" * 60 + "\nAll-Reduce Simulation\n" + "-" * 60)
+    for n in (2, 4, 8):
+        r = simulate_all_reduce(AllReduceConfig(world_size=n, data_size_mb=100.0, bandwidth_gbps=600.0))
+        print(f"\nWorld size: {n}\n  Data size: {r['data_size_mb']:.1f} MB\n  Total time: {r['total_time_us']:.1f} us\n"
+              f"  Effective bandwidth: {r['effective_bandwidth_gbps']:.1f} GB/s\n"
+              f"  Efficiency: {r['bandwidth_efficiency']:.1%}")
+        b = xgmi_all_reduce_bounds(100.0 * 2**20, n)
+        print(f"  MI355X xGMI bounds: {b}")
+    print("\n" + "=" * 60 + "\nCommunication-Compute Overlap Analysis\n" + "-" * 60)
+    for compute_us in (100, 500, 1000):
+        o = compute_communication_overlap_potential(compute_us, 200)
+        print(f"\nCompute: {compute_us} us, Comm: 200 us\n  Sequential: {o['sequential_time_us']:.0f} us\n"
+              f"  Overlapped: {o['overlapped_time_us']:.0f} us\n  Speedup: {o['potential_speedup']:.2f}x\n"
+              f"  Bottleneck: {o['bottleneck']}")
