@@ -63,7 +63,28 @@ def measure_access_pattern(size: int = 1024 * 1024 * 32, warmup: int = 10, itera
             AccessPatternResult("strided", t_s, bw_s, min(bw_s / peak_gbps, 1.0)))
 
 
+def explain_coalescing() -> str:
+    """The reference's coalescing primer (ch05/memory_coalescing.py:85-111),
+    for a 64-lane CDNA4 wave."""
+    return (
+        "\nMemory coalescing on MI355X\n\n"
+        "A wave is 64 lanes; one vector load instruction hands the texture\n"
+        "address unit 64 addresses, and the hardware fetches whole cache lines\n"
+        "(128 B) for them.\n\n"
+        "Coalesced (good): lane i reads bytes 16 i .. 16 i + 15 (global_load_dwordx4)\n"
+        "  -> one instruction moves 1 KiB from 8 lines, every byte used\n\n"
+        "Strided (bad): lane i reads 4 bytes at 128 i\n"
+        "  -> 64 separate lines for 256 useful bytes: 1/32 of each fetch used,\n"
+        "     and the address unit spends a cycle per line\n\n"
+        "Rule: give consecutive lanes consecutive 16-byte chunks (this build's\n"
+        "GEMV and decode kernels read W / the KV cache that way, and its GEMM and\n"
+        "flash kernels stream whole 128-B rows into LDS by LDS-DMA).  The penalty\n"
+        "of the strided pattern here is measured by measure_access_pattern.\n"
+    )
+
+
 if __name__ == "__main__":
+    print(explain_coalescing())
     if torch.cuda.is_available():
         c, s = measure_access_pattern(size=1 << 28)
         print(f"Coalesced: {c.time_us:.1f} us, {c.bandwidth_gbps:.1f} GB/s ({c.efficiency:.1%})")

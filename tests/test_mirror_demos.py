@@ -14,7 +14,7 @@ import torch
 
 from conftest import PKG
 
-MAINS = ["ch06.flash_attention", "ch06.attention_memory", "ch06.online_softmax", "ch09.nccl_primitives",
+MAINS = ["ch05.memory_coalescing", "ch06.flash_attention", "ch06.attention_memory", "ch06.online_softmax", "ch09.nccl_primitives",
          "ch09.tensor_parallel", "ch05.tensor_cores", "ch05.triton_matmul", "ch05.shared_memory",
          "ch08.cuda_graph", "ch09.moe_layer"]
 
