@@ -255,7 +255,8 @@ def headline_summary(r: dict) -> dict:
     """the numbers the round's verdict reads, in one short record (the last
     key of the JSON line, so it survives any tail truncation)"""
     out = {"flash_TFLOP/s": r["roofline"]["achieved"], "flash_frac": r["roofline"]["frac"],
-           "flash_kernel_ms": r["roofline"]["kernel_ms"]}
+           "flash_kernel_ms": r["roofline"]["kernel_ms"],
+           "n_gpus": r.get("n_gpus"), "ranks_seen": r.get("ranks_seen"), "backend": r.get("backend")}
     if "unramped" in r:
         out["flash_unramped_TFLOP/s"] = r["unramped"]["TFLOP/s"]
     if "flash_causal" in r:
@@ -276,6 +277,11 @@ def headline_summary(r: dict) -> dict:
         out["tp_gemm_torch_TFLOP/s"] = t["torch_F.linear_TFLOP/s"]
         for tp, sh in t.get("shard_gemm_per_rank", {}).items():
             out[f"{tp}_shard_TFLOP/s"] = [sh["TFLOP/s"], sh["torch_F.linear_TFLOP/s"]]
+        # N > 1: the all-reduce leg (ch09 RowParallelLinear over RCCL / xGMI)
+        for key in ("allreduce_us", "total_us", "overlapped_total_us", "allreduce_busbw_GB/s",
+                    "xgmi_ring_bound_us"):
+            if key in t:
+                out[f"tp_{key}"] = t[key]
     if "decode_attn" in r:
         out["decode_attn_GB/s"] = r["decode_attn"]["GB/s"]
     if "flash_dtypes" in r:
@@ -715,7 +721,10 @@ def selftest_main(args, world: int, rank: int) -> None:
                           "data": "SELFTEST: launcher rehearsal on CPU, not a measurement",
                           "ranks_seen": int(ranks_seen.item()),
                           "backend": dist.get_backend() if world > 1 else None,
-                          "config": {"workload": "selftest"}}), file=JSON_OUT, flush=True)
+                          "config": {"workload": "selftest"},
+                          "summary": {"n_gpus": world, "ranks_seen": int(ranks_seen.item()),
+                                      "backend": dist.get_backend() if world > 1 else None}}),
+              file=JSON_OUT, flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -65,6 +65,15 @@ const char* pli_last_error(void);
  * tests and tuning: which route the dispatch took. */
 const char* pli_last_route(void);
 
+/* Synchronous debug mode: when on, every kernel launch is
+ * followed by hipDeviceSynchronize + hipGetLastError, and a failure is
+ * returned by the entry point that launched the kernel, its name in
+ * pli_last_error() ("<kernel>: kernel failed (PLI_SYNC): ...").  Starts as
+ * the environment says (PLI_SYNC=1: on; unset or 0: off).  mode 0 / 1 sets
+ * it, mode < 0 only queries; returns the previous state.  Debugging only:
+ * it serialises every call and must not be on while a stream is captured. */
+int pli_debug_sync(int mode);
+
 /*
  * Fused attention forward:  O = softmax(Q K^T * scale [+ causal mask]) V.
  *

@@ -45,10 +45,12 @@ class FlashAttentionConfig:
     num_stages: int = 2
 
 
-# what each FlashAttentionConfig knob means on the HIP path (bf16 D=128,
-# causal or not: attn_fwd_v13 / v13c -- 256-row blocks of 4 waves x 64 rows,
-# 64-key tiles, a 5-slot LDS ring two tiles ahead; fp16 / other D / short Nk
-# run attn_fwd_v12 / v10 / v7)
+# what each FlashAttentionConfig knob means on the HIP path: bf16 and fp16,
+# D = 128 and 64, causal or not, any Nk > 64 (ragged Nk included) run the
+# generated attn_fwd_v13 family (v13 / v13c / v13h / v13hc / v13r / v13rc /
+# the _d64 bodies) -- 256-row blocks of 4 waves x 64 rows, 64-key tiles, a
+# 5-slot LDS ring two tiles ahead; only other head dims and Nk <= 64 fall
+# back to attn_fwd_v12 / v10 / v7 (csrc/flash_v13.hip attn_v13_ok)
 HIP_TILING = {"block_q": 256, "block_k": 64, "num_warps": 4, "num_stages": 5}
 
 

@@ -167,7 +167,10 @@ def benchmark_graph_vs_eager(model_fn: Callable, input_shape: tuple, batch_size:
                              iterations: int = 100, warmup: int = 10, device: str = "cuda") -> dict | None:
     """Per-call time of ``model_fn`` launched eagerly vs captured once and
     replayed as a HIP graph (``ch08/cuda_graph.py:128-182``): wall clock with a
-    sync on both sides of the loop, microseconds per call."""
+    sync on both sides of the loop, microseconds per call, after ``warmup``
+    untimed calls of each form (the graph's are replays).  Returns the
+    reference's keys; checking the replayed output is the caller's business
+    (a model_fn with random ops legitimately differs call to call)."""
     import time
 
     if not torch.cuda.is_available():
@@ -197,9 +200,10 @@ def benchmark_graph_vs_eager(model_fn: Callable, input_shape: tuple, batch_size:
         static_in.copy_(x)
         graph.replay()
 
-    graph_us = per_call(replay)
-    torch.testing.assert_close(static_out, model_fn(x))
-    return {"batch_size": batch_size, "eager_us": eager_us, "graph_us": graph_us, "speedup": eager_us / graph_us}
+    graph_us = per_call(replay)  # (its warm-up calls are graph replays)
+    del static_out
+    return {"batch_size": batch_size, "input_shape": input_shape, "eager_us": eager_us, "graph_us": graph_us,
+            "speedup": eager_us / graph_us}
 
 
 if __name__ == "__main__":

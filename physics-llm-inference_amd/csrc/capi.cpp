@@ -4,6 +4,7 @@
 #include <atomic>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "pli_common.h"
@@ -27,6 +28,23 @@ void clear_error() {
     g_route[0] = 0;
 }
 
+// debug mode (PLI_SYNC=1 in the environment, or pli_debug_sync(1)): every
+// launch is followed by hipDeviceSynchronize + hipGetLastError, so a kernel
+// that faults or fails is reported by the entry point that launched it, with
+// the kernel's name in pli_last_error().  Off by default (the library never
+// synchronises); not for use while a stream is being captured into a graph.
+static std::atomic<int> g_sync{-1};
+
+static int sync_mode() {
+    int m = g_sync.load(std::memory_order_relaxed);
+    if (m < 0) {
+        const char* e = getenv("PLI_SYNC");
+        m = (e && *e && strcmp(e, "0") != 0) ? 1 : 0;
+        g_sync.store(m, std::memory_order_relaxed);
+    }
+    return m;
+}
+
 int launch_status(const char* what) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
@@ -35,6 +53,14 @@ int launch_status(const char* what) {
     }
     const size_t n = strlen(g_route);
     snprintf(g_route + n, sizeof(g_route) - n, "%s%s", n ? "+" : "", what);
+    if (sync_mode()) {
+        e = hipDeviceSynchronize();
+        if (e == hipSuccess) e = hipGetLastError();
+        if (e != hipSuccess) {
+            set_error("%s: kernel failed (PLI_SYNC): %s", what, hipGetErrorString(e));
+            return int(e);
+        }
+    }
     return PLI_OK;
 }
 
@@ -66,5 +92,11 @@ const char* pli_version(void) { return "pli_hip 0.1.0 gfx950"; }
 const char* pli_last_error(void) { return pli::g_err; }
 
 const char* pli_last_route(void) { return pli::g_route; }
+
+int pli_debug_sync(int mode) {
+    const int prev = pli::sync_mode();
+    if (mode >= 0) pli::g_sync.store(mode ? 1 : 0, std::memory_order_relaxed);
+    return prev;
+}
 
 }  // extern "C"

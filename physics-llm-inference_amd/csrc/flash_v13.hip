@@ -146,6 +146,7 @@ void put64(V13Args& a, int at, uint64_t v) {
 // at args.stamp + 128 * (workgroup * 4 + wave); lanes 15-21: the seam sums of
 // tools/v13/kernel.py Gen.seam_stamp)
 #include "flash_v13_stamp_asm.h"
+int g_diag_grid = 0;  // pli_diag_v13_set_grid: persistent grid override (0: the CU count)
 __global__ __launch_bounds__(256, 1) void attn_fwd_v13_stamp(V13Args args) {
     __shared__ __attribute__((aligned(1024))) char smem[163840];
     (void)args;
@@ -261,6 +262,11 @@ int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B,
     a.w[A_TBV] = (uint32_t)(64 * st.vn * 2);
 #ifdef PLI_FLASH_STAMPS
     if (stamps) {
+        // diagnostic: a smaller persistent grid (a multiple of 8) when asked
+        if (g_diag_grid >= 8 && g_diag_grid % 8 == 0 && g_diag_grid < grid) {
+            grid = g_diag_grid;
+            a.w[A_G] = (uint32_t)grid;
+        }
         put64(a, A_STAMP, (uint64_t)(uintptr_t)stamps);
         hipLaunchKernelGGL(attn_fwd_v13_stamp, dim3((unsigned)grid), dim3(256), 0, stream, a);
         return launch_status("attn_fwd_v13_stamp");
@@ -317,4 +323,7 @@ extern "C" int pli_diag_v13_clock(const void* q, const void* k, const void* v, v
     if (rc != 0 || hipDeviceSynchronize() != hipSuccess) return -1;
     return 0;
 }
+// the stamped launches' persistent grid (a multiple of 8 below the CU count;
+// 0 = the product's): the seam's cost against how many CUs seam together
+extern "C" void pli_diag_v13_set_grid(int grid) { pli::g_diag_grid = grid; }
 #endif

@@ -33,6 +33,7 @@ _SIGS = {
     "pli_version": [],
     "pli_last_error": [],
     "pli_last_route": [],
+    "pli_debug_sync": [_c_int],
     "pli_flash_attn_fwd": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
                            ctypes.POINTER(_c_i64), _c_f32, _c_int, _c_int, _vp],
     "pli_gemv": [_vp, _vp, _vp, _c_int, _c_int, _c_i64, _c_int, _vp],
@@ -130,6 +131,14 @@ def last_route() -> str:
     """the kernels this thread's last library call launched ('+'-separated;
     pli_last_route)"""
     return lib().pli_last_route().decode()
+
+
+def debug_sync(mode: int = -1) -> bool:
+    """the library's synchronous debug mode (pli_debug_sync; PLI_SYNC=1 in the
+    environment turns it on at load): mode 1 / 0 sets it, -1 only queries;
+    returns the previous state.  When on, every launch is synchronised and
+    checked, and a failing kernel's name is in the raised PliError."""
+    return bool(lib().pli_debug_sync(int(mode)))
 
 
 def _check(rc: int, what: str) -> None:

@@ -10,10 +10,16 @@ ch09/tensor_parallel.py:43-68) on a process group passed explicitly:
 
 At world size 1 the all-reduce is the identity, so every result must be
 bitwise equal to the same GEMMs run without the group (which also proves the
-collective ran after the GEMM that fills its buffer); at world size 2 (a+b
-commutes) the chunked and plain forms must agree bitwise, and every form must
-match a float64 product within its rounding bound.  Prints one JSON line;
-exit code 0 = pass.  argv: rank world."""
+collective ran after the GEMM that fills its buffer); at world size 2 the
+chunked and plain forms must agree within one output rounding (not bitwise:
+RCCL may pick a different reduction schedule for a 128-row chunk than for
+the whole buffer, and the small-M GEMM a different route), and every form
+must match a float64 product within its rounding bound.  Prints one JSON
+line; exit code 0 = pass.  argv: rank world.
+
+UNVERIFIED ON HARDWARE: the world-size-2 leg has never run -- the GPU pool of
+every round so far had one GPU per box, so tests/test_gpu_rccl.py skips it;
+only the world-size-1 leg (RCCL + the HIP library in one process) has run."""
 import json
 import os
 import sys
@@ -72,8 +78,13 @@ def main():
                   "f32_overlapped_eq_chunked": torch.equal(y4, pc32.to(torch.bfloat16))}
     else:
         pcs = pc_sum(pc)  # every rank calls the collective
-        checks = {"overlapped_eq_chunked_allreduce": world != 2 or torch.equal(y2, pcs),
-                  "f32_overlapped_eq_layer_2ranks": world != 2 or torch.equal(y4, y3)}
+
+        def one_rounding(a, b):  # |a - b| within a bf16 rounding of either (+ fp32 order effects)
+            a, b = a.float(), b.float()
+            return bool(((a - b).abs() <= 2.0 ** -7 * torch.maximum(a.abs(), b.abs()) + 1e-3).all())
+        checks = {"overlapped_vs_chunked_allreduce": one_rounding(y2, pcs),
+                  "f32_overlapped_vs_layer": one_rounding(y4, y3)}
+        res["f32_overlapped_vs_layer_max_diff"] = (y4.float() - y3.float()).abs().max().item()
     dist.all_reduce(mag)
     ref = olin.linear(x, w)
     bound = 1e-2 * (mag.cpu().numpy() + 1.0)

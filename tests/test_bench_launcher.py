@@ -34,6 +34,7 @@ def test_bench_gpus2_launches_two_ranks():
     assert d["n_gpus"] == 2 and d["ranks_seen"] == 2 and d["backend"] == "gloo"
     assert d["steps"] == 3 and d["warmup"] == 1 and d["value"] > 0
     assert d["data"].startswith("SELFTEST")
+    assert d["summary"] == {"n_gpus": 2, "ranks_seen": 2, "backend": "gloo"}  # the tail the driver keeps
 
 
 @pytest.mark.timeout(120)
@@ -65,3 +66,22 @@ def test_headline_summary_and_tail_order():
     assert s["causal_TFLOP/s"] == 1150.0 and s["gemv_us"] == 7.3 and s["gemv_size_matched_probe_GB/s"] == 4510.0
     assert s["tp2_shard_TFLOP/s"] == [1437.0, 1511.0] and s["flash_fp16_d128_TFLOP/s"] == [1300.0, 1108.0]
     assert len(json.dumps(s)) < 2048  # fits the tail with room to spare
+    assert s["n_gpus"] is None and "tp_allreduce_us" not in s  # (a one-GPU record)
+
+
+def test_headline_summary_multi_rank_keys():
+    """N > 1 (verdict r5 item 5): the rank count, backend and the TP
+    all-reduce leg (ch09 RowParallelLinear over RCCL) land in `summary`"""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", BENCH)
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    r = {"roofline": {"achieved": 1390.0, "frac": 0.552, "kernel_ms": 1.58}, "n_gpus": 2, "ranks_seen": 2,
+         "backend": "nccl",
+         "tp_gemm": {"gemm_TFLOP/s": 1400.0, "torch_F.linear_TFLOP/s": 1500.0, "allreduce_us": 95.0,
+                     "total_us": 480.0, "overlapped_total_us": 420.0, "allreduce_busbw_GB/s": 176.0,
+                     "xgmi_ring_bound_us": 90.0}}
+    s = bench.headline_summary(r)
+    assert (s["n_gpus"], s["ranks_seen"], s["backend"]) == (2, 2, "nccl")
+    for key in ("allreduce_us", "total_us", "overlapped_total_us", "allreduce_busbw_GB/s", "xgmi_ring_bound_us"):
+        assert s[f"tp_{key}"] == r["tp_gemm"][key]

@@ -172,3 +172,41 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     with pytest.raises(pli_hip.PliError, match="not built"):
         pli_hip.lib()
     assert not pli_hip.available()
+
+
+def test_debug_sync_switch(built_lib):
+    """PLI_SYNC debug mode: off unless the environment says
+    so, switchable through pli_debug_sync; PLI_SYNC=1 turns it on at load"""
+    import subprocess
+    import sys
+    import pli_hip
+    prev = pli_hip.debug_sync(-1)
+    try:
+        assert pli_hip.debug_sync(1) == prev and pli_hip.debug_sync(-1) is True
+        assert pli_hip.debug_sync(0) is True and pli_hip.debug_sync(-1) is False
+    finally:
+        pli_hip.debug_sync(int(prev))
+    code = "import ctypes, sys; L = ctypes.CDLL(sys.argv[1]); print(L.pli_debug_sync(-1))"
+    for env_val, want in (("1", "1"), ("0", "0"), (None, "0")):
+        env = {k: v for k, v in os.environ.items() if k != "PLI_SYNC"}
+        if env_val is not None:
+            env["PLI_SYNC"] = env_val
+        out = subprocess.run([sys.executable, "-c", code, built_lib], capture_output=True, text=True, env=env,
+                             check=True).stdout.strip()
+        assert out == want, (env_val, out)
+
+
+@pytest.mark.timeout(1500)
+def test_abi_checks_under_asan():
+    """build.py --asan: every source with AddressSanitizer on the host side,
+    and tests/asan/abi_check.c (the argument checks, empty operands,
+    workspace sizing and error strings above, from C) run against it"""
+    import subprocess
+    import sys
+    sys.path.insert(0, PKG)
+    import build as pli_build
+    exe = pli_build.build_asan(jobs=8, verbose=False)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:halt_on_error=1")
+    r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr[-4000:]
+    assert "all checks passed under AddressSanitizer" in r.stdout

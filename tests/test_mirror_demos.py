@@ -52,5 +52,18 @@ def test_gpu_mirror_demos():
     from ch08.cuda_graph import benchmark_graph_vs_eager
     v = verify_tensor_core_usage(1024)
     assert v["likely_tensor_cores"] and v["speedup"] > 1.5
-    r = benchmark_graph_vs_eager(lambda t: torch.sigmoid(torch.relu(t) * 2.0), (1024,), batch_size=4, iterations=50)
+    fn = lambda t: torch.sigmoid(torch.relu(t) * 2.0)  # noqa: E731
+    r = benchmark_graph_vs_eager(fn, (1024,), batch_size=4, iterations=50)
     assert r["eager_us"] > 0 and r["graph_us"] > 0
+    assert set(r) == {"batch_size", "input_shape", "eager_us", "graph_us", "speedup"} and r["input_shape"] == (1024,)
+    # the replayed graph computes what the eager call does (checked here, not in the helper)
+    x = torch.randn(4, 1024, device="cuda")
+    static_in = torch.zeros_like(x)
+    fn(static_in)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        static_out = fn(static_in)
+    static_in.copy_(x)
+    g.replay()
+    torch.testing.assert_close(static_out, fn(x))

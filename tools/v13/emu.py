@@ -364,6 +364,8 @@ class Emu:
         if op == "v_cvt_pk_bf16_f32":
             lo, hi = bf16_rne(gf(o[1])), bf16_rne(gf(o[2]))
             return self.vset(w, o[0], lo | (hi << 16))
+        if op == "v_cvt_f32_f16":  # the low half
+            return self.vset(w, o[0], f2u(f16_to_f32(g(o[1]) & 0xFFFF).astype(np.float32)))
         if op == "v_cvt_pk_f16_f32":
             lo, hi = f16_rne(gf(o[1])), f16_rne(gf(o[2]))
             return self.vset(w, o[0], lo | (hi << 16))

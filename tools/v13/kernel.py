@@ -325,6 +325,10 @@ SEAMWAIT = [False]
 # step after it, its all-zero P(qb 0-1, kp 1) from PV and the row sums (18
 # MFMAs): bitwise equal, +0.2-1.3 % (profiles/r05/flash/ab_beyond_diag.jsonl)
 BEYOND = [4]
+# QSEP (Gen(qsep=k), A/B knob): the tail's 16 (D 64: 8) Q loads of the next
+# block spaced k MFMA gaps apart, one per gap, instead of packed into the
+# first few gaps (0, the round-5 program)
+QSEP = [0]
 # cache-policy bits of the seam's memory operations (A/B: Gen(o_bits=...,
 # q_bits=...), e.g. "nt" / "sc1" / "sc0 sc1"); the product issues them plain
 CACHEBITS = {"o": "", "q": ""}
@@ -896,8 +900,9 @@ class Gen:
     def __init__(self, ndef=4, budget=8, dma_spacing=6, tag="%=", stamp=False, causal=False, abl=(), dma_cost=8,
                  rev=True, qscale=False, dma_pv=0, dma_pv_spacing=16, budget_pv=None, lcheck=None, dtype="bf16",
                  hd=128, short_first=False, ragged=False, oline=False, seam_wait=False, o_bits=0, q_bits=0,
-                 beyond=4):
+                 beyond=4, qsep=0):
         global DMA_COST
+        QSEP[0] = int(qsep)
         OLINE[0] = bool(oline)
         BEYOND[0] = int(beyond)
         bits = {0: "", 1: "nt", 2: "sc1", 3: "sc0 sc1", 4: "sc0 sc1 nt"}
@@ -909,7 +914,6 @@ class Gen:
         assert not (short_first and rev and causal), "short_first streams both blocks forward (rev=False)"
         assert hd in (64, 128)
         GEOM["hd"] = hd
-        assert not (qscale and hd != 128)
         # fp16: P keeps the bit check (P < 2: bit 14 of an fp16 half too) --
         # the l >= 1 test needs muoff >> log2 Nk, which fp16 P (normal down to
         # 2^-14, zero below 2^-24) cannot give; the launcher passes muoff 4
@@ -920,7 +924,6 @@ class Gen:
         assert not (dtype == "f16" and lcheck), "fp16 runs the P-bit check"
         QSCALE[0] = bool(qscale)
         assert not (qscale and lcheck), "QSCALE is built on the P-bit check (lcheck=False)"
-        assert not (qscale and dtype != "bf16")
         LCHECK[0] = bool(lcheck)
         # causal: the second block of each pair streams its tiles in the
         # reversed order of tile_of (its 8 workgroups then read every K/V
@@ -1217,13 +1220,18 @@ class Gen:
         c = []
         n = 0
         for qb in range(4):
-            for ds in range(4):
+            for ds in range(NDS()):
                 for r in range(4):
                     a = Q_(qb, ds)[r]
                     t0, t1, t2 = T(3 * (n % 8)), T(3 * (n % 8) + 1), T(3 * (n % 8) + 2)
-                    c += [I("v_accvgpr_read_b32", t0, a), I("v_lshlrev_b32", t1, 16, t0),
-                          I("v_and_b32", t2, 0xFFFF0000, t0), I("v_mul_f32", t1, sC, t1), I("v_mul_f32", t2, sC, t2),
-                          I("v_cvt_pk_bf16_f32", t0, t1, t2), I("v_accvgpr_write_b32", a, t0)]
+                    if DT["cvt"] == "v_cvt_pk_f16_f32":  # fp16 halves: widen, scale, RNE back
+                        c += [I("v_accvgpr_read_b32", t0, a), I("v_cvt_f32_f16", t1, t0),
+                              I("v_lshrrev_b32", t2, 16, t0), I("v_cvt_f32_f16", t2, t2)]
+                    else:
+                        c += [I("v_accvgpr_read_b32", t0, a), I("v_lshlrev_b32", t1, 16, t0),
+                              I("v_and_b32", t2, 0xFFFF0000, t0)]
+                    c += [I("v_mul_f32", t1, sC, t1), I("v_mul_f32", t2, sC, t2),
+                          I(DT["cvt"], t0, t1, t2), I("v_accvgpr_write_b32", a, t0)]
                     n += 1
         return c
 
@@ -1553,7 +1561,12 @@ class Gen:
         # the next block's Q rows (or this block's again past the last block)
         # (ABL "qload", timing only: no Q loads here -- every block reuses the
         # first block's Q)
-        fills += chain(self.q_offsets(sNQ0, sNQH, loads="qload" not in ABL), earliest=4)
+        qf = chain(self.q_offsets(sNQ0, sNQH, loads="qload" not in ABL), earliest=4)
+        if QSEP[0]:
+            for f in qf:
+                if f.ins[0].op == "global_load_dwordx4":
+                    f.sep, f.cost = QSEP[0], 8
+        fills += qf
         pv = pv_mfmas(X)
         body, left = schedule(pv, fills, self.budget)
         e(body)
