@@ -102,3 +102,37 @@ def test_v13_f16_explicit_scale(scale):
     err = max_err(out, ref)
     tol = 1e-2 if scale < 0.5 else 2.0 ** -8 * v.abs().max().item()
     assert err <= tol, f"scale {scale}: max |err| {err:.4e} > {tol:.4e}"
+
+
+@pytest.mark.parametrize("D", (128, 64))
+@pytest.mark.parametrize("d", (14, 18, 20, 22))
+def test_v13_f16_attention_sink_long_context(d, D):
+    """the fp16 program packs P with mu = row max * c + 4, so P <=
+    2^-4 at the row max and a weight w of the row's largest is stored as the
+    fp16 value 2^-4 w: subnormal below w = 2^-10, zero below 2^-21 (torch's
+    fp16 path, P = 1 at the max, keeps down to 2^-25).  Worst case for that:
+    an attention-sink row -- one dominant key and 32767 keys d log2 units
+    under it (their total weight 2^15 2^-d: 0.5 at d = 16, 1/128 at d = 22)
+    -- against float64 on the same fp16 inputs.  The bound is the fp16 flash
+    tolerance of the other tests (1e-2); the numpy model of the same packing
+     puts the worst case at ~8e-3, at d = 22."""
+    import pli_hip
+    N, Nq = 32768, 64
+    g = torch.Generator(device=DEV).manual_seed(100 + d + D)
+    c = D ** -0.5 * 1.4426950408889634
+    q = torch.zeros(1, 1, Nq, D, device=DEV, dtype=torch.float64)
+    q[..., 0] = 1.0
+    q[..., 1] = 0.05 * torch.randn(1, 1, Nq, device=DEV, dtype=torch.float64, generator=g)
+    k = torch.zeros(1, 1, N, D, device=DEV, dtype=torch.float64)
+    a = 8.0 / c  # the sink's score: 8 log2 units above 0
+    delta = d + 2.0 * torch.rand(N, device=DEV, dtype=torch.float64, generator=g) - 1.0
+    k[0, 0, :, 0] = a - delta / c
+    k[0, 0, 0, 0] = a  # key 0: the sink
+    k[0, 0, :, 1] = torch.randn(N, device=DEV, dtype=torch.float64, generator=g)
+    v = torch.randn(1, 1, N, D, device=DEV, dtype=torch.float64, generator=g)
+    q, k, v = (t.to(torch.float16) for t in (q, k, v))
+    ref = torch_attention(q, k, v)
+    out = pli_hip.flash_attn_fwd(q, k, v)
+    assert pli_hip.last_route().startswith("attn_fwd_v13h")
+    err = max_err(out, ref)
+    assert err <= 1e-2, f"d {d} D {D}: max |err| {err:.3e}"

@@ -322,3 +322,34 @@ def test_v13_beyond_light_steps_vs_f64(case):
     err = np.abs(o - f64_attention(q, k, v, True, dtype=dtype)).max()
     assert err <= 1e-2, f"max |err| {err:.3e}"
     assert analyse(R.program(causal=True, dtype=dtype, hd=D, ragged=Nk % 64 != 0, beyond=True)) == {}
+
+
+BALANCED_CASES = [  # (B, H, Hkv, Nq, Nk, grid, muoff, D, dtype): Gen(causal=True, balanced=True)
+    (1, 2, 1, 256, 512, None, 62.0, 128, "bf16"),    # diagonal offset 4 tiles: plain tiles, then the group
+    (1, 1, 1, 512, 512, None, 0.0, 128, "bf16"),     # two blocks, the rescale path at every tile (dead rows too)
+    (1, 2, 1, 200, 512, None, 62.0, 128, "bf16"),    # virtual rows (+ 56), offset 312
+    (1, 8, 8, 1000, 1024, 16, 62.0, 128, "bf16"),    # the pair walk: reversed blocks start on the group
+    (1, 1, 1, 320, 320, None, 62.0, 128, "bf16"),    # 320 rows: the last block's group clipped at sTD + 1
+    (1, 2, 1, 256, 512, None, 4.0, 128, "f16"),      # fp16 (P-bit check; row sums inside PV)
+    (1, 1, 1, 256, 256, None, -1.0, 64, "f16"),      # D 64 fp16, rescales at nearly every tile
+    (1, 2, 1, 256, 512, None, 62.0, 64, "bf16"),     # D 64
+]
+
+
+@pytest.mark.parametrize("case", BALANCED_CASES,
+                         ids=lambda c: "balanced-b{}h{}kv{}q{}k{}g{}-mu{}-d{}-{}".format(*c))
+def test_v13_balanced_causal_vs_f64(case):
+    """causal with the interleaved q-block rows (Gen(balanced=True)): every
+    wave has one 16-row q-block on each diagonal tile; group steps drop the
+    dead q-blocks' chains, softmax and PV, and mask the diagonal q-block by
+    VALU against LIMW"""
+    B, H, Hkv, Nq, Nk, grid, muoff, D, dtype = case
+    rng = np.random.default_rng(23 + sum(case[:5]) + D)
+    q = rng.standard_normal((B, H, Nq, D))
+    k = rng.standard_normal((B, Hkv, Nk, D))
+    v = rng.standard_normal((B, Hkv, Nk, D))
+    o, em = R.run(q, k, v, grid=grid, muoff=muoff, causal=True, dtype=dtype, balanced=True)
+    err = np.abs(o - f64_attention(q, k, v, True, dtype=dtype)).max()
+    assert err <= 1e-2, f"max |err| {err:.3e}"
+    if muoff <= 0:
+        assert em.counts.get("v_sub_f32", 0) > 0, "the rescale path never ran"

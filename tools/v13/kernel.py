@@ -325,6 +325,36 @@ SEAMWAIT = [False]
 # step after it, its all-zero P(qb 0-1, kp 1) from PV and the row sums (18
 # MFMAs): bitwise equal, +0.2-1.3 % (profiles/r05/flash/ab_beyond_diag.jsonl)
 BEYOND = [4]
+# BALANCED (Gen(causal=True, balanced=True), non-ragged causal): the wave's
+# four 16-row q-blocks are interleaved over the block's 256 rows -- q-block qb
+# of wave w holds rows 64 qb + 16 w + i instead of 64 w + 16 qb + i -- so
+# every wave has one q-block on each of the four diagonal key tiles.  Key tile
+# sTD + m (m = 0..3) is then the same work for all four waves: q-blocks qb < m
+# are past the diagonal (no QK chains, no softmax, P = 0; the next step drops
+# their PV MFMAs), q-block m is the diagonal one (its scores masked by VALU
+# against LIMW = 16 w + i - 4 g), q-blocks above it are whole.  In the
+# row-contiguous layout the waves reach their diagonal tiles one tile apart
+# and wait for each other at every step's barrier (the diagonal group costs
+# ~3.7 tile-times per block; balanced ~2.5)
+BALANCED = [False]
+
+
+def RS():
+    """row stride between a wave's q-blocks (BALANCED: 64, else 16)"""
+    return 64 if BALANCED[0] else 16
+
+
+def WROW():
+    """log2 of the row offset of wave w's first row (BALANCED: 16 w, else 64 w)"""
+    return 4 if BALANCED[0] else 6
+
+
+LIMW = V(206)  # BALANCED: 16 w + i - 4 g (TRI's register: no diagonal C operand)
+
+# NORELOAD (Gen(noreload=True), A/B knob): the block transition does not
+# reload argument dwords 0..36 into s56..s92 (no instruction writes them; the
+# reload's s_load + lgkmcnt(0) sits on the seam's critical path)
+NORELOAD = [False]
 # QSEP (Gen(qsep=k), A/B knob): the tail's 16 (D 64: 8) Q loads of the next
 # block spaced k MFMA gaps apart, one per gap, instead of packed into the
 # first few gaps (0, the round-5 program)
@@ -648,8 +678,8 @@ def block_params(sx, causal=False, uid=0, rev=0):
             c += [I("s_cmp_ge_u32", sT8, 4), I("s_cselect_b32", sRET, sRET, 0)]
     else:
         c += [I("s_mov_b32", sT8, ARG(AI["nt"]))]
-    # q0 = qblk * 256 + 64 * wave
-    c += [I("s_lshl_b32", sT2, sT2, 8), I("s_lshr_b32", sT3, sWKOFF, WSH() - 6), I("s_add_u32", sNQ0, sT2, sT3)]
+    # q0 = qblk * 256 + 64 * wave (BALANCED: + 16 * wave)
+    c += [I("s_lshl_b32", sT2, sT2, 8), I("s_lshr_b32", sT3, sWKOFF, WSH() - WROW()), I("s_add_u32", sNQ0, sT2, sT3)]
     # b = bh / H, h = bh - b * H, hk = h / group
     c += div_magic(sT4, sT5, ARG(AI["magh"]), 5)
     c += [I("s_lshr_b32", sT2, ARG(AI["shifts"]), 16), I("s_mul_i32", sT2, sT4, sT2), I("s_sub_u32", sT3, sT5, sT2)]
@@ -856,16 +886,28 @@ def rag_shift(k, v, sub):
 def mask_tile(tile):
     """causal, straight line (prologue and rare path): scores of the tile
     whose index is in SGPR `tile` with key > row + off set to -inf.  Lane
-    (g, i) holds key 64 tile + 16 kb + 4 g + r of row q0 + 16 qb + i: masked
-    iff 16 (kb - qb) + r > lim = q0 + 64 (off - tile) + i - 4 g"""
+    (g, i) holds key 64 tile + 16 kb + 4 g + r of row q0 + RS qb + i (RS 16,
+    BALANCED 64): masked iff 16 kb - RS qb + r > lim = q0 + 64 (off - tile)
+    + i - 4 g"""
     lim = T(37)
     c = [I("s_sub_u32", sT7, sOFFT, tile), I("s_lshl_b32", sT7, sT7, 6), I("s_add_u32", sT7, sT7, sCQ0),
          I("v_add_u32", lim, sT7, VI), I("v_lshlrev_b32", T(36), 2, VG), I("v_sub_u32", lim, lim, T(36))]
     for qb in range(4):
         for kb in range(4):
             for r in range(4):
-                c += [I("v_cmp_gt_i32_e32", VCC, 16 * (kb - qb) + r, lim),
+                c += [I("v_cmp_gt_i32_e32", VCC, 16 * kb - RS() * qb + r, lim),
                       I("v_cndmask_b32_e32", S_(kb, qb)[r], S_(kb, qb)[r], NINF[0], VCC)]
+    return c
+
+
+def grp_block(kb, qb):
+    """BALANCED: S(kb, qb) of the q-block on its diagonal tile masked to -inf
+    where the key is past the row: key 16 kb + 4 g + r of the tile against
+    row 16 w + i of the q-block's 64-row group (masked iff 16 kb + r > LIMW)"""
+    c = []
+    for r in range(4):
+        c += [I("v_cmp_gt_i32_e32", VCC, 16 * kb + r, LIMW),
+              I("v_cndmask_b32_e32", S_(kb, qb)[r], S_(kb, qb)[r], NINF[0], VCC)]
     return c
 
 
@@ -900,9 +942,12 @@ class Gen:
     def __init__(self, ndef=4, budget=8, dma_spacing=6, tag="%=", stamp=False, causal=False, abl=(), dma_cost=8,
                  rev=True, qscale=False, dma_pv=0, dma_pv_spacing=16, budget_pv=None, lcheck=None, dtype="bf16",
                  hd=128, short_first=False, ragged=False, oline=False, seam_wait=False, o_bits=0, q_bits=0,
-                 beyond=4, qsep=0):
+                 beyond=4, qsep=0, balanced=False, noreload=False):
         global DMA_COST
+        NORELOAD[0] = bool(noreload)
         QSEP[0] = int(qsep)
+        # (balanced applies to the non-ragged causal programs; the others ignore it)
+        BALANCED[0] = bool(balanced) and causal and not ragged
         OLINE[0] = bool(oline)
         BEYOND[0] = int(beyond)
         bits = {0: "", 1: "nt", 2: "sc1", 3: "sc0 sc1", 4: "sc0 sc1 nt"}
@@ -1026,11 +1071,17 @@ class Gen:
            I("s_mov_b32", sSM1, 4 * SLOT)])
         if self.causal:
             e([I("v_mov_b32", NINF[k], 0xFF800000) for k in range(4)])
-            # diagonal block: key 4g + r of the block masked above query i
-            e([I("v_lshlrev_b32", T(0), 2, VG)])
-            for r in range(4):
-                e([I("v_add_u32", T(1), r, T(0)), I("v_cmp_lt_i32_e32", VCC, VI, T(1)),
-                   I("v_cndmask_b32_e32", TRI[r], 0, NINF[0], VCC)])
+            if BALANCED[0]:
+                # LIMW = 16 w + i - 4 g: the diagonal q-block's key 16 kb + 4 g + r
+                # is past row 16 w + i iff 16 kb + r > LIMW
+                e([I("v_lshlrev_b32", T(0), 2, VG), I("s_lshr_b32", sT2, sWKOFF, WSH() - 4),
+                   I("v_add_u32", T(1), sT2, VI), I("v_sub_u32", LIMW, T(1), T(0))])
+            else:
+                # diagonal block: key 4g + r of the block masked above query i
+                e([I("v_lshlrev_b32", T(0), 2, VG)])
+                for r in range(4):
+                    e([I("v_add_u32", T(1), r, T(0)), I("v_cmp_lt_i32_e32", VCC, VI, T(1)),
+                       I("v_cndmask_b32_e32", TRI[r], 0, NINF[0], VCC)])
 
     # ---- per-block scalar setup -----------------------------------------
     def q_offsets(self, q0, qh, loads=True):
@@ -1041,7 +1092,7 @@ class Gen:
         if self.causal:
             c += qshift(sT1, sT2)
         for qb in range(4):
-            c += [I("v_add_u32", T(0), q0, VI), I("v_add_u32", T(0), 16 * qb, T(0))]
+            c += [I("v_add_u32", T(0), q0, VI), I("v_add_u32", T(0), RS() * qb, T(0))]
             if self.causal:
                 c += [I("v_max_u32", T(0), sT1, T(0)), I("v_subrev_u32", T(0), sT1, T(0))]
             c += [I("v_min_u32", T(0), sT0, T(0)), I("v_mul_lo_u32", T(0), T(0), ARG(AI["qn"])),
@@ -1295,6 +1346,20 @@ class Gen:
         if self.rev:
             e(self.tile_of(sT0, sT))
             tl = sT0
+        if BALANCED[0]:
+            # tiles below the diagonal group: the plain step; tile sTD + m:
+            # group step m (every block ends at sTD + 3 or before)
+            gl = [Lb(f"grp{m}_{u}") for m in range(4)]
+            e([I("s_cmp_lt_u32", tl, sTD), I("s_cbranch_scc1", n), I("s_sub_u32", sT1, tl, sTD)] +
+              [x for m in range(3) for x in (I("s_cmp_eq_u32", sT1, m), I("s_cbranch_scc1", gl[m]))] +
+              [I("s_branch", gl[3])])
+            e([label(n)])
+            self.step(X, None)
+            for m in range(4):
+                e([I("s_branch", cont), label(gl[m])])
+                self.step(X, ("grp", m))
+            e([label(cont)])
+            return
         rg, by = Lb(f"rag{u}"), Lb(f"beyond{u}")
         if RAGGED[0]:
             # key tile NT - 1 holds keys Nk - 64 .. Nk - 1: the rag step (a
@@ -1358,6 +1423,21 @@ class Gen:
         """causal (BEYOND): the last tile past this wave's diagonal (forward
         blocks of waves 0-2) adds nothing to O or l -- only the next block's
         Q loads run"""
+        if BALANCED[0]:
+            # the last tile of a forward block is normally group tile sTD + 3,
+            # whose q-blocks 0-2 are dead: the tail's PV runs on q-block 3 only
+            e, Lb = self.emit, self.L
+            u = self.new_uid()
+            g3, done = Lb(f"tailg3_{u}"), Lb(f"tailed{u}")
+            e([I("s_sub_u32", sT1, sNT, 1)])
+            if self.rev:
+                e(self.tile_of(sT1, sT1))
+            e([I("s_add_u32", sT2, sTD, 3), I("s_cmp_eq_u32", sT1, sT2), I("s_cbranch_scc1", g3)])
+            self.tail(X)
+            e([I("s_branch", done), label(g3)])
+            self.tail(X, dead=3)
+            e([label(done)])
+            return
         if not (self.causal and BEYOND[0] >= 2):
             self.tail(X)
             return
@@ -1430,6 +1510,20 @@ class Gen:
             dl = lambda qb, kb: first(kb, qb) - 1  # noqa: E731
             e([I("v_mov_b32", S_(kb, qb)[r], NINF[0]) for qb in range(4) for kb in range(4) if kb > qb
                for r in range(4)])
+        grp = mask[1] if isinstance(mask, tuple) and mask[0] == "grp" else None
+        if grp is not None:
+            # BALANCED, tile sTD + grp: q-blocks below grp are past the
+            # diagonal (no QK chains; their P = 0 below), q-block grp is masked
+            # by VALU as its S blocks complete
+            dead = {S_(kb, qb).i for qb in range(grp) for kb in range(4)}
+            keep = [j for j, m in enumerate(qk) if not (m.op == DT["mfma"] and m.ops[0].i in dead)]
+            newpos = {j: n for n, j in enumerate(keep)}
+            qk = [qk[j] for j in keep]
+            done0, first0 = done, first
+            done = lambda kb, qb: newpos[done0(kb, qb)] if qb >= grp else -3  # noqa: E731
+            first = lambda kb, qb: newpos[first0(kb, qb)] if qb >= grp else 0  # noqa: E731
+            dl = lambda qb, kb: first(kb, qb) - 1  # noqa: E731
+            now = [sl for sl in now if sl[0] >= grp]
         f_def, cvd, last_or_prev = softmax_fills(Xp, dfr, lambda qb, kb: 0, dl, ytag=0)
         if "soft" in ABL:
             f_def = []
@@ -1451,8 +1545,8 @@ class Gen:
                 if "vread" not in ABL and light:
                     fills.append(Fill(ins, 2, earliest=0, tag="vread0"))
                 elif "vread" not in ABL:
-                    fills.append(Fill(ins, 2, earliest=(40 if GEOM["hd"] == 128 and not diag_skip else len(qk) - 32) +
-                                      8 * db, tag="vread"))
+                    fills.append(Fill(ins, 2, earliest=(40 if GEOM["hd"] == 128 and not diag_skip and grp is None
+                                                        else len(qk) - 32) + 8 * db, tag="vread"))
         # softmax(t), zero ACC(X) first (P-bit check)
         z = Fill(I("v_mov_b32", ACC(X), 0), 4, tag="zero")
         if not LCHECK[0]:
@@ -1468,9 +1562,14 @@ class Gen:
                     rag[(kb, qb)] = Fill(rag_block(kb, qb), 16, deps=[rsetup], sep=1, earliest=done(kb, qb) + 3,
                                          tag="ragmask")
                     fills.append(rag[(kb, qb)])
+        if grp is not None:
+            for kb in range(4):
+                rag[(kb, grp)] = Fill(grp_block(kb, grp), 16, earliest=done(kb, grp) + 3, tag="ragmask")
+                fills.append(rag[(kb, grp)])
         f_now, cvn, last_or = softmax_fills(X, now, lambda qb, kb: done(kb, qb) + 3, ytag=len(dfr),
                                             prev_cv=cvd,
-                                            extra_deps=(lambda qb, kb: [rag[(kb, qb)]]) if rag else None)
+                                            extra_deps=(lambda qb, kb: [rag[(kb, qb)]] if (kb, qb) in rag else [])
+                                            if rag else None)
         now_groups = softmax_fills.groups
         if "soft" in ABL or light:
             f_now, now_groups = [], []
@@ -1488,15 +1587,21 @@ class Gen:
         # a slice of tile t that has started finishes before the check: the
         # rare path redoes every P of t from S, and a slice whose fma ran
         # with the old mu must not write its P after that
-        for grp in now_groups:
-            if any(f.gap is not None for f in grp):
-                pend_prev += [f for f in grp if f.gap is None]
+        for sg in now_groups:
+            if any(f.gap is not None for f in sg):
+                pend_prev += [f for f in sg if f.gap is None]
         e(drain(pend_prev, len(qk) - 1))
         left = [f for f in left if f.gap is None]
         # light (BEYOND >= 4): tile t-1 is the diagonal one, whose P(qb, kp = 1)
         # for qb 0, 1 (rows 0-31 x keys 32-63) is all zero: no row sums or PV
         # MFMAs on them
         pdead = {P_(Xp, qb, 1).i for qb in (0, 1)} if light and BEYOND[0] >= 4 else set()
+        if grp is not None:
+            # BALANCED: this tile's dead q-blocks have P = 0; tile t-1 was
+            # group step grp - 1 (either stream order), whose q-blocks below
+            # grp - 1 were dead: no PV MFMAs on them
+            e([I("v_mov_b32", P_(X, qb, kp)[r], 0) for qb in range(grp) for kp in range(2) for r in range(4)])
+            pdead = {P_(Xp, qb, kp).i for qb in range(grp - 1) for kp in range(2)}
         if light:
             if LCHECK[0]:
                 e([m for m in rowsum_mfmas(Xp) if m.ops[2].i not in pdead])
@@ -1537,9 +1642,10 @@ class Gen:
         e(body)
         e(drain(left, B0 + len(pv) - 1))
 
-    def tail(self, X):
+    def tail(self, X, dead=0):
         """last tile T (state X): its deferred slices, its check, PV(T) with
-        the next block's Q loads beside it"""
+        the next block's Q loads beside it (BALANCED: q-blocks below `dead`
+        have P = 0 -- no PV MFMAs on them)"""
         e = self.emit
         e(self.seam_stamp(0))
         dfr, _ = self.deferred()
@@ -1552,12 +1658,31 @@ class Gen:
         if LCHECK[0]:
             e(rowsum_mfmas(X))
         self.check(X, f"rare_t{X}")
-        e(v_reads(0) + v_reads(1))
         fills = []
-        for db in range(2, NDB()):
-            for ins in v_reads(db):
-                fills.append(Fill(ins, 2, earliest=vbuf_free(db) if db >= 3 else 0,
-                                  deadline=pv_first_gap(db) - 6, tag="vread"))
+        if dead:
+            # BALANCED tail on group tile sTD + 3: only q-blocks >= dead are
+            # live, so PV(T) is 2 (4 - dead) MFMAs per d-block -- too few to
+            # hide the V^T reads behind the 3-buffer rotation; every d-block
+            # is read up front into its own buffer instead (the three V^T
+            # buffers, the other P state and this state's dead P words)
+            bufs = [V(128 + 8 * b) for b in range(NVF)] + \
+                [V(64 + 32 * (1 - X) + 8 * j) for j in range(4)] + [V(64 + 32 * X + 8 * j) for j in range(dead)]
+            assert len(bufs) >= NDB()
+            for db in range(NDB()):
+                for ins in v_reads(db):
+                    d = ins.ops[0]
+                    e([I(ins.op, V(bufs[db].i + (d.i - 128) % 8, 2), ins.ops[1], mods=ins.mods)])
+            pv = [mfma(O_(db, qb), V(bufs[db].i + 4 * kp, 4), P_(X, qb, kp), O_(db, qb))
+                  for db in range(NDB()) for kp in range(2) for qb in range(dead, 4)]
+            if not LCHECK[0]:  # (the P-bit check's row sums run with PV)
+                pv += [mfma(L_(qb), ONES, P_(X, qb, kp), L_(qb)) for qb in range(dead, 4) for kp in range(2)]
+        else:
+            e(v_reads(0) + v_reads(1))
+            pv = pv_mfmas(X)
+            for db in range(2, NDB()):
+                for ins in v_reads(db):
+                    fills.append(Fill(ins, 2, earliest=vbuf_free(db) if db >= 3 else 0,
+                                      deadline=pv_first_gap(db) - 6, tag="vread"))
         # the next block's Q rows (or this block's again past the last block)
         # (ABL "qload", timing only: no Q loads here -- every block reuses the
         # first block's Q)
@@ -1567,7 +1692,6 @@ class Gen:
                 if f.ins[0].op == "global_load_dwordx4":
                     f.sep, f.cost = QSEP[0], 8
         fills += qf
-        pv = pv_mfmas(X)
         body, left = schedule(pv, fills, self.budget)
         e(body)
         e(drain(left, len(pv) - 1))
@@ -1590,9 +1714,9 @@ class Gen:
             # of a 128-B line, j >= 8: the second), the Y stores rows 8 + (j & 7)
             if OLINE[0]:
                 e([I("v_and_b32", T(24), 7, VI), I("v_add_u32", T(24), sCQ0, T(24)),
-                   I("v_add_u32", T(24), 16 * qb, T(24))])
+                   I("v_add_u32", T(24), RS() * qb, T(24))])
             else:
-                e([I("v_add_u32", T(24), sCQ0, VI), I("v_add_u32", T(24), 16 * qb, T(24))])
+                e([I("v_add_u32", T(24), sCQ0, VI), I("v_add_u32", T(24), RS() * qb, T(24))])
             if self.causal:
                 e([I("v_subrev_u32", T(24), sT1, T(24))])
             e([I("v_mul_lo_u32", T(25), T(24), ARG(AI["on"])),
@@ -1666,7 +1790,8 @@ class Gen:
             e([I("s_cmp_eq_u32", sHASN, 0), I("s_cbranch_scc1", Lb("end"))])
             e([I("s_add_u32", sL, sL, ARG(AI["G"])), I("s_mov_b64", sCOH, sNOH), I("s_mov_b32", sCQ0, sNQ0),
                I("s_mov_b32", sNT, sNXNT)])
-        e(load_args())
+        if not NORELOAD[0]:
+            e(load_args())
         e(self._next_params())
         e([I("s_branch", Lb("common"))])
 
