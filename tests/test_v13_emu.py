@@ -328,7 +328,7 @@ BALANCED_CASES = [  # (B, H, Hkv, Nq, Nk, grid, muoff, D, dtype): Gen(causal=Tru
     (1, 2, 1, 256, 512, None, 62.0, 128, "bf16"),    # diagonal offset 4 tiles: plain tiles, then the group
     (1, 1, 1, 512, 512, None, 0.0, 128, "bf16"),     # two blocks, the rescale path at every tile (dead rows too)
     (1, 2, 1, 200, 512, None, 62.0, 128, "bf16"),    # virtual rows (+ 56), offset 312
-    (1, 8, 8, 1000, 1024, 16, 62.0, 128, "bf16"),    # the pair walk: reversed blocks start on the group
+    (1, 8, 8, 512, 512, 8, 62.0, 128, "bf16"),       # the pair walk: reversed blocks start on the group
     (1, 1, 1, 320, 320, None, 62.0, 128, "bf16"),    # 320 rows: the last block's group clipped at sTD + 1
     (1, 2, 1, 256, 512, None, 4.0, 128, "f16"),      # fp16 (P-bit check; row sums inside PV)
     (1, 1, 1, 256, 256, None, -1.0, 64, "f16"),      # D 64 fp16, rescales at nearly every tile
@@ -353,3 +353,25 @@ def test_v13_balanced_causal_vs_f64(case):
     assert err <= 1e-2, f"max |err| {err:.3e}"
     if muoff <= 0:
         assert em.counts.get("v_sub_f32", 0) > 0, "the rescale path never ran"
+
+
+@pytest.mark.parametrize("D", (128, 64))
+def test_v13_qscale_f16_first_tile_far_below_zero(D):
+    """The fp16 QSCALE program (the product's non-causal fp16 bodies): every
+    score of the first tile ~ -120 log2 units and lower after it
+    (tests/stress_cases.py "first", shrunk).  The prologue must leave S
+    shifted (c s - mu) in place for the next step's deferred slices, which
+    exp S in place; reading it unshifted gives P = 2^(c s) = 0 for the rows'
+    largest keys (caught on the GPU in round 6: non-finite output)."""
+    rng = np.random.default_rng(31)
+    q = rng.standard_normal((1, 1, 256, D))
+    k = rng.standard_normal((1, 1, 256, D))
+    v = rng.standard_normal((1, 1, 256, D))
+    sgn = np.sign(q[:, :, :1])
+    q = np.abs(q) * sgn
+    k[:, :, :64] = -16.0 * sgn * np.abs(k[:, :, :64]) * np.sqrt(128 / D)
+    k[:, :, 64:] = -20.0 * sgn * np.abs(k[:, :, 64:]) * np.sqrt(128 / D)
+    o, em = R.run(q, k, v, muoff=4.0, dtype="f16", qscale=True)
+    assert np.isfinite(o).all()
+    err = np.abs(o - f64_attention(q, k, v, dtype="f16")).max()
+    assert err <= 2.0 ** -8 * np.abs(v).max(), f"max |err| {err:.3e}"

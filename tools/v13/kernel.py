@@ -255,6 +255,7 @@ class Fill:
 
 
 LDS_GAP = 1024  # LDS bytes per wave per 16-cycle gap (256 B/clk per CU, 4 waves)
+TRANS_PER_GAP = [1]  # transcendental fills per gap (Gen(trans=...), A/B knob)
 
 # timing-only A/B knobs (tools/build_v13_ab.sh; Gen(abl=..., dma_cost=...)):
 # ABL "dma" drops the LDS-DMA loads, "exp" turns v_exp_f32 into v_mov_b32,
@@ -355,6 +356,10 @@ LIMW = V(206)  # BALANCED: 16 w + i - 4 g (TRI's register: no diagonal C operand
 # reload argument dwords 0..36 into s56..s92 (no instruction writes them; the
 # reload's s_load + lgkmcnt(0) sits on the seam's critical path)
 NORELOAD = [False]
+# PROPIPE (Gen(propipe=True), non-causal, A/B knob): the first tile's row
+# max, mu and P of q-block qb run in the gaps of QK(0)'s later q-blocks
+# instead of straight-line after QK(0)
+PROPIPE = [False]
 # QSEP (Gen(qsep=k), A/B knob): the tail's 16 (D 64: 8) Q loads of the next
 # block spaced k MFMA gaps apart, one per gap, instead of packed into the
 # first few gaps (0, the round-5 program)
@@ -373,7 +378,7 @@ def schedule(mfmas, fills, budget=8, gap_offset=0, lds_gap=LDS_GAP):
     for k0, m in enumerate(mfmas):
         k = k0 + gap_offset
         out.append(m)
-        used, trans, lds = 0, False, 0
+        used, trans, lds = 0, 0, 0
         for f in fills:
             if f.gap is not None or f.earliest > k:
                 continue
@@ -381,7 +386,7 @@ def schedule(mfmas, fills, budget=8, gap_offset=0, lds_gap=LDS_GAP):
                 continue
             forced = f.deadline is not None and f.deadline <= k
             if not forced:
-                if f.trans and trans:
+                if f.trans and trans >= TRANS_PER_GAP[0]:
                     continue
                 if f.lds and lds + f.lds > lds_gap:
                     continue
@@ -392,7 +397,7 @@ def schedule(mfmas, fills, budget=8, gap_offset=0, lds_gap=LDS_GAP):
             out.extend(f.ins)
             used += f.cost
             lds += f.lds
-            trans = trans or f.trans
+            trans += int(bool(f.trans))
     for f in fills:
         if f.hard and (f.gap is None or f.gap > f.deadline):
             raise RuntimeError(f"fill {f.tag} {f.ins[0]} missed its hard deadline {f.deadline} (gap {f.gap})")
@@ -830,8 +835,10 @@ def exps_all(X, also_or=False, shifted=False):
         if QSCALE[0] and shifted:
             c += [I("v_exp_f32", y0, s[2 * hh]), I("v_exp_f32", y1, s[2 * hh + 1])]
         elif QSCALE[0]:
-            c += [I("v_sub_f32", y0, s[2 * hh], MU(qb)), I("v_sub_f32", y1, s[2 * hh + 1], MU(qb)),
-                  I("v_exp_f32", y0, y0), I("v_exp_f32", y1, y1)]
+            # S = c s - mu written back in place: the next step's deferred
+            # slices of this tile exp S in place and expect it shifted
+            c += [I("v_sub_f32", s[2 * hh], s[2 * hh], MU(qb)), I("v_sub_f32", s[2 * hh + 1], s[2 * hh + 1], MU(qb)),
+                  I("v_exp_f32", y0, s[2 * hh]), I("v_exp_f32", y1, s[2 * hh + 1])]
         else:
             xm = "clamp" if LCHECK[0] else ""
             c += [I("v_fma_f32", y0, s[2 * hh], sC, Neg(MU(qb))), I("v_fma_f32", y1, s[2 * hh + 1], sC, Neg(MU(qb))),
@@ -942,8 +949,10 @@ class Gen:
     def __init__(self, ndef=4, budget=8, dma_spacing=6, tag="%=", stamp=False, causal=False, abl=(), dma_cost=8,
                  rev=True, qscale=False, dma_pv=0, dma_pv_spacing=16, budget_pv=None, lcheck=None, dtype="bf16",
                  hd=128, short_first=False, ragged=False, oline=False, seam_wait=False, o_bits=0, q_bits=0,
-                 beyond=4, qsep=0, balanced=False, noreload=False):
+                 beyond=4, qsep=0, balanced=False, noreload=False, propipe=False, trans=1):
         global DMA_COST
+        TRANS_PER_GAP[0] = int(trans)
+        PROPIPE[0] = bool(propipe)
         NORELOAD[0] = bool(noreload)
         QSEP[0] = int(qsep)
         # (balanced applies to the non-ragged causal programs; the others ignore it)
@@ -1220,6 +1229,19 @@ class Gen:
         e(k_reads())
         fills = dma_fills(sSP2, earliest0=1, spacing=4, rev=self.rev)
         qk0 = qk_mfmas()
+        if PROPIPE[0] and not self.causal:
+            # non-causal: q-block qb's exact row max, mu and P in the gaps of
+            # QK(0)'s later q-blocks (QK runs q-block major)
+            fills += self.prologue_fills()
+            body, left = schedule(qk0, fills, self.budget)
+            e(body)
+            e(drain(left, len(qk0)))
+            e([I("s_waitcnt", f"vmcnt({NPW()})"), I("s_barrier"), I("v_add_u32", VKA, sSP1, VKL)])
+            e(k_reads())
+            e([I("s_mov_b32", sT, 1)])
+            e(self.seam_stamp(5))
+            self.loop_and_tails()
+            return
         body, left = schedule(qk0, fills, self.budget)
         e(body)
         e(drain(left, len(qk0)))
@@ -1247,6 +1269,54 @@ class Gen:
         e(k_reads())
         e([I("s_mov_b32", sT, 1)])
         e(self.seam_stamp(5))
+        self.loop_and_tails()
+
+    def prologue_fills(self):
+        """PROPIPE: per q-block, the row max of tile 0 and mu (one fill after
+        its S blocks complete), then its P slices (the 4 deferred slices are
+        left to step 1, which computes them from S; QSCALE shifts their S in
+        place, S = c s - mu, as step 1 expects)"""
+        dfr, now = self.deferred()
+        fills, prev_rm, cv = [], None, {}
+        for qb in range(4):
+            ins = row_max(qb, T(20 + qb), T(30), T(31))
+            if QSCALE[0]:
+                ins += [I("v_add_f32", MU(qb), sT8, T(20 + qb))] + \
+                    [I("v_sub_f32", MUC(qb)[r], 0, MU(qb)) for r in range(4)]
+            else:
+                ins += [I("v_mul_f32", T(20 + qb), sC, T(20 + qb)), I("v_add_f32", MU(qb), sT8, T(20 + qb))]
+            rm = Fill(ins, 16, deps=[prev_rm] if prev_rm else [], sep=0, earliest=qk_done_gap(3, qb) + 3,
+                      tag="rowmax")
+            fills.append(rm)
+            prev_rm = rm
+            mine = [sl for sl in now if sl[0] == qb]
+            if QSCALE[0]:
+                n = 0
+                for (q_, kb, hh) in [sl for sl in dfr + now if sl[0] == qb]:
+                    sw = S_(kb, qb)
+                    sh = Fill([I("v_sub_f32", sw[2 * hh], sw[2 * hh], MU(qb)),
+                               I("v_sub_f32", sw[2 * hh + 1], sw[2 * hh + 1], MU(qb))], 8, deps=[rm], sep=1,
+                              tag="shift")
+                    fills.append(sh)
+                    if (q_, kb, hh) in dfr:
+                        continue
+                    slot = (8 * qb + n) % (NY // 2)
+                    n += 1
+                    y0, y1 = Y(2 * slot), Y(2 * slot + 1)
+                    dep = [sh] + ([cv[slot]] if slot in cv else [])
+                    e0 = Fill(I("v_exp_f32", y0, sw[2 * hh]), 8, trans=True, deps=dep, sep=1, tag="exp")
+                    e1 = Fill(I("v_exp_f32", y1, sw[2 * hh + 1]), 8, trans=True, deps=dep, sep=1, tag="exp")
+                    w = P_(0, qb, kb >> 1)[2 * (kb & 1) + hh]
+                    cv[slot] = Fill(I(DT["cvt"], w, y0, y1), 4, deps=[e0, e1], sep=1, tag="cvt")
+                    fills += [e0, e1, cv[slot]]
+            else:
+                f, cv, _ = softmax_fills(0, mine, lambda q_, kb: 0, ytag=8 * qb, prev_cv=cv,
+                                         extra_deps=lambda q_, kb: [rm])
+                fills += [x for x in f if x.tag != "or"]
+        return fills
+
+    def loop_and_tails(self):
+        e, Lb = self.emit, self.L
         # steps t = 1 .. nt-1, two per iteration (P states 1 / 0)
         e([label(Lb("loop"))])
         self.step_dispatch(1)
