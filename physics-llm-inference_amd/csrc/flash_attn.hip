@@ -571,9 +571,28 @@ constexpr int kDefaultVariant = 80;
 // taken, the rescale path once a row max grows by 5 (some P >= 2, the bit-14
 // test), scores 20+ log2 units under the running estimate flush to 0 (weight
 // < 2^-20 of the row's largest: at most Nk * 2^-20 of the sum in total)
+//
+// Round 6: that flush is what limits fp16 at long context.  On an
+// attention-sink row (one dominant key, the rest d log2 units under it) the
+// weights just above 2^-(24 - offset) are quantised to a few subnormal steps
+// and those below it dropped, so the worst-case error grows with Nk * 2^offset:
+// a numpy model of the packing gives, offset 4 / 3 / 2 / 1 (torch's fp16 SDPA
+// in brackets), Nk 4096 2.9e-3 / 1.5e-3 / 7.5e-4 / 1.9e-4 (9.3e-4), 8192
+// 9.6e-3 / 2.5e-3 / 1.5e-3 / 3.4e-4 (1.3e-3), 16384 1.1e-2 / 5.9e-3 / 3.2e-3 /
+// 6.9e-4 (1.5e-3), 32768 2.6e-2 / 1.1e-2 / 5.6e-3 / 1.5e-3 (1.5e-3), 65536
+// 4.6e-2 / 2.7e-2 / 1.1e-2 / 3.1e-3 (2.7e-3).  So the offset
+// falls by one per doubling of Nk past 4096 (floor 1): the worst case stays
+// at ~3e-3, within ~2x of torch's, and the bench's Nk 4096 keeps offset 4.
+// A smaller offset takes the rescale path more often (B8 S4096: 4 / 2 / 0 at
+// 1308 / 1138 / 662 TF/s; B1 S32768: 1393 / 1324 / 1035).
 #ifndef PLI_V13_MUOFF_F16
 #define PLI_V13_MUOFF_F16 4.f
 #endif
+static float v13_muoff_f16(int Nk) {
+    float m = PLI_V13_MUOFF_F16;
+    for (int64_t n = 4096; n < Nk && m > 1.f; n *= 2) m -= 1.f;
+    return m;
+}
 // causal: attn_fwd_v12 causal (74; one block per workgroup where the
 // persistent pair walk does not tile the shape), 60 where v12 does not apply
 // (fp16, D != 128, Nq > Nk, Nk % 64): B8 S4096 H32 D128 bf16 1002 (74, the
@@ -612,7 +631,7 @@ int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int
         const float sweep = bf ? 0.f : -1.f;
         if (cv == (causal != 0) && attn_v13_ok(D, bf ? 1 : 0, causal, Nq, Nk, s7) && c_log2 > 0.f && H < (1 << 16))
             return launch_attn_v13(q, k, v, o, B, H, group, Nq, Nk, s7, scale, stream, variant != 81 && variant != 84,
-                                   (variant == 82 || variant == 85) ? sweep : bf ? PLI_V13_MUOFF : PLI_V13_MUOFF_F16,
+                                   (variant == 82 || variant == 85) ? sweep : bf ? PLI_V13_MUOFF : v13_muoff_f16(Nk),
                                    nullptr, causal != 0, !bf, D);
         variant = causal ? 74 : 71;
     }

@@ -104,21 +104,23 @@ def test_v13_f16_explicit_scale(scale):
     assert err <= tol, f"scale {scale}: max |err| {err:.4e} > {tol:.4e}"
 
 
+@pytest.mark.parametrize("N", (8192, 32768))
 @pytest.mark.parametrize("D", (128, 64))
 @pytest.mark.parametrize("d", (14, 18, 20, 22))
-def test_v13_f16_attention_sink_long_context(d, D):
-    """the fp16 program packs P with mu = row max * c + 4, so P <=
-    2^-4 at the row max and a weight w of the row's largest is stored as the
-    fp16 value 2^-4 w: subnormal below w = 2^-10, zero below 2^-21 (torch's
-    fp16 path, P = 1 at the max, keeps down to 2^-25).  Worst case for that:
-    an attention-sink row -- one dominant key and 32767 keys d log2 units
-    under it (their total weight 2^15 2^-d: 0.5 at d = 16, 1/128 at d = 22)
-    -- against float64 on the same fp16 inputs.  The bound is the fp16 flash
-    tolerance of the other tests (1e-2); the numpy model of the same packing
-     puts the worst case at ~8e-3, at d = 22."""
+def test_v13_f16_attention_sink_long_context(d, D, N):
+    """the fp16 program packs P with mu = row max * c + offset, so
+    a weight w of the row's largest is stored as the fp16 value 2^-offset w:
+    subnormal below w = 2^(offset - 14), zero below 2^(offset - 25).  Worst
+    case for that: an attention-sink row -- one dominant key and N - 1 keys d
+    log2 units under it -- against float64 on the same fp16 inputs.  At a
+    fixed offset 4 the error grows with N (1.4e-2 measured here at N 32768,
+    d 20, in round 6); the launcher now lowers the offset by one per doubling
+    of N past 4096 (csrc/flash_attn.hip v13_muoff_f16), which the numpy model
+    of the packing puts at <= 3e-3 worst case (torch's fp16 SDPA: 1.5e-3 at
+    N 32768).  Bound: 5e-3."""
     import pli_hip
-    N, Nq = 32768, 64
-    g = torch.Generator(device=DEV).manual_seed(100 + d + D)
+    Nq = 64
+    g = torch.Generator(device=DEV).manual_seed(100 + d + D + N)
     c = D ** -0.5 * 1.4426950408889634
     q = torch.zeros(1, 1, Nq, D, device=DEV, dtype=torch.float64)
     q[..., 0] = 1.0
@@ -135,4 +137,4 @@ def test_v13_f16_attention_sink_long_context(d, D):
     out = pli_hip.flash_attn_fwd(q, k, v)
     assert pli_hip.last_route().startswith("attn_fwd_v13h")
     err = max_err(out, ref)
-    assert err <= 1e-2, f"d {d} D {D}: max |err| {err:.3e}"
+    assert err <= 5e-3, f"N {N} d {d} D {D}: max |err| {err:.3e}"

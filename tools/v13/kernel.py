@@ -555,10 +555,12 @@ def softmax_fills(X, slices, earliest_of, deadline_of=None, ytag=0, prev_cv=None
                   deadline=dl, tag="fma", hard=dl is not None)
         if QSCALE[0]:  # P = bf16(exp2(S)), S already c s - mu: in place, no temporaries
             dle = None if dl is None else dl - 1
-            e0 = Fill(I("v_exp_f32", s[2 * hh], s[2 * hh]), 8, trans=True, sep=0, earliest=ea, deadline=dle,
-                      tag="exp", hard=dl is not None)
-            e1 = Fill(I("v_exp_f32", s[2 * hh + 1], s[2 * hh + 1]), 8, trans=True, sep=0, earliest=ea,
+            xd = extra_deps(qb, kb) if extra_deps is not None else []  # (a VALU mask of S(kb, qb) first)
+            xm = "clamp" if LCHECK[0] else ""
+            e0 = Fill(I("v_exp_f32", s[2 * hh], s[2 * hh], mods=xm), 8, trans=True, deps=xd, sep=0, earliest=ea,
                       deadline=dle, tag="exp", hard=dl is not None)
+            e1 = Fill(I("v_exp_f32", s[2 * hh + 1], s[2 * hh + 1], mods=xm), 8, trans=True, deps=xd, sep=0,
+                      earliest=ea, deadline=dle, tag="exp", hard=dl is not None)
             f0 = f1 = None
             y0, y1 = s[2 * hh], s[2 * hh + 1]
         elif "exp" in ABL:
@@ -832,15 +834,15 @@ def exps_all(X, also_or=False, shifted=False):
         y0, y1 = T(0 + 2 * (n % 8)), T(1 + 2 * (n % 8))
         s = S_(kb, qb)
         w = P_(X, qb, kb >> 1)[2 * (kb & 1) + hh]
+        xm = "clamp" if LCHECK[0] else ""
         if QSCALE[0] and shifted:
-            c += [I("v_exp_f32", y0, s[2 * hh]), I("v_exp_f32", y1, s[2 * hh + 1])]
+            c += [I("v_exp_f32", y0, s[2 * hh], mods=xm), I("v_exp_f32", y1, s[2 * hh + 1], mods=xm)]
         elif QSCALE[0]:
             # S = c s - mu written back in place: the next step's deferred
             # slices of this tile exp S in place and expect it shifted
             c += [I("v_sub_f32", s[2 * hh], s[2 * hh], MU(qb)), I("v_sub_f32", s[2 * hh + 1], s[2 * hh + 1], MU(qb)),
-                  I("v_exp_f32", y0, s[2 * hh]), I("v_exp_f32", y1, s[2 * hh + 1])]
+                  I("v_exp_f32", y0, s[2 * hh], mods=xm), I("v_exp_f32", y1, s[2 * hh + 1], mods=xm)]
         else:
-            xm = "clamp" if LCHECK[0] else ""
             c += [I("v_fma_f32", y0, s[2 * hh], sC, Neg(MU(qb))), I("v_fma_f32", y1, s[2 * hh + 1], sC, Neg(MU(qb))),
                   I("v_exp_f32", y0, y0, mods=xm), I("v_exp_f32", y1, y1, mods=xm)]
         c += [I(DT["cvt"], w, y0, y1)]
@@ -977,7 +979,6 @@ class Gen:
             lcheck = dtype == "bf16"
         assert not (dtype == "f16" and lcheck), "fp16 runs the P-bit check"
         QSCALE[0] = bool(qscale)
-        assert not (qscale and lcheck), "QSCALE is built on the P-bit check (lcheck=False)"
         LCHECK[0] = bool(lcheck)
         # causal: the second block of each pair streams its tiles in the
         # reversed order of tile_of (its 8 workgroups then read every K/V
@@ -1304,8 +1305,9 @@ class Gen:
                     n += 1
                     y0, y1 = Y(2 * slot), Y(2 * slot + 1)
                     dep = [sh] + ([cv[slot]] if slot in cv else [])
-                    e0 = Fill(I("v_exp_f32", y0, sw[2 * hh]), 8, trans=True, deps=dep, sep=1, tag="exp")
-                    e1 = Fill(I("v_exp_f32", y1, sw[2 * hh + 1]), 8, trans=True, deps=dep, sep=1, tag="exp")
+                    xm = "clamp" if LCHECK[0] else ""
+                    e0 = Fill(I("v_exp_f32", y0, sw[2 * hh], mods=xm), 8, trans=True, deps=dep, sep=1, tag="exp")
+                    e1 = Fill(I("v_exp_f32", y1, sw[2 * hh + 1], mods=xm), 8, trans=True, deps=dep, sep=1, tag="exp")
                     w = P_(0, qb, kb >> 1)[2 * (kb & 1) + hh]
                     cv[slot] = Fill(I(DT["cvt"], w, y0, y1), 4, deps=[e0, e1], sep=1, tag="cvt")
                     fills += [e0, e1, cv[slot]]
