@@ -360,6 +360,13 @@ NORELOAD = [False]
 # max, mu and P of q-block qb run in the gaps of QK(0)'s later q-blocks
 # instead of straight-line after QK(0)
 PROPIPE = [False]
+# QSPLIT (Gen(qscale=True, qsplit=True), bf16, head dim 64): Q c held as
+# two bf16 parts, hi = bf16(q c) and lo = bf16(q c - hi), and every QK chain
+# runs both (S = K hi^T + K lo^T, -mu as the first C operand): QSCALE's fma
+# saving with the score error of a 16-bit mantissa instead of bf16's 8 --
+# twice the QK MFMAs, which only the head-dim-64 form (MFMA busy ~0.5, the
+# AGPRs a64-127 free) can pay for
+QSPLIT = [False]
 # QSEP (Gen(qsep=k), A/B knob): the tail's 16 (D 64: 8) Q loads of the next
 # block spaced k MFMA gaps apart, one per gap, instead of packed into the
 # first few gaps (0, the round-5 program)
@@ -435,6 +442,16 @@ def drain(fills, k):
 # ---------------------------------------------------------------- pieces
 
 
+def NQK():
+    """MFMAs per QK chain: one per 32-wide d slice, two with QSPLIT (Q hi and lo)"""
+    return NDS() * (2 if QSPLIT[0] else 1)
+
+
+def QL_(qb, ds):
+    """QSPLIT (head dim 64): the low bf16 part of Q c, a64.. (O uses a0-63)"""
+    return A(64 + 4 * (4 * qb + ds), 4)
+
+
 def qk_mfmas(mask=None, muc=False):
     """QK^T of one tile, q-block major.  mask (causal): the C operand of each
     chain's first MFMA -- 'diag' (the wave's diagonal tile: 0 below the
@@ -446,18 +463,21 @@ def qk_mfmas(mask=None, muc=False):
         if mask == "diag" and kb == qb:
             return TRIMU(qb) if muc else TRI
         return MUC(qb) if muc else 0
+    if QSPLIT[0]:
+        return [mfma(S_(kb, qb), K_(kb, j >> 1), (QL_ if j & 1 else Q_)(qb, j >> 1), S_(kb, qb) if j else c0(kb, qb))
+                for qb in range(4) for j in range(NQK()) for kb in range(4)]
     return [mfma(S_(kb, qb), K_(kb, ds), Q_(qb, ds), S_(kb, qb) if ds else c0(kb, qb))
             for qb in range(4) for ds in range(NDS()) for kb in range(4)]
 
 
 def qk_done_gap(kb, qb):
     """QK phase gap after which S(kb, qb) is complete"""
-    return 4 * NDS() * qb + 4 * (NDS() - 1) + kb
+    return 4 * NQK() * qb + 4 * (NQK() - 1) + kb
 
 
 def qk_first(kb, qb):
     """QK phase index of the MFMA that starts S(kb, qb) (it overwrites S)"""
-    return 4 * NDS() * qb + kb
+    return 4 * NQK() * qb + kb
 
 
 def rowsum_mfmas(X, ones=None):
@@ -951,8 +971,10 @@ class Gen:
     def __init__(self, ndef=4, budget=8, dma_spacing=6, tag="%=", stamp=False, causal=False, abl=(), dma_cost=8,
                  rev=True, qscale=False, dma_pv=0, dma_pv_spacing=16, budget_pv=None, lcheck=None, dtype="bf16",
                  hd=128, short_first=False, ragged=False, oline=False, seam_wait=False, o_bits=0, q_bits=0,
-                 beyond=4, qsep=0, balanced=False, noreload=False, propipe=False, trans=1):
+                 beyond=4, qsep=0, balanced=False, noreload=False, propipe=False, trans=1, qsplit=False):
         global DMA_COST
+        # (head dim 64 only: the AGPRs for Q lo; other forms ignore it)
+        QSPLIT[0] = bool(qsplit) and bool(qscale) and dtype == "bf16" and hd == 64
         TRANS_PER_GAP[0] = int(trans)
         PROPIPE[0] = bool(propipe)
         NORELOAD[0] = bool(noreload)
@@ -1355,6 +1377,12 @@ class Gen:
                               I("v_and_b32", t2, 0xFFFF0000, t0)]
                     c += [I("v_mul_f32", t1, sC, t1), I("v_mul_f32", t2, sC, t2),
                           I(DT["cvt"], t0, t1, t2), I("v_accvgpr_write_b32", a, t0)]
+                    if QSPLIT[0]:
+                        # lo = bf16(q c - hi): the residual of each half, RNE
+                        h1, h2 = T(24 + 2 * (n % 4)), T(25 + 2 * (n % 4))
+                        c += [I("v_lshlrev_b32", h1, 16, t0), I("v_and_b32", h2, 0xFFFF0000, t0),
+                              I("v_sub_f32", t1, t1, h1), I("v_sub_f32", t2, t2, h2),
+                              I("v_cvt_pk_bf16_f32", t0, t1, t2), I("v_accvgpr_write_b32", QL_(qb, ds)[r], t0)]
                     n += 1
         return c
 
