@@ -375,3 +375,28 @@ def test_v13_qscale_f16_first_tile_far_below_zero(D):
     assert np.isfinite(o).all()
     err = np.abs(o - f64_attention(q, k, v, dtype="f16")).max()
     assert err <= 2.0 ** -8 * np.abs(v).max(), f"max |err| {err:.3e}"
+
+
+@pytest.mark.parametrize("kind", ("randn", "q4", "first"))
+def test_v13_qsplit_d64_matches_exact_scale(kind):
+    """QSPLIT (Gen(qscale=True, qsplit=True), bf16 head dim 64): Q c as two
+    bf16 parts, hi + lo, each QK chain running both -- QSCALE's fma saving
+    without bf16(q c)'s 2^-9 score error.  Its error against f64 must be the
+    exact-scale program's, on plain, q x 4 (peaky) and far-negative rows,
+    where plain QSCALE is 2.5-8x worse"""
+    rng = np.random.default_rng(41)
+    q = rng.standard_normal((1, 1, 256, 64))
+    k = rng.standard_normal((1, 1, 512, 64))
+    v = rng.standard_normal((1, 1, 512, 64))
+    if kind == "q4":
+        q = q * 4.0
+    elif kind == "first":
+        sgn = np.sign(q[:, :, :1])
+        q = np.abs(q) * sgn
+        k[:, :, :64] = -16.0 * sgn * np.abs(k[:, :, :64]) * np.sqrt(2.0)
+        k[:, :, 64:] = -20.0 * sgn * np.abs(k[:, :, 64:]) * np.sqrt(2.0)
+    ref = f64_attention(q, k, v)
+    o_exact, _ = R.run(q, k, v, muoff=62.0)
+    o_split, _ = R.run(q, k, v, muoff=62.0, qscale=True, qsplit=True)
+    e_exact, e_split = np.abs(o_exact - ref).max(), np.abs(o_split - ref).max()
+    assert e_split <= 1.05 * e_exact + 1e-4, f"{kind}: qsplit {e_split:.3e} vs exact {e_exact:.3e}"
