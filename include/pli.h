@@ -69,7 +69,8 @@ const char* pli_last_route(void);
  * followed by hipDeviceSynchronize + hipGetLastError, and a failure is
  * returned by the entry point that launched the kernel, its name in
  * pli_last_error() ("<kernel>: kernel failed (PLI_SYNC): ...").  Starts as
- * the environment says (PLI_SYNC=1: on; unset or 0: off).  mode 0 / 1 sets
+ * the environment says (PLI_SYNC=1 or HIP_LAUNCH_BLOCKING=1: on; else off).
+ * mode 0 / 1 sets
  * it, mode < 0 only queries; returns the previous state.  Debugging only:
  * it serialises every call and must not be on while a stream is captured. */
 int pli_debug_sync(int mode);

@@ -28,7 +28,8 @@ void clear_error() {
     g_route[0] = 0;
 }
 
-// debug mode (PLI_SYNC=1 in the environment, or pli_debug_sync(1)): every
+// debug mode (PLI_SYNC=1 or HIP_LAUNCH_BLOCKING=1 in the environment, or
+// pli_debug_sync(1)): every
 // launch is followed by hipDeviceSynchronize + hipGetLastError, so a kernel
 // that faults or fails is reported by the entry point that launched it, with
 // the kernel's name in pli_last_error().  Off by default (the library never
@@ -38,8 +39,12 @@ static std::atomic<int> g_sync{-1};
 static int sync_mode() {
     int m = g_sync.load(std::memory_order_relaxed);
     if (m < 0) {
-        const char* e = getenv("PLI_SYNC");
-        m = (e && *e && strcmp(e, "0") != 0) ? 1 : 0;
+        // PLI_SYNC=1, or the runtime's own HIP_LAUNCH_BLOCKING=1
+        m = 0;
+        for (const char* name : {"PLI_SYNC", "HIP_LAUNCH_BLOCKING"}) {
+            const char* e = getenv(name);
+            if (e && *e && strcmp(e, "0") != 0) m = 1;
+        }
         g_sync.store(m, std::memory_order_relaxed);
     }
     return m;

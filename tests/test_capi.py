@@ -187,10 +187,11 @@ def test_debug_sync_switch(built_lib):
     finally:
         pli_hip.debug_sync(int(prev))
     code = "import ctypes, sys; L = ctypes.CDLL(sys.argv[1]); print(L.pli_debug_sync(-1))"
-    for env_val, want in (("1", "1"), ("0", "0"), (None, "0")):
-        env = {k: v for k, v in os.environ.items() if k != "PLI_SYNC"}
+    for name, env_val, want in (("PLI_SYNC", "1", "1"), ("PLI_SYNC", "0", "0"), ("PLI_SYNC", None, "0"),
+                                ("HIP_LAUNCH_BLOCKING", "1", "1")):
+        env = {k: v for k, v in os.environ.items() if k not in ("PLI_SYNC", "HIP_LAUNCH_BLOCKING")}
         if env_val is not None:
-            env["PLI_SYNC"] = env_val
+            env[name] = env_val
         out = subprocess.run([sys.executable, "-c", code, built_lib], capture_output=True, text=True, env=env,
                              check=True).stdout.strip()
         assert out == want, (env_val, out)
