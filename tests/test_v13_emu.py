@@ -400,3 +400,28 @@ def test_v13_qsplit_d64_matches_exact_scale(kind):
     o_split, _ = R.run(q, k, v, muoff=62.0, qscale=True, qsplit=True)
     e_exact, e_split = np.abs(o_exact - ref).max(), np.abs(o_split - ref).max()
     assert e_split <= 1.05 * e_exact + 1e-4, f"{kind}: qsplit {e_split:.3e} vs exact {e_exact:.3e}"
+
+
+TAILEPI_CASES = [  # (B, H, Hkv, Nq, Nk, grid, muoff, causal, D)
+    (1, 2, 2, 256, 320, 1, 62.0, False, 128),   # persistent: the next block's Q loads beside the stores
+    (2, 2, 1, 200, 128, 1, 62.0, False, 128),   # ragged Nq: rows past Nq masked in the units
+    (1, 1, 1, 256, 256, None, 0.0, False, 128),  # the rescale path at every tile, the last one too
+    (1, 2, 1, 200, 512, None, 62.0, True, 128),  # causal virtual rows (the units' row shift)
+    (1, 8, 8, 512, 512, 8, 62.0, True, 128),    # the pair walk (light tails keep the plain epilogue)
+    (1, 2, 2, 256, 200, 1, 62.0, False, 64),    # head dim 64, ragged Nk
+]
+
+
+@pytest.mark.parametrize("case", TAILEPI_CASES,
+                         ids=lambda c: "tailepi-b{}h{}kv{}q{}k{}g{}-mu{}-causal{}-d{}".format(*c))
+def test_v13_tail_epilogue_vs_f64(case):
+    """Gen(tailepi=2): the epilogue's normalise / pack / store of O as fills
+    of the tail's PV(T), unit by unit once PV(T) has finished their d-blocks"""
+    B, H, Hkv, Nq, Nk, grid, muoff, causal, D = case
+    rng = np.random.default_rng(43 + sum(case[:5]) + D)
+    q = rng.standard_normal((B, H, Nq, D))
+    k = rng.standard_normal((B, Hkv, Nk, D))
+    v = rng.standard_normal((B, Hkv, Nk, D))
+    o, em = R.run(q, k, v, grid=grid, muoff=muoff, causal=causal, tailepi=2)
+    err = np.abs(o - f64_attention(q, k, v, causal)).max()
+    assert err <= 1e-2, f"max |err| {err:.3e}"

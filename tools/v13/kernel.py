@@ -367,6 +367,25 @@ PROPIPE = [False]
 # twice the QK MFMAs, which only the head-dim-64 form (MFMA busy ~0.5, the
 # AGPRs a64-127 free) can pay for
 QSPLIT = [False]
+# TAILEPI (Gen(tailepi=True), the row-sum-check programs): the epilogue's
+# normalise / pack / store of O runs in the gaps of the tail's PV(T), one
+# unit per (q-block, d-block pair) as soon as PV(T) has finished those d-blocks
+# (l is final before PV(T) under LCHECK; S's registers are dead after the
+# tail's check and hold the epilogue's temporaries), instead of after it
+TAILEPI = [False]
+EP_R = [V(k) for k in range(8)]      # TAILEPI: O values of one unit (in S's registers)
+EP_W = V(8, 4)                       # TAILEPI: the unit's packed store words
+EP_ROW, EP_LANE = V(12), V(13)
+
+
+def EP_OOFF(qb):
+    return V(16 + qb)
+
+
+def EP_RCP(qb):
+    return V(20 + qb)
+
+
 # QSEP (Gen(qsep=k), A/B knob): the tail's 16 (D 64: 8) Q loads of the next
 # block spaced k MFMA gaps apart, one per gap, instead of packed into the
 # first few gaps (0, the round-5 program)
@@ -971,8 +990,10 @@ class Gen:
     def __init__(self, ndef=4, budget=8, dma_spacing=6, tag="%=", stamp=False, causal=False, abl=(), dma_cost=8,
                  rev=True, qscale=False, dma_pv=0, dma_pv_spacing=16, budget_pv=None, lcheck=None, dtype="bf16",
                  hd=128, short_first=False, ragged=False, oline=False, seam_wait=False, o_bits=0, q_bits=0,
-                 beyond=4, qsep=0, balanced=False, noreload=False, propipe=False, trans=1, qsplit=False):
+                 beyond=4, qsep=0, balanced=False, noreload=False, propipe=False, trans=1, qsplit=False,
+                 tailepi=False):
         global DMA_COST
+        TAILEPI[0] = int(tailepi)  # 1: one fill per unit, 2: four (reads + muls x 2, pack, store)
         # (head dim 64 only: the AGPRs for Q lo; other forms ignore it)
         QSPLIT[0] = bool(qsplit) and bool(qscale) and dtype == "bf16" and hd == 64
         TRANS_PER_GAP[0] = int(trans)
@@ -1002,6 +1023,7 @@ class Gen:
         assert not (dtype == "f16" and lcheck), "fp16 runs the P-bit check"
         QSCALE[0] = bool(qscale)
         LCHECK[0] = bool(lcheck)
+        TAILEPI[0] = TAILEPI[0] if LCHECK[0] and not OLINE[0] else 0
         # causal: the second block of each pair streams its tiles in the
         # reversed order of tile_of (its 8 workgroups then read every K/V
         # tile at the same time)
@@ -1792,9 +1814,65 @@ class Gen:
                 if f.ins[0].op == "global_load_dwordx4":
                     f.sep, f.cost = QSEP[0], 8
         fills += qf
+        tailepi = TAILEPI[0] and not dead
+        if tailepi:
+            fills += self.epi_units(pv)
         body, left = schedule(pv, fills, self.budget)
         e(body)
         e(drain(left, len(pv) - 1))
+        if tailepi:
+            e([I("s_branch", self.L("epinext"))])
+
+    def epi_units(self, pv):
+        """TAILEPI: the epilogue as fills of the tail's PV(T): a setup (1 / l,
+        the O row offsets) and one unit per (q-block, d-block pair) -- read the
+        pair's 8 accumulators, times 1 / l, pack, swap halves, store (rows past
+        Nq masked) -- placed after PV(T)'s last MFMA on those d-blocks.  Uses
+        S's registers (dead after the tail's check) and sT4:sT7, never the
+        SGPRs of the Q-load chain beside it"""
+        setup = [I("v_rcp_f32", EP_RCP(qb), L_(qb)[0]) for qb in range(4)]
+        if self.causal:
+            setup += qshift(sT4, sT5)
+        setup += [I("v_and_b32", EP_LANE, 1, VG), I("v_lshlrev_b32", EP_LANE, 5, EP_LANE),
+                  I("v_lshrrev_b32", EP_ROW, 1, VG), I("v_lshlrev_b32", EP_ROW, 4, EP_ROW),
+                  I("v_add_u32", EP_LANE, EP_LANE, EP_ROW)]
+        row = lambda qb: [I("v_add_u32", EP_ROW, sCQ0, VI), I("v_add_u32", EP_ROW, RS() * qb, EP_ROW)] + \
+            ([I("v_subrev_u32", EP_ROW, sT4, EP_ROW)] if self.causal else [])  # noqa: E731
+        for qb in range(4):
+            setup += row(qb) + [I("v_mul_lo_u32", EP_OOFF(qb), EP_ROW, ARG(AI["on"])),
+                                I("v_add_u32", EP_OOFF(qb), EP_OOFF(qb), EP_LANE)]
+        fsetup = Fill(setup, 16, earliest=1, tag="episetup")
+        last = {}
+        for j, m in enumerate(pv):
+            if m.ops[0].f == "a":
+                last[m.ops[0].i] = j
+        fills = [fsetup]
+        prev = fsetup
+        for dbp in range(NDB() // 2):
+            for qb in range(4):
+                parts = []
+                for half, db in enumerate((2 * dbp, 2 * dbp + 1)):
+                    rr = EP_R[4 * half:4 * half + 4]
+                    parts.append([I("v_accvgpr_read_b32", rr[r], O_(db, qb)[r]) for r in range(4)] +
+                                 [I("v_mul_f32", rr[r], rr[r], EP_RCP(qb)) for r in range(4)])
+                parts.append([I(DT["cvt"], EP_W[2 * h], EP_R[4 * h], EP_R[4 * h + 1]) for h in (0, 1)] +
+                             [I(DT["cvt"], EP_W[2 * h + 1], EP_R[4 * h + 2], EP_R[4 * h + 3]) for h in (0, 1)] +
+                             [I("v_permlane16_swap_b32", EP_W[0], EP_W[2]),
+                              I("v_permlane16_swap_b32", EP_W[1], EP_W[3])])
+                st = row(qb) + [I("v_cmp_gt_u32_e32", VCC, ARG(AI["nq"]), EP_ROW),
+                                I("s_and_saveexec_b64", S(sT6.i, 2), VCC)]
+                if "epi_store" not in ABL:
+                    st += [I("global_store_dwordx4", EP_OOFF(qb), EP_W, sCOH,
+                             mods=f"offset:{64 * dbp} {CACHEBITS['o']}".rstrip())]
+                parts.append(st + [I("s_mov_b64", EXEC, S(sT6.i, 2))])
+                if TAILEPI[0] != 2:  # one fill per unit
+                    parts = [[x for pt in parts for x in pt]]
+                ready = max(last[O_(db, qb).i] for db in (2 * dbp, 2 * dbp + 1)) + 1
+                for pt in parts:
+                    f = Fill(pt, 4 * len(pt), deps=[prev], sep=0, earliest=ready, tag="epiunit")
+                    fills.append(f)
+                    prev = f
+        return fills
 
     # ---- epilogue ---------------------------------------------------------
     def epilogue(self):
@@ -1879,6 +1957,8 @@ class Gen:
                     e([I("global_store_dwordx4", OOFF(qb), V(W(4 * dbp).i, 4), sCOH,
                          mods=f"offset:{off} {CACHEBITS['o']}".rstrip())])
             e([I("s_mov_b64", EXEC, S(sT2.i, 2))])
+        if TAILEPI[0]:
+            e([label(Lb("epinext"))])
         e(self.seam_stamp(2))
         # next block
         if self.rev:
