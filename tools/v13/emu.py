@@ -33,6 +33,23 @@ import numpy as np
 from .isa import Neg, Reg
 
 LANES = 64
+# ds_read_b64_tr_b16: source lane and byte offset of lane l's four words
+_TR_SRC = np.array([[16 * (l // 16) + 4 * q + ((l % 16) >> 2) for q in range(4)] for l in range(64)])
+_TR_OFF = np.array([2 * ((l % 16) & 3) for l in range(64)])
+# MFMA output: lane l holds D[4 (l // 16) + r, l % 16], r = 0..3
+_MF_ROW = 4 * (np.arange(64) // 16)[None, :] + np.arange(4)[:, None]
+_MF_COL = np.broadcast_to(np.arange(64) % 16, (4, 64))
+
+
+_KIND = {}  # opcode -> isa.Ins.kind()
+
+
+def _bf16_halves(u):
+    """(n, 4) uint32 words -> (n, 8) float64: half j = word j // 2, bits 16 (j % 2)"""
+    h = np.empty((u.shape[0], 8), dtype=np.uint32)
+    h[:, 0::2] = u << 16
+    h[:, 1::2] = u & 0xFFFF0000
+    return h.view(np.float32).astype(np.float64)
 M32 = 0xFFFFFFFF
 
 
@@ -103,6 +120,16 @@ class Heap:
     def write(self, addr, data):
         arr, off = self.find(addr, len(data))
         arr[off:off + len(data)] = data
+
+    def lanes(self, addrs, n):
+        """the buffer and (lanes, n) byte indices of a vector access whose lanes
+        all fall inside one allocation, else None (the caller then goes lane
+        by lane, which raises on the out-of-bounds lane)"""
+        lo, hi = int(addrs.min()), int(addrs.max())
+        for start, arr in self.bufs:
+            if start <= lo and hi + n <= start + arr.size:
+                return arr, (addrs - start)[:, None] + np.arange(n)[None, :]
+        return None
 
     def view(self, start):
         for s, arr in self.bufs:
@@ -252,7 +279,9 @@ class Emu:
         w.pc += 1
         if op in ("label", "s_nop", "s_waitcnt"):
             return
-        k = ins.kind()
+        k = _KIND.get(op)
+        if k is None:
+            k = _KIND[op] = ins.kind()  # (a function of the opcode alone)
         if self.structural and not op.startswith("s_"):
             if op == "global_load_lds_dwordx4":
                 self.dma_log.append((w.wid, self.sc(w, o[1]), self.off(ins), w.m0))
@@ -272,25 +301,27 @@ class Emu:
     # ---- MFMA -------------------------------------------------------------
     def mfma(self, w, ins):
         d, a, b, c = ins.ops
-        ra, rb = self.regs(w, a), self.regs(w, b)
-        dec = f16_to_f32 if ins.op.endswith("_f16") else bf16_to_f32
-        # halves j = 0..7 of lane l: word j // 2, bits 16 (j % 2) (vectorised;
-        # the same A, B and A @ B as the per-element form)
-        lane = np.arange(LANES)
-        jj = np.arange(8)[:, None]
-        ha = (np.asarray(ra, dtype=np.uint32)[jj // 2, lane] >> (16 * (jj % 2)).astype(np.uint32)) & 0xFFFF
-        hb = (np.asarray(rb, dtype=np.uint32)[jj // 2, lane] >> (16 * (jj % 2)).astype(np.uint32)) & 0xFFFF
-        A = np.zeros((16, 32))
-        B = np.zeros((32, 16))
-        A[lane % 16, 8 * (lane // 16) + jj] = dec(ha).astype(np.float64)
-        B[8 * (lane // 16) + jj, lane % 16] = dec(hb).astype(np.float64)
+        f16 = ins.op.endswith("_f16")
+        # halves j = 0..7 of lane l: word j // 2, bits 16 (j % 2); A[i, k] with
+        # i = l % 16, k = 8 (l // 16) + j (B transposed the same way)
+        ua = np.ascontiguousarray(np.asarray(self.regs(w, a), dtype=np.uint32).T)  # (64 lanes, 4 words)
+        ub = np.ascontiguousarray(np.asarray(self.regs(w, b), dtype=np.uint32).T)
+        if f16:
+            fa = ua.view(np.float16).astype(np.float64)  # (64, 8): half j of lane l
+            fb = ub.view(np.float16).astype(np.float64)
+        else:
+            fa = _bf16_halves(ua)
+            fb = _bf16_halves(ub)
+        # lane l = 16 g + i: A row i, columns 8 g .. 8 g + 7
+        A = fa.reshape(4, 16, 8).transpose(1, 0, 2).reshape(16, 32)
+        B = fb.reshape(4, 16, 8).transpose(0, 2, 1).reshape(32, 16)
         D = A @ B
         if isinstance(c, int):
             assert c == 0
             C = np.zeros((4, LANES))
         else:
             C = u2f(self.regs(w, c)).astype(np.float64)
-        out = C + D[4 * (lane // 16) + np.arange(4)[:, None], lane % 16]
+        out = C + D[_MF_ROW, _MF_COL]
         self.regs(w, d)[:] = f2u(out.astype(np.float32))
 
     # ---- VALU -------------------------------------------------------------
@@ -298,6 +329,19 @@ class Emu:
         op, o = ins.op, ins.ops
         g = lambda x: self.vec(w, x)  # noqa: E731
         gf = lambda x: u2f(self.vec(w, x))  # noqa: E731
+        # (the softmax stream's ops first: the chain is walked per instruction)
+        if op == "v_fma_f32":
+            r = (gf(o[1]).astype(np.float64) * gf(o[2]) + gf(o[3])).astype(np.float32)
+            return self.vset(w, o[0], f2u(r))
+        if op == "v_exp_f32":
+            with np.errstate(over="ignore"):
+                r = np.exp2(gf(o[1]))
+            if "clamp" in ins.mods.split():  # VOP3 clamp: [0, 1] (NaN -> 0)
+                r = np.where(np.isnan(r), np.float32(0), np.clip(r, np.float32(0), np.float32(1)))
+            return self.vset(w, o[0], f2u(r.astype(np.float32)))
+        if op == "v_cvt_pk_bf16_f32":
+            lo, hi = bf16_rne(gf(o[1])), bf16_rne(gf(o[2]))
+            return self.vset(w, o[0], lo | (hi << 16))
         if op == "v_mov_b32":
             return self.vset(w, o[0], g(o[1]))
         if op == "v_writelane_b32":  # vdst[lane] = scalar (EXEC ignored)
@@ -339,9 +383,6 @@ class Emu:
         if op == "v_mbcnt_hi_u32_b32":
             lane = np.arange(LANES)
             return self.vset(w, o[0], (np.maximum(lane - 32, 0) + g(o[2])).astype(np.uint32))
-        if op == "v_fma_f32":
-            r = (gf(o[1]).astype(np.float64) * gf(o[2]) + gf(o[3])).astype(np.float32)
-            return self.vset(w, o[0], f2u(r))
         if op == "v_mul_f32":
             return self.vset(w, o[0], f2u(gf(o[1]) * gf(o[2])))
         if op == "v_add_f32":
@@ -352,18 +393,9 @@ class Emu:
             return self.vset(w, o[0], f2u(np.maximum(gf(o[1]), gf(o[2]))))
         if op == "v_max3_f32":
             return self.vset(w, o[0], f2u(np.maximum(np.maximum(gf(o[1]), gf(o[2])), gf(o[3]))))
-        if op == "v_exp_f32":
-            with np.errstate(over="ignore"):
-                r = np.exp2(gf(o[1]))
-            if "clamp" in ins.mods.split():  # VOP3 clamp: [0, 1] (NaN -> 0)
-                r = np.where(np.isnan(r), np.float32(0), np.clip(r, np.float32(0), np.float32(1)))
-            return self.vset(w, o[0], f2u(r.astype(np.float32)))
         if op == "v_rcp_f32":
             with np.errstate(divide="ignore"):
                 return self.vset(w, o[0], f2u(np.float32(1.0) / gf(o[1])))
-        if op == "v_cvt_pk_bf16_f32":
-            lo, hi = bf16_rne(gf(o[1])), bf16_rne(gf(o[2]))
-            return self.vset(w, o[0], lo | (hi << 16))
         if op == "v_cvt_f32_f16":  # the low half
             return self.vset(w, o[0], f2u(f16_to_f32(g(o[1]) & 0xFFFF).astype(np.float32)))
         if op == "v_cvt_pk_f16_f32":
@@ -539,23 +571,25 @@ class Emu:
         addr = self.vec(w, o[1]).astype(np.int64) + off
         if op == "ds_read_b128":
             dst = self.regs(w, o[0])
-            for l in range(LANES):
-                if w.exec[l]:
-                    dst[:, l] = self.lds_read(int(addr[l]), 16).view(np.uint32)
+            act = np.nonzero(w.exec)[0]
+            a = addr[act]
+            assert act.size == 0 or (a.min() >= 0 and a.max() + 16 <= self.lds.size), "LDS read out of bounds"
+            data = self.lds[a[:, None] + np.arange(16)[None, :]]  # (lanes, 16 bytes), gathered
+            dst[:, act] = np.ascontiguousarray(data).view(np.uint32).T
             return
         if op == "ds_read_b64_tr_b16":
             assert w.exec.all()
             dst = self.regs(w, o[0])
-            for grp in range(4):
-                for i in range(16):
-                    l = 16 * grp + i
-                    vals = []
-                    for q in range(4):
-                        src = 16 * grp + 4 * q + (i >> 2)
-                        a = int(addr[src]) + 2 * (i & 3)
-                        vals.append(int(self.lds_read(a, 2).view(np.uint16)[0]))
-                    dst[0, l] = vals[0] | (vals[1] << 16)
-                    dst[1, l] = vals[2] | (vals[3] << 16)
+            # lane l = 16 grp + i takes the 16-bit word at byte 2 (i & 3) of lane
+            # 16 grp + 4 q + (i >> 2)'s address, for q = 0..3 (vectorised)
+            a = addr[_TR_SRC] + _TR_OFF[:, None]  # (64, 4) byte addresses
+            assert a.min() >= 0 and a.max() + 2 <= self.lds.size, "LDS read out of bounds"
+            if (a & 1).any():
+                vals = self.lds[a].astype(np.uint32) | (self.lds[a + 1].astype(np.uint32) << 8)
+            else:
+                vals = self.lds.view(np.uint16)[a >> 1].astype(np.uint32)
+            dst[0, :] = vals[:, 0] | (vals[:, 1] << 16)
+            dst[1, :] = vals[:, 2] | (vals[:, 3] << 16)
             return
         raise NotImplementedError(op)
 
@@ -567,26 +601,41 @@ class Emu:
             assert w.exec.all()
             voff = self.vec(w, o[0])
             base = self.sc(w, o[1])
+            la = w.m0 + off
+            assert 0 <= la and la + 16 * LANES <= self.lds.size, f"LDS-DMA out of bounds {la}"
+            g = self.heap.lanes(base + voff.astype(np.int64) + off, 16)
+            if g is not None:
+                self.lds[la:la + 16 * LANES] = g[0][g[1]].ravel()
+                return
             for l in range(LANES):
-                data = self.heap.read(base + int(voff[l]) + off, 16)
-                la = w.m0 + off + 16 * l
-                assert 0 <= la and la + 16 <= self.lds.size, f"LDS-DMA out of bounds {la}"
-                self.lds[la:la + 16] = data
+                self.lds[la + 16 * l:la + 16 * l + 16] = self.heap.read(base + int(voff[l]) + off, 16)
             return
         if op == "global_load_dwordx4":
             dst = self.regs(w, o[0])
             voff = self.vec(w, o[1])
             base = self.sc(w, o[2])
-            for l in range(LANES):
-                if w.exec[l]:
-                    dst[:, l] = self.heap.read(base + int(voff[l]) + off, 16).view(np.uint32)
+            act = np.nonzero(w.exec)[0]
+            if act.size == 0:
+                return
+            g = self.heap.lanes(base + voff[act].astype(np.int64) + off, 16)
+            if g is not None:
+                dst[:, act] = np.ascontiguousarray(g[0][g[1]]).view(np.uint32).T
+                return
+            for l in act:
+                dst[:, l] = self.heap.read(base + int(voff[l]) + off, 16).view(np.uint32)
             return
         if op == "global_store_dwordx4":
             voff = self.vec(w, o[0])
             src = self.regs(w, o[1])
             base = self.sc(w, o[2])
-            for l in range(LANES):
-                if w.exec[l]:
-                    self.heap.write(base + int(voff[l]) + off, src[:, l].copy().view(np.uint8))
+            act = np.nonzero(w.exec)[0]
+            if act.size == 0:
+                return
+            g = self.heap.lanes(base + voff[act].astype(np.int64) + off, 16)
+            if g is not None:
+                g[0][g[1]] = np.ascontiguousarray(np.asarray(src, dtype=np.uint32)[:, act].T).view(np.uint8)
+                return
+            for l in act:
+                self.heap.write(base + int(voff[l]) + off, src[:, l].copy().view(np.uint8))
             return
         raise NotImplementedError(op)
