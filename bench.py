@@ -260,7 +260,8 @@ def bench_flash_dtypes(stream) -> dict:
                                                        "TFLOP/s": 4 * B * H * D_ * pairs / (ms * 1e-3) / 1e12}
         out[f"{dt}_d{D_}"] = r
         del q, k, v, o
-    out["kernels"] = "attn_fwd_v13h (fp16 D128), attn_fwd_v13_d64 / v13h_d64 (D64) and their causal forms"
+    out["kernels"] = ("attn_fwd_v13h (fp16 D128), attn_fwd_pp64 (bf16 D64, since round 6), attn_fwd_v13h_d64 "
+                      "(fp16 D64) and the v13 causal forms")
     return out
 
 

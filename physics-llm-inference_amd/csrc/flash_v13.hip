@@ -182,19 +182,23 @@ bool attn_v13_ok(int D, int is_bf16, int causal, int Nq, int Nk, const V7Strides
     return true;
 }
 
+bool attn_pp64_ok(int D, bool fp16, bool causal, int Nk) { return D == 64 && !fp16 && !causal && Nk % 64 == 0; }
+
 int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B, int H, int group, int Nq,
                     int Nk, const V7Strides& st, float scale, hipStream_t stream, bool persistent, float muoff,
-                    uint32_t* stamps, bool causal, bool fp16, int D) {
+                    uint32_t* stamps, bool causal, bool fp16, int D, bool pp64) {
     PLI_REQUIRE(attn_v13_ok(D, fp16 ? 0 : 1, causal, Nq, Nk, st), "attn_fwd_v13: shape not supported");
     PLI_REQUIRE(H > 0 && H < (1 << 16), "attn_fwd_v13: H = %d past the packed 16-bit head count", H);
     PLI_REQUIRE(!((fp16 || D != 128 || Nk % 64 != 0 || causal) && stamps),
                 "attn_fwd_v13: the stamp build is bf16, D = 128, non-causal, Nk % 64 == 0");
     const int nqv = causal ? Nq + ((Nk - Nq) & 63) : Nq;  // causal: virtual rows, (Nk - nqv) % 64 == 0
-    const int qblocks = cdiv(nqv, 256);
+    // attn_fwd_pp64: 512-row blocks (8 waves of 64 rows), one per workgroup
+    const bool pp = pp64 && !stamps && attn_pp64_ok(D, fp16, causal, Nk);
+    const int qblocks = cdiv(nqv, pp ? 512 : 256);
     const int64_t nb = (int64_t)B * H * qblocks;
     PLI_REQUIRE(nb < (1ll << 31) && nb > 0, "attn_fwd_v13: grid too large");
     int grid = (int)nb;
-    if (persistent) {
+    if (persistent && !pp) {
         const int g = cu_count(stream) / 8 * 8;
         if (g >= 8 && nb > g) grid = g;
     }
@@ -274,6 +278,7 @@ int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B,
 #else
     (void)stamps;
 #endif
+    if (pp) return launch_pp64((unsigned)grid, a, stream);
     if (D == 64) return launch_v13_d64(fp16, causal, ragged, (unsigned)grid, a, stream);
     if (ragged && causal) {
         if (fp16) {

@@ -57,7 +57,7 @@ def test_v12_no_compiler_agpr_use_or_spill(tmp_path, src):
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
-@pytest.mark.parametrize("src", ["flash_v13.hip", "flash_v13_d64.hip"])
+@pytest.mark.parametrize("src", ["flash_v13.hip", "flash_v13_d64.hip", "flash_pp64.hip"])
 def test_v13_asm_only_kernels_build_clean(tmp_path, src):
     """attn_fwd_v13's bodies are one inline-asm statement each (tools/
     gen_flash_v13.py): the clobber list names no register hipcc reserves

@@ -1,0 +1,77 @@
+"""Emulator driver for attn_fwd_pp64 (tools/v14/pp64.py): the argument block
+of launch_attn_v13 with 512-row blocks (csrc/flash_v13.hip, pp64 route) and
+one workgroup of 8 waves per block."""
+from __future__ import annotations
+
+import math
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from v13 import emu as E  # noqa: E402
+from v13 import run as R  # noqa: E402
+from v13.isa import S, finalize  # noqa: E402
+from v14.pp64 import PP64  # noqa: E402
+
+_PROG = {}
+
+
+def program():
+    if "p" not in _PROG:
+        prog = PP64(tag="emu").build(in_kernarg=S(0, 2), in_wg=S(2), in_wave=S(3))
+        _PROG["p"], _ = finalize(prog)
+    return _PROG["p"]
+
+
+def run(q, k, v, scale=None, muoff=62.0, layout="bhsd"):
+    """q [B,H,Nq,64], k / v [B,Hkv,Nk,64] -> O [B,H,Nq,64] (bf16-rounded inputs)"""
+    B, H, Nq, D = q.shape
+    Hkv, Nk = k.shape[1], k.shape[2]
+    assert D == 64 and Nk % 64 == 0 and Nk >= 64
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    heap = E.Heap()
+
+    def put(x, lay):
+        b16 = E.bf16_rne(np.asarray(x, dtype=np.float32)).astype(np.uint16)
+        if lay == "bshd":
+            b16 = np.ascontiguousarray(b16.transpose(0, 2, 1, 3))
+            Bx, Sx, Hx, Dx = b16.shape
+            strides = (Sx * Hx * Dx, Dx, Hx * Dx)
+        else:
+            Bx, Hx, Sx, Dx = b16.shape
+            strides = (Hx * Sx * Dx, Sx * Dx, Dx)
+        return heap.alloc(b16.nbytes + 256, b16.tobytes()), strides
+
+    qa, sq = put(q, layout)
+    ka, sk = put(k, layout)
+    va, sv = put(v, layout)
+    oa = heap.alloc(B * H * Nq * D * 2 + 256)
+    so = (Nq * H * D, D, H * D) if layout == "bshd" else (H * Nq * D, Nq * D, D)
+    qblocks = -(-Nq // 512)
+    nb = B * H * qblocks
+    args = R.args_for(qa, ka, va, oa, B, H, Hkv, Nq, Nk, list(sq) + list(sk) + list(sv) + list(so), scale, nb,
+                      muoff, False)
+    from v13.kernel import AI
+    args[AI["qblocks"]], args[AI["nblocks"]] = qblocks, nb
+    args[AI["magq"]], shq = R.magic(qblocks)
+    args[AI["shifts"]] = (int(args[AI["shifts"]]) & ~31) | shq
+    kaddr = heap.alloc(args.nbytes, args.tobytes())
+    em = E.Emu(program(), heap)
+    for wg in range(nb):
+        waves = []
+        for wv in range(8):
+            w = E.Wave()
+            w.s[0], w.s[1], w.s[2], w.s[3] = kaddr & 0xFFFFFFFF, kaddr >> 32, wg, wv
+            w.wid = (wg, wv)
+            waves.append(w)
+        em.lds[:] = 0
+        em.run_wg(waves)
+    raw = heap.view(oa)[:B * H * Nq * D * 2].view(np.uint16)
+    if layout == "bshd":
+        o = E.bf16_to_f32(raw.reshape(B, Nq, H, D).astype(np.uint32)).transpose(0, 2, 1, 3)
+    else:
+        o = E.bf16_to_f32(raw.reshape(B, H, Nq, D).astype(np.uint32))
+    return np.ascontiguousarray(o), em
