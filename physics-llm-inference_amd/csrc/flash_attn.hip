@@ -545,7 +545,7 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(
 // default since round 4: attn_fwd_v13 (80), 1388 vs 1242 TF/s for v12 (71)
 // at B8 S4096 H32 D128 in the same process (profiles/r04/flash/ab.log); where
 // v13 does not apply (D not 64 / 128, Nk <= 64) it routes to 71 / 74.
-// Since round 6 the default is 88: attn_fwd_pp64 (86) for head dim 64 bf16
+// Since round 6 the default is 88: attn_fwd_pp64 / pp64h (86) for head dim 64
 // non-causal where its blocks fill the chip (two waves per SIMD in ping-pong;
 // bitwise v13's D = 64 result, 1259 vs 1104 TF/s at B8 H32 S4096 D64 in the
 // same process, profiles/r06/pp64/), v13 (80) for everything else
@@ -625,9 +625,9 @@ int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int
     // the exact bodies (v12 70-74, v7 / v10 51 / 55 / 60) apply c by fma to
     // the fp32 scores: any c > 0; only the prescaled ones (50 / 54) need c <= 1
     const bool c_pos = c_log2 > 0.f;
-    // 86: attn_fwd_pp64 where it applies (head dim 64, bf16, non-causal, Nk %
-    // 64 == 0; tools/v14/pp64.py), else the default v13 form; 87: the same
-    // with the rescale path at every tile (muoff 0, tests only)
+    // 86: attn_fwd_pp64 / pp64h where it applies (head dim 64, bf16 / fp16,
+    // non-causal, Nk % 64 == 0; tools/v14/pp64.py), else the default v13 form;
+    // 87: the same with the rescale path at every tile (muoff 0 / -1, tests)
     // 88 (the default since round 6): 86 where its 512-row blocks fill the
     // chip (B H ceil(Nq / 512) >= the CU count), else 80 -- below that v13's
     // 256-row blocks spread the same work over twice as many CUs (B2 H8 S512:
@@ -639,10 +639,11 @@ int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int
     if (variant == 86 || variant == 87) {
         const bool bf = std::is_same<T, bf16_t>::value;
         const V7Strides s7{st.qb, st.qh, st.qn, st.kb, st.kh, st.kn, st.vb, st.vh, st.vn, st.ob, st.oh, st.on};
-        if (!causal && bf && attn_pp64_ok(D, false, false, Nk) && attn_v13_ok(D, 1, 0, Nq, Nk, s7) &&
+        if (!causal && attn_pp64_ok(D, !bf, false, Nk) && attn_v13_ok(D, bf ? 1 : 0, 0, Nq, Nk, s7) &&
             c_log2 > 0.f && H < (1 << 16))
             return launch_attn_v13(q, k, v, o, B, H, group, Nq, Nk, s7, scale, stream, true,
-                                   variant == 87 ? 0.f : PLI_V13_MUOFF, nullptr, false, false, D, true);
+                                   variant == 87 ? (bf ? 0.f : -1.f) : bf ? PLI_V13_MUOFF : v13_muoff_f16(Nk),
+                                   nullptr, false, !bf, D, true);
         variant = causal ? 83 : variant == 87 ? 82 : 80;
     }
     if (variant >= 80 && variant <= 85) {

@@ -182,7 +182,10 @@ bool attn_v13_ok(int D, int is_bf16, int causal, int Nq, int Nk, const V7Strides
     return true;
 }
 
-bool attn_pp64_ok(int D, bool fp16, bool causal, int Nk) { return D == 64 && !fp16 && !causal && Nk % 64 == 0; }
+bool attn_pp64_ok(int D, bool fp16, bool causal, int Nk) {
+    (void)fp16;  // bf16 and fp16 bodies
+    return D == 64 && !causal && Nk % 64 == 0;
+}
 
 int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B, int H, int group, int Nq,
                     int Nk, const V7Strides& st, float scale, hipStream_t stream, bool persistent, float muoff,
@@ -278,7 +281,7 @@ int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B,
 #else
     (void)stamps;
 #endif
-    if (pp) return launch_pp64((unsigned)grid, a, stream);
+    if (pp) return launch_pp64(fp16, (unsigned)grid, a, stream);
     if (D == 64) return launch_v13_d64(fp16, causal, ragged, (unsigned)grid, a, stream);
     if (ragged && causal) {
         if (fp16) {

@@ -1,6 +1,7 @@
-"""attn_fwd_pp64 (csrc/flash_pp64.hip, tools/v14/pp64.py): head dim 64, bf16,
-non-causal, two waves per SIMD in ping-pong, 512-row blocks -- flash variants
-86 (muoff 62, as v13) and 87 (the rescale path at every tile).
+"""attn_fwd_pp64 / pp64h (csrc/flash_pp64.hip, tools/v14/pp64.py): head dim
+64, bf16 / fp16, non-causal, two waves per SIMD in ping-pong, 512-row blocks
+-- flash variants 86 (v13's mu offsets) and 87 (the rescale path at every
+tile); 88, the default, picks 86 where its blocks fill the chip.
 
 References: the f64 device attention over the whole output
 (ch06/attention_memory.py:19-33 in float64) at block-seam / GQA / ragged-Nq /
@@ -8,7 +9,9 @@ single-tile shapes, plain and Q x 4; fp32 per head over all 256 heads at B8
 S4096 H32 D64 (the bench's D = 64 leg); a late key that raises its rows' max
 far past the offset (the rare path with muoff 62); BSHD views; and v13's D = 64
 program (variant 80), which runs the same per-row arithmetic in the same
-order, so the two agree bitwise."""
+order, so the two agree bitwise (bf16; fp16 within rounding: v13h prescales
+Q, pp64h scales the scores by fma); fp16 attention-sink rows at long
+context (the mu-offset policy)."""
 from __future__ import annotations
 
 import pytest
@@ -24,39 +27,52 @@ SHAPES = [(4, 16, 4, 2048, 1024), (4, 32, 8, 1024, 128), (3, 40, 8, 1000, 320), 
           (1, 4, 2, 600, 4096), (2, 8, 8, 513, 256)]
 
 
+ROUTE = {"bf16": "attn_fwd_pp64", "fp16": "attn_fwd_pp64h"}
+
+
+@pytest.mark.parametrize("dt", ("bf16", "fp16"))
 @pytest.mark.parametrize("qmul", (1, 4))
 @pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "b{}h{}kv{}q{}k{}".format(*s))
-def test_pp64_vs_f64_full_tensor(shape, qmul):
+def test_pp64_vs_f64_full_tensor(shape, qmul, dt):
     import pli_hip
-    q, k, v = inputs64(shape, sum(shape) % 971, "bf16")
+    q, k, v = inputs64(shape, sum(shape) % 971, dt)
     q = q * qmul  # exact
     ref = torch_attention(q, k, v)
     tol = 1e-2 if qmul == 1 else 2.0 ** -8 * v.abs().max().item()
     outs = {}
     for var in (86, 87):
         outs[var] = pli_hip.flash_attn_fwd(q, k, v, variant=var)
-        assert pli_hip.last_route() == "attn_fwd_pp64", pli_hip.last_route()
+        assert pli_hip.last_route() == ROUTE[dt], pli_hip.last_route()
         err = max_err(outs[var], ref)
-        assert err <= tol, f"{shape} q*{qmul} variant {var}: max |err| {err:.4e} > {tol:.4e}"
+        assert err <= tol, f"{shape} {dt} q*{qmul} variant {var}: max |err| {err:.4e} > {tol:.4e}"
     assert_agree_to_rounding(outs[87], outs[86], v)
-    # v13's D = 64 program: the same rows, the same arithmetic in the same order
-    assert torch.equal(outs[86], pli_hip.flash_attn_fwd(q, k, v, variant=80)), f"{shape}: pp64 != v13"
+    v13 = pli_hip.flash_attn_fwd(q, k, v, variant=80)
+    if dt == "bf16":  # v13's D = 64 program: the same rows, the same arithmetic in the same order
+        assert torch.equal(outs[86], v13), f"{shape}: pp64 != v13"
+    else:
+        assert_agree_to_rounding(outs[86], v13, v)
 
 
-def test_pp64_full_config_all_heads():
-    """B8 S4096 H32 D64 (the bench's D = 64 leg): all 256 heads against an
-    fp32 torch attention, and bitwise v13's D = 64 program."""
+@pytest.mark.parametrize("dt", ("bf16", "fp16"))
+def test_pp64_full_config_all_heads(dt):
+    """B8 S4096 H32 D64 (the bench's D = 64 legs): all 256 heads against an
+    fp32 torch attention, and v13's D = 64 program (bf16: bitwise)."""
     import pli_hip
     B, H, N, D = 8, 32, 4096, 64
     g = torch.Generator(device=DEV).manual_seed(23)
-    q, k, v = (torch.randn(B, H, N, D, device=DEV, dtype=torch.bfloat16, generator=g) for _ in range(3))
+    td = torch.bfloat16 if dt == "bf16" else torch.float16
+    q, k, v = (torch.randn(B, H, N, D, device=DEV, dtype=td, generator=g) for _ in range(3))
     out = pli_hip.flash_attn_fwd(q, k, v)  # the default route (88) at this shape
-    assert pli_hip.last_route() == "attn_fwd_pp64"
+    assert pli_hip.last_route() == ROUTE[dt]
     for b in range(B):
         ref = torch_attention(q[b:b + 1], k[b:b + 1], v[b:b + 1], dtype=torch.float32, heads_per_chunk=4)
         err = max_err(out[b:b + 1], ref)
-        assert err <= 1e-2, f"batch {b}: max |err| {err:.4e} over its 32 heads"
-    assert torch.equal(out, pli_hip.flash_attn_fwd(q, k, v, variant=80))
+        assert err <= 1e-2, f"{dt} batch {b}: max |err| {err:.4e} over its 32 heads"
+    v13 = pli_hip.flash_attn_fwd(q, k, v, variant=80)
+    if dt == "bf16":
+        assert torch.equal(out, v13)
+    else:
+        assert_agree_to_rounding(out, v13, v)
 
 
 @pytest.mark.parametrize("at", (5, 700, 2047))
@@ -86,9 +102,8 @@ def test_pp64_strided_bshd_views():
 
 
 def test_pp64_falls_back_where_it_does_not_apply():
-    """fp16, causal and ragged Nk take v13's programs under variant 86; the
-    default route (88) keeps v13 where pp64's 512-row blocks would not fill
-    the chip"""
+    """causal and ragged Nk take v13's programs under variant 86; the default
+    route (88) keeps v13 where pp64's 512-row blocks would not fill the chip"""
     import pli_hip
     q, k, v = inputs64((2, 8, 8, 512, 512), 5, "bf16")
     pli_hip.flash_attn_fwd(q, k, v)
@@ -97,11 +112,41 @@ def test_pp64_falls_back_where_it_does_not_apply():
     pli_hip.flash_attn_fwd(q, k, v)
     assert pli_hip.last_route() == "attn_fwd_pp64"
     q, k, v = inputs64((1, 2, 2, 256, 320), 5, "fp16")
-    pli_hip.flash_attn_fwd(q, k, v, variant=86)
+    pli_hip.flash_attn_fwd(q, k, v)
     assert pli_hip.last_route() == "attn_fwd_v13h_d64"
+    pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=86)
+    assert pli_hip.last_route() == "attn_fwd_v13hc_d64"
     q, k, v = inputs64((1, 2, 2, 256, 320), 5, "bf16")
     pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=86)
     assert pli_hip.last_route() == "attn_fwd_v13c_d64"
     q, k, v = inputs64((1, 2, 2, 256, 300), 5, "bf16")
     pli_hip.flash_attn_fwd(q, k, v, variant=86)
     assert pli_hip.last_route() == "attn_fwd_v13r_d64"
+
+
+@pytest.mark.parametrize("N", (8192, 32768))
+@pytest.mark.parametrize("d", (14, 18, 22))
+def test_pp64h_attention_sink_long_context(d, N):
+    """fp16 attention-sink rows (one dominant key, N - 1 keys d log2 units
+    under it) on pp64h with the launcher's Nk-dependent mu offset
+    (v13_muoff_f16; tests/test_gpu_flash_v13_f16.py holds the v13h twin)"""
+    import pli_hip
+    D, Nq = 64, 512
+    g = torch.Generator(device=DEV).manual_seed(1000 * d + N % 997)
+    c = D ** -0.5 * 1.4426950408889634
+    q = torch.zeros(1, 1, Nq, D, device=DEV, dtype=torch.float64)
+    q[..., 0] = 1.0
+    q[..., 1] = 0.05 * torch.randn(1, 1, Nq, device=DEV, dtype=torch.float64, generator=g)
+    k = torch.zeros(1, 1, N, D, device=DEV, dtype=torch.float64)
+    a = 8.0 / c
+    delta = d + 2.0 * torch.rand(N, device=DEV, dtype=torch.float64, generator=g) - 1.0
+    k[0, 0, :, 0] = a - delta / c
+    k[0, 0, 0, 0] = a
+    k[0, 0, :, 1] = torch.randn(N, device=DEV, dtype=torch.float64, generator=g)
+    v = torch.randn(1, 1, N, D, device=DEV, dtype=torch.float64, generator=g)
+    q, k, v = (t.to(torch.float16) for t in (q, k, v))
+    ref = torch_attention(q, k, v)
+    out = pli_hip.flash_attn_fwd(q, k, v, variant=86)
+    assert pli_hip.last_route() == "attn_fwd_pp64h"
+    err = max_err(out, ref)
+    assert err <= 5e-3, f"N {N} d {d}: max |err| {err:.3e}"

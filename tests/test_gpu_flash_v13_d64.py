@@ -49,8 +49,15 @@ def test_v13_d64_vs_f64_full_tensor(shape, qmul, dt):
         assert err <= tol, f"{shape} {dt} q*{qmul} variant {var}: max |err| {err:.4e} > {tol:.4e}"
     assert torch.equal(outs[80], outs[81]), f"{shape}: 80 != 81"
     assert_agree_to_rounding(outs[82], outs[80], v)
-    # the default route is this program (D = 64 routed to v10 before round 5)
-    assert torch.equal(pli_hip.flash_attn_fwd(q, k, v), outs[80])
+    # the default route is this program (D = 64 routed to v10 before round 5),
+    # or since round 6 attn_fwd_pp64 where its 512-row blocks fill the chip:
+    # bitwise v13 for bf16, within rounding for fp16 (pp64h scales by fma,
+    # v13h prescales Q)
+    d = pli_hip.flash_attn_fwd(q, k, v)
+    if pli_hip.last_route() == "attn_fwd_pp64h":
+        assert_agree_to_rounding(d, outs[80], v)
+    else:
+        assert torch.equal(d, outs[80])
 
 
 @pytest.mark.parametrize("dt", ("bf16", "fp16"))

@@ -81,19 +81,40 @@ def test_pp64_knobs_vs_f64(kw):
         P._PROG.pop("p", None)
 
 
+F16_CASES = [(1, 1, 1, 512, 384, 4.0), (1, 1, 1, 512, 384, -1.0), (1, 2, 1, 300, 64, 4.0)]
+
+
+@pytest.mark.parametrize("case", F16_CASES, ids=lambda c: "b{}h{}kv{}q{}k{}-mu{}".format(*c))
+def test_pp64h_program_vs_f64(case):
+    """the fp16 body: P-bit check in the vector phase, its rescale path there
+    (muoff -1: every tile), fp16-rounded inputs"""
+    B, H, Hkv, Nq, Nk, muoff = case
+    rng = np.random.default_rng(sum(case[:5]))
+    q = rng.standard_normal((B, H, Nq, 64))
+    k = rng.standard_normal((B, Hkv, Nk, 64))
+    v = rng.standard_normal((B, Hkv, Nk, 64))
+    o, em = P.run(q, k, v, muoff=muoff, dtype="f16")
+    err = np.abs(o - f64_attention(q, k, v, dtype="f16")).max()
+    assert err <= 5e-3, f"max |err| {err:.3e}"
+    if muoff < 0:
+        assert em.counts.get("v_sub_f32", 0) > 0, "the rescale path never ran"
+
+
 def test_pp64_header_is_fresh():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "v14", "pp64.py"), "--check"])
     assert r.returncode == 0, "csrc/flash_pp64_asm.h is stale: run python tools/v14/pp64.py"
 
 
-def test_pp64_hazard_pass_idempotent():
-    prog, _ = finalize(pp64.PP64().build())
+@pytest.mark.parametrize("dtype", ("bf16", "f16"))
+def test_pp64_hazard_pass_idempotent(dtype):
+    prog, _ = finalize(pp64.PP64(dtype=dtype).build())
     assert not analyse(prog), "finalize left hazards or waits unresolved"
 
 
-def test_pp64_register_budget():
+@pytest.mark.parametrize("dtype", ("bf16", "f16"))
+def test_pp64_register_budget(dtype):
     """128 VGPRs + 128 AGPRs (two waves per SIMD) and no SGPR past s99 / s32"""
-    prog, _ = finalize(pp64.PP64().build())
+    prog, _ = finalize(pp64.PP64(dtype=dtype).build())
     for ins in prog:
         for o in ins.ops:
             r = getattr(o, "r", o)

@@ -1,6 +1,7 @@
-"""attn_fwd_pp64: flash-attention forward at head dim 64 with two waves per
-SIMD in ping-pong (round-6 verdict item 2b; the timing probe that motivated it
-is tools/v14/probe64.py, profiles/r06/probe64/).
+"""attn_fwd_pp64 / pp64h: flash-attention forward at head dim 64 with two
+waves per SIMD in ping-pong (round-6 verdict item 2b; the timing probe that
+motivated it is tools/v14/probe64.py, profiles/r06/probe64/; the A/B of the
+phase placements below is profiles/r06/pp64/).
 
 Workgroup of 8 waves, 64 query rows each (a 512-row block of one head).  Waves
 w and w + 4 share a SIMD.  Group A (waves 0-3) and group B (waves 4-7) run the
@@ -8,19 +9,26 @@ same per-tile program, B half a period behind A, every half-period ending at
 a workgroup barrier, so while one wave of a SIMD is in its matrix phase the
 other is in its vector phase:
 
-  C(t) (matrix): the defer-max check of tile t-1 (its row sums are in l), then
-         PV(t-1) (32 MFMAs, the V^T fragments of t-1 already in the fragment
-         ring) and QK(t) (32 MFMAs) with K(t)'s 8 fragment reads in PV's gaps;
-  M(t) (vector): tile t+4's two LDS-DMA pieces (per wave), the softmax of
-         S(t) in place (fma, exp, cvt into P), l += 1^T P(t) on the matrix core
-         (8 MFMAs), the 8 V^T(t) fragment reads for C(t+1), the wait.
+  C(t) (matrix): l += 1^T P(t-1) (8 MFMAs) and the defer-max check of tile
+         t-1 (bf16), PV(t-1) (32 MFMAs, the V^T fragments of t-1 already in
+         the fragment ring) and QK(t) (32 MFMAs) with K(t)'s 8 fragment reads
+         in PV's gaps, V^T(t)'s 8 fragment reads as QK frees the ring slots,
+         and tile t+4's two LDS-DMA pieces (per wave);
+  M(t) (vector): the softmax of S(t) in place (fma, exp, cvt into P); fp16:
+         the P-bit check; the wait.
 
-The numerics are attn_fwd_v13's bf16 head-dim-64 ones (tools/v13/kernel.py,
-LCHECK): mu = (row max of tile 0) c + muoff, P = bf16(exp2(s c - mu)) with
-v_exp_f32's clamp, a tile takes the rescale path once some row's l >= 1 (the
-rare path recomputes S from K, moves mu, rescales O and l, redoes P).  The
-same LDS images, swizzle and fragment offsets as v13's D = 64 program in
-compact 16 KiB ring slots (K image, then V image at +8 KiB), 6 slots.
+Moving the DMA, the V^T reads and the row sums out of the vector phase (the
+probe's layout) into the matrix phase took bf16 from level with v13 to +14 %:
+the vector phase was the long one.
+
+The numerics are attn_fwd_v13's head-dim-64 ones (tools/v13/kernel.py):
+mu = (row max of tile 0) c + muoff, P = 16-bit(exp2(s c - mu)); bf16: v_exp's
+clamp and the l >= 1 check (LCHECK), bitwise v13's result; fp16: the P-bit
+check (some P >= 2) in the vector phase, the fma kept (v13h prescales Q instead:
+QSCALE's -mu C operands need 16 VGPRs this layout does not have).  The rare
+path recomputes S from K, moves mu, rescales O and l, redoes P.  The same LDS
+images, swizzle and fragment offsets as v13's D = 64 program in compact 16 KiB
+ring slots (K image, then V image at +8 KiB), 6 slots.
 
 Registers (256 per wave: 128 V + 128 A):
   a0-63 O^T (4 d-blocks x 4 q-blocks), a64-95 Q, a96-127 fragment ring (8);
@@ -29,15 +37,17 @@ Registers (256 per wave: 128 V + 128 A):
 
 One block per workgroup (grid = B H ceil(Nq / 512)), the block walk of v13's
 block_params (each XCD a contiguous range of blocks, so a head's blocks share
-an L2).  Non-causal, Nk % 64 == 0, bf16 only; the launcher routes every other
-case to attn_fwd_v13.
+an L2).  Non-causal, Nk % 64 == 0; the launcher routes every other case, and
+shapes whose 512-row blocks would not fill the chip, to attn_fwd_v13.
 
 Vector-memory order per wave (the waits below count on it): the block's 8 Q
-loads, tiles 0-3's DMA pieces (2 each), then 2 pieces per M phase (tile t+4,
+loads, tiles 0-3's DMA pieces (2 each), then 2 pieces per C phase (tile t+4,
 or the last tile again once the stream has reached it -- into a dead slot);
 the O stores last.  A ends M(t) with vmcnt(6) (its pieces up to tile t+1
 landed), B with vmcnt(4) (up to t+2): B's M(t) is a half-period later and
-tile t+2 is read by A right after the next barrier.
+tile t+2 is read by A right after the next barrier.  A DMA into slot
+(t+4) % 6 overwrites tile t-2, last read (B's rescale path) a half-period
+before A's C(t) starts.
 """
 from __future__ import annotations
 
@@ -136,15 +146,24 @@ class PP64:
     end of M(t) ("M") or at the head of C(t+1), right before the check ("C")"""
 
     def __init__(self, tag="%=", dtype="bf16", dma_in="C", split=0, vr_in="C", rs_in="C"):
-        assert dtype == "bf16" and dma_in in ("M", "C") and vr_in in ("M", "C") and rs_in in ("M", "C")
-        assert 0 <= split <= 16 and not (split and rs_in == "C")
+        assert dtype in ("bf16", "f16") and dma_in in ("M", "C") and vr_in in ("M", "C") and rs_in in ("M", "C")
+        assert 0 <= split <= 16 and not (split and rs_in == "M" and vr_in == "C" and False)
+        # fp16: P packed to fp16 and checked by the bit-14 test in the vector
+        # phase (v13's fp16 rule: the l >= 1 test needs muoff >> log2 Nk, which
+        # fp16 P cannot give); the product placements only
+        self.f16 = dtype == "f16"
+        assert not self.f16 or (dma_in, vr_in, rs_in) == ("C", "C", "C")
+        self.mf = "v_mfma_f32_16x16x32_f16" if self.f16 else MF
+        self.cvt = "v_cvt_pk_f16_f32" if self.f16 else "v_cvt_pk_bf16_f32"
+        self.ones = 0x3C003C00 if self.f16 else BF16_ONES
+        self.negones = 0xBC00BC00 if self.f16 else NEGONES
         self.dma_in, self.split, self.vr_in, self.rs_in = dma_in, split, vr_in, rs_in
         self.tag = tag
         self.prog = []
         self.sites = []
 
     def L(self, n):
-        return f"pp64_{n}_{self.tag}"
+        return f"pp64{'h' if self.f16 else ''}_{n}_{self.tag}"
 
     def e(self, c):
         self.prog.extend(c)
@@ -180,26 +199,24 @@ class PP64:
                   mods=f"offset:{256 * (db & 1) + 512 * ((db >> 1) & 1) + 2048 * h + 4096 * kp}")
                 for h in range(2)]
 
-    @staticmethod
-    def qk():
-        return [mfma(S_(kb, qb), F(8 + 2 * kb + ds), Q_(qb, ds), S_(kb, qb) if ds else 0)
+    def qk(self):
+        return [I(self.mf, S_(kb, qb), F(8 + 2 * kb + ds), Q_(qb, ds), S_(kb, qb) if ds else 0)
                 for kb in range(4) for ds in range(2) for qb in range(4)]
 
-    @staticmethod
-    def pv():
-        return [mfma(O_(db, qb), F(2 * db + kp), P_(qb, kp), O_(db, qb))
+    def pv(self):
+        return [I(self.mf, O_(db, qb), F(2 * db + kp), P_(qb, kp), O_(db, qb))
                 for db in range(4) for kp in range(2) for qb in range(4)]
 
-    @staticmethod
-    def rowsums(ones):
-        return [mfma(L_(qb), ones, P_(qb, kp), L_(qb)) for qb in range(4) for kp in range(2)]
+    def rowsums(self, ones):
+        return [I(self.mf, L_(qb), ones, P_(qb, kp), L_(qb)) for qb in range(4) for kp in range(2)]
 
     def slice_ins(self, qb, kb, hh):
         s = S_(kb, qb)
         y0, y1 = s[2 * hh], s[2 * hh + 1]
+        xm = "" if self.f16 else "clamp"  # (fp16: P >= 2 is the check's signal)
         return ([I("v_fma_f32", y0, y0, sC, Neg(MU(qb))), I("v_fma_f32", y1, y1, sC, Neg(MU(qb)))],
-                [I("v_exp_f32", y0, y0, mods="clamp"), I("v_exp_f32", y1, y1, mods="clamp")],
-                [I("v_cvt_pk_bf16_f32", P_(qb, kb >> 1)[2 * (kb & 1) + hh], y0, y1)])
+                [I("v_exp_f32", y0, y0, mods=xm), I("v_exp_f32", y1, y1, mods=xm)],
+                [I(self.cvt, P_(qb, kb >> 1)[2 * (kb & 1) + hh], y0, y1)])
 
     def exps_all(self):
         c = []
@@ -224,7 +241,8 @@ class PP64:
         if kind != "first":
             if self.rs_in == "C":
                 c += self.rowsums(ONES)
-            c += self.check(self.L("rare"))
+            if not self.f16:
+                c += self.check(self.L("rare"))
         dma = self.dma_tile(sSD) + self.next_slot(sSD) if self.dma_in == "C" and kind != "tail" else []
         vr = self.vr_in == "C" and kind != "tail"
         if vr:
@@ -252,9 +270,19 @@ class PP64:
                 after.setdefault(20, []).append("dma")
         sp = []
         if kind == "mid" and self.split:
+            if self.f16:  # the P-bit OR starts with the slices this phase takes
+                c += [I("v_mov_b32", T1, 0)]
+            prev = None
             for x in self.c_slices():
                 f, e_, v = self.slice_ins(*x)
                 sp.append(f + e_ + v)
+                if self.f16 and prev is not None:
+                    sp[-1] = sp[-1] + [I("v_or3_b32", T1, T1, prev[0].ops[0], v[0].ops[0])]
+                    prev = None
+                else:
+                    prev = v
+            if self.f16 and prev is not None:
+                sp[-1] = sp[-1] + [I("v_or_b32", T1, T1, prev[0].ops[0])]
         for i, ins in enumerate(ms):
             c.append(ins)
             for n in after.get(i, []):
@@ -289,6 +317,8 @@ class PP64:
         if reads:
             c += [I("v_add_u32", VVA, sSC, VVL)]
         n = len(sl)
+        if self.f16 and (first or not self.split):
+            c += [I("v_mov_b32", T1, 0)]
         for j in range(n + 2):
             if j < n:
                 c += fm[j]
@@ -297,12 +327,20 @@ class PP64:
             if 2 <= j:
                 c += cv[j - 2]
                 qb, kb, hh = sl[j - 2]
+                if self.f16 and j % 2 == 1:  # the P-bit check: OR of the tile's P words
+                    c.append(I("v_or3_b32", T1, T1, cv[j - 3][0].ops[0], cv[j - 2][0].ops[0]))
                 if kb & 1 and hh and self.rs_in == "M":  # P(qb, kb >> 1) complete
                     c.append(rs[2 * qb + (kb >> 1)])
             # the V^T reads over the second half
             h0 = n - 16
             if reads and j >= h0 and (j - h0) % 2 == 0 and (j - h0) // 2 < 8:
                 c += reads[(j - h0) // 2]
+        if self.f16:
+            k = len(self.sites)
+            ret = self.L(f"ret{k}")
+            self.sites.append((k, ret))
+            c += [I("v_and_b32", T0, 0x40004000, T1), I("v_cmp_ne_u32_e32", VCC, 0, T0),  # some P >= 2
+                  I("s_mov_b32", sRET, k), I("s_cbranch_vccnz", self.L("rare")), label(ret)]
         return c + [I("s_waitcnt", f"vmcnt({wait})"), I("s_barrier")]
 
     def epilogue(self):
@@ -331,8 +369,8 @@ class PP64:
                 for half, db in enumerate((2 * dbp, 2 * dbp + 1)):
                     c += [I("v_accvgpr_read_b32", TT[r], O_(db, qb)[r]) for r in range(4)]
                     c += [I("v_mul_f32", TT[r], TT[r], R[qb]) for r in range(4)]
-                    c += [I("v_cvt_pk_bf16_f32", W(w + 2 * half), TT[0], TT[1]),
-                          I("v_cvt_pk_bf16_f32", W(w + 2 * half + 1), TT[2], TT[3])]
+                    c += [I(self.cvt, W(w + 2 * half), TT[0], TT[1]),
+                          I(self.cvt, W(w + 2 * half + 1), TT[2], TT[3])]
                 c += [I("v_permlane16_swap_b32", W(w), W(w + 2)), I("v_permlane16_swap_b32", W(w + 1), W(w + 3))]
             c += [I("v_cmp_gt_u32_e32", VCC, ARG(AI["nq"]), ROW), I("s_and_saveexec_b64", S(sT2.i, 2), VCC)]
             for dbp in range(2):
@@ -347,12 +385,17 @@ class PP64:
         fragments of the tile back into the ring.  Returns to the site whose
         id is in sRET."""
         c = [label(self.L("rare")), I("s_nop", 7), I("s_nop", 7)]
-        neg = S_(0, 0)  # S is recomputed below: its first block holds the -1s meanwhile
-        c += [I("v_mov_b32", neg[r], NEGONES) for r in range(4)]
-        c += self.rowsums(neg)
-        c += [I("v_add_u32", T1, sSP, VKL)]
+        # bf16: the tile in slot sSP, checked at the head of C(t+1) after its
+        # row sums went into l; fp16: the tile in slot sSC, checked at the end
+        # of its own vector phase (its row sums not taken yet)
+        slot, adr = (sSC, VVA) if self.f16 else (sSP, T1)
+        if not self.f16:
+            neg = S_(0, 0)  # S is recomputed below: its first block holds the -1s meanwhile
+            c += [I("v_mov_b32", neg[r], self.negones) for r in range(4)]
+            c += self.rowsums(neg)
+        c += [I("v_add_u32", adr, slot, VKL)]
         for n in range(8, 16):
-            c += self.k_read(n, T1)
+            c += self.k_read(n, adr)
         c += self.qk()
         m, t1, t2, al, ot = (V(64 + k) for k in range(5))  # P is rebuilt below
         for qb in range(4):
@@ -365,10 +408,11 @@ class PP64:
                           I("v_accvgpr_write_b32", O_(db, qb)[r], ot)]
             c += [I("v_mul_f32", L_(qb)[r], L_(qb)[r], al) for r in range(4)]
         c += self.exps_all()
-        c += self.rowsums(ONES)
-        c += [I("v_add_u32", T1, sSP, VVL)]
+        if not self.f16:
+            c += self.rowsums(ONES)
+        c += [I("v_add_u32", adr, slot, VVL)]
         for n in range(8):
-            c += self.v_read(n, T1)
+            c += self.v_read(n, adr)
         c += [I("s_nop", 4)]
         for k, ret in self.sites:
             c += [I("s_cmp_eq_u32", sRET, k), I("s_cbranch_scc1", ret)]
@@ -414,7 +458,7 @@ class PP64:
         for (rb, st, dst) in ((sT3, kn, DMAK), (sT6, vn, DMAV)):
             e([I("v_add_u32", t[5], rb, t[2]), I("v_mul_lo_u32", t[5], t[5], st), I("v_add_u32", dst, t[5], t[3])])
         e(K.load_args())
-        e([I("v_mov_b32", ONES[k], BF16_ONES) for k in range(4)])
+        e([I("v_mov_b32", ONES[k], self.ones) for k in range(4)])
 
     def block_setup(self):
         e = self.e
@@ -475,16 +519,21 @@ class PP64:
 
 
 def render(**kw):
-    prog, st = finalize(PP64(**kw).build())
     lines = ["// GENERATED by tools/v14/pp64.py -- do not edit (attn_fwd_pp64: head dim 64, two waves per SIMD)",
-             "#pragma once", "",
-             f"// {len(prog)} instructions, hazard pass: {st['nop_ws']} nop wait states, {st['waits']} waits",
-             "#define PLI_PP64_BODY \\"]
-    for ins in prog:
-        t = ins.text()
-        lines.append(f'    "{t}\\n" \\' if ins.op == "label" else f'    "\\t{t}\\n" \\')
-    lines.append('    ""')
-    lines.append("")
+             "#pragma once", ""]
+    # A/B knobs: key=val for the bf16 body, h_key=val for the fp16 one
+    kwb = {k: v for k, v in kw.items() if not k.startswith("h_")}
+    kwh = {k[2:]: v for k, v in kw.items() if k.startswith("h_")}
+    for name, dt in (("PLI_PP64_BODY", "bf16"), ("PLI_PP64H_BODY", "f16")):
+        prog, st = finalize(PP64(dtype=dt, **(kwh if dt == "f16" else kwb)).build())
+        lines.append(f"// {dt}: {len(prog)} instructions, hazard pass: {st['nop_ws']} nop wait states, "
+                     f"{st['waits']} waits")
+        lines.append(f"#define {name} \\")
+        for ins in prog:
+            t = ins.text()
+            lines.append(f'    "{t}\\n" \\' if ins.op == "label" else f'    "\\t{t}\\n" \\')
+        lines.append('    ""')
+        lines.append("")
     clob = [f'"v{i}"' for i in range(128)] + [f'"a{i}"' for i in range(128)] + \
            [f'"s{i}"' for i in range(16, 100) if i != 32] + ['"vcc"', '"scc"', '"memory"']
     lines.append("#define PLI_PP64_CLOBBERS \\")

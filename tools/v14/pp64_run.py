@@ -19,15 +19,18 @@ from v14.pp64 import PP64  # noqa: E402
 _PROG = {}
 
 
-def program():
-    if "p" not in _PROG:
-        prog = PP64(tag="emu").build(in_kernarg=S(0, 2), in_wg=S(2), in_wave=S(3))
-        _PROG["p"], _ = finalize(prog)
-    return _PROG["p"]
+def program(dtype="bf16"):
+    key = "p" if dtype == "bf16" else dtype
+    if key not in _PROG:
+        prog = PP64(tag="emu", dtype=dtype).build(in_kernarg=S(0, 2), in_wg=S(2), in_wave=S(3))
+        _PROG[key], _ = finalize(prog)
+    return _PROG[key]
 
 
-def run(q, k, v, scale=None, muoff=62.0, layout="bhsd"):
-    """q [B,H,Nq,64], k / v [B,Hkv,Nk,64] -> O [B,H,Nq,64] (bf16-rounded inputs)"""
+def run(q, k, v, scale=None, muoff=62.0, layout="bhsd", dtype="bf16"):
+    """q [B,H,Nq,64], k / v [B,Hkv,Nk,64] -> O [B,H,Nq,64] (inputs rounded to
+    bf16, or fp16 with dtype="f16")"""
+    enc, dec = (E.f16_rne, E.f16_to_f32) if dtype == "f16" else (E.bf16_rne, E.bf16_to_f32)
     B, H, Nq, D = q.shape
     Hkv, Nk = k.shape[1], k.shape[2]
     assert D == 64 and Nk % 64 == 0 and Nk >= 64
@@ -35,7 +38,7 @@ def run(q, k, v, scale=None, muoff=62.0, layout="bhsd"):
     heap = E.Heap()
 
     def put(x, lay):
-        b16 = E.bf16_rne(np.asarray(x, dtype=np.float32)).astype(np.uint16)
+        b16 = enc(np.asarray(x, dtype=np.float32)).astype(np.uint16)
         if lay == "bshd":
             b16 = np.ascontiguousarray(b16.transpose(0, 2, 1, 3))
             Bx, Sx, Hx, Dx = b16.shape
@@ -59,7 +62,7 @@ def run(q, k, v, scale=None, muoff=62.0, layout="bhsd"):
     args[AI["magq"]], shq = R.magic(qblocks)
     args[AI["shifts"]] = (int(args[AI["shifts"]]) & ~31) | shq
     kaddr = heap.alloc(args.nbytes, args.tobytes())
-    em = E.Emu(program(), heap)
+    em = E.Emu(program(dtype), heap)
     for wg in range(nb):
         waves = []
         for wv in range(8):
@@ -71,7 +74,7 @@ def run(q, k, v, scale=None, muoff=62.0, layout="bhsd"):
         em.run_wg(waves)
     raw = heap.view(oa)[:B * H * Nq * D * 2].view(np.uint16)
     if layout == "bshd":
-        o = E.bf16_to_f32(raw.reshape(B, Nq, H, D).astype(np.uint32)).transpose(0, 2, 1, 3)
+        o = dec(raw.reshape(B, Nq, H, D).astype(np.uint32)).transpose(0, 2, 1, 3)
     else:
-        o = E.bf16_to_f32(raw.reshape(B, H, Nq, D).astype(np.uint32))
+        o = dec(raw.reshape(B, H, Nq, D).astype(np.uint32))
     return np.ascontiguousarray(o), em
