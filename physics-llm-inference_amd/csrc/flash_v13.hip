@@ -201,7 +201,9 @@ int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B,
     const int64_t nb = (int64_t)B * H * qblocks;
     PLI_REQUIRE(nb < (1ll << 31) && nb > 0, "attn_fwd_v13: grid too large");
     int grid = (int)nb;
-    if (persistent && !pp) {
+    // (pp64's persistent walk streams the next block's first four key tiles
+    // during the current block: it needs Nk >= 256)
+    if (persistent && (!pp || Nk / 64 >= 4)) {
         const int g = cu_count(stream) / 8 * 8;
         if (g >= 8 && nb > g) grid = g;
     }

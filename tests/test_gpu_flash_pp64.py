@@ -24,7 +24,9 @@ pytestmark = pytest.mark.gpu
 
 SHAPES = [(4, 16, 4, 2048, 1024), (4, 32, 8, 1024, 128), (3, 40, 8, 1000, 320), (2, 4, 1, 2048, 192),
           (1, 2, 2, 1, 128), (2, 4, 4, 300, 128), (8, 36, 4, 256, 128), (1, 3, 1, 64, 256), (2, 2, 1, 200, 128),
-          (1, 4, 2, 600, 4096), (2, 8, 8, 513, 256)]
+          (1, 4, 2, 600, 4096), (2, 8, 8, 513, 256),
+          # the persistent walk (more blocks than workgroups, uneven per workgroup, ragged Nq)
+          (5, 36, 4, 1000, 512), (2, 48, 8, 2100, 384)]
 
 
 ROUTE = {"bf16": "attn_fwd_pp64", "fp16": "attn_fwd_pp64h"}

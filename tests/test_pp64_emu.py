@@ -2,7 +2,8 @@
 csrc/flash_pp64.hip) on the CPU: the 8-wave workgroup run by the emulator of
 tools/v13/emu.py against a float64 attention on bf16-rounded inputs.  Covers
 one and many key tiles (the stream parking on the last tile, the 6-slot
-ring), the rescale path at every tile (muoff 0) and after a late spike, GQA,
+ring), the persistent walk (the stream crossing into the next block, the
+block change inside a matrix phase), the rescale path at every tile (muoff 0) and after a late spike, GQA,
 BSHD strides and a ragged query count, every A/B knob placement, the
 committed header's freshness and the hazard pass's idempotence."""
 from __future__ import annotations
@@ -30,6 +31,27 @@ CASES = [  # (B, H, Hkv, Nq, Nk, layout, muoff)
     (1, 2, 1, 300, 320, "bshd", 62.0),    # GQA, BSHD strides, ragged Nq
     (2, 1, 1, 1024, 128, "bhsd", 62.0),   # two blocks per head, two batches
 ]
+PERSISTENT = [  # (B, H, Hkv, Nq, Nk, layout, muoff, grid): blocks L, L + G, ... per workgroup
+    (1, 2, 1, 1024, 256, "bhsd", 62.0, 1),    # four blocks on one workgroup
+    (1, 2, 2, 1000, 384, "bshd", 62.0, 3),    # uneven walk, ragged Nq, BSHD
+    (2, 2, 1, 512, 320, "bhsd", 0.0, 2),      # the rescale path at every tile across block changes
+]
+
+
+@pytest.mark.parametrize("dtype", ("bf16", "f16"))
+@pytest.mark.parametrize("case", PERSISTENT, ids=lambda c: "b{}h{}kv{}q{}k{}-{}-mu{}-g{}".format(*c))
+def test_pp64_persistent_walk_vs_f64(case, dtype):
+    B, H, Hkv, Nq, Nk, lay, muoff, G = case
+    if dtype == "f16":
+        muoff = 4.0 if muoff > 0 else -1.0
+    rng = np.random.default_rng(sum(case[:5]))
+    q = rng.standard_normal((B, H, Nq, 64))
+    k = rng.standard_normal((B, Hkv, Nk, 64))
+    v = rng.standard_normal((B, Hkv, Nk, 64))
+    o, em = P.run(q, k, v, muoff=muoff, layout=lay, dtype=dtype, grid=G)
+    err = np.abs(o - f64_attention(q, k, v, dtype=dtype)).max()
+    assert err <= (1e-2 if dtype == "bf16" else 5e-3), f"max |err| {err:.3e}"
+
 
 
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "b{}h{}kv{}q{}k{}-{}-mu{}".format(*c))

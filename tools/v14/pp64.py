@@ -118,17 +118,22 @@ ARG, AI = K.ARG, K.AI
 sDK, sDV, sDI, sT = S(36, 2), S(38, 2), S(40), S(41)
 sSC, sSP, sSD, sWPC, sMUO = S(42), S(43), S(44), S(45), S(46)
 sM0 = S(47)  # m0 at entry (hipcc reserves m0: restored at exit, not clobbered)
+# the persistent walk: the current block's O head and first row (block_params
+# writes the NEXT block's into sNQH / sNOH / sNQ0), whether block L + G exists,
+# and its K / V heads for the DMA stream
+sCOH, sCQ0, sHASN = S(24, 2), S(26), S(27)
+sNXK, sNXV = S(50, 2), S(34, 2)
 
 
 def slices():
     return [(qb, kb, hh) for qb in range(4) for kb in range(4) for hh in range(2)]
 
 
-def block_params_512():
+def block_params_512(sx):
     """kernel.py's block_params with 512-row blocks: q0 = 512 qblk + 64 wave"""
     K.GEOM["hd"] = 64  # WSH 11: sWKOFF = wave << 11 gives 64 wave
     K.RAGGED[0] = K.BALANCED[0] = K.SHORTFIRST[0] = False
-    c = K.block_params(sL, causal=False, uid=0)
+    c = K.block_params(sx, causal=False, uid=0)
     hits = [i for i, ins in enumerate(c) if ins.op == "s_lshl_b32" and ins.ops[0] is not None
             and str(ins.ops[0]) == str(K.sT2) and str(ins.ops[1]) == str(K.sT2) and ins.ops[2] == 8]
     assert len(hits) == 1, hits
@@ -178,7 +183,11 @@ class PP64:
                 I("s_add_u32", sDI, sDI, 1), I("s_cmp_lt_u32", sDI, sNT),
                 I("s_cselect_b32", sT6, sTBK, 0), I("s_cselect_b32", sT7, sTBV, 0),
                 I("s_add_u32", sDK[0], sDK[0], sT6), I("s_addc_u32", sDK[1], sDK[1], 0),
-                I("s_add_u32", sDV[0], sDV[0], sT7), I("s_addc_u32", sDV[1], sDV[1], 0)]
+                I("s_add_u32", sDV[0], sDV[0], sT7), I("s_addc_u32", sDV[1], sDV[1], 0),
+                # past the block's last tile: the next block's tile 0 if there is one
+                I("s_cmp_eq_u32", sDI, sNT), I("s_cselect_b32", sT6, sHASN, 0), I("s_cmp_eq_u32", sT6, 1),
+                I("s_cselect_b64", sDK, sNXK, sDK), I("s_cselect_b64", sDV, sNXV, sDV),
+                I("s_cselect_b32", sDI, 0, sDI)]
 
     @staticmethod
     def next_slot(r):
@@ -236,7 +245,9 @@ class PP64:
     # ---- phases -------------------------------------------------------------
     def phase_c(self, kind):
         """kind 'first' (QK(0) only), 'mid' (check, PV(t-1), QK(t)), 'tail'
-        (check, PV(T))"""
+        (check, PV(T)), 'trans' (the persistent walk's block change: check,
+        the next block's Q loads, PV(T), the epilogue, O and l zeroed, the
+        block registers moved on, QK of the next block's tile 0)"""
         c = [I("s_mov_b32", sSP, sSC)] + self.next_slot(sSC) + [I("v_add_u32", VKA, sSC, VKL)]
         if kind != "first":
             if self.rs_in == "C":
@@ -244,6 +255,12 @@ class PP64:
             if not self.f16:
                 c += self.check(self.L("rare"))
         dma = self.dma_tile(sSD) + self.next_slot(sSD) if self.dma_in == "C" and kind != "tail" else []
+        if kind == "trans":
+            # after the check (its rescale path reads this block's Q); the
+            # pieces right behind the Q loads, so the wait QK(0) needs for Q
+            # leaves them and the epilogue's stores in flight
+            c += self.q_loads() + dma
+            dma = []
         vr = self.vr_in == "C" and kind != "tail"
         if vr:
             c += [I("v_add_u32", VVA, sSC, VVL)]
@@ -260,7 +277,9 @@ class PP64:
             return c
         ms = self.pv()
         after = {}
-        if kind == "mid":
+        if kind == "trans":
+            after[31] = ["epi"]
+        if kind in ("mid", "trans"):
             ms += self.qk()
             for n in range(8, 16):
                 after.setdefault(4 * (n - 8) + 3, []).append(n)
@@ -286,12 +305,52 @@ class PP64:
         for i, ins in enumerate(ms):
             c.append(ins)
             for n in after.get(i, []):
+                if n == "epi":
+                    c += self.block_change()
+                    continue
                 c += dma if n == "dma" else self.v_read(n - 100, VVA) if n >= 100 else self.k_read(n, VKA)
             if sp and i >= 44 and (i - 44) % 2 == 0:
                 c += sp.pop(0)
         for x in sp:
             c += x
         return c
+
+    def q_loads(self):
+        """the Q rows min(q0 + 16 qb + i, Nq - 1) of the block in sNQH / sNQ0,
+        8 g elements into the row (S's registers as temporaries)"""
+        LANE, VI, VG, TA, TB = V(0), V(1), V(2), V(3), V(4)
+        c = [I("v_mbcnt_lo_u32_b32", LANE, -1, 0), I("v_mbcnt_hi_u32_b32", LANE, -1, LANE),
+             I("v_and_b32", VI, 15, LANE), I("v_lshrrev_b32", VG, 4, LANE), I("v_lshlrev_b32", TB, 4, VG),
+             I("s_sub_u32", sT6, ARG(AI["nq"]), 1)]
+        for qb in range(4):
+            c += [I("v_add_u32", TA, sNQ0, VI), I("v_add_u32", TA, 16 * qb, TA), I("v_min_u32", TA, sT6, TA),
+                  I("v_mul_lo_u32", TA, TA, ARG(AI["qn"])), I("v_add_u32", V(8 + qb), TA, TB)]
+        for qb in range(4):
+            for ds in range(2):
+                c += [I("global_load_dwordx4", Q_(qb, ds), V(8 + qb), sNQH, mods=f"offset:{64 * ds}")]
+        return c
+
+    def next_params(self):
+        """sHASN = L + G < nblocks; if so block L + G's Q / O heads and first
+        row into sNQH / sNOH / sNQ0 and its K / V heads into sNXK / sNXV"""
+        skip = self.L(f"nonext{len(self.prog)}_{self.nuid()}")
+        return ([I("s_add_u32", sT7, sL, ARG(AI["G"])), I("s_cmp_lt_u32", sT7, ARG(AI["nblocks"])),
+                 I("s_cselect_b32", sHASN, 1, 0), I("s_cbranch_scc0", skip)] + block_params_512(sT7) +
+                [I("s_mov_b64", sNXK, S(K.sT0.i, 2)), I("s_mov_b64", sNXV, S(sT2.i, 2)), label(skip)])
+
+    def nuid(self):
+        self.uid = getattr(self, "uid", 0) + 1
+        return self.uid
+
+    def block_change(self):
+        """inside the block-change matrix phase, after PV(T): this block's
+        epilogue, O and l zeroed, the next block current, its successor's
+        parameters"""
+        c = self.epilogue()
+        c += [I("v_accvgpr_write_b32", A(k), 0) for k in range(64)]
+        c += [I("v_mov_b32", L_(qb)[r], 0) for qb in range(4) for r in range(4)]
+        c += [I("s_add_u32", sL, sL, ARG(AI["G"])), I("s_mov_b64", sCOH, sNOH), I("s_mov_b32", sCQ0, sNQ0)]
+        return c + self.next_params()
 
     def c_slices(self):
         """the slices the matrix phase takes (key block 0, q-block major)"""
@@ -360,7 +419,7 @@ class PP64:
         c += [I("v_mbcnt_lo_u32_b32", LANE, -1, 0), I("v_mbcnt_hi_u32_b32", LANE, -1, LANE),
               I("v_and_b32", VI, 15, LANE), I("v_lshrrev_b32", VG, 4, LANE)]
         for qb in range(4):
-            c += [I("v_add_u32", ROW, sNQ0, VI), I("v_add_u32", ROW, 16 * qb, ROW),
+            c += [I("v_add_u32", ROW, sCQ0, VI), I("v_add_u32", ROW, 16 * qb, ROW),
                   I("v_mul_lo_u32", TA, ROW, ARG(AI["on"])),
                   I("v_and_b32", TB, 1, VG), I("v_lshlrev_b32", TB, 5, TB), I("v_add_u32", TA, TA, TB),
                   I("v_lshrrev_b32", TB, 1, VG), I("v_lshlrev_b32", TB, 4, TB), I("v_add_u32", OOFF[qb], TA, TB)]
@@ -374,7 +433,7 @@ class PP64:
                 c += [I("v_permlane16_swap_b32", W(w), W(w + 2)), I("v_permlane16_swap_b32", W(w + 1), W(w + 3))]
             c += [I("v_cmp_gt_u32_e32", VCC, ARG(AI["nq"]), ROW), I("s_and_saveexec_b64", S(sT2.i, 2), VCC)]
             for dbp in range(2):
-                c.append(I("global_store_dwordx4", OOFF[qb], V(W(4 * dbp).i, 4), sNOH, mods=f"offset:{64 * dbp}"))
+                c.append(I("global_store_dwordx4", OOFF[qb], V(W(4 * dbp).i, 4), sCOH, mods=f"offset:{64 * dbp}"))
             c += [I("s_mov_b64", EXEC, S(sT2.i, 2))]
         return c
 
@@ -462,21 +521,12 @@ class PP64:
 
     def block_setup(self):
         e = self.e
-        e(block_params_512())
+        e(block_params_512(sL))
         # K head in s52:53, V head in s94:95, nt in sT8
         e([I("s_mov_b64", sDK, S(K.sT0.i, 2)), I("s_mov_b64", sDV, S(sT2.i, 2)), I("s_mov_b32", sNT, sT8),
-           I("s_mov_b32", sDI, 0)])
-        # Q rows min(q0 + 16 qb + i, Nq - 1), 8 g elements into the row
-        LANE, VI, VG, TA, TB = V(0), V(1), V(2), V(3), V(4)
-        e([I("v_mbcnt_lo_u32_b32", LANE, -1, 0), I("v_mbcnt_hi_u32_b32", LANE, -1, LANE),
-           I("v_and_b32", VI, 15, LANE), I("v_lshrrev_b32", VG, 4, LANE), I("v_lshlrev_b32", TB, 4, VG),
-           I("s_sub_u32", sT6, ARG(AI["nq"]), 1)])
-        for qb in range(4):
-            e([I("v_add_u32", TA, sNQ0, VI), I("v_add_u32", TA, 16 * qb, TA), I("v_min_u32", TA, sT6, TA),
-               I("v_mul_lo_u32", TA, TA, ARG(AI["qn"])), I("v_add_u32", V(8 + qb), TA, TB)])
-        for qb in range(4):
-            for ds in range(2):
-                e([I("global_load_dwordx4", Q_(qb, ds), V(8 + qb), sNQH, mods=f"offset:{64 * ds}")])
+           I("s_mov_b32", sDI, 0), I("s_mov_b64", sCOH, sNOH), I("s_mov_b32", sCQ0, sNQ0)])
+        e(self.q_loads())
+        e(self.next_params())
         for j in range(4):
             e(self.dma_tile(j * SLOT))
         e([I("s_mov_b32", sSD, 4 * SLOT), I("s_mov_b32", sSC, (NSLOT - 1) * SLOT)])
@@ -494,11 +544,20 @@ class PP64:
         e(self.phase_c("first"))
         e([I("s_barrier")])
         e(self.phase_m(True, wait))
-        e([I("s_mov_b32", sT, 1), label(lp), I("s_cmp_ge_u32", sT, sNT), I("s_cbranch_scc1", tail)])
+        end = self.L(f"end{grp}")
+        e([I("s_mov_b32", sT, 1), label(lp), I("s_cmp_ge_u32", sT, sNT), I("s_cbranch_scc1", end)])
         e(self.phase_c("mid"))
         e([I("s_barrier")])
         e(self.phase_m(False, wait))
-        e([I("s_add_u32", sT, sT, 1), I("s_branch", lp), label(tail)])
+        e([I("s_add_u32", sT, sT, 1), I("s_branch", lp)])
+        # the block's last tile: the next block of the persistent walk, or the tail
+        e([label(end), I("s_cmp_eq_u32", sHASN, 0), I("s_cbranch_scc1", tail)])
+        e(self.phase_c("trans"))
+        e([I("s_barrier")])
+        # the block change issued 16 more vector-memory operations (8 Q loads,
+        # 8 O stores) after the pieces this wait is for
+        e(self.phase_m(True, wait + 16))
+        e([I("s_mov_b32", sT, 1), I("s_branch", lp), label(tail)])
         e(self.phase_c("tail"))
         e(self.epilogue())
         if grp == 0:

@@ -27,7 +27,7 @@ def program(dtype="bf16"):
     return _PROG[key]
 
 
-def run(q, k, v, scale=None, muoff=62.0, layout="bhsd", dtype="bf16"):
+def run(q, k, v, scale=None, muoff=62.0, layout="bhsd", dtype="bf16", grid=None):
     """q [B,H,Nq,64], k / v [B,Hkv,Nk,64] -> O [B,H,Nq,64] (inputs rounded to
     bf16, or fp16 with dtype="f16")"""
     enc, dec = (E.f16_rne, E.f16_to_f32) if dtype == "f16" else (E.bf16_rne, E.bf16_to_f32)
@@ -55,7 +55,8 @@ def run(q, k, v, scale=None, muoff=62.0, layout="bhsd", dtype="bf16"):
     so = (Nq * H * D, D, H * D) if layout == "bshd" else (H * Nq * D, Nq * D, D)
     qblocks = -(-Nq // 512)
     nb = B * H * qblocks
-    args = R.args_for(qa, ka, va, oa, B, H, Hkv, Nq, Nk, list(sq) + list(sk) + list(sv) + list(so), scale, nb,
+    G = nb if grid is None else grid  # grid < nb: the persistent walk (L, L + G, ...)
+    args = R.args_for(qa, ka, va, oa, B, H, Hkv, Nq, Nk, list(sq) + list(sk) + list(sv) + list(so), scale, G,
                       muoff, False)
     from v13.kernel import AI
     args[AI["qblocks"]], args[AI["nblocks"]] = qblocks, nb
@@ -63,7 +64,7 @@ def run(q, k, v, scale=None, muoff=62.0, layout="bhsd", dtype="bf16"):
     args[AI["shifts"]] = (int(args[AI["shifts"]]) & ~31) | shq
     kaddr = heap.alloc(args.nbytes, args.tobytes())
     em = E.Emu(program(dtype), heap)
-    for wg in range(nb):
+    for wg in range(G):
         waves = []
         for wv in range(8):
             w = E.Wave()
