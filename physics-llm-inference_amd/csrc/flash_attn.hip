@@ -625,26 +625,30 @@ int launch_mfma(const void* q, const void* k, const void* v, void* o, int B, int
     // the exact bodies (v12 70-74, v7 / v10 51 / 55 / 60) apply c by fma to
     // the fp32 scores: any c > 0; only the prescaled ones (50 / 54) need c <= 1
     const bool c_pos = c_log2 > 0.f;
-    // 86: attn_fwd_pp64 / pp64h where it applies (head dim 64, bf16 / fp16,
-    // non-causal, Nk % 64 == 0; tools/v14/pp64.py), else the default v13 form;
-    // 87: the same with the rescale path at every tile (muoff 0 / -1, tests)
+    // 86: attn_fwd_pp64 / pp64h (causal: pp64c / pp64hc) where it applies
+    // (head dim 64, bf16 / fp16, Nk % 64 == 0; causal with Nq and Nk - Nq
+    // multiples of 64; tools/v14/pp64.py), else the default v13 form; 87: the
+    // same with the rescale path at every tile (muoff 0 / -1, tests)
     // 88 (the default since round 6): 86 where its 512-row blocks fill the
     // chip (B H ceil(Nq / 512) >= the CU count), else 80 -- below that v13's
     // 256-row blocks spread the same work over twice as many CUs (B2 H8 S512:
     // 61 vs 85 TF/s on pp64, profiles/r06/pp64/)
+    // (causal stays on v13c: pp64c -- the causal pp64 forms, one block per
+    // workgroup heaviest first -- measured 725 vs 946 TF/s bf16, 802 vs 941
+    // fp16 at B8 H32 S4096 D64, profiles/r06/pp64/ab9_causal_*.jsonl)
     if (variant == 88) {
-        variant = (int64_t)B * H * cdiv(Nq, 512) >= cu_count(stream) ? 86 : 80;
-        if (causal) variant = 83;
+        const bool fill = (int64_t)B * H * cdiv(Nq, 512) >= cu_count(stream);
+        variant = causal ? 83 : fill ? 86 : 80;
     }
     if (variant == 86 || variant == 87) {
         const bool bf = std::is_same<T, bf16_t>::value;
         const V7Strides s7{st.qb, st.qh, st.qn, st.kb, st.kh, st.kn, st.vb, st.vh, st.vn, st.ob, st.oh, st.on};
-        if (!causal && attn_pp64_ok(D, !bf, false, Nk) && attn_v13_ok(D, bf ? 1 : 0, 0, Nq, Nk, s7) &&
+        if (attn_pp64_ok(D, !bf, causal != 0, Nq, Nk) && attn_v13_ok(D, bf ? 1 : 0, causal, Nq, Nk, s7) &&
             c_log2 > 0.f && H < (1 << 16))
             return launch_attn_v13(q, k, v, o, B, H, group, Nq, Nk, s7, scale, stream, true,
                                    variant == 87 ? (bf ? 0.f : -1.f) : bf ? PLI_V13_MUOFF : v13_muoff_f16(Nk),
-                                   nullptr, false, !bf, D, true);
-        variant = causal ? 83 : variant == 87 ? 82 : 80;
+                                   nullptr, causal != 0, !bf, D, true);
+        variant = causal ? (variant == 87 ? 85 : 83) : variant == 87 ? 82 : 80;
     }
     if (variant >= 80 && variant <= 85) {
         const bool bf = std::is_same<T, bf16_t>::value;

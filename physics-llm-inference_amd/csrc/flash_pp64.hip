@@ -36,10 +36,23 @@ PLI_PP64_KERNEL(attn_fwd_pp64, PLI_PP64_BODY)
 // vector phase (v13's fp16 rule), the mu offset from the launcher's
 // v13_muoff_f16
 PLI_PP64_KERNEL(attn_fwd_pp64h, PLI_PP64H_BODY)
+// causal (bottom-right, Nq and Nk - Nq multiples of 64): per wave, the
+// diagonal key tile masked by VALU, the tiles past it P = 0; one block per
+// workgroup, heaviest first (block_params' remap walk)
+PLI_PP64_KERNEL(attn_fwd_pp64c, PLI_PP64C_BODY)
+PLI_PP64_KERNEL(attn_fwd_pp64hc, PLI_PP64HC_BODY)
 
 }  // namespace
 
-int launch_pp64(bool fp16, unsigned grid, const V13Args& a, hipStream_t stream) {
+int launch_pp64(bool fp16, bool causal, unsigned grid, const V13Args& a, hipStream_t stream) {
+    if (causal) {
+        if (fp16) {
+            hipLaunchKernelGGL(attn_fwd_pp64hc, dim3(grid), dim3(512), 0, stream, a);
+            return launch_status("attn_fwd_pp64hc");
+        }
+        hipLaunchKernelGGL(attn_fwd_pp64c, dim3(grid), dim3(512), 0, stream, a);
+        return launch_status("attn_fwd_pp64c");
+    }
     if (fp16) {
         hipLaunchKernelGGL(attn_fwd_pp64h, dim3(grid), dim3(512), 0, stream, a);
         return launch_status("attn_fwd_pp64h");

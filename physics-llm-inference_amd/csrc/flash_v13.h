@@ -18,9 +18,9 @@ static_assert(sizeof(V13Args) == 256, "V13Args layout");
 // ragged -- Nk % 64 != 0, non-causal) on `grid` workgroups of 256 threads;
 // returns the launch status
 int launch_v13_d64(bool fp16, bool causal, bool ragged, unsigned grid, const V13Args& a, hipStream_t stream);
-// attn_fwd_pp64 / pp64h (flash_pp64.hip): head dim 64, bf16 / fp16, non-causal,
-// Nk % 64 == 0, the arguments with 512-row blocks, one block per workgroup of
-// 512 threads
-int launch_pp64(bool fp16, unsigned grid, const V13Args& a, hipStream_t stream);
+// attn_fwd_pp64 / pp64h / pp64c / pp64hc (flash_pp64.hip): head dim 64, bf16 /
+// fp16, Nk % 64 == 0 (causal: Nq and Nk - Nq too), the arguments with
+// 512-row blocks, workgroups of 512 threads
+int launch_pp64(bool fp16, bool causal, unsigned grid, const V13Args& a, hipStream_t stream);
 
 }  // namespace pli

@@ -182,9 +182,10 @@ bool attn_v13_ok(int D, int is_bf16, int causal, int Nq, int Nk, const V7Strides
     return true;
 }
 
-bool attn_pp64_ok(int D, bool fp16, bool causal, int Nk) {
+bool attn_pp64_ok(int D, bool fp16, bool causal, int Nq, int Nk) {
     (void)fp16;  // bf16 and fp16 bodies
-    return D == 64 && !causal && Nk % 64 == 0;
+    if (D != 64 || Nk % 64 != 0) return false;
+    return !causal || (Nq % 64 == 0 && Nk >= Nq && (Nk - Nq) % 64 == 0);
 }
 
 int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B, int H, int group, int Nq,
@@ -196,14 +197,14 @@ int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B,
                 "attn_fwd_v13: the stamp build is bf16, D = 128, non-causal, Nk % 64 == 0");
     const int nqv = causal ? Nq + ((Nk - Nq) & 63) : Nq;  // causal: virtual rows, (Nk - nqv) % 64 == 0
     // attn_fwd_pp64: 512-row blocks (8 waves of 64 rows), one per workgroup
-    const bool pp = pp64 && !stamps && attn_pp64_ok(D, fp16, causal, Nk);
+    const bool pp = pp64 && !stamps && attn_pp64_ok(D, fp16, causal, Nq, Nk);
     const int qblocks = cdiv(nqv, pp ? 512 : 256);
     const int64_t nb = (int64_t)B * H * qblocks;
     PLI_REQUIRE(nb < (1ll << 31) && nb > 0, "attn_fwd_v13: grid too large");
     int grid = (int)nb;
     // (pp64's persistent walk streams the next block's first four key tiles
     // during the current block: it needs Nk >= 256)
-    if (persistent && (!pp || Nk / 64 >= 4)) {
+    if (persistent && (!pp || (Nk / 64 >= 4 && !causal))) {
         const int g = cu_count(stream) / 8 * 8;
         if (g >= 8 && nb > g) grid = g;
     }
@@ -212,7 +213,9 @@ int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B,
     // workgroups of a head in step on one XCD; G/8 and QB/2 powers of two),
     // else one block per workgroup, heaviest first
     uint32_t cw = 0, hx = 0;
-    if (causal) {
+    if (causal && pp) {
+        cw = 2u;  // pp64c: block_params' remap walk, heaviest block first, one per workgroup
+    } else if (causal) {
         const int64_t bh = nb / qblocks, w = grid / 8, hq = qblocks / 2;
         auto pw2 = [](int64_t x) { return x > 0 && (x & (x - 1)) == 0; };
         const bool pair = grid < nb && qblocks % 2 == 0 && hq > 0 && w % hq == 0 && bh % 8 == 0 &&
@@ -283,7 +286,7 @@ int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B,
 #else
     (void)stamps;
 #endif
-    if (pp) return launch_pp64(fp16, (unsigned)grid, a, stream);
+    if (pp) return launch_pp64(fp16, causal, (unsigned)grid, a, stream);
     if (D == 64) return launch_v13_d64(fp16, causal, ragged, (unsigned)grid, a, stream);
     if (ragged && causal) {
         if (fp16) {

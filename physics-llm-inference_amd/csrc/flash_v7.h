@@ -23,8 +23,9 @@ bool attn_v12_ok(int D, int is_bf16, int causal, int Nk);
 bool attn_v13_ok(int D, int is_bf16, int causal, int Nq, int Nk, const V7Strides& st);
 // attn_fwd_v13 (flash_v13.hip, flash_v13_d64.hip): bf16 or fp16 (fp16 =
 // true), head dim D = 128 or 64; pp64: attn_fwd_pp64 (flash_pp64.hip) where
-// it applies (D = 64, bf16 / fp16, non-causal, Nk % 64 == 0)
-bool attn_pp64_ok(int D, bool fp16, bool causal, int Nk);
+// it applies (D = 64, bf16 / fp16, Nk % 64 == 0; causal: Nq % 64 == 0 and
+// Nk - Nq a non-negative multiple of 64)
+bool attn_pp64_ok(int D, bool fp16, bool causal, int Nq, int Nk);
 int launch_attn_v13(const void* q, const void* k, const void* v, void* o, int B, int H, int group, int Nq,
                     int Nk, const V7Strides& st, float scale, hipStream_t stream, bool persistent, float muoff,
                     uint32_t* stamps = nullptr, bool causal = false, bool fp16 = false, int D = 128,

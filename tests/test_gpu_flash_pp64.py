@@ -116,9 +116,10 @@ def test_pp64_falls_back_where_it_does_not_apply():
     q, k, v = inputs64((1, 2, 2, 256, 320), 5, "fp16")
     pli_hip.flash_attn_fwd(q, k, v)
     assert pli_hip.last_route() == "attn_fwd_v13h_d64"
+    q, k, v = inputs64((1, 2, 2, 200, 320), 5, "fp16")  # causal, Nq % 64 != 0
     pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=86)
     assert pli_hip.last_route() == "attn_fwd_v13hc_d64"
-    q, k, v = inputs64((1, 2, 2, 256, 320), 5, "bf16")
+    q, k, v = inputs64((1, 2, 2, 200, 320), 5, "bf16")  # causal, Nq % 64 != 0
     pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=86)
     assert pli_hip.last_route() == "attn_fwd_v13c_d64"
     q, k, v = inputs64((1, 2, 2, 256, 300), 5, "bf16")
@@ -152,3 +153,45 @@ def test_pp64h_attention_sink_long_context(d, N):
     assert pli_hip.last_route() == "attn_fwd_pp64h"
     err = max_err(out, ref)
     assert err <= 5e-3, f"N {N} d {d}: max |err| {err:.3e}"
+
+
+CROUTE = {"bf16": "attn_fwd_pp64c", "fp16": "attn_fwd_pp64hc"}
+CAUSAL = [(4, 32, 8, 1024, 1024), (2, 16, 4, 2048, 2048), (3, 40, 8, 1024, 1024), (2, 8, 2, 256, 512),
+          (1, 4, 4, 128, 128), (4, 32, 8, 1024, 2048), (2, 8, 2, 576, 576), (1, 2, 1, 64, 4096)]
+
+
+@pytest.mark.parametrize("dt", ("bf16", "fp16"))
+@pytest.mark.parametrize("shape", CAUSAL, ids=lambda s: "b{}h{}kv{}q{}k{}".format(*s))
+def test_pp64_causal_vs_f64_full_tensor(shape, dt):
+    """the causal forms (bottom-right; Nq and Nk - Nq multiples of 64): the
+    diagonal tiles masked by VALU, P = 0 past them; 87 (rescale every tile)
+    within rounding of 86, and v13c's D = 64 program within rounding"""
+    import pli_hip
+    q, k, v = inputs64(shape, sum(shape) % 967, dt)
+    ref = torch_attention(q, k, v, causal=True)
+    outs = {}
+    for var in (86, 87):
+        outs[var] = pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=var)
+        assert pli_hip.last_route() == CROUTE[dt], pli_hip.last_route()
+        err = max_err(outs[var], ref)
+        assert err <= 1e-2, f"{shape} {dt} causal variant {var}: max |err| {err:.4e}"
+    assert_agree_to_rounding(outs[87], outs[86], v)
+    assert_agree_to_rounding(outs[86], pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=83), v)
+
+
+@pytest.mark.parametrize("dt", ("bf16", "fp16"))
+def test_pp64_causal_full_config_all_heads(dt):
+    """B8 S4096 H32 D64 causal (the bench's causal D = 64 legs): all 256 heads
+    against an fp32 torch attention"""
+    import pli_hip
+    B, H, N, D = 8, 32, 4096, 64
+    g = torch.Generator(device=DEV).manual_seed(31)
+    td = torch.bfloat16 if dt == "bf16" else torch.float16
+    q, k, v = (torch.randn(B, H, N, D, device=DEV, dtype=td, generator=g) for _ in range(3))
+    out = pli_hip.flash_attn_fwd(q, k, v, causal=True, variant=86)
+    assert pli_hip.last_route() == CROUTE[dt]
+    for b in range(B):
+        ref = torch_attention(q[b:b + 1], k[b:b + 1], v[b:b + 1], dtype=torch.float32, heads_per_chunk=4,
+                              causal=True)
+        err = max_err(out[b:b + 1], ref)
+        assert err <= 1e-2, f"{dt} batch {b}: max |err| {err:.4e} over its 32 heads"

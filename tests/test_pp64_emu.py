@@ -122,21 +122,49 @@ def test_pp64h_program_vs_f64(case):
         assert em.counts.get("v_sub_f32", 0) > 0, "the rescale path never ran"
 
 
+CAUSAL = [  # (B, H, Hkv, Nq, Nk, layout, muoff): bottom-right mask, Nq and Nk - Nq multiples of 64
+    (1, 1, 1, 512, 512, "bhsd", 62.0),     # one block: each wave's diagonal tile, tiles past it
+    (1, 2, 1, 1024, 1024, "bhsd", 62.0),   # two blocks of 8 / 16 tiles (heaviest first), GQA
+    (1, 1, 1, 512, 768, "bshd", 62.0),     # diagonal offset 4 tiles, BSHD
+    (1, 1, 1, 1024, 1024, "bhsd", 0.0),    # the rescale path at every tile (and not on the tiles past it)
+    (1, 1, 1, 576, 576, "bhsd", 62.0),     # a ragged last block (rows past Nq)
+]
+
+
+@pytest.mark.parametrize("dtype", ("bf16", "f16"))
+@pytest.mark.parametrize("case", CAUSAL, ids=lambda c: "b{}h{}kv{}q{}k{}-{}-mu{}".format(*c))
+def test_pp64_causal_vs_f64(case, dtype):
+    B, H, Hkv, Nq, Nk, lay, muoff = case
+    if dtype == "f16":
+        muoff = 4.0 if muoff > 0 else -1.0
+    rng = np.random.default_rng(Nq + Nk)
+    q = rng.standard_normal((B, H, Nq, 64))
+    k = rng.standard_normal((B, Hkv, Nk, 64))
+    v = rng.standard_normal((B, Hkv, Nk, 64))
+    o, em = P.run(q, k, v, muoff=muoff, layout=lay, dtype=dtype, causal=True)
+    err = np.abs(o - f64_attention(q, k, v, causal=True, dtype=dtype)).max()
+    assert err <= 1e-2, f"max |err| {err:.3e}"
+    if muoff <= 0:
+        assert em.counts.get("v_sub_f32", 0) > 0, "the rescale path never ran"
+
+
 def test_pp64_header_is_fresh():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "v14", "pp64.py"), "--check"])
     assert r.returncode == 0, "csrc/flash_pp64_asm.h is stale: run python tools/v14/pp64.py"
 
 
+@pytest.mark.parametrize("causal", (False, True))
 @pytest.mark.parametrize("dtype", ("bf16", "f16"))
-def test_pp64_hazard_pass_idempotent(dtype):
-    prog, _ = finalize(pp64.PP64(dtype=dtype).build())
+def test_pp64_hazard_pass_idempotent(dtype, causal):
+    prog, _ = finalize(pp64.PP64(dtype=dtype, causal=causal).build())
     assert not analyse(prog), "finalize left hazards or waits unresolved"
 
 
+@pytest.mark.parametrize("causal", (False, True))
 @pytest.mark.parametrize("dtype", ("bf16", "f16"))
-def test_pp64_register_budget(dtype):
+def test_pp64_register_budget(dtype, causal):
     """128 VGPRs + 128 AGPRs (two waves per SIMD) and no SGPR past s99 / s32"""
-    prog, _ = finalize(pp64.PP64(dtype=dtype).build())
+    prog, _ = finalize(pp64.PP64(dtype=dtype, causal=causal).build())
     for ins in prog:
         for o in ins.ops:
             r = getattr(o, "r", o)

@@ -121,23 +121,34 @@ sM0 = S(47)  # m0 at entry (hipcc reserves m0: restored at exit, not clobbered)
 # the persistent walk: the current block's O head and first row (block_params
 # writes the NEXT block's into sNQH / sNOH / sNQ0), whether block L + G exists,
 # and its K / V heads for the DMA stream
-sCOH, sCQ0, sHASN = S(24, 2), S(26), S(27)
+sCOH, sCQ0, sHASN = S(24, 2), S(26), S(33)
 sNXK, sNXV = S(50, 2), S(34, 2)
+# causal: the key-tile offset (Nk - Nq) / 64 (kernel.py's register, which
+# block_params reads) and the wave's diagonal tile
+sOFFT, sDIAG = K.sOFFT, S(48)
 
 
 def slices():
     return [(qb, kb, hh) for qb in range(4) for kb in range(4) for hh in range(2)]
 
 
-def block_params_512(sx):
-    """kernel.py's block_params with 512-row blocks: q0 = 512 qblk + 64 wave"""
+def block_params_512(sx, causal=False, uid=0):
+    """kernel.py's block_params with 512-row blocks: q0 = 512 qblk + 64 wave;
+    causal (the remap walk, heaviest block first): the block's key tiles
+    min(nt, 8 qblk + 8 + offt)"""
     K.GEOM["hd"] = 64  # WSH 11: sWKOFF = wave << 11 gives 64 wave
     K.RAGGED[0] = K.BALANCED[0] = K.SHORTFIRST[0] = False
-    c = K.block_params(sx, causal=False, uid=0)
-    hits = [i for i, ins in enumerate(c) if ins.op == "s_lshl_b32" and ins.ops[0] is not None
-            and str(ins.ops[0]) == str(K.sT2) and str(ins.ops[1]) == str(K.sT2) and ins.ops[2] == 8]
-    assert len(hits) == 1, hits
-    c[hits[0]] = I("s_lshl_b32", K.sT2, K.sT2, 9)
+    c = K.block_params(sx, causal=causal, uid=f"pp{uid}", rev=0)
+
+    def patch(op, a, b, old, new):
+        hits = [i for i, ins in enumerate(c) if ins.op == op and str(ins.ops[0]) == str(a)
+                and str(ins.ops[1]) == str(b) and ins.ops[2] == old]
+        assert len(hits) == 1, (op, hits)
+        c[hits[0]] = I(op, a, b, new)
+    patch("s_lshl_b32", K.sT2, K.sT2, 8, 9)
+    if causal:
+        patch("s_lshl_b32", sT8, K.sT2, 2, 3)
+        patch("s_add_u32", sT8, sT8, 4, 8)
     return c
 
 
@@ -150,7 +161,7 @@ class PP64:
     (A/B knobs, tools/v14/build_pp64_ab.sh); rs_in: l += 1^T P(t) at the
     end of M(t) ("M") or at the head of C(t+1), right before the check ("C")"""
 
-    def __init__(self, tag="%=", dtype="bf16", dma_in="C", split=0, vr_in="C", rs_in="C"):
+    def __init__(self, tag="%=", dtype="bf16", dma_in="C", split=0, vr_in="C", rs_in="C", causal=False):
         assert dtype in ("bf16", "f16") and dma_in in ("M", "C") and vr_in in ("M", "C") and rs_in in ("M", "C")
         assert 0 <= split <= 16 and not (split and rs_in == "M" and vr_in == "C" and False)
         # fp16: P packed to fp16 and checked by the bit-14 test in the vector
@@ -163,12 +174,18 @@ class PP64:
         self.ones = 0x3C003C00 if self.f16 else BF16_ONES
         self.negones = 0xBC00BC00 if self.f16 else NEGONES
         self.dma_in, self.split, self.vr_in, self.rs_in = dma_in, split, vr_in, rs_in
+        # causal (bottom-right, Nq and Nk - Nq multiples of 64): per wave, key
+        # tiles before its diagonal tile run as above, the diagonal tile is
+        # masked by VALU before the softmax, tiles past it get P = 0; one
+        # block per workgroup, heaviest first
+        self.causal = causal
+        assert not (causal and split)
         self.tag = tag
         self.prog = []
         self.sites = []
 
     def L(self, n):
-        return f"pp64{'h' if self.f16 else ''}_{n}_{self.tag}"
+        return f"pp64{'h' if self.f16 else ''}{'c' if self.causal else ''}_{n}_{self.tag}"
 
     def e(self, c):
         self.prog.extend(c)
@@ -335,7 +352,7 @@ class PP64:
         row into sNQH / sNOH / sNQ0 and its K / V heads into sNXK / sNXV"""
         skip = self.L(f"nonext{len(self.prog)}_{self.nuid()}")
         return ([I("s_add_u32", sT7, sL, ARG(AI["G"])), I("s_cmp_lt_u32", sT7, ARG(AI["nblocks"])),
-                 I("s_cselect_b32", sHASN, 1, 0), I("s_cbranch_scc0", skip)] + block_params_512(sT7) +
+                 I("s_cselect_b32", sHASN, 1, 0), I("s_cbranch_scc0", skip)] + block_params_512(sT7, False, self.nuid()) +
                 [I("s_mov_b64", sNXK, S(K.sT0.i, 2)), I("s_mov_b64", sNXV, S(sT2.i, 2)), label(skip)])
 
     def nuid(self):
@@ -352,12 +369,41 @@ class PP64:
         c += [I("s_add_u32", sL, sL, ARG(AI["G"])), I("s_mov_b64", sCOH, sNOH), I("s_mov_b32", sCQ0, sNQ0)]
         return c + self.next_params()
 
+    def diag_mask(self):
+        """the wave's diagonal key tile: 64 t = q0 + Nk - Nq, so key 16 kb +
+        4 g + r of the tile is past row 16 qb + i iff kb > qb, or kb == qb and
+        4 g + r > i: those scores -> -inf (P's registers as temporaries)"""
+        LANE, VI, G4, TR, NINF = V(64), V(65), V(66), V(67), V(68)
+        c = [I("v_mov_b32", S_(kb, qb)[r], 0xFF800000) for qb in range(4) for kb in range(qb + 1, 4) for r in range(4)]
+        c += [I("v_mbcnt_lo_u32_b32", LANE, -1, 0), I("v_mbcnt_hi_u32_b32", LANE, -1, LANE),
+              I("v_and_b32", VI, 15, LANE), I("v_lshrrev_b32", G4, 4, LANE), I("v_lshlrev_b32", G4, 2, G4),
+              I("v_mov_b32", NINF, 0xFF800000)]
+        for r in range(4):
+            c += [I("v_add_u32", TR, r, G4), I("v_cmp_lt_i32_e32", VCC, VI, TR)]
+            c += [I("v_cndmask_b32_e32", S_(qb, qb)[r], S_(qb, qb)[r], NINF, VCC) for qb in range(4)]
+        return c
+
     def c_slices(self):
         """the slices the matrix phase takes (key block 0, q-block major)"""
         return [(qb, kb, hh) for kb in range(2) for qb in range(4) for hh in range(2)][:self.split]
 
     def phase_m(self, first, wait):
-        """tile t's softmax, row sums and V^T reads; tile t+4's DMA"""
+        """tile t's softmax (and the knobs' row sums, V^T reads, DMA); causal:
+        the wave's diagonal tile masked first, the tiles past it P = 0"""
+        if not self.causal:
+            return self.m_body(first) + [I("s_waitcnt", f"vmcnt({wait})"), I("s_barrier")]
+        u = self.nuid()
+        dg, by, done = self.L(f"mdiag{u}"), self.L(f"mbeyond{u}"), self.L(f"mdone{u}")
+        c = [I("s_cmp_eq_u32", sT, sDIAG), I("s_cbranch_scc1", dg)]
+        if not first:  # (tile 0 is never past a diagonal)
+            c += [I("s_cmp_gt_u32", sT, sDIAG), I("s_cbranch_scc1", by)]
+        c += self.m_body(first) + [I("s_branch", done), label(dg)] + self.diag_mask() + self.m_body(first)
+        if not first:
+            c += [I("s_branch", done), label(by)]
+            c += [I("v_mov_b32", P_(qb, kp)[r], 0) for qb in range(4) for kp in range(2) for r in range(4)]
+        return c + [label(done), I("s_waitcnt", f"vmcnt({wait})"), I("s_barrier")]
+
+    def m_body(self, first):
         c = self.dma_tile(sSD) + self.next_slot(sSD) if self.dma_in == "M" else []
         if first:
             # exact row max of tile 0 -> mu = max c + muoff (P's registers as temporaries)
@@ -400,7 +446,7 @@ class PP64:
             self.sites.append((k, ret))
             c += [I("v_and_b32", T0, 0x40004000, T1), I("v_cmp_ne_u32_e32", VCC, 0, T0),  # some P >= 2
                   I("s_mov_b32", sRET, k), I("s_cbranch_vccnz", self.L("rare")), label(ret)]
-        return c + [I("s_waitcnt", f"vmcnt({wait})"), I("s_barrier")]
+        return c
 
     def epilogue(self):
         """O / l, packed to bf16, stored (rows >= Nq masked); S's and P's
@@ -448,6 +494,10 @@ class PP64:
         # row sums went into l; fp16: the tile in slot sSC, checked at the end
         # of its own vector phase (its row sums not taken yet)
         slot, adr = (sSC, VVA) if self.f16 else (sSP, T1)
+        if self.causal and not self.f16:
+            # a tile past the wave's diagonal has P = 0: l >= 1 from earlier
+            # tiles (muoff 0 keeps it there) is no reason to touch it
+            c += [I("s_sub_u32", sT6, sT, 1), I("s_cmp_gt_u32", sT6, sDIAG), I("s_cbranch_scc1", self.L("rare_ret"))]
         if not self.f16:
             neg = S_(0, 0)  # S is recomputed below: its first block holds the -1s meanwhile
             c += [I("v_mov_b32", neg[r], self.negones) for r in range(4)]
@@ -456,6 +506,10 @@ class PP64:
         for n in range(8, 16):
             c += self.k_read(n, adr)
         c += self.qk()
+        if self.causal:  # the checked tile: sT (fp16, vector phase) or sT - 1 (bf16, next matrix phase)
+            skip = self.L("rare_nomask")
+            c += [I("s_sub_u32", sT6, sT, 0 if self.f16 else 1), I("s_cmp_eq_u32", sT6, sDIAG),
+                  I("s_cbranch_scc0", skip)] + self.diag_mask() + [label(skip)]
         m, t1, t2, al, ot = (V(64 + k) for k in range(5))  # P is rebuilt below
         for qb in range(4):
             c += K.row_max(qb, m, t1, t2)
@@ -472,7 +526,7 @@ class PP64:
         c += [I("v_add_u32", adr, slot, VVL)]
         for n in range(8):
             c += self.v_read(n, adr)
-        c += [I("s_nop", 4)]
+        c += [I("s_nop", 4), label(self.L("rare_ret"))]
         for k, ret in self.sites:
             c += [I("s_cmp_eq_u32", sRET, k), I("s_cbranch_scc1", ret)]
         c += [I("s_branch", self.L("exit"))]  # unreachable
@@ -521,12 +575,17 @@ class PP64:
 
     def block_setup(self):
         e = self.e
-        e(block_params_512(sL))
+        if self.causal:
+            e([I("s_load_dword", sOFFT, sKA, 4 * AI["offt"]), I("s_waitcnt", "lgkmcnt(0)")])
+        e(block_params_512(sL, self.causal, self.nuid()))
         # K head in s52:53, V head in s94:95, nt in sT8
         e([I("s_mov_b64", sDK, S(K.sT0.i, 2)), I("s_mov_b64", sDV, S(sT2.i, 2)), I("s_mov_b32", sNT, sT8),
            I("s_mov_b32", sDI, 0), I("s_mov_b64", sCOH, sNOH), I("s_mov_b32", sCQ0, sNQ0)])
         e(self.q_loads())
-        e(self.next_params())
+        if self.causal:  # one block per workgroup; the wave's diagonal key tile (q0 + Nk - Nq) / 64
+            e([I("s_mov_b32", sHASN, 0), I("s_lshr_b32", sDIAG, sCQ0, 6), I("s_add_u32", sDIAG, sDIAG, sOFFT)])
+        else:
+            e(self.next_params())
         for j in range(4):
             e(self.dma_tile(j * SLOT))
         e([I("s_mov_b32", sSD, 4 * SLOT), I("s_mov_b32", sSC, (NSLOT - 1) * SLOT)])
@@ -541,6 +600,7 @@ class PP64:
         e([I("s_waitcnt", f"vmcnt({wait})"), I("s_barrier")])
         if grp == 1:
             e([I("s_barrier")])  # B runs half a period behind A
+        e([I("s_mov_b32", sT, 0)])  # (the vector phase's tile index; causal reads it)
         e(self.phase_c("first"))
         e([I("s_barrier")])
         e(self.phase_m(True, wait))
@@ -553,7 +613,7 @@ class PP64:
         # the block's last tile: the next block of the persistent walk, or the tail
         e([label(end), I("s_cmp_eq_u32", sHASN, 0), I("s_cbranch_scc1", tail)])
         e(self.phase_c("trans"))
-        e([I("s_barrier")])
+        e([I("s_barrier"), I("s_mov_b32", sT, 0)])
         # the block change issued 16 more vector-memory operations (8 Q loads,
         # 8 O stores) after the pieces this wait is for
         e(self.phase_m(True, wait + 16))
@@ -583,9 +643,13 @@ def render(**kw):
     # A/B knobs: key=val for the bf16 body, h_key=val for the fp16 one
     kwb = {k: v for k, v in kw.items() if not k.startswith("h_")}
     kwh = {k[2:]: v for k, v in kw.items() if k.startswith("h_")}
-    for name, dt in (("PLI_PP64_BODY", "bf16"), ("PLI_PP64H_BODY", "f16")):
-        prog, st = finalize(PP64(dtype=dt, **(kwh if dt == "f16" else kwb)).build())
-        lines.append(f"// {dt}: {len(prog)} instructions, hazard pass: {st['nop_ws']} nop wait states, "
+    for name, dt, cz in (("PLI_PP64_BODY", "bf16", False), ("PLI_PP64H_BODY", "f16", False),
+                         ("PLI_PP64C_BODY", "bf16", True), ("PLI_PP64HC_BODY", "f16", True)):
+        kwx = dict(kwh if dt == "f16" else kwb)
+        if cz:
+            kwx.pop("split", None)
+        prog, st = finalize(PP64(dtype=dt, causal=cz, **kwx).build())
+        lines.append(f"// {dt}{' causal' if cz else ''}: {len(prog)} instructions, hazard pass: {st['nop_ws']} nop wait states, "
                      f"{st['waits']} waits")
         lines.append(f"#define {name} \\")
         for ins in prog:

@@ -19,15 +19,15 @@ from v14.pp64 import PP64  # noqa: E402
 _PROG = {}
 
 
-def program(dtype="bf16"):
-    key = "p" if dtype == "bf16" else dtype
+def program(dtype="bf16", causal=False):
+    key = ("p" if dtype == "bf16" else dtype) + ("c" if causal else "")
     if key not in _PROG:
-        prog = PP64(tag="emu", dtype=dtype).build(in_kernarg=S(0, 2), in_wg=S(2), in_wave=S(3))
+        prog = PP64(tag="emu", dtype=dtype, causal=causal).build(in_kernarg=S(0, 2), in_wg=S(2), in_wave=S(3))
         _PROG[key], _ = finalize(prog)
     return _PROG[key]
 
 
-def run(q, k, v, scale=None, muoff=62.0, layout="bhsd", dtype="bf16", grid=None):
+def run(q, k, v, scale=None, muoff=62.0, layout="bhsd", dtype="bf16", grid=None, causal=False):
     """q [B,H,Nq,64], k / v [B,Hkv,Nk,64] -> O [B,H,Nq,64] (inputs rounded to
     bf16, or fp16 with dtype="f16")"""
     enc, dec = (E.f16_rne, E.f16_to_f32) if dtype == "f16" else (E.bf16_rne, E.bf16_to_f32)
@@ -62,8 +62,11 @@ def run(q, k, v, scale=None, muoff=62.0, layout="bhsd", dtype="bf16", grid=None)
     args[AI["qblocks"]], args[AI["nblocks"]] = qblocks, nb
     args[AI["magq"]], shq = R.magic(qblocks)
     args[AI["shifts"]] = (int(args[AI["shifts"]]) & ~31) | shq
+    if causal:  # bottom-right, Nq and Nk - Nq multiples of 64: the remap walk, heaviest first
+        assert Nq % 64 == 0 and (Nk - Nq) % 64 == 0 and Nk >= Nq and grid is None
+        args[AI["cw"]], args[AI["offt"]] = 2, (Nk - Nq) // 64
     kaddr = heap.alloc(args.nbytes, args.tobytes())
-    em = E.Emu(program(dtype), heap)
+    em = E.Emu(program(dtype, causal), heap)
     for wg in range(G):
         waves = []
         for wv in range(8):
