@@ -121,7 +121,7 @@ sM0 = S(47)  # m0 at entry (hipcc reserves m0: restored at exit, not clobbered)
 # the persistent walk: the current block's O head and first row (block_params
 # writes the NEXT block's into sNQH / sNOH / sNQ0), whether block L + G exists,
 # and its K / V heads for the DMA stream
-sCOH, sCQ0, sHASN = S(24, 2), S(26), S(33)
+sCOH, sCQ0 = S(24, 2), S(26)
 sNXK, sNXV = S(50, 2), S(34, 2)
 # causal: the key-tile offset (Nk - Nq) / 64 (kernel.py's register, which
 # block_params reads) and the wave's diagonal tile
@@ -180,6 +180,12 @@ class PP64:
         # block per workgroup, heaviest first
         self.causal = causal
         assert not (causal and split)
+        # whether block L + G exists (the persistent walk); causal needs s27
+        # for block_params' key-tile offset.  (Not s33: the bf16 body with
+        # sHASN in s33 ran 10 % slower, 1092 vs 1212-1244 TF/s, same process,
+        # profiles/r06/pp64/ab10_regress_*.jsonl -- s33 is the ABI's frame pointer)
+        global sHASN
+        sHASN = S(49) if causal else S(27)
         self.tag = tag
         self.prog = []
         self.sites = []
@@ -600,7 +606,8 @@ class PP64:
         e([I("s_waitcnt", f"vmcnt({wait})"), I("s_barrier")])
         if grp == 1:
             e([I("s_barrier")])  # B runs half a period behind A
-        e([I("s_mov_b32", sT, 0)])  # (the vector phase's tile index; causal reads it)
+        if self.causal:
+            e([I("s_mov_b32", sT, 0)])  # (the vector phase's tile index)
         e(self.phase_c("first"))
         e([I("s_barrier")])
         e(self.phase_m(True, wait))
@@ -613,7 +620,7 @@ class PP64:
         # the block's last tile: the next block of the persistent walk, or the tail
         e([label(end), I("s_cmp_eq_u32", sHASN, 0), I("s_cbranch_scc1", tail)])
         e(self.phase_c("trans"))
-        e([I("s_barrier"), I("s_mov_b32", sT, 0)])
+        e([I("s_barrier")])
         # the block change issued 16 more vector-memory operations (8 Q loads,
         # 8 O stores) after the pieces this wait is for
         e(self.phase_m(True, wait + 16))
