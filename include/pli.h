@@ -373,7 +373,13 @@ int pli_attn_decode_dev(const void* q, const void* k, const void* v, void* o,
  *   multiple of 64 from 128, or any Nk > 64 (attn_fwd_v13r / v13hr: the last
  *   key tile fetched from key Nk - 64, its overlap masked in P); 83 / 84 /
  *   85 the causal forms (83 = causal default for any Nq <= Nk and Nk > 64,
- *   ragged Nk on attn_fwd_v13rc / v13hrc; other shapes take 74 / 60).  Prescaled variants round Q * scale * log2(e) to
+ *   ragged Nk on attn_fwd_v13rc / v13hrc; other shapes take 74 / 60);
+ *   86 / 87 attn_fwd_pp64 / pp64h (head dim 64, two waves per SIMD,
+ *   512-row blocks; causal: pp64c / pp64hc with Nq and Nk - Nq multiples
+ *   of 64) / the same with the rescale path at every tile, other shapes
+ *   take 80 / 83 (82 / 85); 88 (the default since round 6) = 86 for
+ *   non-causal D = 64 where B H ceil(Nq / 512) fills the CUs, else 80 /
+ *   83.  Prescaled variants round Q * scale * log2(e) to
  *   the 16-bit input type (2^-9 relative score error in bf16).  The v13
  *   forms, v12 and the exact v7 / v10 bodies (51 / 55 / 60) take any
  *   scale > 0; the prescaled 50 / 54 take scale * log2(e) <= 1 (larger

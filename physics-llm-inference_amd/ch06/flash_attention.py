@@ -22,7 +22,9 @@ ahead (causal runs the same program with the mask, attn_fwd_v13c, at any
 diagonal offset; fp16 on
 the f16 MFMA; D = 64 on half-width images; key counts that are not a multiple
 of 64 on the ragged form, attn_fwd_v13r; Nk <= 64 and other head dims take
-attn_fwd_v12 / v10 / v7).  The GPU path ignores the requested values (results do not
+attn_fwd_v12 / v10 / v7; since round 6 non-causal D = 64 shapes that fill
+the chip run attn_fwd_pp64 -- 512 rows per workgroup, 8 waves of 64, two
+per SIMD in ping-pong).  The GPU path ignores the requested values (results do not
 depend on the blocking; the kernel's tiles are set by the MFMA / LDS
 mapping); the CPU recurrence uses ``block_q``/``block_k`` as the reference
 does.  Non-positive or non-integer fields are rejected on both paths.  Softmax statistics are fp32 on both paths (the reference keeps
@@ -50,7 +52,9 @@ class FlashAttentionConfig:
 # generated attn_fwd_v13 family (v13 / v13c / v13h / v13hc / v13r / v13rc /
 # the _d64 bodies) -- 256-row blocks of 4 waves x 64 rows, 64-key tiles, a
 # 5-slot LDS ring two tiles ahead; only other head dims and Nk <= 64 fall
-# back to attn_fwd_v12 / v10 / v7 (csrc/flash_v13.hip attn_v13_ok)
+# back to attn_fwd_v12 / v10 / v7 (csrc/flash_v13.hip attn_v13_ok).  Non-causal
+# D = 64 where B H ceil(Nq / 512) fills the CUs: attn_fwd_pp64 (512-row blocks
+# of 8 waves, a 6-slot ring four tiles ahead; tools/v14/pp64.py)
 HIP_TILING = {"block_q": 256, "block_k": 64, "num_warps": 4, "num_stages": 5}
 
 

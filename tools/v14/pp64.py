@@ -161,7 +161,7 @@ class PP64:
     (A/B knobs, tools/v14/build_pp64_ab.sh); rs_in: l += 1^T P(t) at the
     end of M(t) ("M") or at the head of C(t+1), right before the check ("C")"""
 
-    def __init__(self, tag="%=", dtype="bf16", dma_in="C", split=0, vr_in="C", rs_in="C", causal=False):
+    def __init__(self, tag="%=", dtype="bf16", dma_in="C", split=0, vr_in="C", rs_in="C", causal=False, hchk="M"):
         assert dtype in ("bf16", "f16") and dma_in in ("M", "C") and vr_in in ("M", "C") and rs_in in ("M", "C")
         assert 0 <= split <= 16 and not (split and rs_in == "M" and vr_in == "C" and False)
         # fp16: P packed to fp16 and checked by the bit-14 test in the vector
@@ -180,6 +180,12 @@ class PP64:
         # block per workgroup, heaviest first
         self.causal = causal
         assert not (causal and split)
+        # fp16's P-bit check at the end of M(t) ("M") or at the head of
+        # C(t+1), before that tile's row sums ("C": the OR of P(t)'s words
+        # moves out of the vector phase; the rescale path then runs in the
+        # matrix phase like bf16's, with no row sums to take back)
+        assert hchk in ("M", "C") and not (hchk == "C" and split)
+        self.hchk = hchk if self.f16 else "M"
         # whether block L + G exists (the persistent walk); causal needs s27
         # for block_params' key-tile offset.  (Not s33: the bf16 body with
         # sHASN in s33 ran 10 % slower, 1092 vs 1212-1244 TF/s, same process,
@@ -273,6 +279,8 @@ class PP64:
         block registers moved on, QK of the next block's tile 0)"""
         c = [I("s_mov_b32", sSP, sSC)] + self.next_slot(sSC) + [I("v_add_u32", VKA, sSC, VKL)]
         if kind != "first":
+            if self.f16 and self.hchk == "C":
+                c += self.pbit_check([P_(qb, kp)[w] for qb in range(4) for kp in range(2) for w in range(4)])
             if self.rs_in == "C":
                 c += self.rowsums(ONES)
             if not self.f16:
@@ -375,6 +383,19 @@ class PP64:
         c += [I("s_add_u32", sL, sL, ARG(AI["G"])), I("s_mov_b64", sCOH, sNOH), I("s_mov_b32", sCQ0, sNQ0)]
         return c + self.next_params()
 
+    def pbit_check(self, words):
+        """fp16: the rescale path when some P >= 2 (bit 14 of a half) among words"""
+        c = [I("v_or3_b32", T1, words[0], words[1], words[2])]
+        for k in range(3, len(words) - 1, 2):
+            c.append(I("v_or3_b32", T1, T1, words[k], words[k + 1]))
+        if len(words) % 2 == 0:
+            c.append(I("v_or_b32", T1, T1, words[-1]))
+        k = len(self.sites)
+        ret = self.L(f"ret{k}")
+        self.sites.append((k, ret))
+        return c + [I("v_and_b32", T0, 0x40004000, T1), I("v_cmp_ne_u32_e32", VCC, 0, T0),
+                    I("s_mov_b32", sRET, k), I("s_cbranch_vccnz", self.L("rare")), label(ret)]
+
     def diag_mask(self):
         """the wave's diagonal key tile: 64 t = q0 + Nk - Nq, so key 16 kb +
         4 g + r of the tile is past row 16 qb + i iff kb > qb, or kb == qb and
@@ -428,7 +449,8 @@ class PP64:
         if reads:
             c += [I("v_add_u32", VVA, sSC, VVL)]
         n = len(sl)
-        if self.f16 and (first or not self.split):
+        mchk = self.f16 and self.hchk == "M"
+        if mchk and (first or not self.split):
             c += [I("v_mov_b32", T1, 0)]
         for j in range(n + 2):
             if j < n:
@@ -438,7 +460,7 @@ class PP64:
             if 2 <= j:
                 c += cv[j - 2]
                 qb, kb, hh = sl[j - 2]
-                if self.f16 and j % 2 == 1:  # the P-bit check: OR of the tile's P words
+                if mchk and j % 2 == 1:  # the P-bit check: OR of the tile's P words
                     c.append(I("v_or3_b32", T1, T1, cv[j - 3][0].ops[0], cv[j - 2][0].ops[0]))
                 if kb & 1 and hh and self.rs_in == "M":  # P(qb, kb >> 1) complete
                     c.append(rs[2 * qb + (kb >> 1)])
@@ -446,7 +468,7 @@ class PP64:
             h0 = n - 16
             if reads and j >= h0 and (j - h0) % 2 == 0 and (j - h0) // 2 < 8:
                 c += reads[(j - h0) // 2]
-        if self.f16:
+        if mchk:
             k = len(self.sites)
             ret = self.L(f"ret{k}")
             self.sites.append((k, ret))
@@ -499,8 +521,9 @@ class PP64:
         # bf16: the tile in slot sSP, checked at the head of C(t+1) after its
         # row sums went into l; fp16: the tile in slot sSC, checked at the end
         # of its own vector phase (its row sums not taken yet)
-        slot, adr = (sSC, VVA) if self.f16 else (sSP, T1)
-        if self.causal and not self.f16:
+        mmode = self.f16 and self.hchk == "M"  # (checked in its own vector phase)
+        slot, adr = (sSC, VVA) if mmode else (sSP, T1)
+        if self.causal and not mmode:
             # a tile past the wave's diagonal has P = 0: l >= 1 from earlier
             # tiles (muoff 0 keeps it there) is no reason to touch it
             c += [I("s_sub_u32", sT6, sT, 1), I("s_cmp_gt_u32", sT6, sDIAG), I("s_cbranch_scc1", self.L("rare_ret"))]
@@ -514,7 +537,7 @@ class PP64:
         c += self.qk()
         if self.causal:  # the checked tile: sT (fp16, vector phase) or sT - 1 (bf16, next matrix phase)
             skip = self.L("rare_nomask")
-            c += [I("s_sub_u32", sT6, sT, 0 if self.f16 else 1), I("s_cmp_eq_u32", sT6, sDIAG),
+            c += [I("s_sub_u32", sT6, sT, 0 if mmode else 1), I("s_cmp_eq_u32", sT6, sDIAG),
                   I("s_cbranch_scc0", skip)] + self.diag_mask() + [label(skip)]
         m, t1, t2, al, ot = (V(64 + k) for k in range(5))  # P is rebuilt below
         for qb in range(4):
