@@ -333,6 +333,24 @@ class Emu:
         if op == "v_fma_f32":
             r = (gf(o[1]).astype(np.float64) * gf(o[2]) + gf(o[3])).astype(np.float32)
             return self.vset(w, o[0], f2u(r))
+        if op == "v_pk_fma_f32":  # two fp32 fmas on register pairs; op_sel / op_sel_hi pick each source dword
+            md = {}
+            for part in ins.mods.split():
+                if ":" in part:
+                    key, val = part.split(":", 1)
+                    md[key] = [int(x) for x in val.strip("[]").split(",")]
+            sel = (md.get("op_sel", [0, 0, 0]), md.get("op_sel_hi", [1, 1, 1]))
+            neg = (md.get("neg_lo", [0, 0, 0]), md.get("neg_hi", [0, 0, 0]))
+
+            def dw(x, k):
+                return u2f(self.vec(w, Reg(x.f, x.i + k, 1)))
+            res = []
+            for h in range(2):
+                a, b, c_ = ((-1.0 if neg[h][j] else 1.0) * dw(o[1 + j], sel[h][j]).astype(np.float64) for j in range(3))
+                res.append((a * b + c_).astype(np.float32))
+            for h in range(2):
+                self.vset(w, Reg("v", o[0].i + h, 1), f2u(res[h]))
+            return
         if op == "v_exp_f32":
             with np.errstate(over="ignore"):
                 r = np.exp2(gf(o[1]))

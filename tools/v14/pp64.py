@@ -252,7 +252,12 @@ class PP64:
         s = S_(kb, qb)
         y0, y1 = s[2 * hh], s[2 * hh + 1]
         xm = "" if self.f16 else "clamp"  # (fp16: P >= 2 is the check's signal)
-        return ([I("v_fma_f32", y0, y0, sC, Neg(MU(qb))), I("v_fma_f32", y1, y1, sC, Neg(MU(qb)))],
+        # (the pair on one v_pk_fma_f32 -- hipcc's broadcast form, op_sel_hi
+        # [1,0,h] -- was built and measured: 15 % slower both dtypes and the
+        # bf16 output wrong, max diff 6-16, while the emulator, which models
+        # no hazard for it, agreed with f64; profiles/r06/pp64/ab13_pkfma_*)
+        fm = [I("v_fma_f32", y0, y0, sC, Neg(MU(qb))), I("v_fma_f32", y1, y1, sC, Neg(MU(qb)))]
+        return (fm,
                 [I("v_exp_f32", y0, y0, mods=xm), I("v_exp_f32", y1, y1, mods=xm)],
                 [I(self.cvt, P_(qb, kb >> 1)[2 * (kb & 1) + hh], y0, y1)])
 
