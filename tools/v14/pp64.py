@@ -161,7 +161,8 @@ class PP64:
     (A/B knobs, tools/v14/build_pp64_ab.sh); rs_in: l += 1^T P(t) at the
     end of M(t) ("M") or at the head of C(t+1), right before the check ("C")"""
 
-    def __init__(self, tag="%=", dtype="bf16", dma_in="C", split=0, vr_in="C", rs_in="C", causal=False, hchk="M"):
+    def __init__(self, tag="%=", dtype="bf16", dma_in="C", split=0, vr_in="C", rs_in="C", causal=False, hchk="M",
+                 dma_at=20):
         assert dtype in ("bf16", "f16") and dma_in in ("M", "C") and vr_in in ("M", "C") and rs_in in ("M", "C")
         assert 0 <= split <= 16 and not (split and rs_in == "M" and vr_in == "C" and False)
         # fp16: P packed to fp16 and checked by the bit-14 test in the vector
@@ -186,6 +187,7 @@ class PP64:
         # matrix phase like bf16's, with no row sums to take back)
         assert hchk in ("M", "C") and not (hchk == "C" and split)
         self.hchk = hchk if self.f16 else "M"
+        self.dma_at = dma_at  # (matrix-phase MFMA after which the DMA pieces issue; A/B knob)
         # whether block L + G exists (the persistent walk); causal needs s27
         # for block_params' key-tile offset.  (Not s33: the bf16 body with
         # sHASN in s33 ran 10 % slower, 1092 vs 1212-1244 TF/s, same process,
@@ -322,7 +324,7 @@ class PP64:
                 if vr:
                     after.setdefault(32 + 4 * (n - 8) + 3, []).append(n - 8 + 100)
             if dma:
-                after.setdefault(20, []).append("dma")
+                after.setdefault(self.dma_at, []).append("dma")
         sp = []
         if kind == "mid" and self.split:
             if self.f16:  # the P-bit OR starts with the slices this phase takes
