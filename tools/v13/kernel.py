@@ -991,7 +991,7 @@ class Gen:
                  rev=True, qscale=False, dma_pv=0, dma_pv_spacing=16, budget_pv=None, lcheck=None, dtype="bf16",
                  hd=128, short_first=False, ragged=False, oline=False, seam_wait=False, o_bits=0, q_bits=0,
                  beyond=4, qsep=0, balanced=False, noreload=False, propipe=False, trans=1, qsplit=False,
-                 tailepi=False):
+                 tailepi=False, pad=0):
         global DMA_COST
         TAILEPI[0] = int(tailepi)  # 1: one fill per unit, 2: four (reads + muls x 2, pack, store)
         # (head dim 64 only: the AGPRs for Q lo; other forms ignore it)
@@ -1038,6 +1038,7 @@ class Gen:
         ABL.update(abl)
         DMA_COST = dma_cost
         self.stamp = stamp  # diagnostic build: s_memtime / s_memrealtime at entry and exit
+        self.pad = int(pad)  # A/B knob: s_nop 0 before the step loop (moves the loop's code address)
         self.causal = causal
         self.prog = []
         self.sites = []  # (site id, rare block name, return label)
@@ -1364,6 +1365,8 @@ class Gen:
     def loop_and_tails(self):
         e, Lb = self.emit, self.L
         # steps t = 1 .. nt-1, two per iteration (P states 1 / 0)
+        if self.pad:
+            e([I("s_nop", 0)] * self.pad)
         e([label(Lb("loop"))])
         self.step_dispatch(1)
         e([I("s_add_u32", sT, sT, 1), I("s_cmp_ge_u32", sT, sNT), I("s_cbranch_scc1", Lb("tail1"))])
