@@ -1,7 +1,7 @@
 # GPU box: the causal pp64 forms -- the pp64 tests (all forms), then causal
 # D = 64 against v13c (83) in one process, both dtypes
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
-O=$GRAFT_REPO_ROOT/gpurun_out/${PP_TAG:-pp64_5}
+O=$GRAFT_REPO_ROOT/gpurun_out/${PP_TAG:-pp64_causal}
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_gpu_flash_pp64.py -x -q -p no:cacheprovider --timeout 200 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?; tail -4 $O/pytest.log; [ $rc -eq 0 ] || exit $rc

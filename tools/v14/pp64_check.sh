@@ -1,7 +1,7 @@
 # GPU box: pp64 bf16 + fp16 -- its tests, the D = 64 / fp16 / parity suites,
 # then the product route against v13 (variant 80) in one process, both dtypes
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
-O=$GRAFT_REPO_ROOT/gpurun_out/${PP_TAG:-pp64_3}
+O=$GRAFT_REPO_ROOT/gpurun_out/${PP_TAG:-pp64_check}
 mkdir -p $O
 timeout -k 10 700 python -u -m pytest tests/test_gpu_flash_pp64.py tests/test_gpu_flash_v13_d64.py tests/test_gpu_flash_v13_f16.py tests/test_gpu_parity.py tests/test_gpu_ch01_ch05.py -x -q -p no:cacheprovider --timeout 200 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?; tail -4 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
